@@ -1,0 +1,234 @@
+#!/usr/bin/env python
+"""Training throughput of the MI355X-native optical-flow hot path (BASELINE.json metric:
+image-pairs/sec training, 384x512, batch 8 per GPU, at 1/2/4/8 MI355X; EPE vs ref).
+
+One step = forward (Siamese encoder + 4 flow modules) + photometric loss + backward + (N>1:
+RCCL all-reduce of gradient buckets, overlapped with the backward) + Keras-Adam update, on a
+synthetic batch resident in HBM.  Launch: ``python bench.py`` (N=1) or
+``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
+
+Prints ONE JSON line (rank 0) with the contract fields plus:
+  roofline      -- dominant kernel (the fp32 MFMA implicit-GEMM conv) measured with hipEvents
+                   around every conv launch of extra instrumented steps on the launch stream:
+                   achieved = algorithmic FLOPs / launch duration, vs the fp32 MFMA peak.
+  cpu_baseline  -- the CPU oracle (reference semantics restated in torch-CPU fp32) timed on
+                   this host on a bounded sample (1 pair at 384x512), rank 0 only.
+  parity        -- EPE / loss error between the HIP path and that oracle run on the same
+                   pair and initial weights.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (spec)
+KIND_NAMES = {0: "conv_gemm_f32<fwd>", 1: "conv_gemm_f32<dgrad>", 2: "conv_gemm_f32<wgrad>"}
+
+
+def gflop_per_pair(H, W, max_disp=3):
+    """Algorithmic training FLOPs per image pair (SURVEY.md §8 d): every conv's fwd + dgrad +
+    wgrad (2 FLOP/MAC, logical channels, TF-'same' output sizes) minus the stem dgrad, plus
+    3x the cost-volume forward."""
+    from optical_flow_amd.params import ENC_CHANNELS, HEAD_WIDTHS, encoder_blocks, head_cin
+    macs = 0.0
+    h, w = H // 2, W // 2
+    stem = 2 * h * w * 7 * 7 * 3 * 64             # both Siamese branches
+    macs += 2 * stem                               # fwd + wgrad (no input grad for images)
+    hh, ww = h // 2, w // 2
+    for prefix, cin, cout, stride, proj in encoder_blocks():
+        ho, wo = hh // stride, ww // stride
+        m = 2 * ho * wo                            # two branches
+        macs += 3 * m * 9 * cin * cout             # conv_a
+        macs += 3 * m * 9 * cout * cout            # conv_b
+        if proj:
+            macs += 3 * m * cin * cout
+        hh, ww = ho, wo
+    corr = 0.0
+    for level in range(4):
+        s = 16 >> level
+        ph, pw = H // s, W // s
+        cin = head_cin(level, max_disp)
+        for cout in HEAD_WIDTHS:
+            macs += 3 * ph * pw * 9 * cin * cout
+            cin = cout
+        c = ENC_CHANNELS[3 - level]
+        corr += 2.0 * ph * pw * (2 * max_disp + 1) ** 2 * c
+    return (2 * macs + 3 * corr) / 1e9
+
+
+def cpu_baseline(pair_np, vals, steps=2):
+    """Oracle train_step (torch CPU fp32, reference semantics) on one pair; returns
+    (pairs/s, threads, flows_at_init, loss_at_init)."""
+    from oracle import ref_flow as R
+    from optical_flow_amd.params import encoder_blocks
+    threads = torch.get_num_threads()
+    p = {k: torch.tensor(v) for k, v in vals.items()}
+    blocks = list(encoder_blocks())
+    x = torch.tensor(pair_np)
+    loss0, flows0, _ = R.train_step(x, p, blocks, None)      # warm-up + reference outputs
+    opt = R.KerasAdam()
+    t0 = time.time()
+    n = 0
+    while n < steps:
+        R.train_step(x, p, blocks, opt)
+        n += 1
+        if time.time() - t0 > 25.0:
+            break
+    dt = time.time() - t0
+    return n * x.shape[0] / dt, threads, flows0, float(loss0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--height", type=int, default=384)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--timing-steps", type=int, default=2)
+    args = ap.parse_args()
+
+    from optical_flow_amd import _lib, ops
+    from optical_flow_amd.data import synthetic_batch
+    from optical_flow_amd.dist import init_from_env
+    from optical_flow_amd.loss import LossLayer
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import flow_net_spec, init_params
+    from optical_flow_amd.train import KerasAdam, Trainer
+
+    rank, world, local = init_from_env()
+    torch.cuda.set_device(local)
+    _lib.load()
+    H, W, B = args.height, args.width, args.batch
+    vals = init_params(flow_net_spec(), 0)                 # identical weights on every rank
+    net = FlowNet(H, W, values=vals)
+    trainer = Trainer(net, KerasAdam(net.store), LossLayer())
+    batch = torch.from_numpy(synthetic_batch(B, H, W, seed=1234, rank=rank)).cuda()
+
+    # ---- parity probe: HIP forward on pair 0 with the initial weights -------------------
+    with torch.no_grad():
+        flows_hip = [f.cpu() for f in net(batch[:1].contiguous())]
+        loss_hip = float(LossLayer()(batch[:1].contiguous(), [f.cuda() for f in flows_hip]))
+
+    # ---- training throughput --------------------------------------------------------------
+    for i in range(args.warmup):
+        trainer.train_step(batch, i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss, _ = trainer.train_step(batch, args.warmup + i)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed)
+    pairs = world * B * args.steps
+    value = pairs / elapsed
+    final_loss = float(loss)
+
+    # ---- dominant-kernel roofline (instrumented extra steps, outside the timed region) ----
+    lib = _lib.lib()
+    lib.of_timing_enable(1)
+    for i in range(args.timing_steps):
+        trainer.train_step(batch, 10_000 + i)
+    torch.cuda.synchronize()
+    lib.of_timing_enable(0)
+    cap = 4096
+    kinds = (C.c_int * cap)()
+    flops = (C.c_double * cap)()
+    ms = (C.c_float * cap)()
+    n = lib.of_timing_read(cap, kinds, flops, ms)
+    per = {}
+    for i in range(n):
+        k = kinds[i]
+        tf, tm, cnt = per.get(k, (0.0, 0.0, 0))
+        per[k] = (tf + flops[i], tm + ms[i], cnt + 1)
+    dom = max(per, key=lambda k: per[k][1]) if per else None
+    roof = None
+    conv_ms_step = sum(v[1] for v in per.values()) / max(args.timing_steps, 1)
+    if dom is not None:
+        tf, tm, cnt = per[dom]
+        achieved = tf / (tm * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": KIND_NAMES[dom], "achieved": round(achieved, 2),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "launches": cnt, "avg_launch_ms": round(tm / cnt, 4),
+                "gflop_per_launch": round(tf / cnt / 1e9, 3),
+                "all_conv": {KIND_NAMES[k]: {"launches": v[2], "ms": round(v[1], 3),
+                                             "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
+                             for k, v in sorted(per.items())}}
+
+    # ---- CPU baseline + EPE vs the oracle (rank 0 only) ----------------------------------
+    cpu = None
+    parity = None
+    if rank == 0 and not args.no_cpu_baseline:
+        pair = batch[:1].cpu().numpy()
+        cps, threads, flows_ref, loss_ref = cpu_baseline(pair, vals, args.cpu_steps)
+        cpu = {"value": round(cps, 4), "unit": "image-pairs/s", "cores": threads,
+               "kind": "port",
+               "sample": "%d oracle train steps (torch-CPU fp32 restatement of the reference "
+                         "semantics) on 1 pair at %dx%d, after 1 untimed step"
+                         % (args.cpu_steps, H, W)}
+        epe = [float((a - b.float()).norm(dim=-1).mean()) for a, b in zip(flows_hip, flows_ref)]
+        rel = [float((a - b.float()).abs().max() / b.abs().max()) for a, b in
+               zip(flows_hip, flows_ref)]
+        parity = {"epe": [round(e, 6) for e in epe], "flow_rel_inf": [float("%.3e" % r) for r in rel],
+                  "loss_rel": float("%.3e" % (abs(loss_hip - loss_ref) / abs(loss_ref))),
+                  "note": "HIP fp32 vs CPU oracle fp32, same pair and initial weights, flows "
+                          "[H/2, H/4, H/8, H/16]"}
+
+    gfp = gflop_per_pair(H, W)
+    if rank == 0:
+        out = {
+            "metric": "image-pairs/sec training, %dx%d batch=%d per GPU" % (H, W, B),
+            "value": round(value, 3),
+            "unit": "image-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (U[0,1)-mean pairs, image2 = shifted image1 + noise; resident in HBM)",
+            "config": {"workload": "full model.py encoder-decoder + loss.py photometric loss, "
+                                   "train step (fwd+bwd+Keras Adam)",
+                       "height": H, "width": W, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": "dp%d" % world, "params": 4938760},
+            "algorithmic_gflop_per_pair": round(gfp, 2),
+            "model_tflops": round(gfp * value / 1e3, 2),
+            "conv_ms_per_step": round(conv_ms_step, 3),
+            "final_loss": final_loss,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,197 @@
+/*
+ * oflow.h -- C ABI of the MI355X-native optical-flow training hot path (liboflow.so).
+ *
+ * The reference (xianlopez/optical_flow) has no FFI: its hot path is Python functions on
+ * TensorFlow tensors.  Each entry point below replaces the TF kernels behind one reference
+ * call site (cited per function), so the Python mirror in optical_flow_amd/ can keep the
+ * reference's function names and signatures (see INTEGRATION.md for the ctypes binding).
+ *
+ * Conventions
+ *   - Activations are NHWC; "ld" arguments are pixel strides in elements (>= channels),
+ *     so producers can write straight into a channel slice of a wider buffer (virtual
+ *     concat, model.py:100-102).
+ *   - Kernels are HWIO (Keras layout).  Conv weights are re-packed once per step by
+ *     of_conv_pack_weights() into the GEMM-ready layouts the conv kernels read.
+ *   - Every launch is stream-ordered on `stream` (a hipStream_t passed as void*); no entry
+ *     point synchronises, allocates, or frees device memory, so the calls are graph-capturable.
+ *     The caller owns every buffer; scratch comes from a caller-provided workspace whose size
+ *     is returned by a *_workspace() query.
+ *   - Return value: OF_OK (0) or an error code; of_last_error() gives a thread-local message.
+ *     No C++ exception crosses the ABI.
+ *   - dtype: fp32 everywhere in ABI v1 (the reference computes in fp32).
+ */
+#ifndef OFLOW_H
+#define OFLOW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OF_ABI_VERSION 1
+
+enum { OF_OK = 0, OF_EINVAL = 1, OF_EHIP = 2, OF_EUNSUPPORTED = 3 };
+enum { OF_ACT_NONE = 0, OF_ACT_RELU = 1, OF_ACT_LEAKY = 2 };
+
+/* Convolution geometry.  Replaces layers.Conv2D(padding='same') (model.py:12,104-114 and the
+ * resnet submodule's convs), whose TF kernels are Conv2D / Conv2DBackpropInput /
+ * Conv2DBackpropFilter. */
+typedef struct of_conv_desc {
+  int32_t n, h, w;       /* input batch, height, width                                     */
+  int32_t cin;           /* logical input channels (the kernel's I dimension)             */
+  int32_t cin_p;         /* channels per pixel the kernel reads (>= cin, multiple of 4;
+                            channels [cin, cin_p) of the input must hold zeros)            */
+  int32_t cout;          /* output channels (the kernel's O dimension)                    */
+  int32_t kh, kw, stride;
+  int32_t pad_top, pad_left;   /* TF 'same' split, see of_same_pads()                     */
+  int32_t ho, wo;        /* output height, width                                           */
+} of_conv_desc;
+
+int         of_abi_version(void);
+const char* of_last_error(void);
+/* Keras/TF padding='same' split for one spatial dim (P3): out = ceil(n/s),
+ * total = max((out-1)*s + k - n, 0), before = total/2, after = total - before. */
+int of_same_pads(int n, int k, int s, int* before, int* after, int* out);
+
+/* Packed weight sizes (elements) for of_conv_pack_weights(): fwd = [Kf][Nf], bwd = [Kd][Nd]. */
+int64_t of_conv_wfwd_elems(const of_conv_desc* d);
+int64_t of_conv_wbwd_elems(const of_conv_desc* d);
+/* w_hwio: [kh][kw][cin][cout] fp32 -> w_fwd (GEMM B for the forward) and, if non-NULL,
+ * w_bwd (GEMM B for the input-gradient pass: per tap, the (cout x cin) transpose). */
+int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fwd,
+                         float* w_bwd, void* stream);
+
+/* Forward: z = conv(x, w) + bias;  y = act(BN(z) + residual) with the inference-mode
+ * BatchNorm BN(z) = (z - mean) * gamma / sqrt(var + bn_eps) + beta (identity when
+ * bn_gamma == NULL); z is also stored when z != NULL (needed for the BN gamma gradient).
+ * x: [n][h][w] pixels of ldx elements (cin_p used); y/z: [n][ho][wo] pixels of ldy/ldz;
+ * bias and bn_*: [cout] or NULL; residual: NULL or pixels of ldr; act: OF_ACT_*, alpha is
+ * the LeakyReLU slope.  Replaces Conv2D + BiasAdd + FusedBatchNorm(inference) + AddV2 +
+ * Relu/LeakyRelu. */
+int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w_fwd,
+                  const float* bias, const float* bn_gamma, const float* bn_beta,
+                  const float* bn_mean, const float* bn_var, float bn_eps,
+                  const float* residual, int ldr, int act, float alpha,
+                  float* z, int ldz, float* y, int ldy, void* stream);
+
+/* Input gradient (Conv2DBackpropInput; for stride 2 this is the transposed convolution):
+ * dx[.., ci] = sum_{tap,co} dy * w, for ci < cin_p, then (fused) multiplied by the
+ * activation derivative of act_src (the forward output that fed this conv) when
+ * act_src != NULL: relu' = [s>0], leaky' = s>0 ? 1 : alpha.
+ * dy: [n][ho][wo] pixels of lddy elements, round_up(cout,4) channels read (pad must be 0). */
+int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
+                    const float* act_src, int ld_act, int act, float alpha,
+                    float* dx, int lddx, void* stream);
+
+/* Weight (+ bias) gradient (Conv2DBackpropFilter + BiasAddGrad): dw in HWIO [kh][kw][cin][cout],
+ * db [cout] (NULL to skip); accumulate != 0 adds into dw/db (gradient arenas).
+ * Deterministic split-K with a slab reduction in `workspace`. */
+size_t of_conv2d_wgrad_workspace(const of_conv_desc* d);
+int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float* dy, int lddy,
+                    float* dw, float* db, int accumulate, void* workspace, size_t ws_bytes,
+                    void* stream);
+
+/* Activation backward: dz = dy * act'(y) over n elements (y = forward output). */
+int of_act_bwd(const float* dy, const float* y, int act, float alpha, float* dz, int64_t n,
+               void* stream);
+
+/* Per-channel column sums of a [npix][ld] matrix (first c channels): out[c] (+)= sum.
+ * Workspace: of_colsum_workspace(npix, c) bytes. */
+size_t of_colsum_workspace(int64_t npix, int c);
+int of_colsum(const float* x, int64_t npix, int c, int ld, float* out, int accumulate,
+              void* workspace, void* stream);
+
+/* Inference BatchNorm + (residual) + activation backward (model.py:14-15, resnet blocks):
+ * dt = dy * act'(y) (act: OF_ACT_NONE or OF_ACT_RELU); dres = dt (if dres);
+ * dz = dt * gamma*invstd; dgamma = sum dt*(z-mean)*invstd; dbeta = sum dt; dbias = sum dz
+ * (each of the three [c] vectors optional; accumulate != 0 adds into them).
+ * y, z, dy, dz, dres dense [npix][c]; workspace: of_bn_act_bwd_workspace(npix, c) bytes. */
+size_t of_bn_act_bwd_workspace(int64_t npix, int c);
+int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
+                  const float* z, const float* gamma, const float* mean, const float* var,
+                  float eps, float* dz, float* dres, float* dgamma, float* dbeta, float* dbias,
+                  int accumulate, void* workspace, void* stream);
+
+/* Max-pool 2x2/2 'valid' (layers.MaxPool2D(), model.py:17) and its gradient (to the first
+ * maximum in row-major window order). x: [n][h][w][c] dense. */
+int of_maxpool2_fwd(const float* x, int n, int h, int w, int c, float* y, void* stream);
+int of_maxpool2_bwd(const float* x, const float* dy, int n, int h, int w, int c, float* dx,
+                    void* stream);
+
+/* Cost volume (create_cost_volume, model.py:29-42; P8): out[p][k], k=i*(2d+1)+j =
+ * sum_c f1[p][c]*f2[p+(i-d, j-d)][c] with zero padding.  out has ldo >= (2d+1)^2. */
+int of_corr_fwd(const float* f1, int ld1, const float* f2, int ld2, int n, int h, int w,
+                int c, int max_disp, float* out, int ldo, void* stream);
+/* Its gradient: df1 = (accumulate ? df1 : 0) + sum_k dcv*f2_shift; df2 likewise. */
+int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const float* f2,
+                int ld2, int n, int h, int w, int c, int max_disp, float* df1, int lddf1,
+                int acc1, float* df2, int lddf2, int acc2, void* stream);
+
+/* Bilinear backward warp with the reference index convention (warp_features, model.py:55-73
+ * + bilinear_interpolation, transformations.py:85-129; P1, P2):
+ * out[b,i,j] = bilinear(inp[b], x = i + flow[b,i,j,0], y = j + flow[b,i,j,1]). */
+int of_warp_fwd(const float* inp, int n, int h, int w, int c, const float* flow, float* out,
+                void* stream);
+/* dinp += scatter (atomics; caller zeroes or accumulates), dflow = d/d(flow) (written). */
+int of_warp_bwd(const float* dout, const float* inp, int n, int h, int w, int c,
+                const float* flow, float* dinp, float* dflow, void* stream);
+/* bilinear_interpolation(input, sampling_points) (transformations.py:85-129): the same sampler
+ * with absolute (x, y) points instead of grid + flow. */
+int of_bilinear_fwd(const float* inp, int n, int h, int w, int c, const float* pts, float* out,
+                    void* stream);
+int of_bilinear_bwd(const float* dout, const float* inp, int n, int h, int w, int c,
+                    const float* pts, float* dinp, float* dpts, void* stream);
+
+/* upscale_flow (model.py:76-77; P6, P7): out = resize_bilinear_x2(in) * scale, half-pixel
+ * centres.  in: [n][h][w][c] dense, out: [n][2h][2w] pixels of ldo (channel slice). */
+int of_upscale2x_fwd(const float* in, int n, int h, int w, int c, float scale, float* out,
+                     int ldo, void* stream);
+int of_upscale2x_bwd(const float* dout, int lddo, int n, int h, int w, int c, float scale,
+                     float* din, int accumulate, void* stream);
+
+/* Image pyramid of LossLayer (loss.py:17-18): for s=1..levels, out_s = resize(batch, H/2^s,
+ * W/2^s) (half-pixel bilinear, no antialias == mean of 2x2 taps); each out_s dense 6-ch. */
+int of_pyramid6(const float* batch, int n, int h, int w, int levels, float* const* outs,
+                void* stream);
+/* Split (B,H,W,6) pairs into the Siamese encoder batch (2B,H,W,4): image1s, then image2s,
+ * channel 3 zero (model.py:122-123, 131-132). */
+int of_split_pair(const float* batch, int n, int h, int w, float* out, void* stream);
+
+/* Photometric L1 term of one scale (loss.py:26-28): sum over (b,i,j,c<3) of
+ * |img[...,c] - warp(img[...,3:], flow)[...,c]| ; written as per-block partials to
+ * `partials` (of_photo_l1_partials(n,h,w) floats), then of_sum_partials reduces. */
+int of_photo_l1_partials(int n, int h, int w);
+int of_photo_l1_fwd(const float* img6, const float* flow, int n, int h, int w,
+                    float* partials, void* stream);
+/* d/d(flow) of g * coef * sum|...| (coef = 1/(levels*n*h*w*3) on the host, g = *dloss read
+ * on the device, 1 if dloss == NULL); dflow written (ld 2). */
+int of_photo_l1_bwd(const float* img6, const float* flow, int n, int h, int w, float coef,
+                    const float* dloss, float* dflow, void* stream);
+/* out[0] = sum_i coef_j * partials_j[i] over `count` groups (deterministic). */
+int of_sum_partials(const float* const* parts, const int* counts, const float* coefs,
+                    int ngroups, float* out, void* stream);
+
+/* Keras Adam (train.py:34,56; P13), one launch over a flat parameter arena, g' = g*gscale
+ * (gscale folds the 1/world of a data-parallel gradient average):
+ * m += (g'-m)(1-b1); v += (g'^2-v)(1-b2); p -= lr_t * m / (sqrt(v) + eps). */
+int of_adam_keras(float* p, const float* g, float* m, float* v, int64_t n, float lr_t,
+                  float beta1, float beta2, float eps, float gscale, void* stream);
+
+/* Elementwise helpers used by the host glue. */
+int of_add_inplace(float* y, const float* x, int64_t n, void* stream);        /* y += x */
+int of_copy_strided(const float* src, int lds, float* dst, int ldd, int64_t npix, int c,
+                    void* stream);                                             /* per pixel */
+int of_fill(float* y, float v, int64_t n, void* stream);
+
+/* Per-launch timing of the conv kernels (bench instrumentation): when enabled, every conv
+ * launch records a hipEvent pair on its stream; of_timing_read() returns the count and fills
+ * kinds (0 fwd, 1 dgrad, 2 wgrad), flops and elapsed ms (synchronises the events). */
+int of_timing_enable(int on);
+int of_timing_read(int max, int* kinds, double* flops, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OFLOW_H */

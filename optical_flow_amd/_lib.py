@@ -1,0 +1,118 @@
+"""ctypes binding of liboflow.so (include/oflow.h).
+
+This is the only place the product touches the native library.  There is NO fallback: if
+the .so is missing or a call fails, an exception is raised (a silent CPU/torch path would
+void every parity claim).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboflow.so")
+
+OF_OK, OF_EINVAL, OF_EHIP, OF_EUNSUPPORTED = 0, 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in
+                ("n", "h", "w", "cin", "cin_p", "cout", "kh", "kw", "stride", "pad_top",
+                 "pad_left", "ho", "wo")]
+
+
+P = C.c_void_p
+I = C.c_int
+I64 = C.c_int64
+F = C.c_float
+SZ = C.c_size_t
+PD = C.POINTER(ConvDesc)
+
+# name -> (restype, argtypes); must match include/oflow.h
+PROTOTYPES = {
+    "of_abi_version": (I, []),
+    "of_last_error": (C.c_char_p, []),
+    "of_same_pads": (I, [I, I, I, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "of_conv_wfwd_elems": (I64, [PD]),
+    "of_conv_wbwd_elems": (I64, [PD]),
+    "of_conv_pack_weights": (I, [PD, P, P, P, P]),
+    "of_conv2d_fwd": (I, [PD, P, I, P, P, P, P, P, P, F, P, I, I, F, P, I, P, I, P]),
+    "of_conv2d_dgrad": (I, [PD, P, I, P, P, I, I, F, P, I, P]),
+    "of_conv2d_wgrad_workspace": (SZ, [PD]),
+    "of_conv2d_wgrad": (I, [PD, P, I, P, I, P, P, I, P, SZ, P]),
+    "of_act_bwd": (I, [P, P, I, F, P, I64, P]),
+    "of_colsum_workspace": (SZ, [I64, I]),
+    "of_colsum": (I, [P, I64, I, I, P, I, P, P]),
+    "of_bn_act_bwd_workspace": (SZ, [I64, I]),
+    "of_bn_act_bwd": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, P, I, P, P]),
+    "of_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
+    "of_maxpool2_bwd": (I, [P, P, I, I, I, I, P, P]),
+    "of_corr_fwd": (I, [P, I, P, I, I, I, I, I, I, P, I, P]),
+    "of_corr_bwd": (I, [P, I, P, I, P, I, I, I, I, I, I, P, I, I, P, I, I, P]),
+    "of_warp_fwd": (I, [P, I, I, I, I, P, P, P]),
+    "of_warp_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
+    "of_bilinear_fwd": (I, [P, I, I, I, I, P, P, P]),
+    "of_bilinear_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
+    "of_upscale2x_fwd": (I, [P, I, I, I, I, F, P, I, P]),
+    "of_upscale2x_bwd": (I, [P, I, I, I, I, I, F, P, I, P]),
+    "of_pyramid6": (I, [P, I, I, I, I, C.POINTER(P), P]),
+    "of_split_pair": (I, [P, I, I, I, P, P]),
+    "of_photo_l1_partials": (I, [I, I, I]),
+    "of_photo_l1_fwd": (I, [P, P, I, I, I, P, P]),
+    "of_photo_l1_bwd": (I, [P, P, I, I, I, F, P, P, P]),
+    "of_sum_partials": (I, [C.POINTER(P), C.POINTER(I), C.POINTER(F), I, P, P]),
+    "of_adam_keras": (I, [P, P, P, P, I64, F, F, F, F, F, P]),
+    "of_add_inplace": (I, [P, P, I64, P]),
+    "of_copy_strided": (I, [P, I, P, I, I64, I, P]),
+    "of_fill": (I, [P, F, I64, P]),
+    "of_timing_enable": (I, [I]),
+    "of_timing_read": (I, [I, C.POINTER(I), C.POINTER(C.c_double), C.POINTER(F)]),
+}
+
+
+class OflowError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load liboflow.so; raises if it is absent (build it with optical_flow_amd.build)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise OflowError("liboflow.so not found at %s: run `python -m optical_flow_amd.build` "
+                             "(the HIP path has no fallback)" % path)
+        lib = C.CDLL(path)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.of_abi_version() != 1:
+            raise OflowError("liboflow ABI mismatch")
+        _lib = lib
+        return lib
+
+
+def lib():
+    return _lib if _lib is not None else load()
+
+
+def check(status: int, what: str = ""):
+    if status != OF_OK:
+        msg = lib().of_last_error().decode(errors="replace")
+        if status == OF_EINVAL:
+            raise AssertionError("%s: %s" % (what, msg))
+        raise OflowError("%s failed (%d): %s" % (what, status, msg))
+
+
+def call(name: str, *args):
+    st = getattr(lib(), name)(*args)
+    check(st, name)
+    return st

@@ -1,0 +1,113 @@
+// Error reporting and conv launch timing for liboflow.
+#include "common.h"
+
+#include <mutex>
+#include <vector>
+
+namespace oflow {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(OF_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+  return OF_OK;
+}
+
+// ---- timing: hipEvent pairs recorded on the launch stream, read back on demand ----------
+struct TimedLaunch {
+  int kind;
+  double flops;
+  hipEvent_t start, stop;
+};
+
+static std::mutex g_tmu;
+static bool g_timing = false;
+static std::vector<TimedLaunch> g_launches;
+static std::vector<hipEvent_t> g_event_pool;
+static hipEvent_t g_pending_start = nullptr;
+
+static hipEvent_t get_event() {
+  if (!g_event_pool.empty()) {
+    hipEvent_t e = g_event_pool.back();
+    g_event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+bool timing_on() { return g_timing; }
+
+void timing_begin(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_pending_start = get_event();
+  if (g_pending_start) (void)hipEventRecord(g_pending_start, s);
+}
+
+void timing_end(hipStream_t s, int kind, double flops) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  if (!g_pending_start) return;
+  hipEvent_t stop = get_event();
+  if (!stop) return;
+  (void)hipEventRecord(stop, s);
+  g_launches.push_back({kind, flops, g_pending_start, stop});
+  g_pending_start = nullptr;
+}
+
+}  // namespace oflow
+
+using namespace oflow;
+
+extern "C" {
+
+int of_abi_version(void) { return OF_ABI_VERSION; }
+
+const char* of_last_error(void) { return g_last_error.c_str(); }
+
+int of_same_pads(int n, int k, int s, int* before, int* after, int* out) {
+  OF_CHECK_ARG(n > 0 && k > 0 && s > 0 && before && after && out, "same_pads: args");
+  const int o = (n + s - 1) / s;
+  int total = (o - 1) * s + k - n;
+  if (total < 0) total = 0;
+  *before = total / 2;
+  *after = total - total / 2;
+  *out = o;
+  return OF_OK;
+}
+
+int of_timing_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_timing = on != 0;
+  return OF_OK;
+}
+
+int of_timing_read(int max, int* kinds, double* flops, float* ms) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  int n = 0;
+  for (auto& t : g_launches) {
+    if (hipEventSynchronize(t.stop) != hipSuccess) return -1;
+    if (n < max) {
+      float e = 0.f;
+      (void)hipEventElapsedTime(&e, t.start, t.stop);
+      if (kinds) kinds[n] = t.kind;
+      if (flops) flops[n] = t.flops;
+      if (ms) ms[n] = e;
+    }
+    ++n;
+    g_event_pool.push_back(t.start);
+    g_event_pool.push_back(t.stop);
+  }
+  g_launches.clear();
+  return n < max ? n : max;
+}
+
+}  // extern "C"

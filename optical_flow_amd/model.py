@@ -1,0 +1,331 @@
+"""MI355X-native mirror of the reference ``model.py`` (xianlopez/optical_flow).
+
+Same public names and argument meaning as ``/root/reference/model.py``:
+
+* ``reset18_encoder(height, width, name)``                       (model.py:10-26)
+* ``create_cost_volume(features1, features2, max_disp)``          (model.py:29-42)
+* ``warp_features(flow_1_to_2, features2)``                       (model.py:55-73)
+* ``upscale_flow(flow)``                                          (model.py:76-77)
+* ``flow_module(features1, features2, previous_flow, max_disp)``  (model.py:80-116)
+* ``build_flow_net(height, width, pretrained_weights_path, max_disp=3)`` (model.py:119-143)
+
+Tensors are torch NHWC float32 on the GPU; every op runs as HIP kernels (``ops.py``).  The
+returned ``FlowNet`` keeps the Keras ``Model`` surface the driver uses: ``__call__`` ->
+``[flow3, flow2, flow1, flow0]`` (fine -> coarse), ``trainable_weights``, ``summary()``,
+``save_weights(path)``, ``load_weights(path)``.
+
+Parameters live in one flat device arena (``ParamStore``) with a matching gradient arena, so
+the optimizer is a single fused launch and the data-parallel all-reduce works on contiguous
+buckets.  The arena is ordered by backward completion (finest flow head first, encoder
+stem last) so buckets become ready in order during the backward pass.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from collections import OrderedDict
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import ops
+from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, call
+from .params import (ENC_CHANNELS, HEAD_WIDTHS, encoder_blocks, encoder_spec, flow_net_spec,
+                     head_cin, head_spec, init_params)
+
+
+# =================================================================== parameter arena ====
+class ParamStore:
+    """Flat fp32 device arenas for the trainable weights, their gradients, and the
+    non-trainable BN moving statistics.  ``params[name]`` are leaf views (HWIO kernels)."""
+
+    def __init__(self, spec, values: Optional[Dict[str, np.ndarray]] = None, device="cuda",
+                 order: Optional[List[str]] = None, seed: int = 0):
+        if values is None:
+            values = init_params(spec, seed)
+        self.spec = OrderedDict((p.name, p) for p in spec)
+        train = [p for p in spec if p.trainable]
+        if order is not None:
+            rank = {n: i for i, n in enumerate(order)}
+            train = sorted(train, key=lambda p: rank.get(p.name, len(rank)))
+        self.arena_order = [p.name for p in train]
+        self.offsets = OrderedDict()
+        off = 0
+        for p in train:
+            self.offsets[p.name] = off
+            off += (p.size + 3) // 4 * 4          # 16-byte aligned views
+        self.numel = max(off, 4)
+        self.arena = torch.zeros(self.numel, device=device)
+        self.grad_arena = torch.zeros(self.numel, device=device)
+        bufs = [p for p in spec if not p.trainable]
+        self.buf_offsets = OrderedDict()
+        off = 0
+        for p in bufs:
+            self.buf_offsets[p.name] = off
+            off += (p.size + 3) // 4 * 4
+        self.buffers = torch.zeros(max(off, 4), device=device)
+        self.params: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+        for p in spec:
+            if p.trainable:
+                o = self.offsets[p.name]
+                v = self.arena[o:o + p.size].view(p.shape)
+                v.requires_grad_(True)
+                g = self.grad_arena[o:o + p.size].view(p.shape)
+                v._of_grad = g
+                v.grad = g
+            else:
+                o = self.buf_offsets[p.name]
+                v = self.buffers[o:o + p.size].view(p.shape)
+            self.params[p.name] = v
+        self.version = 0
+        self.load(values)
+
+    def __getitem__(self, name) -> torch.Tensor:
+        return self.params[name]
+
+    def trainable(self) -> List[torch.Tensor]:
+        return [self.params[n] for n, p in self.spec.items() if p.trainable]
+
+    @torch.no_grad()
+    def load(self, values: Dict[str, np.ndarray], strict: bool = True):
+        missing = [n for n in self.spec if n not in values]
+        if strict and missing:
+            raise KeyError("missing weights: %s" % missing[:5])
+        for n, v in values.items():
+            if n not in self.params:
+                if strict:
+                    raise KeyError("unexpected weight %s" % n)
+                continue
+            t = torch.as_tensor(np.asarray(v, np.float32))
+            assert tuple(t.shape) == tuple(self.spec[n].shape), (n, t.shape, self.spec[n].shape)
+            self.params[n].copy_(t.to(self.params[n].device))
+        self.version += 1
+
+    def state(self) -> "OrderedDict[str, np.ndarray]":
+        return OrderedDict((n, self.params[n].detach().cpu().numpy()) for n in self.spec)
+
+    def zero_grad(self):
+        call("of_fill", C.c_void_p(self.grad_arena.data_ptr()), 0.0, self.numel, ops._stream())
+
+    def grads(self) -> "OrderedDict[str, torch.Tensor]":
+        return OrderedDict((n, self.params[n]._of_grad) for n, p in self.spec.items()
+                           if p.trainable)
+
+
+def backward_order(max_disp=3) -> List[str]:
+    """Arena order = gradient completion order of the backward pass."""
+    names = []
+    for level in (3, 2, 1, 0):
+        names += [p.name for p in head_spec(level, max_disp) if p.trainable]
+    names += [p.name for p in reversed(encoder_spec()) if p.trainable]
+    return names
+
+
+# ========================================================================= encoder ======
+class Encoder:
+    """reset18_encoder (model.py:10-26): conv1 7x7/2 + BN + ReLU -> out0 (H/2, 64);
+    max-pool; three resnet_layer_simple stages -> H/4 x64, H/8 x128, H/16 x256.
+    The stage body is the assumed standard basic block (params.py)."""
+
+    def __init__(self, store: ParamStore, name="ResNet18"):
+        self.store = store
+        self.name = name
+        ver = lambda: store.version
+        P = store.params
+
+        def bn(prefix):
+            return (P[prefix + "/gamma"], P[prefix + "/beta"], P[prefix + "/moving_mean"],
+                    P[prefix + "/moving_variance"])
+
+        self.conv1 = ops.ConvLayer(P["ResNet18/conv1/kernel"], P["ResNet18/conv1/bias"], stride=2,
+                                   act=ACT_RELU, bn=bn("ResNet18/layer1_bn"), cin_p=4,
+                                   version_of=ver, name="conv1")
+        self.blocks = []
+        for prefix, cin, cout, stride, proj in encoder_blocks():
+            a = ops.ConvLayer(P[prefix + "/conv_a/kernel"], P[prefix + "/conv_a/bias"],
+                              stride=stride, act=ACT_RELU, bn=bn(prefix + "/bn_a"),
+                              version_of=ver, name=prefix + "/conv_a")
+            b = ops.ConvLayer(P[prefix + "/conv_b/kernel"], P[prefix + "/conv_b/bias"], stride=1,
+                              act=ACT_RELU, bn=bn(prefix + "/bn_b"), version_of=ver,
+                              name=prefix + "/conv_b")
+            p = None
+            if proj:
+                p = ops.ConvLayer(P[prefix + "/proj/kernel"], P[prefix + "/proj/bias"],
+                                  stride=stride, act=ACT_NONE, bn=bn(prefix + "/bn_proj"),
+                                  version_of=ver, name=prefix + "/proj")
+            self.blocks.append((a, b, p))
+
+    def forward4(self, x4):
+        """x4: (N, H, W, 4) images with a zero 4th channel -> 4 feature maps."""
+        x = self.conv1(x4)
+        outs = [x]
+        x = ops.maxpool2(x)
+        for i, (a, b, p) in enumerate(self.blocks):
+            y = a(x)
+            sc = p(x) if p is not None else x
+            x = b(y, residual=sc)
+            if i % 2 == 1:
+                outs.append(x)
+        return outs
+
+    def __call__(self, images):
+        """images: (N, H, W, 3) -> [H/2 x64, H/4 x64, H/8 x128, H/16 x256]."""
+        return self.forward4(ops._pad_channels(images, 4))
+
+
+def reset18_encoder(height, width, name="ResNet18", seed=0, device="cuda"):
+    """model.py:10-26.  ``height``/``width`` fix nothing here (the kernels take any size
+    divisible by 16); kept for signature parity.  Owns its own parameter store."""
+    store = ParamStore(encoder_spec(), seed=seed, device=device)
+    enc = Encoder(store, name)
+    enc.input_shape = (height, width, 3)
+    return enc
+
+
+# =================================================================== flow primitives ====
+def create_cost_volume(features1, features2, max_disp):
+    """model.py:29-42 (P8): unnormalised 49-offset correlation, zero padding."""
+    assert features1.shape == features2.shape
+    return ops.cost_volume(features1, features2, max_disp)
+
+
+def warp_features(flow_1_to_2, features2):
+    """model.py:55-73 with the reference's index convention (P1): the grid is
+    meshgrid(range(h), range(w), 'ij') + flow, sampled as (x=ch0, y=ch1)."""
+    _, height, width, _ = features2.shape
+    assert flow_1_to_2.shape[1] == height
+    assert flow_1_to_2.shape[2] == width
+    assert flow_1_to_2.shape[3] == 2
+    return ops.warp(features2, flow_1_to_2)
+
+
+def upscale_flow(flow):
+    """model.py:76-77: bilinear resize x2 (half-pixel centres) times 2.0 (P6, P7)."""
+    return ops.upscale2x(flow, 2.0)
+
+
+class FlowHead:
+    """The six 3x3 convs a ``flow_module`` call creates (model.py:104-114): 128, 128, 96, 64,
+    32 with LeakyReLU(0.3), then a linear 2-channel flow conv."""
+
+    def __init__(self, store: ParamStore, level: int, max_disp: int = 3):
+        self.level = level
+        self.max_disp = max_disp
+        self.cin = head_cin(level, max_disp)
+        self.cp = ops._c4(self.cin)
+        P = store.params
+        ver = lambda: store.version
+        self.convs = []
+        for i, cout in enumerate(HEAD_WIDTHS):
+            pre = "flow_module_%d/conv%d" % (level, i)
+            self.convs.append(ops.ConvLayer(P[pre + "/kernel"], P[pre + "/bias"], stride=1,
+                                            act=ACT_LEAKY if i < 5 else ACT_NONE,
+                                            cin_p=self.cp if i == 0 else None, version_of=ver,
+                                            name=pre))
+
+    def __call__(self, features1, features2, previous_flow):
+        return flow_module(features1, features2, previous_flow, self.max_disp, head=self)
+
+
+def flow_module(features1, features2, previous_flow, max_disp, head: Optional[FlowHead] = None):
+    """model.py:80-116: [upscale + warp] -> cost volume -> concat -> 6 convs.  Keras creates
+    new conv layers per call; here ``head`` carries them (a fresh randomly initialised head
+    is created when omitted, mirroring that)."""
+    assert features1.shape[1] == features2.shape[1]
+    assert features1.shape[2] == features2.shape[2]
+    assert features1.shape[3] == features2.shape[3]
+    if head is None:
+        c = features1.shape[3]
+        level = {256: 0, 128: 1, 64: 2 if previous_flow is not None else 3}.get(c, 2)
+        if previous_flow is None and c != 256:
+            raise ValueError("a standalone flow_module needs an explicit head for this shape")
+        store = ParamStore(head_spec(level, max_disp), device=features1.device)
+        head = FlowHead(store, level, max_disp)
+        head._store = store
+    if previous_flow is not None:
+        assert previous_flow.shape[0] == features1.shape[0]
+        assert previous_flow.shape[1] * 2 == features1.shape[1]
+        assert previous_flow.shape[2] * 2 == features1.shape[2]
+        assert previous_flow.shape[3] == 2
+        flow_up = upscale_flow(previous_flow)
+        features2_warped = warp_features(flow_up, features2)
+    else:
+        flow_up = None
+        features2_warped = features2
+    x = ops.corr_concat(features1, features2_warped, flow_up, max_disp, head.cp)
+    for conv in head.convs:
+        x = conv(x)
+    return x
+
+
+# ========================================================================= flow net ======
+class FlowNet:
+    """The Keras ``Model`` returned by build_flow_net (model.py:119-143)."""
+
+    def __init__(self, height, width, max_disp=3, seed=0, device="cuda", values=None):
+        assert height % 16 == 0 and width % 16 == 0, "H and W must be divisible by 16 (P17)"
+        self.height, self.width, self.max_disp = height, width, max_disp
+        self.store = ParamStore(flow_net_spec(max_disp), values=values, device=device,
+                                order=backward_order(max_disp), seed=seed)
+        self.encoder = Encoder(self.store)
+        self.heads = [FlowHead(self.store, level, max_disp) for level in range(4)]
+        self.name = "flow_net"
+
+    @property
+    def trainable_weights(self) -> List[torch.Tensor]:
+        return self.store.trainable()
+
+    @property
+    def weight_names(self) -> List[str]:
+        return [n for n, p in self.store.spec.items() if p.trainable]
+
+    def __call__(self, batch_imgs):
+        """(B, H, W, 6) -> [flow3 (H/2), flow2 (H/4), flow1 (H/8), flow0 (H/16)]."""
+        assert batch_imgs.shape[1] == self.height and batch_imgs.shape[2] == self.width
+        assert batch_imgs.shape[3] == 6
+        imgs = ops.split_pair(batch_imgs)            # image1s then image2s (model.py:122-123)
+        feats = self.encoder.forward4(imgs)          # shared encoder, both images (P12)
+        flows = []
+        prev = None
+        for level in range(4):
+            f1, f2 = ops.halves(feats[3 - level])
+            prev = self.heads[level](f1, f2, prev)
+            flows.append(prev)
+        return flows[::-1]
+
+    # ---- Keras Model surface used by train.py ------------------------------------------
+    def summary(self, print_fn=print):
+        total = 0
+        print_fn("Model: \"%s\"" % self.name)
+        for n, p in self.store.spec.items():
+            total += p.size if p.trainable else 0
+            print_fn("  %-44s %-18s %s" % (n, str(p.shape), "" if p.trainable else "(non-trainable)"))
+        print_fn("Trainable params: %d" % total)
+
+    def save_weights(self, path):
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        np.savez(path if path.endswith(".npz") else path + ".npz", **self.store.state())
+
+    def load_weights(self, path, strict=True):
+        p = path if os.path.exists(path) else path + ".npz"
+        with np.load(p, allow_pickle=False) as z:
+            self.store.load({k: z[k] for k in z.files}, strict=strict)
+
+
+def build_flow_net(height, width, pretrained_weights_path=None, max_disp=3, seed=0,
+                   device="cuda"):
+    """model.py:119-143.  ``pretrained_weights_path``: an .npz of encoder weights named as in
+    params.encoder_spec() (Keras-checkpoint import is out of scope, SURVEY.md §8 f); the
+    reference asserts every encoder object is matched (model.py:129) -- so does this."""
+    net = FlowNet(height, width, max_disp, seed=seed, device=device)
+    if pretrained_weights_path is not None:
+        with np.load(pretrained_weights_path, allow_pickle=False) as z:
+            vals = {k: z[k] for k in z.files}
+        enc_names = [p.name for p in encoder_spec()]
+        missing = [n for n in enc_names if n not in vals]
+        assert not missing, "pretrained encoder weights missing: %s" % missing[:5]
+        net.store.load({n: vals[n] for n in enc_names}, strict=False)
+    return net

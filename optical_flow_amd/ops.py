@@ -1,0 +1,532 @@
+"""Autograd glue over liboflow: every forward and backward below is one or more HIP kernels
+launched through the C ABI on torch's current HIP stream.  torch only allocates the tensors.
+
+Tensors are NHWC float32 on the GPU.  Each Function cites the reference op it replaces.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, ConvDesc, call
+
+LEAKY_ALPHA = 0.3      # keras LeakyReLU() default (model.py:105)
+BN_EPS = 1e-3          # keras BatchNormalization default (model.py:14)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check_dev(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("optical_flow_amd ops run on the GPU only (got a %s tensor): the "
+                               "HIP path has no CPU fallback" % t.device)
+        if t.dtype != torch.float32:
+            raise TypeError("expected float32, got %s" % t.dtype)
+
+
+def _c4(c):
+    return (c + 3) // 4 * 4
+
+
+def same_pads(n, k, s):
+    b, a, o = C.c_int(), C.c_int(), C.c_int()
+    call("of_same_pads", n, k, s, C.byref(b), C.byref(a), C.byref(o))
+    return b.value, a.value, o.value
+
+
+# ------------------------------------------------------------------- gradient arenas ----
+_GRAD_READY_HOOK = None
+
+
+def set_grad_ready_hook(fn):
+    """fn(param) is called once a Function has enqueued all kernels writing param's gradient
+    (used by dist.GradBucketReducer to start bucket all-reduces during the backward)."""
+    global _GRAD_READY_HOOK
+    _GRAD_READY_HOOK = fn
+
+
+def _grad_ready(*params):
+    if _GRAD_READY_HOOK is not None:
+        for p in params:
+            if p is not None:
+                _GRAD_READY_HOOK(p)
+
+
+def grad_target(param: torch.Tensor):
+    """Where a Function writes the gradient of ``param``: straight into the parameter's
+    gradient-arena view (accumulating, returns None to autograd) when the model installed
+    one, else a fresh tensor that is returned to autograd."""
+    g = getattr(param, "_of_grad", None)
+    if g is not None:
+        return g, 1, None
+    t = torch.empty_like(param)
+    return t, 0, t
+
+
+# ====================================================================== convolution ====
+class ConvLayer:
+    """One ``layers.Conv2D(filters, k, strides, padding='same')`` (model.py:12,104-114) with an
+    optional inference BatchNorm (model.py:14) and activation, holding references to its
+    parameters (HWIO kernel, bias, BN vectors) and its per-step packed weights."""
+
+    def __init__(self, kernel, bias, stride=1, act=ACT_NONE, alpha=LEAKY_ALPHA, bn=None,
+                 cin_p=None, version_of=None, name=""):
+        self.kernel, self.bias = kernel, bias
+        kh, kw, cin, cout = kernel.shape
+        self.kh, self.kw, self.cin, self.cout = kh, kw, cin, cout
+        self.cin_p = cin_p if cin_p is not None else _c4(cin)
+        self.stride, self.act, self.alpha = stride, act, alpha
+        self.bn = bn                      # (gamma, beta, moving_mean, moving_variance) or None
+        self.version_of = version_of      # callable -> int, bumps when the weights change
+        self.name = name
+        self._pack_key = None
+        self._wf = self._wd = None
+        self._descs = {}
+
+    def desc(self, n, h, w) -> ConvDesc:
+        key = (n, h, w)
+        d = self._descs.get(key)
+        if d is None:
+            pt, _, ho = same_pads(h, self.kh, self.stride)
+            pl, _, wo = same_pads(w, self.kw, self.stride)
+            d = ConvDesc(n, h, w, self.cin, self.cin_p, self.cout, self.kh, self.kw, self.stride,
+                         pt, pl, ho, wo)
+            self._descs[key] = d
+        return d
+
+    def packed(self, d: ConvDesc):
+        key = (self.kernel.data_ptr(), self.version_of() if self.version_of else None)
+        if self._wf is None:
+            lib = _lib.lib()
+            self._wf = torch.empty(lib.of_conv_wfwd_elems(C.byref(d)), device=self.kernel.device)
+            self._wd = torch.empty(lib.of_conv_wbwd_elems(C.byref(d)), device=self.kernel.device)
+        if key != self._pack_key or self.version_of is None:
+            call("of_conv_pack_weights", C.byref(d), _ptr(self.kernel), _ptr(self._wf),
+                 _ptr(self._wd), _stream())
+            self._pack_key = key
+        return self._wf, self._wd
+
+    def __call__(self, x, residual=None):
+        bn = self.bn or (None, None, None, None)
+        return _ConvFn.apply(x, self.kernel, self.bias, bn[0], bn[1], residual, self)
+
+
+def _pad_channels(t: torch.Tensor, cp: int) -> torch.Tensor:
+    """Copy an NHWC tensor into a zero-padded one with cp channels (the conv ABI reads
+    round_up(C,4) channels)."""
+    n, h, w, c = t.shape
+    if c == cp and t.is_contiguous():
+        return t
+    out = torch.empty((n, h, w, cp), device=t.device, dtype=t.dtype)
+    if cp != c:
+        call("of_fill", _ptr(out), 0.0, out.numel(), _stream())
+    t = t.contiguous()
+    call("of_copy_strided", _ptr(t), c, _ptr(out), cp, n * h * w, c, _stream())
+    return out
+
+
+class _ConvFn(torch.autograd.Function):
+    """Conv2D + BiasAdd [+ FusedBatchNorm(inference)] [+ AddV2 residual] [+ Relu/LeakyRelu]
+    forward; Conv2DBackpropInput / Conv2DBackpropFilter / BiasAddGrad / BN grads backward."""
+
+    @staticmethod
+    def forward(ctx, x, kernel, bias, gamma, beta, residual, layer: ConvLayer):
+        _check_dev(x, kernel, bias, residual)
+        n, h, w, cx = x.shape
+        assert cx == layer.cin_p, "conv %s: input has %d channels, expected %d (cin_p)" % (
+            layer.name, cx, layer.cin_p)
+        x = x.contiguous()
+        d = layer.desc(n, h, w)
+        wf, _ = layer.packed(d)
+        y = torch.empty((n, d.ho, d.wo, layer.cout), device=x.device)
+        z = torch.empty_like(y) if layer.bn is not None else None
+        bn = layer.bn
+        if residual is not None:
+            residual = residual.contiguous()
+            assert residual.shape == y.shape
+        call("of_conv2d_fwd", C.byref(d), _ptr(x), cx, _ptr(wf), _ptr(bias),
+             _ptr(bn[0]) if bn else None, _ptr(bn[1]) if bn else None,
+             _ptr(bn[2]) if bn else None, _ptr(bn[3]) if bn else None, BN_EPS,
+             _ptr(residual), layer.cout, layer.act, layer.alpha,
+             _ptr(z), layer.cout, _ptr(y), layer.cout, _stream())
+        ctx.layer = layer
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y, z)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        layer: ConvLayer = ctx.layer
+        x, y, z = ctx.saved_tensors
+        n, h, w, cx = x.shape
+        d = layer.desc(n, h, w)
+        _, wd = layer.packed(d)
+        dy = dy.contiguous()
+        s = _stream()
+        need_x, need_k, need_b, need_g, need_be, need_res = ctx.needs_input_grad[:6]
+        ret_k = ret_b = ret_g = ret_be = dres = dx = None
+        npix = n * d.ho * d.wo
+        # ---- pre-activation gradient dz -------------------------------------------------
+        if layer.bn is not None:
+            gamma, beta, mean, var = layer.bn
+            dz = torch.empty_like(dy)
+            dres = torch.empty_like(dy) if (ctx.has_res and need_res) else None
+            tg = grad_target(gamma) if need_g else (None, 0, None)
+            tb = grad_target(beta) if need_be else (None, 0, None)
+            tbias = grad_target(layer.bias) if need_b else (None, 0, None)
+            ret_g, ret_be, ret_b = tg[2], tb[2], tbias[2]
+            acc = tg[1] if need_g else (tb[1] if need_be else tbias[1])
+            # per-target accumulate flags must agree (all arena or all fresh)
+            assert all(t[0] is None or t[1] == acc for t in (tg, tb, tbias))
+            ws = torch.empty(_lib.lib().of_bn_act_bwd_workspace(npix, layer.cout) // 4 + 1,
+                             device=dy.device)
+            call("of_bn_act_bwd", npix, layer.cout, layer.act, _ptr(dy), _ptr(y), _ptr(z),
+                 _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, _ptr(dz), _ptr(dres),
+                 _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
+            bias_done = True
+        else:
+            if layer.act != ACT_NONE:
+                dz = torch.empty_like(dy)
+                call("of_act_bwd", _ptr(dy), _ptr(y), layer.act, layer.alpha, _ptr(dz),
+                     dy.numel(), s)
+            else:
+                dz = dy
+            if ctx.has_res and need_res:
+                dres = dz
+            bias_done = False
+        dzp = _pad_channels(dz, _c4(layer.cout))
+        # ---- weight (+bias) gradient ----------------------------------------------------
+        if need_k or (need_b and not bias_done):
+            tk = grad_target(layer.kernel)
+            tbias = grad_target(layer.bias) if (need_b and not bias_done) else (None, 0, None)
+            wsb = _lib.lib().of_conv2d_wgrad_workspace(C.byref(d))
+            ws = torch.empty(wsb // 4 + 1, device=dy.device)
+            if tbias[0] is not None and tbias[1] != tk[1]:
+                # mixed arena / fresh targets: compute the bias into a temp, then place it
+                tmpb = torch.empty_like(layer.bias)
+                call("of_conv2d_wgrad", C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
+                     _ptr(tk[0]), _ptr(tmpb), tk[1], _ptr(ws), wsb, s)
+                if tbias[1]:
+                    call("of_add_inplace", _ptr(tbias[0]), _ptr(tmpb), tmpb.numel(), s)
+                else:
+                    tbias = (tmpb, 0, tmpb)
+            else:
+                call("of_conv2d_wgrad", C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
+                     _ptr(tk[0]), _ptr(tbias[0]), tk[1], _ptr(ws), wsb, s)
+            ret_k = tk[2] if need_k else None
+            if need_b and not bias_done:
+                ret_b = tbias[2]
+        _grad_ready(layer.kernel if need_k else None, layer.bias if need_b else None,
+                    *(layer.bn[:2] if layer.bn is not None else ()))
+        # ---- input gradient -------------------------------------------------------------
+        if need_x:
+            dx = torch.empty((n, h, w, cx), device=dy.device)
+            call("of_conv2d_dgrad", C.byref(d), _ptr(dzp), dzp.shape[-1], _ptr(wd), None, 0,
+                 ACT_NONE, 0.0, _ptr(dx), cx, s)
+        return dx, ret_k, ret_b, ret_g, ret_be, dres, None
+
+
+# ========================================================================= max pool ====
+class _MaxPool2(torch.autograd.Function):
+    """layers.MaxPool2D() (model.py:17): 2x2 / stride 2 / valid."""
+
+    @staticmethod
+    def forward(ctx, x):
+        _check_dev(x)
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        y = torch.empty((n, h // 2, w // 2, c), device=x.device)
+        call("of_maxpool2_fwd", _ptr(x), n, h, w, c, _ptr(y), _stream())
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        n, h, w, c = x.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        call("of_maxpool2_bwd", _ptr(x), _ptr(dy), n, h, w, c, _ptr(dx), _stream())
+        return dx
+
+
+def maxpool2(x):
+    return _MaxPool2.apply(x)
+
+
+# ===================================================================== cost volume =====
+class _CostVolume(torch.autograd.Function):
+    """create_cost_volume(f1, f2, max_disp) (model.py:29-42)."""
+
+    @staticmethod
+    def forward(ctx, f1, f2, max_disp):
+        _check_dev(f1, f2)
+        f1, f2 = f1.contiguous(), f2.contiguous()
+        n, h, w, c = f1.shape
+        nk = (2 * max_disp + 1) ** 2
+        out = torch.empty((n, h, w, nk), device=f1.device)
+        call("of_corr_fwd", _ptr(f1), c, _ptr(f2), c, n, h, w, c, max_disp, _ptr(out), nk,
+             _stream())
+        ctx.save_for_backward(f1, f2)
+        ctx.max_disp = max_disp
+        return out
+
+    @staticmethod
+    def backward(ctx, dcv):
+        f1, f2 = ctx.saved_tensors
+        n, h, w, c = f1.shape
+        dcv = dcv.contiguous()
+        df1 = torch.empty_like(f1) if ctx.needs_input_grad[0] else None
+        df2 = torch.empty_like(f2) if ctx.needs_input_grad[1] else None
+        call("of_corr_bwd", _ptr(dcv), dcv.shape[-1], _ptr(f1), c, _ptr(f2), c, n, h, w, c,
+             ctx.max_disp, _ptr(df1), c, 0, _ptr(df2), c, 0, _stream())
+        return df1, df2, None
+
+
+def cost_volume(f1, f2, max_disp=3):
+    return _CostVolume.apply(f1, f2, max_disp)
+
+
+class _CorrConcat(torch.autograd.Function):
+    """The flow-module input ``concat([features1, cost_volume, flow_up])`` (model.py:97-102)
+    built in one zero-padded NHWC buffer of ``cp`` channels: the cost volume kernel writes
+    straight into its channel slice (virtual concat, no separate concat pass)."""
+
+    @staticmethod
+    def forward(ctx, f1, f2w, flow_up, max_disp, cp):
+        _check_dev(f1, f2w, flow_up)
+        f1, f2w = f1.contiguous(), f2w.contiguous()
+        n, h, w, c = f1.shape
+        nk = (2 * max_disp + 1) ** 2
+        used = c + nk + (2 if flow_up is not None else 0)
+        assert used <= cp
+        x = torch.empty((n, h, w, cp), device=f1.device)
+        s = _stream()
+        if used < cp:
+            call("of_fill", _ptr(x), 0.0, x.numel(), s)
+        call("of_copy_strided", _ptr(f1), c, _ptr(x), cp, n * h * w, c, s)
+        call("of_corr_fwd", _ptr(f1), c, _ptr(f2w), c, n, h, w, c, max_disp,
+             C.c_void_p(x.data_ptr() + 4 * c), cp, s)
+        if flow_up is not None:
+            fu = flow_up.contiguous()
+            call("of_copy_strided", _ptr(fu), 2, C.c_void_p(x.data_ptr() + 4 * (c + nk)), cp,
+                 n * h * w, 2, s)
+        ctx.save_for_backward(f1, f2w)
+        ctx.meta = (max_disp, cp, nk, flow_up is not None)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        f1, f2w = ctx.saved_tensors
+        max_disp, cp, nk, has_flow = ctx.meta
+        n, h, w, c = f1.shape
+        dx = dx.contiguous()
+        s = _stream()
+        df1 = torch.empty_like(f1)
+        call("of_copy_strided", _ptr(dx), cp, _ptr(df1), c, n * h * w, c, s)
+        df2 = torch.empty_like(f2w) if ctx.needs_input_grad[1] else None
+        call("of_corr_bwd", C.c_void_p(dx.data_ptr() + 4 * c), cp, _ptr(f1), c, _ptr(f2w), c, n,
+             h, w, c, max_disp, _ptr(df1), c, 1, _ptr(df2), c, 0, s)
+        dflow = None
+        if has_flow and ctx.needs_input_grad[2]:
+            dflow = torch.empty((n, h, w, 2), device=dx.device)
+            call("of_copy_strided", C.c_void_p(dx.data_ptr() + 4 * (c + nk)), cp, _ptr(dflow), 2,
+                 n * h * w, 2, s)
+        return df1, df2, dflow, None, None
+
+
+def corr_concat(f1, f2w, flow_up, max_disp, cp):
+    return _CorrConcat.apply(f1, f2w, flow_up, max_disp, cp)
+
+
+# ============================================================================ warp =====
+class _Warp(torch.autograd.Function):
+    """warp_features (model.py:55-73) / bilinear_interpolation (transformations.py:85-129)."""
+
+    @staticmethod
+    def forward(ctx, inp, flow, absolute):
+        _check_dev(inp, flow)
+        inp, flow = inp.contiguous(), flow.contiguous()
+        n, h, w, c = inp.shape
+        assert flow.shape == (n, h, w, 2), "flow must be (B, h, w, 2) like features"
+        out = torch.empty_like(inp)
+        call("of_bilinear_fwd" if absolute else "of_warp_fwd", _ptr(inp), n, h, w, c,
+             _ptr(flow), _ptr(out), _stream())
+        ctx.save_for_backward(inp, flow)
+        ctx.absolute = absolute
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        inp, flow = ctx.saved_tensors
+        n, h, w, c = inp.shape
+        dout = dout.contiguous()
+        s = _stream()
+        dinp = None
+        if ctx.needs_input_grad[0]:
+            dinp = torch.empty_like(inp)
+            call("of_fill", _ptr(dinp), 0.0, dinp.numel(), s)
+        dflow = torch.empty_like(flow)
+        call("of_bilinear_bwd" if ctx.absolute else "of_warp_bwd", _ptr(dout), _ptr(inp), n, h,
+             w, c, _ptr(flow), _ptr(dinp), _ptr(dflow), s)
+        return dinp, (dflow if ctx.needs_input_grad[1] else None), None
+
+
+def warp(inp, flow):
+    return _Warp.apply(inp, flow, False)
+
+
+def bilinear(inp, points):
+    return _Warp.apply(inp, points, True)
+
+
+# ====================================================================== upscale x2 =====
+class _Upscale2x(torch.autograd.Function):
+    """upscale_flow (model.py:76-77): resize x2 (half-pixel bilinear) times 2.0."""
+
+    @staticmethod
+    def forward(ctx, x, scale):
+        _check_dev(x)
+        x = x.contiguous()
+        n, h, w, c = x.shape
+        out = torch.empty((n, 2 * h, 2 * w, c), device=x.device)
+        call("of_upscale2x_fwd", _ptr(x), n, h, w, c, scale, _ptr(out), c, _stream())
+        ctx.shape = (n, h, w, c)
+        ctx.scale = scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        n, h, w, c = ctx.shape
+        dout = dout.contiguous()
+        dx = torch.empty((n, h, w, c), device=dout.device)
+        call("of_upscale2x_bwd", _ptr(dout), c, n, h, w, c, ctx.scale, _ptr(dx), 0, _stream())
+        return dx, None
+
+
+def upscale2x(x, scale=2.0):
+    return _Upscale2x.apply(x, scale)
+
+
+# ================================================================= Siamese batching ====
+def split_pair(batch_imgs):
+    """(B,H,W,6) -> (2B,H,W,4): image1s then image2s, 4th channel zero (model.py:122-123);
+    the images are constants of the graph (no gradient)."""
+    _check_dev(batch_imgs)
+    b = batch_imgs.contiguous()
+    n, h, w, c = b.shape
+    assert c == 6
+    out = torch.empty((2 * n, h, w, 4), device=b.device)
+    call("of_split_pair", _ptr(b), n, h, w, _ptr(out), _stream())
+    return out
+
+
+class _Halves(torch.autograd.Function):
+    """Split a (2B, ...) Siamese activation into its two (B, ...) halves; the backward writes
+    both halves' gradients into one buffer (no zero-fill + add of slice backward)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        n = x.shape[0] // 2
+        ctx.shape = x.shape
+        return x.narrow(0, 0, n), x.narrow(0, n, n)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        shape = ctx.shape
+        n = shape[0] // 2
+        dev = (g1 if g1 is not None else g2).device
+        out = torch.empty(shape, device=dev)
+        half = out.numel() // 2
+        s = _stream()
+        for k, g in enumerate((g1, g2)):
+            dst = C.c_void_p(out.data_ptr() + 4 * k * half)
+            if g is None:
+                call("of_fill", dst, 0.0, half, s)
+            else:
+                g = g.contiguous()
+                call("of_copy_strided", _ptr(g), 1, dst, 1, half, 1, s)
+        return out
+
+
+def halves(x):
+    return _Halves.apply(x)
+
+
+# ================================================================ photometric loss =====
+class _PhotoLoss(torch.autograd.Function):
+    """LossLayer.__call__ (loss.py:5-32): mean over scales of mean |img1_s - warp(img2_s)|.
+    The image pyramid (tf.image.resize) is built by one kernel per level; the warp, the
+    difference, |.| and the reduction are fused per scale; the backward writes d(flow) per
+    scale directly (the images are constants)."""
+
+    @staticmethod
+    def forward(ctx, batch_imgs, *flows):
+        _check_dev(batch_imgs, *flows)
+        b = batch_imgs.contiguous()
+        n, H, W, c = b.shape
+        assert c == 6
+        ns = len(flows)
+        s = _stream()
+        pyr = []
+        for k in range(ns):
+            h = int(H / (2.0 ** (k + 1)))
+            w = int(W / (2.0 ** (k + 1)))
+            assert flows[k].shape[1] == h and flows[k].shape[2] == w, \
+                "flow %d has shape %s, expected (B,%d,%d,2)" % (k, tuple(flows[k].shape), h, w)
+            pyr.append(torch.empty((n, h, w, 6), device=b.device))
+        # every level is a resize of the full-resolution batch (loss.py:17-18)
+        outs = (C.c_void_p * ns)(*[p.data_ptr() for p in pyr])
+        call("of_pyramid6", _ptr(b), n, H, W, ns, outs, s)
+        nparts, parts, coefs = [], [], []
+        for k in range(ns):
+            h, w = pyr[k].shape[1], pyr[k].shape[2]
+            npart = _lib.lib().of_photo_l1_partials(n, h, w)
+            pt = torch.empty(npart, device=b.device)
+            call("of_photo_l1_fwd", _ptr(pyr[k]), _ptr(flows[k].contiguous()), n, h, w, _ptr(pt),
+                 s)
+            parts.append(pt)
+            nparts.append(npart)
+            coefs.append(1.0 / (ns * n * h * w * 3))
+        loss = torch.empty((), device=b.device)
+        call("of_sum_partials", (C.c_void_p * ns)(*[p.data_ptr() for p in parts]),
+             (C.c_int * ns)(*nparts), (C.c_float * ns)(*coefs), ns, _ptr(loss), s)
+        ctx.save_for_backward(*pyr, *[f.contiguous() for f in flows])
+        ctx.ns = ns
+        ctx.coefs = coefs
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        ns = ctx.ns
+        saved = ctx.saved_tensors
+        pyr, flows = saved[:ns], saved[ns:]
+        dloss = dloss.contiguous()
+        s = _stream()
+        grads = []
+        for k in range(ns):
+            n, h, w, _ = pyr[k].shape
+            if not ctx.needs_input_grad[1 + k]:
+                grads.append(None)
+                continue
+            df = torch.empty_like(flows[k])
+            call("of_photo_l1_bwd", _ptr(pyr[k]), _ptr(flows[k]), n, h, w, ctx.coefs[k],
+                 _ptr(dloss), _ptr(df), s)
+            grads.append(df)
+        return (None, *grads)
+
+
+def photometric_loss(batch_imgs, flows):
+    return _PhotoLoss.apply(batch_imgs, *flows)

@@ -1,0 +1,132 @@
+"""Mirror of the reference ``train.py`` driver (train.py:1-88) on synthetic pairs.
+
+``train_step(batch_imgs, step_count)`` keeps the reference's shape (train.py:47-61): forward
+through the flow net, the photometric loss, gradients of the trainable weights, one Keras-Adam
+update; returns ``(loss_value, flows)``.  Differences that are out of scope:
+no KITTI reader (synthetic pairs with the reference value contract, data.py), no TensorBoard
+writer (a JSONL step log instead), no cv2 display.  Data parallelism (one process per GPU,
+RCCL all-reduce of gradient buckets overlapped with the backward) is build-added.
+
+Run:  python -m optical_flow_amd.train --height 384 --width 512 --batch 8 --steps 20
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+from . import ops
+from ._lib import call
+from .data import synthetic_batch
+from .dist import GradBucketReducer, init_from_env
+from .loss import LossLayer
+from .model import FlowNet, build_flow_net
+
+
+class KerasAdam:
+    """tf.keras.optimizers.Adam (train.py:34): beta_1 0.9, beta_2 0.999, epsilon 1e-7,
+    ResourceApplyAdam update with lr_t = lr*sqrt(1-b2^t)/(1-b1^t) (P13).  One fused launch
+    over the model's parameter arena."""
+
+    def __init__(self, store, learning_rate=1e-4, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+        self.store = store
+        self.learning_rate = learning_rate
+        self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
+        self.iterations = 0
+        self.m = torch.zeros_like(store.arena)
+        self.v = torch.zeros_like(store.arena)
+
+    def apply_gradients(self, grad_scale: float = 1.0):
+        t = self.iterations + 1
+        lr_t = self.learning_rate * math.sqrt(1.0 - self.beta_2 ** t) / (1.0 - self.beta_1 ** t)
+        s = self.store
+        call("of_adam_keras", C.c_void_p(s.arena.data_ptr()), C.c_void_p(s.grad_arena.data_ptr()),
+             C.c_void_p(self.m.data_ptr()), C.c_void_p(self.v.data_ptr()), s.numel, lr_t,
+             self.beta_1, self.beta_2, self.epsilon, grad_scale, ops._stream())
+        self.iterations += 1
+        s.version += 1       # packed conv weights are refreshed lazily on next use
+
+
+class Trainer:
+    """Holds the model, optimizer, loss and (optional) DP reducer; ``train_step`` is the
+    hot loop body of train.py:72-82."""
+
+    def __init__(self, flow_net: FlowNet, optimizer: KerasAdam = None, loss_layer=None,
+                 data_parallel: bool = None):
+        self.flow_net = flow_net
+        self.optimizer = optimizer or KerasAdam(flow_net.store)
+        self.loss_layer = loss_layer or LossLayer()
+        if data_parallel is None:
+            data_parallel = torch.distributed.is_initialized() and \
+                torch.distributed.get_world_size() > 1
+        self.reducer = GradBucketReducer(flow_net.store) if data_parallel else None
+
+    def train_step(self, batch_imgs, step_count=0):
+        store = self.flow_net.store
+        store.zero_grad()
+        if self.reducer is not None:
+            self.reducer.begin()
+        flows = self.flow_net(batch_imgs)
+        loss_value = self.loss_layer(batch_imgs, flows)
+        loss_value.backward()
+        scale = self.reducer.finish() if self.reducer is not None else 1.0
+        self.optimizer.apply_gradients(grad_scale=scale)
+        return loss_value.detach(), [f.detach() for f in flows]
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--height", type=int, default=192)       # train.py:15
+    ap.add_argument("--width", type=int, default=640)        # train.py:16
+    ap.add_argument("--batch", type=int, default=4)          # train.py:20
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10, help="batches per epoch")
+    ap.add_argument("--lr", type=float, default=1e-4)        # train.py:34
+    ap.add_argument("--lr-drop-epoch", type=int, default=15)  # train.py:69-70
+    ap.add_argument("--pretrained", default=None)
+    ap.add_argument("--save-dir", default=None)
+    ap.add_argument("--log", default=None, help="JSONL step log")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args(argv)
+
+    rank, world, local = init_from_env()
+    torch.cuda.set_device(local)
+    net = build_flow_net(args.height, args.width, args.pretrained, seed=args.seed)
+    if rank == 0:
+        net.summary()
+    opt = KerasAdam(net.store, learning_rate=args.lr)
+    trainer = Trainer(net, opt)
+    log = open(args.log, "a") if (args.log and rank == 0) else None
+    step = 0
+    for epoch in range(args.epochs):
+        if epoch == args.lr_drop_epoch:
+            opt.learning_rate = args.lr * 0.1
+        t0 = time.time()
+        for b in range(args.steps):
+            batch = torch.from_numpy(synthetic_batch(args.batch, args.height, args.width,
+                                                     seed=1234 + step, rank=rank)).cuda()
+            loss, flows = trainer.train_step(batch, step)
+            lv = float(loss)
+            if rank == 0:
+                sys.stdout.write("\rbatch %d/%d, loss: %.2e    " % (b + 1, args.steps, lv))
+                sys.stdout.flush()
+                if log:
+                    log.write(json.dumps({"step": step, "loss": lv, "t": time.time() - t0}) + "\n")
+            step += 1
+        if rank == 0:
+            print("\nEpoch computed in %.3fs" % (time.time() - t0))
+            if args.save_dir:
+                net.save_weights(os.path.join(args.save_dir, "flow_net_%d" % epoch, "weights"))
+    if log:
+        log.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,227 @@
+"""Per-kernel parity: every HIP kernel through the C ABI vs the CPU oracle (float64) on the
+same seeded inputs.  Tolerance: 1e-3 relative (REL_TOL), per BASELINE.json's north star."""
+import pytest
+import torch
+
+from helpers import REL_TOL, dev, f64, rel_inf, rel_l2, rng_tensor
+from oracle import ref_flow as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from optical_flow_amd import ops
+    return ops
+
+
+# ------------------------------------------------------------------------------- conv ----
+CONV_CASES = [
+    # (n, h, w, cin, cout, k, stride, act, bn, residual)
+    (2, 16, 24, 16, 32, 3, 1, "leaky", False, False),
+    (2, 16, 24, 115, 128, 3, 1, "leaky", False, False),     # decoder c0 (cin padded)
+    (1, 12, 16, 32, 2, 3, 1, "none", False, False),         # flow conv (cout 2)
+    (2, 16, 16, 64, 96, 3, 1, "leaky", False, False),       # cout 96 tile
+    (2, 32, 48, 3, 64, 7, 2, "relu", True, False),          # conv1 7x7/2 + BN + ReLU
+    (2, 16, 16, 64, 128, 3, 2, "relu", True, False),        # stride-2 block conv
+    (2, 16, 16, 64, 128, 1, 2, "none", True, False),        # 1x1/2 projection + BN
+    (2, 8, 8, 128, 128, 3, 1, "relu", True, True),          # conv_b + BN + residual + ReLU
+    (1, 6, 10, 256, 256, 3, 1, "relu", True, False),        # odd sizes, 2 n-tiles
+    (3, 9, 7, 20, 40, 3, 2, "leaky", False, False),         # odd spatial, stride 2
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: "x".join(map(str, c[:7])) + c[7])
+def test_conv_fwd_bwd(case):
+    ops = _ops()
+    from optical_flow_amd._lib import ACT_LEAKY, ACT_NONE, ACT_RELU
+    n, h, w, cin, cout, k, s, act, use_bn, use_res = case
+    seed = hash(case) % 1000
+    x = rng_tensor((n, h, w, cin), seed)
+    wt = rng_tensor((k, k, cin, cout), seed + 1, scale=(2.0 / (k * k * cin)) ** 0.5)
+    b = rng_tensor((cout,), seed + 2, scale=0.1)
+    g = rng_tensor((cout,), seed + 3, lo=0.5, hi=1.5)
+    be = rng_tensor((cout,), seed + 4, scale=0.1)
+    mu = rng_tensor((cout,), seed + 5, scale=0.1)
+    var = rng_tensor((cout,), seed + 6, lo=0.5, hi=1.5)
+    # --- oracle
+    xo, wo_, bo, go, beo = [f64(t).requires_grad_(True) for t in (x, wt, b, g, be)]
+    zo = R.conv2d_same(xo, wo_, bo, s)
+    yo = zo
+    p = {"bn/gamma": go, "bn/beta": beo, "bn/moving_mean": f64(mu), "bn/moving_variance": f64(var)}
+    if use_bn:
+        yo = R.batchnorm_inference(yo, p, "bn")
+    res = rng_tensor(tuple(yo.shape), seed + 7) if use_res else None
+    reso = f64(res).requires_grad_(True) if use_res else None
+    if use_res:
+        yo = yo + reso
+    yo = {"relu": torch.relu, "leaky": R.leaky_relu, "none": lambda t: t}[act](yo)
+    gy = rng_tensor(tuple(yo.shape), seed + 8)
+    (yo * f64(gy)).sum().backward()
+    # --- device
+    cin_p = (cin + 3) // 4 * 4
+    xd = torch.zeros((n, h, w, cin_p), device="cuda")
+    xd[..., :cin] = dev(x)
+    wd, bd, gd, bed = [dev(t).requires_grad_(True) for t in (wt, b, g, be)]
+    layer = ops.ConvLayer(wd, bd, stride=s,
+                          act={"relu": ACT_RELU, "leaky": ACT_LEAKY, "none": ACT_NONE}[act],
+                          bn=(gd, bed, dev(mu), dev(var)) if use_bn else None, cin_p=cin_p)
+    xd.requires_grad_(True)
+    resd = dev(res).requires_grad_(True) if use_res else None
+    yd = layer(xd, residual=resd)
+    assert yd.shape == yo.shape
+    assert rel_inf(yd, yo) < REL_TOL, "forward"
+    (yd * dev(gy)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_inf(xd.grad[..., :cin], xo.grad) < REL_TOL, "dgrad"
+    assert rel_inf(xd.grad[..., cin:], torch.zeros(1)) == 0 or cin == cin_p
+    assert rel_l2(wd.grad, wo_.grad) < REL_TOL, "wgrad"
+    assert rel_l2(bd.grad, bo.grad) < REL_TOL, "bias grad"
+    if use_bn:
+        assert rel_l2(gd.grad, go.grad) < REL_TOL, "gamma grad"
+        assert rel_l2(bed.grad, beo.grad) < REL_TOL, "beta grad"
+    if use_res:
+        assert rel_inf(resd.grad, reso.grad) < REL_TOL, "residual grad"
+
+
+# ----------------------------------------------------------------------- cost volume ----
+@pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6)])
+def test_cost_volume(shape):
+    ops = _ops()
+    f1, f2 = rng_tensor(shape, 1), rng_tensor(shape, 2)
+    a, b = f64(f1).requires_grad_(True), f64(f2).requires_grad_(True)
+    cv = R.create_cost_volume(a, b, 3)
+    g = rng_tensor(tuple(cv.shape), 3)
+    (cv * f64(g)).sum().backward()
+    ad, bd = dev(f1).requires_grad_(True), dev(f2).requires_grad_(True)
+    cvd = ops.cost_volume(ad, bd, 3)
+    assert rel_inf(cvd, cv) < REL_TOL
+    (cvd * dev(g)).sum().backward()
+    assert rel_inf(ad.grad, a.grad) < REL_TOL
+    assert rel_inf(bd.grad, b.grad) < REL_TOL
+
+
+def test_corr_concat():
+    ops = _ops()
+    n, h, w, c = 2, 8, 12, 64
+    f1, f2, fl = rng_tensor((n, h, w, c), 4), rng_tensor((n, h, w, c), 5), rng_tensor((n, h, w, 2), 6)
+    a, b, fo = [f64(t).requires_grad_(True) for t in (f1, f2, fl)]
+    xo = torch.cat([a, R.create_cost_volume(a, b, 3), fo], -1)
+    g = rng_tensor(tuple(xo.shape), 7)
+    (xo * f64(g)).sum().backward()
+    ad, bd, fd = [dev(t).requires_grad_(True) for t in (f1, f2, fl)]
+    xd = ops.corr_concat(ad, bd, fd, 3, 116)
+    assert rel_inf(xd[..., :115], xo) < REL_TOL
+    assert xd[..., 115:].abs().max().item() == 0
+    gd = torch.zeros((n, h, w, 116), device="cuda")
+    gd[..., :115] = dev(g)
+    (xd * gd).sum().backward()
+    for d_, o_ in ((ad, a), (bd, b), (fd, fo)):
+        assert rel_inf(d_.grad, o_.grad) < REL_TOL
+
+
+# ------------------------------------------------------------------------------ warp ----
+@pytest.mark.parametrize("shape,flow_scale", [((2, 12, 20, 64), 3.0), ((2, 16, 16, 128), 1.5),
+                                              ((1, 10, 14, 3), 4.0), ((2, 8, 24, 32), 20.0)])
+def test_warp(shape, flow_scale):
+    ops = _ops()
+    n, h, w, c = shape
+    f2 = rng_tensor(shape, 11)
+    fl = rng_tensor((n, h, w, 2), 12, scale=flow_scale)
+    a, fo = f64(f2).requires_grad_(True), f64(fl).requires_grad_(True)
+    out = R.warp_features(fo, a)
+    g = rng_tensor(tuple(out.shape), 13)
+    (out * f64(g)).sum().backward()
+    ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
+    od = ops.warp(ad, fd)
+    assert rel_inf(od, out) < REL_TOL
+    (od * dev(g)).sum().backward()
+    assert rel_inf(ad.grad, a.grad) < REL_TOL
+    assert rel_inf(fd.grad, fo.grad) < REL_TOL
+
+
+def test_bilinear_interpolation_absolute():
+    from optical_flow_amd.transformations import bilinear_interpolation
+    n, h, w, c = 2, 9, 11, 8
+    inp = rng_tensor((n, h, w, c), 21)
+    pts = rng_tensor((n, h, w, 2), 22, lo=-3.0, hi=14.0)
+    a, po = f64(inp).requires_grad_(True), f64(pts).requires_grad_(True)
+    out = R.bilinear_interpolation(a, po)
+    g = rng_tensor(tuple(out.shape), 23)
+    (out * f64(g)).sum().backward()
+    ad, pd = dev(inp).requires_grad_(True), dev(pts).requires_grad_(True)
+    od = bilinear_interpolation(ad, pd)
+    assert rel_inf(od, out) < REL_TOL
+    (od * dev(g)).sum().backward()
+    assert rel_inf(ad.grad, a.grad) < REL_TOL
+    assert rel_inf(pd.grad, po.grad) < REL_TOL
+
+
+# -------------------------------------------------------------------------- upscale -----
+@pytest.mark.parametrize("shape", [(2, 6, 8, 2), (1, 24, 32, 2), (2, 5, 7, 3)])
+def test_upscale(shape):
+    ops = _ops()
+    x = rng_tensor(shape, 31)
+    xo = f64(x).requires_grad_(True)
+    yo = R.upscale_flow(xo)
+    g = rng_tensor(tuple(yo.shape), 32)
+    (yo * f64(g)).sum().backward()
+    xd = dev(x).requires_grad_(True)
+    yd = ops.upscale2x(xd, 2.0)
+    assert rel_inf(yd, yo) < REL_TOL
+    (yd * dev(g)).sum().backward()
+    assert rel_inf(xd.grad, xo.grad) < REL_TOL
+
+
+# ------------------------------------------------------------------------- max pool -----
+def test_maxpool():
+    ops = _ops()
+    x = rng_tensor((2, 8, 12, 64), 41)
+    xo = f64(x).requires_grad_(True)
+    yo = R.maxpool2(xo)
+    g = rng_tensor(tuple(yo.shape), 42)
+    (yo * f64(g)).sum().backward()
+    xd = dev(x).requires_grad_(True)
+    yd = ops.maxpool2(xd)
+    assert rel_inf(yd, yo) == 0.0
+    (yd * dev(g)).sum().backward()
+    assert rel_inf(xd.grad, xo.grad) < REL_TOL
+
+
+# ------------------------------------------------------------------- photometric loss ---
+@pytest.mark.parametrize("size", [(2, 64, 96), (1, 128, 256)])
+def test_photometric_loss(size):
+    from optical_flow_amd.loss import LossLayer
+    from optical_flow_amd.data import synthetic_batch
+    n, H, W = size
+    batch = torch.from_numpy(synthetic_batch(n, H, W, seed=5))
+    flows = [rng_tensor((n, H >> (s + 1), W >> (s + 1), 2), 50 + s, scale=2.0) for s in range(4)]
+    fo = [f64(f).requires_grad_(True) for f in flows]
+    lo = R.photometric_loss(f64(batch), fo)
+    lo.backward()
+    fd = [dev(f).requires_grad_(True) for f in flows]
+    ld = LossLayer()(dev(batch), fd)
+    assert abs(ld.item() - lo.item()) / abs(lo.item()) < REL_TOL
+    ld.backward()
+    for a, b in zip(fd, fo):
+        assert rel_l2(a.grad, b.grad) < REL_TOL
+
+
+# ------------------------------------------------------------------------------ adam ----
+def test_keras_adam():
+    from optical_flow_amd.train import KerasAdam
+    from optical_flow_amd.model import ParamStore
+    from optical_flow_amd.params import head_spec, init_params
+    spec = head_spec(3)
+    vals = init_params(spec, 3)
+    store = ParamStore(spec, vals, device="cuda")
+    opt = KerasAdam(store, learning_rate=1e-2)
+    ref = R.KerasAdam(lr=1e-2)
+    pref = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+    for it in range(3):
+        grads = {k: rng_tensor(v.shape, 100 + it * 7 + i) for i, (k, v) in enumerate(vals.items())}
+        for k, g in grads.items():
+            store.params[k]._of_grad.copy_(g.cuda())
+        opt.apply_gradients()
+        ref.step(pref, {k: g.double() for k, g in grads.items()})
+    for k in vals:
+        assert rel_inf(store.params[k], pref[k]) < 1e-5
