@@ -148,11 +148,13 @@ def main():
 
     # ---- dominant-kernel roofline (instrumented extra steps, outside the timed region) ----
     lib = _lib.lib()
+    ops.TIMING_TAGS = []
     lib.of_timing_enable(1)
     for i in range(args.timing_steps):
         trainer.train_step(batch, 10_000 + i)
     torch.cuda.synchronize()
     lib.of_timing_enable(0)
+    tags, ops.TIMING_TAGS = ops.TIMING_TAGS, None
     cap = 4096
     kinds = (C.c_int * cap)()
     flops = (C.c_double * cap)()
@@ -163,6 +165,10 @@ def main():
         k = kinds[i]
         tf, tm, cnt = per.get(k, (0.0, 0.0, 0))
         per[k] = (tf + flops[i], tm + ms[i], cnt + 1)
+    if os.environ.get("OFLOW_TIMING_DUMP") and rank == 0 and len(tags) == n:
+        with open(os.environ["OFLOW_TIMING_DUMP"], "w") as f:
+            json.dump([{"layer": tags[i][0], "kind": kinds[i], "gflop": flops[i] / 1e9,
+                        "ms": ms[i]} for i in range(n)], f)
     dom = max(per, key=lambda k: per[k][1]) if per else None
     roof = None
     conv_ms_step = sum(v[1] for v in per.values()) / max(args.timing_steps, 1)

@@ -70,20 +70,28 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
  * bias and bn_*: [cout] or NULL; residual: NULL or pixels of ldr; act: OF_ACT_*, alpha is
  * the LeakyReLU slope.  Replaces Conv2D + BiasAdd + FusedBatchNorm(inference) + AddV2 +
  * Relu/LeakyRelu. */
+size_t of_conv2d_fwd_workspace(const of_conv_desc* d);
 int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w_fwd,
                   const float* bias, const float* bn_gamma, const float* bn_beta,
                   const float* bn_mean, const float* bn_var, float bn_eps,
                   const float* residual, int ldr, int act, float alpha,
-                  float* z, int ldz, float* y, int ldy, void* stream);
+                  float* z, int ldz, float* y, int ldy, void* workspace, size_t ws_bytes,
+                  void* stream);
 
-/* Input gradient (Conv2DBackpropInput; for stride 2 this is the transposed convolution):
+/* Workspace (fwd / dgrad): grids with fewer tiles than CUs split K over workgroups into fp32
+ * slabs of of_conv2d_{fwd,dgrad}_workspace() bytes; with workspace == NULL (or too small) the
+ * call runs unsplit (same result). */
+
+/* Input gradient (Conv2DBackpropInput; for stride 2 this is the transposed convolution, run
+ * as four row/column-parity phase groups that each visit only their taps):
  * dx[.., ci] = sum_{tap,co} dy * w, for ci < cin_p, then (fused) multiplied by the
  * activation derivative of act_src (the forward output that fed this conv) when
  * act_src != NULL: relu' = [s>0], leaky' = s>0 ? 1 : alpha.
  * dy: [n][ho][wo] pixels of lddy elements, round_up(cout,4) channels read (pad must be 0). */
+size_t of_conv2d_dgrad_workspace(const of_conv_desc* d);
 int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
                     const float* act_src, int ld_act, int act, float alpha,
-                    float* dx, int lddx, void* stream);
+                    float* dx, int lddx, void* workspace, size_t ws_bytes, void* stream);
 
 /* Weight (+ bias) gradient (Conv2DBackpropFilter + BiasAddGrad): dw in HWIO [kh][kw][cin][cout],
  * db [cout] (NULL to skip); accumulate != 0 adds into dw/db (gradient arenas).

@@ -38,8 +38,10 @@ PROTOTYPES = {
     "of_conv_wfwd_elems": (I64, [PD]),
     "of_conv_wbwd_elems": (I64, [PD]),
     "of_conv_pack_weights": (I, [PD, P, P, P, P]),
-    "of_conv2d_fwd": (I, [PD, P, I, P, P, P, P, P, P, F, P, I, I, F, P, I, P, I, P]),
-    "of_conv2d_dgrad": (I, [PD, P, I, P, P, I, I, F, P, I, P]),
+    "of_conv2d_fwd_workspace": (SZ, [PD]),
+    "of_conv2d_fwd": (I, [PD, P, I, P, P, P, P, P, P, F, P, I, I, F, P, I, P, I, P, SZ, P]),
+    "of_conv2d_dgrad_workspace": (SZ, [PD]),
+    "of_conv2d_dgrad": (I, [PD, P, I, P, P, I, I, F, P, I, P, SZ, P]),
     "of_conv2d_wgrad_workspace": (SZ, [PD]),
     "of_conv2d_wgrad": (I, [PD, P, I, P, I, P, P, I, P, SZ, P]),
     "of_act_bwd": (I, [P, P, I, F, P, I64, P]),

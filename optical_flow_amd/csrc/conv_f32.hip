@@ -8,19 +8,27 @@
 //
 //   FWD   C[m=out pixel][n=cout]  = sum_{k=(tap,ci)}  x[pix(m,tap)][ci] * Wf[k][n]
 //   DGRAD C[m=in  pixel][n=ci]    = sum_{k=(tap,co)} dy[pix^-1(m,tap)][co] * Wd[k][n]
-//         (stride-2 layers: the transposed convolution; taps whose source is not on the
-//          stride lattice contribute zero)
+//         stride 2 = the transposed convolution, run as 4 "phase groups": the input pixels
+//         of one (row, col) parity only see the taps of matching parity, so each group's
+//         K loop visits exactly its taps (no zero-masked MACs) and the packed Wd holds the
+//         taps grouped by phase.
 //   WGRAD C[m=(tap,ci)][n=cout]  = sum_{k=out pixel} x[pix(k,tap)][ci] * dy[k][n]
-//         (split-K over pixels into fp32 slabs, reduced deterministically)
+//         (split-K over pixels into fp32 slabs, reduced deterministically; the bias
+//          gradient = column sums of dy rides along in the same pass).
 //
 // Tiling: BM x BN x 16 per 256-thread workgroup (4 waves), each wave an (BM/WAVES_M) x
 // (BN/WAVES_N) block of 32x32 MFMA tiles.  LDS holds both operands k-major ([k][m], [k][n]) so
 // the MFMA operand fetch is one conflict-free ds_read_b32 per lane (lanes 0-31 row k,
-// lanes 32-63 row k+1).  Global->LDS is register-staged and double-buffered: the loads of
-// chunk c+1 are issued before the MFMAs of chunk c, one barrier per chunk.  Fused epilogues:
-// bias, BN-inference affine, residual add, ReLU/LeakyReLU (fwd); activation derivative of
-// the producer layer (dgrad).  Block ids are remapped so neighbouring tiles share an XCD L2.
+// lanes 32-63 row k+1); the fragments of k-step s+1 are read while the MFMAs of step s issue.
+// Global->LDS is register-staged and double-buffered: the loads of chunk c+1 are issued
+// before the MFMAs of chunk c, one barrier per chunk.  Grids with fewer tiles than the chip
+// has CUs split K over workgroups into fp32 slabs; a separate pass sums them and runs the
+// epilogue.  Fused epilogues: bias, BN-inference affine, residual add, ReLU/LeakyReLU (fwd);
+// the producer layer's activation derivative (dgrad).  Work-group ids are remapped so that
+// consecutive tiles (and all tiles of one K slice) run on one XCD and share its L2.
 #include "common.h"
+
+#include <algorithm>
 
 namespace oflow {
 
@@ -28,31 +36,102 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 constexpr int BK = 16;
+constexpr int MAX_GROUPS = 4;
+constexpr int kCUs = 256;          // MI355X compute units
+
+// A group = GEMM rows sharing one tap list (dgrad stride-2 phase classes); plain convs have
+// a single identity group.
+struct Group {
+  int tiles_begin;   // first m-tile of this group in the flattened tile space
+  int m_tiles;
+  int M;             // rows of the group
+  int hc, wc;        // phase mode: rows are (b, u, v), input pixel (2u+ry, 2v+rx)
+  int ry, rx;
+  int r0, s0, ns;    // taps (r0 + dt*(t/ns), s0 + dt*(t%ns)), t < ntaps
+  int ntaps;
+  int K;             // K of the group (multiple of BK)
+  int64_t b_off;     // first packed-B row of the group
+};
 
 struct GemmArgs {
   int n, h, w, ho, wo;
   int kh, kw, stride, pt, pl;
   int kc;                 // channels per tap along K (fwd: cin_p, dgrad: cout_p) / M (wgrad)
-  int taps;
-  int M, N, K;            // fwd/dgrad: K = padded taps*kc; wgrad: K = output pixels
+  int dt;                 // tap step inside a group (1, or 2 for phase groups)
+  int phase;              // dgrad phase-group mode (stride 2)
+  int M, N, K;            // wgrad: M = taps*cin_p, K = output pixels
   const float* A; int lda;
   const float* B; int ldb; int nb;
-  float* C; int ldc;
+  float* C; int ldc;      // final output (epilogue)
   const float* bias;
   const float* bn_g; const float* bn_b; const float* bn_m; const float* bn_v; float bn_eps;
   const float* res; int ldr;
   float* z; int ldz;
   int act; float alpha;
   const float* act_src; int ld_act;
-  int k_per_split;
+  int splits;             // K slices over workgroups
+  int k_per_split;        // elements of K per slice (multiple of BK)
+  float* slab; int slab_ld;   // partials (wgrad always; fwd/dgrad when splits > 1)
   int64_t split_stride;
-  int m_tiles, n_tiles;
+  int n_tiles;
+  int tiles_total;        // sum over groups of m_tiles * n_tiles
+  int colsum;             // wgrad: column sums of B (bias grad) into slab row M
+  int bm;                 // M tile of the launched configuration
+  int ngroups;
+  Group grp[MAX_GROUPS];
 };
+
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
 
 __device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
   if (act == OF_ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == OF_ACT_LEAKY) return v > 0.f ? v : alpha * v;
   return v;
+}
+
+// Output pixel row of group-local GEMM row m (identity unless dgrad phase groups).
+__device__ __forceinline__ int64_t out_row(const GemmArgs& a, const Group& g, int m) {
+  if (!a.phase) return m;
+  const int hw = g.hc * g.wc;
+  const int b = m / hw, rem = m - b * hw;
+  const int u = rem / g.wc, v = rem - u * g.wc;
+  return ((int64_t)b * a.h + 2 * u + g.ry) * a.w + 2 * v + g.rx;
+}
+
+// Fused epilogue for one element (fwd / dgrad), v = the full K sum.
+template <int MODE>
+__device__ __forceinline__ void epilogue_store(const GemmArgs& a, int64_t row, int n, float v,
+                                               float bias, float scale, float shift) {
+  if (MODE == MODE_FWD) {
+    v += bias;
+    if (a.z) a.z[row * a.ldz + n] = v;
+    if (a.bn_g) v = v * scale + shift;
+    if (a.res) v += a.res[row * a.ldr + n];
+    v = act_fwd(v, a.act, a.alpha);
+  } else if (MODE == MODE_DGRAD) {
+    if (a.act_src) {
+      const float s = a.act_src[row * a.ld_act + n];
+      v *= s > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
+    }
+  }
+  a.C[row * a.ldc + n] = v;
+}
+
+template <int MODE>
+__device__ __forceinline__ void column_params(const GemmArgs& a, int n, float& bias,
+                                              float& scale, float& shift) {
+  bias = 0.f;
+  scale = 1.f;
+  shift = 0.f;
+  if (MODE == MODE_FWD) {
+    if (a.bias) bias = a.bias[n];
+    if (a.bn_g) {
+      scale = a.bn_g[n] * rsqrtf(a.bn_v[n] + a.bn_eps);
+      shift = a.bn_b[n] - a.bn_m[n] * scale;
+    }
+  }
 }
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
@@ -75,25 +154,32 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
 
-  // XCD-aware bijective remap: consecutive tiles -> one XCD's L2 (cdna guide T1).
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
+  // XCD-aware bijective remap: consecutive work ids -> one XCD's L2 (cdna guide T1).
   int wgid;
   {
+    const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int tile_n = wgid % a.n_tiles;
-  const int tile_m = wgid / a.n_tiles;
+  // work id = split * tiles_total + tile: all tiles of one K slice are consecutive.
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_n = tile % a.n_tiles;
+  const int tile_mg = tile / a.n_tiles;
+  int gi = 0;
+#pragma unroll
+  for (int g = 1; g < MAX_GROUPS; ++g)
+    if (g < a.ngroups && tile_mg >= a.grp[g].tiles_begin) gi = g;
+  const Group& G = a.grp[gi];
+  const int tile_m = tile_mg - G.tiles_begin;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int M = G.M;
 
   // ---------------- K range -------------------------------------------------------------
-  int k_begin = 0, k_end = a.K;
-  if (MODE == MODE_WGRAD) {
-    k_begin = blockIdx.z * a.k_per_split;
-    k_end = min(a.K, k_begin + a.k_per_split);
-  }
-  const int nchunks = (k_end - k_begin + BK - 1) / BK;
+  const int Kg = (MODE == MODE_WGRAD) ? a.K : G.K;
+  const int k_begin = split * a.k_per_split;
+  const int k_end = min(Kg, k_begin + a.k_per_split);
+  const int nchunks = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
 
   // ---------------- A loader state ------------------------------------------------------
   // K-contig (fwd/dgrad): thread -> (row = tid/4 + 64*i, kq = tid%4), 4 channels of one tap.
@@ -102,44 +188,57 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   const int src_w = (MODE == MODE_DGRAD) ? a.wo : a.w;
   int a_py[A_SLOTS], a_px[A_SLOTS], a_b[A_SLOTS];
   bool a_ok[A_SLOTS];
-  int ks_r = 0, ks_s = 0, ks_ci = 0, ks_tap = 0;   // fwd/dgrad: per-thread k state
-  int wm_r = 0, wm_s = 0, wm_ci = 0;                // wgrad: per-thread fixed m
+  int ks_t = 0, ks_si = 0, ks_r = 0, ks_s = 0, ks_ci = 0;   // fwd/dgrad: per-thread k state
+  int wm_r = 0, wm_s = 0, wm_ci = 0;                         // wgrad: per-thread fixed m
   bool wm_ok = false;
-  int a_oy[A_SLOTS], a_ox[A_SLOTS], a_kb[A_SLOTS];  // wgrad: per-slot pixel state
+  int a_oy[A_SLOTS], a_ox[A_SLOTS], a_kb[A_SLOTS];           // wgrad: per-slot pixel state
 
   if constexpr (A_KCONTIG) {
     const int kq = tid & 3;
-    const int hw = a.ho * a.wo;   // fwd: rows are output pixels
-    const int hw_in = a.h * a.w;  // dgrad: rows are input pixels
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
       const int m = m0 + (tid >> 2) + 64 * i;
-      a_ok[i] = m < a.M;
+      a_ok[i] = m < M;
       const int mm = a_ok[i] ? m : 0;
       if (MODE == MODE_FWD) {
+        const int hw = a.ho * a.wo;
         const int b = mm / hw, rem = mm - b * hw;
         const int oy = rem / a.wo, ox = rem - oy * a.wo;
         a_b[i] = b * a.h;
         a_py[i] = oy * a.stride - a.pt;
         a_px[i] = ox * a.stride - a.pl;
       } else {
-        const int b = mm / hw_in, rem = mm - b * hw_in;
-        const int iy = rem / a.w, ix = rem - iy * a.w;
+        int b, iy, ix;
+        if (a.phase) {
+          const int hw = G.hc * G.wc;
+          b = mm / hw;
+          const int rem = mm - b * hw;
+          const int u = rem / G.wc, v = rem - u * G.wc;
+          iy = 2 * u + G.ry;
+          ix = 2 * v + G.rx;
+        } else {
+          const int hw = a.h * a.w;
+          b = mm / hw;
+          const int rem = mm - b * hw;
+          iy = rem / a.w;
+          ix = rem - iy * a.w;
+        }
         a_b[i] = b * a.ho;
         a_py[i] = iy + a.pt;
         a_px[i] = ix + a.pl;
       }
     }
-    const int k0 = kq * 4;
-    ks_tap = k0 / a.kc;
-    ks_ci = k0 - ks_tap * a.kc;
-    ks_r = ks_tap / a.kw;
-    ks_s = ks_tap - ks_r * a.kw;
+    const int k0 = k_begin + kq * 4;
+    ks_t = k0 / a.kc;
+    ks_ci = k0 - ks_t * a.kc;
+    ks_si = ks_t % G.ns;
+    ks_r = G.r0 + a.dt * (ks_t / G.ns);
+    ks_s = G.s0 + a.dt * ks_si;
   } else {
     constexpr int MQ = BM / 4;
     const int mq = tid % MQ;
     const int m = m0 + 4 * mq;
-    wm_ok = m < a.M;
+    wm_ok = m < M;
     const int mm = wm_ok ? m : 0;
     const int tap = mm / a.kc;
     wm_ci = mm - tap * a.kc;
@@ -164,7 +263,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
 
   auto load_a = [&]() {
     if constexpr (A_KCONTIG) {
-      const bool tap_ok = ks_tap < a.taps;
+      const bool tap_ok = ks_t < G.ntaps;
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -175,10 +274,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
           sx = a_px[i] + ks_s;
         } else {
           const int ty = a_py[i] - ks_r, tx = a_px[i] - ks_s;
-          if (a.stride == 1) {
+          if (a.phase) {                 // parity guaranteed by the group
+            sy = ty >> 1;
+            sx = tx >> 1;
+          } else if (a.stride == 1) {
             sy = ty;
             sx = tx;
-          } else {
+          } else {                       // generic stride: zero-masked taps
             ok = ok && ty >= 0 && tx >= 0 && (ty % a.stride) == 0 && (tx % a.stride) == 0;
             sy = ty / a.stride;
             sx = tx / a.stride;
@@ -212,11 +314,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
       ks_ci += BK;
       while (ks_ci >= a.kc) {
         ks_ci -= a.kc;
-        ++ks_tap;
-        if (++ks_s >= a.kw) {
-          ks_s = 0;
-          ++ks_r;
+        ++ks_t;
+        if (++ks_si >= G.ns) {
+          ks_si = 0;
+          ks_r += a.dt;
         }
+        ks_s = G.s0 + a.dt * ks_si;
       }
     } else {
 #pragma unroll
@@ -256,6 +359,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   };
 
   // ---------------- B loader --------------------------------------------------------------
+  const float* Bp = a.B + ((MODE == MODE_WGRAD) ? 0 : G.b_off * a.ldb);
   int b_k = k_begin;   // first k row of the current chunk
   auto load_b = [&]() {
     constexpr int NQ = BN / 4;
@@ -269,7 +373,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
         const int k = b_k + krow;
         bool ok = n < a.nb;
         if (MODE == MODE_WGRAD) ok = ok && k < k_end;
-        if (ok) v = *reinterpret_cast<const float4*>(a.B + (int64_t)k * a.ldb + n);
+        if (ok) v = *reinterpret_cast<const float4*>(Bp + (int64_t)k * a.ldb + n);
       }
       rb[i] = v;
     }
@@ -299,6 +403,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   const int wn0 = (wave % WAVES_N) * WN;
   const int lrow = lane & 31, lk = lane >> 5;
 
+  const bool do_colsum = (MODE == MODE_WGRAD) && a.colsum && tile_m == 0;
+  float colacc = 0.f;
+
   if (nchunks > 0) {
     load_a();
     load_b();
@@ -318,19 +425,32 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
     }
     const float* as = As[buf];
     const float* bs = Bs[buf];
+    if (do_colsum && tid < BN) {
+#pragma unroll
+      for (int k = 0; k < BK; ++k) colacc += bs[k * SB + tid];
+    }
+    // Operand fragments of k-step st+1 are read while the MFMAs of step st issue.
+    float av[2][TM], bv[2][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) av[0][i] = as[lk * SA + wm0 + 32 * i + lrow];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[0][j] = bs[lk * SB + wn0 + 32 * j + lrow];
 #pragma unroll
     for (int st = 0; st < BK / 2; ++st) {
-      const int kk = 2 * st + lk;
-      float av[TM], bv[TN];
+      const int cur = st & 1;
+      if (st + 1 < BK / 2) {
+        const int kk = 2 * (st + 1) + lk;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = as[kk * SA + wm0 + 32 * i + lrow];
+        for (int i = 0; i < TM; ++i) av[cur ^ 1][i] = as[kk * SA + wm0 + 32 * i + lrow];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = bs[kk * SB + wn0 + 32 * j + lrow];
+        for (int j = 0; j < TN; ++j) bv[cur ^ 1][j] = bs[kk * SB + wn0 + 32 * j + lrow];
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+          acc[i][j] =
+              __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][i], bv[cur][j], acc[i][j], 0, 0, 0);
     }
     if (more) {
       store_a(buf ^ 1);
@@ -340,42 +460,70 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   }
 
   // ---------------- epilogue ---------------------------------------------------------------
-  float* C = a.C;
-  if (MODE == MODE_WGRAD) C += (int64_t)blockIdx.z * a.split_stride;
+  if (MODE == MODE_WGRAD || a.splits > 1) {
+    // raw partial sums into this K slice's slab; rows of group g start at tiles_begin*BM
+    float* S = a.slab + (int64_t)split * a.split_stride;
+    const int row_base = (MODE == MODE_WGRAD) ? 0 : G.tiles_begin * BM;
+    if (do_colsum && tid < BN && n0 + tid < a.N) S[(int64_t)M * a.slab_ld + n0 + tid] = colacc;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn0 + 32 * j + lrow;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (m < M) S[(int64_t)(row_base + m) * a.slab_ld + n] = acc[i][j][r];
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn0 + 32 * j + lrow;
     if (n >= a.N) continue;
-    float bias = 0.f, scale = 1.f, shift = 0.f;
-    if (MODE == MODE_FWD) {
-      if (a.bias) bias = a.bias[n];
-      if (a.bn_g) {
-        scale = a.bn_g[n] * rsqrtf(a.bn_v[n] + a.bn_eps);
-        shift = a.bn_b[n] - a.bn_m[n] * scale;
-      }
-    }
+    float bias, scale, shift;
+    column_params<MODE>(a, n, bias, scale, shift);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (m >= a.M) continue;
-        float v = acc[i][j][r];
-        if (MODE == MODE_FWD) {
-          v += bias;
-          if (a.z) a.z[(int64_t)m * a.ldz + n] = v;
-          if (a.bn_g) v = v * scale + shift;
-          if (a.res) v += a.res[(int64_t)m * a.ldr + n];
-          v = act_fwd(v, a.act, a.alpha);
-        } else if (MODE == MODE_DGRAD) {
-          if (a.act_src) {
-            const float s = a.act_src[(int64_t)m * a.ld_act + n];
-            v *= s > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
-          }
-        }
-        C[(int64_t)m * a.ldc + n] = v;
+        if (m >= M) continue;
+        epilogue_store<MODE>(a, out_row(a, G, m), n, acc[i][j][r], bias, scale, shift);
       }
     }
+  }
+}
+
+// Split-K epilogue for fwd/dgrad: sum the K slices' slabs, then the fused epilogue.
+template <int MODE>
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a) {
+  const int64_t rows = (int64_t)(a.tiles_total / a.n_tiles) * a.bm;
+  const int64_t total = rows * a.N;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(idx % a.N);
+    const int64_t srow = idx / a.N;
+    const int tm = (int)(srow / a.bm);
+    int gi = 0;
+    for (int g = 1; g < a.ngroups; ++g)
+      if (tm >= a.grp[g].tiles_begin) gi = g;
+    const Group& G = a.grp[gi];
+    const int m = (int)(srow - (int64_t)G.tiles_begin * a.bm);
+    if (m >= G.M) continue;
+    const float* src = a.slab + srow * a.slab_ld + n;
+    float v0 = 0.f, v1 = 0.f;
+    int z = 0;
+    for (; z + 1 < a.splits; z += 2) {
+      v0 += src[(int64_t)z * a.split_stride];
+      v1 += src[(int64_t)(z + 1) * a.split_stride];
+    }
+    if (z < a.splits) v0 += src[(int64_t)z * a.split_stride];
+    float bias, scale, shift;
+    column_params<MODE>(a, n, bias, scale, shift);
+    epilogue_store<MODE>(a, out_row(a, G, m), n, v0 + v1, bias, scale, shift);
   }
 }
 
@@ -393,33 +541,77 @@ __global__ void pack_fwd_kernel(const float* __restrict__ w, int taps, int cin, 
   }
 }
 
-__global__ void pack_bwd_kernel(const float* __restrict__ w, int taps, int cin, int cout,
-                                int cout_p, int kd, int nd, float* __restrict__ out) {
-  const int64_t total = (int64_t)kd * nd;
+// Input-gradient weights: rows (group tap t, co) group after group, each group's block
+// padded to BK rows; columns ci.  Wd[row][ci] = W[r][s][ci][co].
+struct PackGroups {
+  int ngroups;
+  int dt;
+  int r0[MAX_GROUPS], s0[MAX_GROUPS], ns[MAX_GROUPS], ntaps[MAX_GROUPS];
+  int64_t row_begin[MAX_GROUPS + 1];
+};
+
+__global__ void pack_bwd_kernel(const float* __restrict__ w, PackGroups pg, int kw, int cin,
+                                int cout, int cout_p, int nd, float* __restrict__ out) {
+  const int64_t total = pg.row_begin[pg.ngroups] * nd;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int k = (int)(idx / nd), n = (int)(idx - (int64_t)k * nd);
-    const int tap = k / cout_p, co = k - tap * cout_p;
+    const int64_t row = idx / nd;
+    const int n = (int)(idx - row * nd);
+    int g = 0;
+    for (int q = 1; q < pg.ngroups; ++q)
+      if (row >= pg.row_begin[q]) g = q;
+    const int k = (int)(row - pg.row_begin[g]);
+    const int t = k / cout_p, co = k - t * cout_p;
     float v = 0.f;
-    if (tap < taps && co < cout && n < cin) v = w[((int64_t)tap * cin + n) * cout + co];
+    if (t < pg.ntaps[g] && co < cout && n < cin) {
+      const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
+      const int s = pg.s0[g] + pg.dt * (t % pg.ns[g]);
+      v = w[((int64_t)(r * kw + s) * cin + n) * cout + co];
+    }
     out[idx] = v;
   }
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
-                                    int64_t split_stride, int taps, int kc, int cin, int cout,
-                                    int ldc, float* __restrict__ dw, int accum) {
-  const int64_t total = (int64_t)taps * cin * cout;
+// dw[tap][ci][co] (HWIO) = sum_z slab[z][tap*kc + ci][co]; optional db[co] = sum_z slab[z][M][co].
+// One thread per (row, 4-column group); 4 slices in flight per iteration.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws,
+                                                           int splits, int64_t split_stride,
+                                                           int taps, int kc, int cin, int cout,
+                                                           int ldc, float* __restrict__ dw,
+                                                           float* __restrict__ db, int accum) {
+  const int cq = (cout + 3) / 4;
+  const int rows = taps * cin + (db ? 1 : 0);
+  const int64_t total = (int64_t)rows * cq;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int co = (int)(idx % cout);
-    const int64_t t2 = idx / cout;
-    const int ci = (int)(t2 % cin);
-    const int tap = (int)(t2 / cin);
-    const int64_t off = ((int64_t)tap * kc + ci) * ldc + co;
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += ws[z * split_stride + off];
-    dw[idx] = accum ? dw[idx] + s : s;
+    const int q = (int)(idx % cq);
+    const int row = (int)(idx / cq);
+    const bool is_bias = row == taps * cin;
+    int64_t m;
+    if (is_bias) {
+      m = (int64_t)taps * kc;
+    } else {
+      const int tap = row / cin, ci = row - tap * cin;
+      m = (int64_t)tap * kc + ci;
+    }
+    const float* src = ws + m * ldc + 4 * q;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+    int z = 0;
+    for (; z + 3 < splits; z += 4) {
+      add4(s0, *reinterpret_cast<const float4*>(src + (int64_t)z * split_stride));
+      add4(s1, *reinterpret_cast<const float4*>(src + (int64_t)(z + 1) * split_stride));
+      add4(s2, *reinterpret_cast<const float4*>(src + (int64_t)(z + 2) * split_stride));
+      add4(s3, *reinterpret_cast<const float4*>(src + (int64_t)(z + 3) * split_stride));
+    }
+    for (; z < splits; ++z)
+      add4(s0, *reinterpret_cast<const float4*>(src + (int64_t)z * split_stride));
+    add4(s0, s1);
+    add4(s2, s3);
+    add4(s0, s2);
+    const float v[4] = {s0.x, s0.y, s0.z, s0.w};
+    float* dst = is_bias ? db + 4 * q : dw + (int64_t)row * cout + 4 * q;
+    const int nv = min(4, cout - 4 * q);
+    for (int e = 0; e < nv; ++e) dst[e] = accum ? dst[e] + v[e] : v[e];
   }
 }
 
@@ -427,18 +619,44 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
 namespace {
 
 struct Geo {
-  int taps, cin_p, cout_p, kf, nf, kd, nd;
+  int taps, cin_p, cout_p, kf, nf, nd;
+  bool phase;            // dgrad as stride-2 phase groups
+  PackGroups pg;
+  int64_t kd;            // packed bwd rows
 };
 
 Geo geo(const of_conv_desc* d) {
-  Geo g;
+  Geo g{};
   g.taps = d->kh * d->kw;
   g.cin_p = d->cin_p;
   g.cout_p = (int)round_up(d->cout, 4);
   g.kf = (int)round_up((int64_t)g.taps * g.cin_p, BK);
   g.nf = g.cout_p;
-  g.kd = (int)round_up((int64_t)g.taps * g.cout_p, BK);
   g.nd = g.cin_p;
+  g.phase = d->stride == 2;
+  PackGroups& pg = g.pg;
+  pg.row_begin[0] = 0;
+  if (g.phase) {
+    pg.ngroups = 4;
+    pg.dt = 2;
+    for (int c = 0; c < 4; ++c) {
+      const int qy = c >> 1, qx = c & 1;
+      const int nr = std::max(0, (d->kh - qy + 1) / 2), ns = std::max(0, (d->kw - qx + 1) / 2);
+      pg.r0[c] = qy;
+      pg.s0[c] = qx;
+      pg.ns[c] = std::max(ns, 1);
+      pg.ntaps[c] = nr * ns;
+      pg.row_begin[c + 1] = pg.row_begin[c] + round_up((int64_t)pg.ntaps[c] * g.cout_p, BK);
+    }
+  } else {
+    pg.ngroups = 1;
+    pg.dt = 1;
+    pg.r0[0] = pg.s0[0] = 0;
+    pg.ns[0] = d->kw;
+    pg.ntaps[0] = g.taps;
+    pg.row_begin[1] = round_up((int64_t)g.taps * g.cout_p, BK);
+  }
+  g.kd = pg.row_begin[pg.ngroups];
   return g;
 }
 
@@ -451,23 +669,10 @@ int validate(const of_conv_desc* d) {
   return OF_OK;
 }
 
-template <int MODE>
-int launch_cfg(GemmArgs& a, hipStream_t s, int splits) {
-  // Tile choice by GEMM N (output channels of this pass).
-  const int N = a.N;
-  dim3 block(256);
-  auto go = [&](auto kern, int bm, int bn) {
-    a.m_tiles = (int)cdiv(a.M, bm);
-    a.n_tiles = (int)cdiv(N, bn);
-    dim3 grid(a.m_tiles * a.n_tiles, 1, splits);
-    hipLaunchKernelGGL(kern, grid, block, 0, s, a);
-    return check_launch("conv_gemm_f32");
-  };
-  if (N > 96) return go(conv_gemm_f32<128, 128, 2, 2, MODE>, 128, 128);
-  if (N > 64) return go(conv_gemm_f32<128, 96, 4, 1, MODE>, 128, 96);
-  if (N > 32) return go(conv_gemm_f32<128, 64, 2, 2, MODE>, 128, 64);
-  return go(conv_gemm_f32<128, 32, 4, 1, MODE>, 128, 32);
-}
+// Tile configuration by GEMM N: (BM, BN).  Narrow N gets taller M tiles so every wave still
+// owns >= 2 MFMA accumulators and the per-chunk staging cost is amortised.
+int pick_bn(int N) { return N > 96 ? 128 : N > 64 ? 96 : N > 32 ? 64 : 32; }
+int pick_bm(int N) { return N > 64 ? 128 : 256; }
 
 GemmArgs base_args(const of_conv_desc* d) {
   GemmArgs a{};
@@ -481,9 +686,153 @@ GemmArgs base_args(const of_conv_desc* d) {
   a.stride = d->stride;
   a.pt = d->pad_top;
   a.pl = d->pad_left;
-  a.taps = d->kh * d->kw;
-  a.alpha = 0.f;
+  a.dt = 1;
+  a.splits = 1;
   return a;
+}
+
+void single_group(GemmArgs& a, const of_conv_desc* d, int M, int K) {
+  a.ngroups = 1;
+  a.bm = pick_bm(a.N);
+  Group& g = a.grp[0];
+  g = Group{};
+  g.m_tiles = (int)cdiv(M, a.bm);
+  g.M = M;
+  g.ns = d->kw;
+  g.ntaps = d->kh * d->kw;
+  g.K = K;
+  a.n_tiles = (int)cdiv(a.N, pick_bn(a.N));
+  a.tiles_total = g.m_tiles * a.n_tiles;
+}
+
+// fwd/dgrad split-K: split when the tile grid cannot fill the chip.
+void plan_splits(GemmArgs& a, int kmax) {
+  a.splits = 1;
+  a.k_per_split = (int)round_up(kmax, BK);
+  if (a.tiles_total >= 2 * kCUs) return;
+  const int nchunks = (int)cdiv(kmax, BK);
+  int s = std::max(1, (4 * kCUs) / a.tiles_total);
+  s = std::min(s, std::max(1, nchunks / 12));
+  if (s <= 1) return;
+  a.k_per_split = (int)round_up(cdiv(kmax, s), BK);
+  a.splits = (int)cdiv(kmax, a.k_per_split);
+}
+
+int64_t slab_rows(const GemmArgs& a) { return (int64_t)(a.tiles_total / a.n_tiles) * a.bm; }
+
+size_t fd_workspace(const GemmArgs& a) {
+  if (a.splits <= 1) return 0;
+  return (size_t)a.splits * slab_rows(a) * round_up(a.N, 4) * sizeof(float);
+}
+
+// Attach the split-K slab; without (enough) workspace fall back to one K slice.
+void attach_slab(GemmArgs& a, void* ws, size_t ws_bytes) {
+  if (a.splits > 1 && ws && ws_bytes >= fd_workspace(a)) {
+    a.slab = static_cast<float*>(ws);
+    a.slab_ld = (int)round_up(a.N, 4);
+    a.split_stride = slab_rows(a) * a.slab_ld;
+    return;
+  }
+  int kmax = 0;
+  for (int g = 0; g < a.ngroups; ++g) kmax = std::max(kmax, a.grp[g].K);
+  a.splits = 1;
+  a.k_per_split = (int)round_up(kmax, BK);
+}
+
+GemmArgs fwd_args(const of_conv_desc* d, const Geo& g) {
+  GemmArgs a = base_args(d);
+  a.kc = g.cin_p;
+  a.N = d->cout;
+  a.M = d->n * d->ho * d->wo;
+  single_group(a, d, a.M, g.kf);
+  plan_splits(a, g.kf);
+  a.ldb = g.nf;
+  a.nb = g.nf;
+  return a;
+}
+
+GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g) {
+  GemmArgs a = base_args(d);
+  a.kc = g.cout_p;
+  a.N = g.cin_p;
+  a.ldb = g.nd;
+  a.nb = g.nd;
+  int kmax = 0;
+  if (g.phase) {
+    a.phase = 1;
+    a.dt = 2;
+    a.ngroups = 4;
+    a.bm = pick_bm(a.N);
+    a.n_tiles = (int)cdiv(a.N, pick_bn(a.N));
+    int tiles = 0;
+    for (int c = 0; c < 4; ++c) {
+      Group& G = a.grp[c];
+      G = Group{};
+      const int qy = c >> 1, qx = c & 1;
+      // input rows iy with (iy + pt) % 2 == qy  ->  iy = 2u + ry
+      G.ry = (((qy - d->pad_top) % 2) + 2) % 2;
+      G.rx = (((qx - d->pad_left) % 2) + 2) % 2;
+      G.hc = std::max(0, (d->h - G.ry + 1) / 2);
+      G.wc = std::max(0, (d->w - G.rx + 1) / 2);
+      G.M = d->n * G.hc * G.wc;
+      G.m_tiles = (int)cdiv(G.M, a.bm);
+      G.tiles_begin = tiles;
+      tiles += G.m_tiles;
+      G.r0 = g.pg.r0[c];
+      G.s0 = g.pg.s0[c];
+      G.ns = g.pg.ns[c];
+      G.ntaps = g.pg.ntaps[c];
+      G.K = (int)(g.pg.row_begin[c + 1] - g.pg.row_begin[c]);
+      G.b_off = g.pg.row_begin[c];
+      kmax = std::max(kmax, G.K);
+    }
+    a.tiles_total = tiles * a.n_tiles;
+    a.M = d->n * d->h * d->w;
+  } else {
+    a.M = d->n * d->h * d->w;
+    single_group(a, d, a.M, (int)g.kd);
+    kmax = (int)g.kd;
+  }
+  plan_splits(a, kmax);
+  return a;
+}
+
+template <int MODE>
+int launch_gemm(const GemmArgs& a, hipStream_t s) {
+  const int bn = pick_bn(a.N);
+  dim3 grid(a.tiles_total * a.splits), block(256);
+  if (bn == 128) hipLaunchKernelGGL((conv_gemm_f32<128, 128, 2, 2, MODE>), grid, block, 0, s, a);
+  else if (bn == 96) hipLaunchKernelGGL((conv_gemm_f32<128, 96, 4, 1, MODE>), grid, block, 0, s, a);
+  else if (bn == 64) hipLaunchKernelGGL((conv_gemm_f32<256, 64, 4, 1, MODE>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((conv_gemm_f32<256, 32, 4, 1, MODE>), grid, block, 0, s, a);
+  int st = check_launch("conv_gemm_f32");
+  if (st || MODE == MODE_WGRAD || a.splits == 1) return st;
+  const int64_t total = slab_rows(a) * a.N;
+  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
+  hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(blocks), dim3(256), 0, s, a);
+  return check_launch("conv_splitk_epilogue");
+}
+
+struct WgradPlan {
+  int splits, k_per_split, M, ldc;
+  int64_t split_stride;
+};
+
+WgradPlan wgrad_plan(const of_conv_desc* d) {
+  Geo g = geo(d);
+  WgradPlan p;
+  p.M = g.taps * g.cin_p;
+  p.ldc = g.cout_p;
+  const int K = d->n * d->ho * d->wo;
+  const int tiles = (int)(cdiv(p.M, pick_bm(d->cout)) * cdiv(d->cout, pick_bn(d->cout)));
+  // Fill up to 4 workgroups per CU without overshooting a multiple of the CU count (an
+  // overshoot leaves a few CUs with one extra long-running workgroup: a tail).
+  int splits = std::max(1, (4 * kCUs) / tiles);
+  splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * BK)));
+  p.k_per_split = (int)round_up(cdiv(K, splits), BK);
+  p.splits = (int)cdiv(K, p.k_per_split);
+  p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
+  return p;
 }
 
 }  // namespace
@@ -502,7 +851,7 @@ int64_t of_conv_wfwd_elems(const of_conv_desc* d) {
 int64_t of_conv_wbwd_elems(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return -1;
   Geo g = geo(d);
-  return (int64_t)g.kd * g.nd;
+  return g.kd * g.nd;
 }
 
 int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fwd,
@@ -520,20 +869,30 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
     if ((st = check_launch("pack_fwd"))) return st;
   }
   if (w_bwd) {
-    const int64_t total = (int64_t)g.kd * g.nd;
+    const int64_t total = g.kd * g.nd;
     const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
-    hipLaunchKernelGGL(pack_bwd_kernel, dim3(blocks), dim3(256), 0, s, w_hwio, g.taps, d->cin,
-                       d->cout, g.cout_p, g.kd, g.nd, w_bwd);
+    hipLaunchKernelGGL(pack_bwd_kernel, dim3(blocks), dim3(256), 0, s, w_hwio, g.pg, d->kw,
+                       d->cin, d->cout, g.cout_p, g.nd, w_bwd);
     if ((st = check_launch("pack_bwd"))) return st;
   }
   return OF_OK;
+}
+
+size_t of_conv2d_fwd_workspace(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return 0;
+  return fd_workspace(fwd_args(d, geo(d)));
+}
+
+size_t of_conv2d_dgrad_workspace(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return 0;
+  return fd_workspace(dgrad_args(d, geo(d)));
 }
 
 int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w_fwd,
                   const float* bias, const float* bn_gamma, const float* bn_beta,
                   const float* bn_mean, const float* bn_var, float bn_eps,
                   const float* residual, int ldr, int act, float alpha, float* z, int ldz,
-                  float* y, int ldy, void* stream) {
+                  float* y, int ldy, void* workspace, size_t ws_bytes, void* stream) {
   int st = validate(d);
   if (st) return st;
   OF_CHECK_ARG(x && w_fwd && y, "conv fwd: NULL pointer");
@@ -545,16 +904,11 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   OF_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_fwd & 15) == 0,
                "conv fwd: x / w must be 16-byte aligned");
   Geo g = geo(d);
-  GemmArgs a = base_args(d);
-  a.kc = g.cin_p;
-  a.M = d->n * d->ho * d->wo;
-  a.N = d->cout;
-  a.K = g.kf;
+  GemmArgs a = fwd_args(d, g);
+  attach_slab(a, workspace, ws_bytes);
   a.A = x;
   a.lda = ldx;
   a.B = w_fwd;
-  a.ldb = g.nf;
-  a.nb = g.nf;
   a.C = y;
   a.ldc = ldy;
   a.bias = bias;
@@ -570,16 +924,16 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   a.act = act;
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
-  const double flops = 2.0 * a.M * d->cout * (double)g.taps * d->cin;
+  const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   if (timing_on()) timing_begin(s);
-  st = launch_cfg<MODE_FWD>(a, s, 1);
+  st = launch_gemm<MODE_FWD>(a, s);
   if (timing_on()) timing_end(s, 0, flops);
   return st;
 }
 
 int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
                     const float* act_src, int ld_act, int act, float alpha, float* dx,
-                    int lddx, void* stream) {
+                    int lddx, void* workspace, size_t ws_bytes, void* stream) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
@@ -589,16 +943,11 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
   OF_CHECK_ARG(!act_src || ld_act >= d->cin_p, "conv dgrad: ld_act");
   OF_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)w_bwd & 15) == 0,
                "conv dgrad: dy / w must be 16-byte aligned");
-  GemmArgs a = base_args(d);
-  a.kc = g.cout_p;
-  a.M = d->n * d->h * d->w;
-  a.N = g.cin_p;
-  a.K = g.kd;
+  GemmArgs a = dgrad_args(d, g);
+  attach_slab(a, workspace, ws_bytes);
   a.A = dy;
   a.lda = lddy;
   a.B = w_bwd;
-  a.ldb = g.nd;
-  a.nb = g.nd;
   a.C = dx;
   a.ldc = lddx;
   a.act_src = act_src;
@@ -608,40 +957,15 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   if (timing_on()) timing_begin(s);
-  st = launch_cfg<MODE_DGRAD>(a, s, 1);
+  st = launch_gemm<MODE_DGRAD>(a, s);
   if (timing_on()) timing_end(s, 1, flops);
   return st;
 }
 
-namespace {
-struct WgradPlan {
-  int splits, k_per_split, M, ldc;
-  int64_t split_stride;
-};
-WgradPlan wgrad_plan(const of_conv_desc* d) {
-  Geo g = geo(d);
-  WgradPlan p;
-  p.M = g.taps * g.cin_p;
-  p.ldc = g.cout_p;
-  const int K = d->n * d->ho * d->wo;
-  const int bn = d->cout > 96 ? 128 : d->cout > 64 ? 96 : d->cout > 32 ? 64 : 32;
-  const int tiles = (int)(cdiv(p.M, 128) * cdiv(d->cout, bn));
-  // Aim for ~1024 workgroups; at least 4 chunks of K per split.
-  int splits = (int)std::max<int64_t>(1, cdiv(1024, tiles));
-  const int max_splits = (int)std::max<int64_t>(1, cdiv(K, 4 * BK));
-  splits = std::min(splits, max_splits);
-  p.k_per_split = (int)round_up(cdiv(K, splits), BK);
-  p.splits = (int)cdiv(K, p.k_per_split);
-  p.split_stride = (int64_t)p.M * p.ldc;
-  return p;
-}
-}  // namespace
-
 size_t of_conv2d_wgrad_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
   WgradPlan p = wgrad_plan(d);
-  const size_t slabs = (size_t)p.splits * p.split_stride * sizeof(float);
-  return std::max(slabs, of_colsum_workspace((int64_t)d->n * d->ho * d->wo, d->cout));
+  return (size_t)p.splits * p.split_stride * sizeof(float);
 }
 
 int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float* dy, int lddy,
@@ -653,41 +977,37 @@ int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float*
   OF_CHECK_ARG(x && dy && dw && workspace, "conv wgrad: NULL pointer");
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv wgrad: lddy");
-  WgradPlan p = wgrad_plan(d);
   OF_CHECK_ARG(ws_bytes >= of_conv2d_wgrad_workspace(d), "conv wgrad: workspace too small");
+  WgradPlan p = wgrad_plan(d);
   GemmArgs a = base_args(d);
   a.kc = g.cin_p;
-  a.M = p.M;
   a.N = d->cout;
   a.K = d->n * d->ho * d->wo;
+  single_group(a, d, p.M, a.K);
+  a.M = p.M;
   a.A = x;
   a.lda = ldx;
   a.B = dy;
   a.ldb = lddy;
   a.nb = g.cout_p;
-  a.C = static_cast<float*>(workspace);
-  a.ldc = p.ldc;
+  a.slab = static_cast<float*>(workspace);
+  a.slab_ld = p.ldc;
+  a.splits = p.splits;
   a.k_per_split = p.k_per_split;
   a.split_stride = p.split_stride;
+  a.colsum = db != nullptr;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
   if (timing_on()) timing_begin(s);
-  st = launch_cfg<MODE_WGRAD>(a, s, p.splits);
+  st = launch_gemm<MODE_WGRAD>(a, s);
   if (timing_on()) timing_end(s, 2, flops);
   if (st) return st;
-  {
-    const int64_t total = (int64_t)g.taps * d->cin * d->cout;
-    const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s,
-                       static_cast<const float*>(workspace), p.splits, p.split_stride, g.taps,
-                       g.cin_p, d->cin, d->cout, p.ldc, dw, accumulate);
-    if ((st = check_launch("wgrad_reduce"))) return st;
-  }
-  if (db) {
-    // bias gradient = column sums of dy; reuse the (now consumed) slab workspace.
-    st = of_colsum(dy, a.K, d->cout, lddy, db, accumulate, workspace, stream);
-  }
-  return st;
+  const int64_t total = ((int64_t)g.taps * d->cin + 1) * cdiv(d->cout, 4);
+  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s,
+                     static_cast<const float*>(workspace), p.splits, p.split_stride, g.taps,
+                     g.cin_p, d->cin, d->cout, p.ldc, dw, db, accumulate);
+  return check_launch("wgrad_reduce");
 }
 
 }  // extern "C"

@@ -16,7 +16,8 @@ template <int D>
 __global__ __launch_bounds__(256) void corr_fwd_kernel(const float* __restrict__ f1, int ld1,
                                                        const float* __restrict__ f2, int ld2,
                                                        int h, int w, int c,
-                                                       float* __restrict__ out, int ldo) {
+                                                       float* __restrict__ out, int ldo,
+                                                       int vec) {
   constexpr int ND = 2 * D + 1, NK = ND * ND;
   constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D;
   __shared__ float tile[HY * HX * CPS];
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(256) void corr_fwd_kernel(const float* __restrict__
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if ((unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w && 4 * cq < cc) {
         const float* src = f2 + (img + (int64_t)sy * w + sx) * ld2 + c0 + 4 * cq;
-        if (4 * cq + 4 <= cc) {
+        if (vec && 4 * cq + 4 <= cc) {
           v = *reinterpret_cast<const float4*>(src);
         } else {
           float t[4] = {0.f, 0.f, 0.f, 0.f};
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(256) void corr_bwd_kernel(const float* __restrict__
                                                        const float* __restrict__ src, int lds,
                                                        int h, int w, int c,
                                                        float* __restrict__ df, int lddf,
-                                                       int accumulate) {
+                                                       int accumulate, int vec) {
   constexpr int ND = 2 * D + 1, NK = ND * ND;
   constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D;
   __shared__ float tile[HY * HX * CPS];
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(256) void corr_bwd_kernel(const float* __restrict__
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if ((unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w && 4 * cq < cc) {
         const float* s = src + (img + (int64_t)sy * w + sx) * lds + c0 + 4 * cq;
-        if (4 * cq + 4 <= cc) {
+        if (vec && 4 * cq + 4 <= cc) {
           v = *reinterpret_cast<const float4*>(s);
         } else {
           float t[4] = {0.f, 0.f, 0.f, 0.f};
@@ -256,70 +257,50 @@ __global__ __launch_bounds__(256) void warp_fwd_scalar(const float* __restrict__
   }
 }
 
-// Backward.  Q lanes share a pixel (Q = c/4 in {1..64}, power of two); dflow reduced over the
-// pixel's lanes with xor-shuffles; dinp scattered with fp32 atomics (GatherNd's adjoint).
-template <int Q>
-__global__ __launch_bounds__(256) void warp_bwd_vec(const float* __restrict__ dout,
-                                                    const float* __restrict__ inp, int n,
-                                                    int h, int w, int c,
-                                                    const float* __restrict__ flow,
-                                                    float* __restrict__ dinp,
-                                                    float* __restrict__ dflow, int absolute) {
+// Backward, one wave per pixel, lanes over channels: the four corner scatters of a wave are
+// 64 consecutive floats each (256 contiguous bytes per atomic wave-instruction: the shape
+// that runs at the chip-wide atomic rate), loads are coalesced rows, and d(flow) is a
+// 64-lane xor-shuffle reduction.  dinp scatter with fp32 atomics (GatherNd's adjoint).
+__global__ __launch_bounds__(256) void warp_bwd_wave(const float* __restrict__ dout,
+                                                     const float* __restrict__ inp, int n,
+                                                     int h, int w, int c,
+                                                     const float* __restrict__ flow,
+                                                     float* __restrict__ dinp,
+                                                     float* __restrict__ dflow, int absolute) {
   const int64_t npix = (int64_t)n * h * w;
-  const int64_t total = npix * Q;
-  // grid-stride in whole waves so shuffle groups stay intact
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < total;
-       base += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t idx = base + threadIdx.x;
-    const bool live = idx < total;
-    const int64_t p = live ? idx / Q : 0;
-    const int q = (int)(idx % Q);
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t p = wave0; p < npix; p += nwaves) {
     const int j = (int)(p % w);
     const int64_t t2 = p / w;
     const int i = (int)(t2 % h);
     const int64_t img = (t2 / h) * h * w;
     const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
     const WarpTap t = warp_tap(i, j, f.x, f.y, h, w, img, absolute);
+    const float a = t.a, b = t.b;
+    const float w00 = a * b, w01 = a * (1.f - b), w10 = (1.f - a) * b,
+                w11 = (1.f - a) * (1.f - b);
     float gx = 0.f, gy = 0.f;
-    if (live) {
-      const float4 g = *reinterpret_cast<const float4*>(dout + p * c + 4 * q);
-      const float4 v00 = *reinterpret_cast<const float4*>(inp + t.o00 * c + 4 * q);
-      const float4 v01 = *reinterpret_cast<const float4*>(inp + t.o01 * c + 4 * q);
-      const float4 v10 = *reinterpret_cast<const float4*>(inp + t.o10 * c + 4 * q);
-      const float4 v11 = *reinterpret_cast<const float4*>(inp + t.o11 * c + 4 * q);
-      const float a = t.a, b = t.b;
-      // d out/dx = -(b (v00 - v10) + (1-b)(v01 - v11)); d out/dy = -(a (v00 - v01) + (1-a)(v10 - v11))
-      auto acc = [&](float gg, float p00, float p01, float p10, float p11) {
-        gx -= gg * (b * (p00 - p10) + (1.f - b) * (p01 - p11));
-        gy -= gg * (a * (p00 - p01) + (1.f - a) * (p10 - p11));
-      };
-      acc(g.x, v00.x, v01.x, v10.x, v11.x);
-      acc(g.y, v00.y, v01.y, v10.y, v11.y);
-      acc(g.z, v00.z, v01.z, v10.z, v11.z);
-      acc(g.w, v00.w, v01.w, v10.w, v11.w);
+    for (int e = lane; e < c; e += 64) {
+      const float g = dout[p * c + e];
+      const float p00 = inp[t.o00 * c + e], p01 = inp[t.o01 * c + e];
+      const float p10 = inp[t.o10 * c + e], p11 = inp[t.o11 * c + e];
+      gx -= g * (b * (p00 - p10) + (1.f - b) * (p01 - p11));
+      gy -= g * (a * (p00 - p01) + (1.f - a) * (p10 - p11));
       if (dinp) {
-        const float w00 = a * b, w01 = a * (1.f - b), w10 = (1.f - a) * b,
-                    w11 = (1.f - a) * (1.f - b);
-        float* d00 = dinp + t.o00 * c + 4 * q;
-        float* d01 = dinp + t.o01 * c + 4 * q;
-        float* d10 = dinp + t.o10 * c + 4 * q;
-        float* d11 = dinp + t.o11 * c + 4 * q;
-        atomicAdd(d00 + 0, w00 * g.x); atomicAdd(d00 + 1, w00 * g.y);
-        atomicAdd(d00 + 2, w00 * g.z); atomicAdd(d00 + 3, w00 * g.w);
-        atomicAdd(d01 + 0, w01 * g.x); atomicAdd(d01 + 1, w01 * g.y);
-        atomicAdd(d01 + 2, w01 * g.z); atomicAdd(d01 + 3, w01 * g.w);
-        atomicAdd(d10 + 0, w10 * g.x); atomicAdd(d10 + 1, w10 * g.y);
-        atomicAdd(d10 + 2, w10 * g.z); atomicAdd(d10 + 3, w10 * g.w);
-        atomicAdd(d11 + 0, w11 * g.x); atomicAdd(d11 + 1, w11 * g.y);
-        atomicAdd(d11 + 2, w11 * g.z); atomicAdd(d11 + 3, w11 * g.w);
+        atomicAdd(dinp + t.o00 * c + e, w00 * g);
+        atomicAdd(dinp + t.o01 * c + e, w01 * g);
+        atomicAdd(dinp + t.o10 * c + e, w10 * g);
+        atomicAdd(dinp + t.o11 * c + e, w11 * g);
       }
     }
 #pragma unroll
-    for (int o = Q / 2; o > 0; o >>= 1) {
+    for (int o = 32; o > 0; o >>= 1) {
       gx += __shfl_xor(gx, o, 64);
       gy += __shfl_xor(gy, o, 64);
     }
-    if (live && q == 0) *reinterpret_cast<float2*>(dflow + 2 * p) = make_float2(gx, gy);
+    if (lane == 0) *reinterpret_cast<float2*>(dflow + 2 * p) = make_float2(gx, gy);
   }
 }
 
@@ -607,11 +588,11 @@ int of_corr_fwd(const float* f1, int ld1, const float* f2, int ld2, int n, int h
   OF_CHECK_ARG(f1 && f2 && out, "corr fwd: NULL pointer");
   OF_CHECK_ARG(max_disp == 3, "corr: only max_disp=3 (the reference default) is compiled");
   OF_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0, "corr fwd: dims");
-  OF_CHECK_ARG(ld1 >= c && ld2 >= c && ld2 % 4 == 0 && ldo >= 49, "corr fwd: strides");
-  OF_CHECK_ARG(((uintptr_t)f2 & 15) == 0, "corr fwd: f2 must be 16-byte aligned");
+  OF_CHECK_ARG(ld1 >= c && ld2 >= c && ldo >= 49, "corr fwd: strides");
+  const int vec = (ld2 % 4 == 0 && ((uintptr_t)f2 & 15) == 0) ? 1 : 0;
   dim3 grid(cdiv(w, CT_X), cdiv(h, CT_Y), n);
   hipLaunchKernelGGL(corr_fwd_kernel<3>, grid, dim3(256), 0, as_stream(stream), f1, ld1, f2, ld2,
-                     h, w, c, out, ldo);
+                     h, w, c, out, ldo, vec);
   return check_launch("corr_fwd");
 }
 
@@ -620,20 +601,20 @@ int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const flo
                 float* df2, int lddf2, int acc2, void* stream) {
   OF_CHECK_ARG(dcv && f1 && f2, "corr bwd: NULL pointer");
   OF_CHECK_ARG(max_disp == 3, "corr: only max_disp=3 (the reference default) is compiled");
-  OF_CHECK_ARG(ld1 % 4 == 0 && ld2 % 4 == 0, "corr bwd: ld1/ld2 must be multiples of 4");
-  OF_CHECK_ARG(((uintptr_t)f1 & 15) == 0 && ((uintptr_t)f2 & 15) == 0,
-               "corr bwd: f1/f2 must be 16-byte aligned");
+  OF_CHECK_ARG(ld1 >= c && ld2 >= c, "corr bwd: strides");
+  const int vec1 = (ld1 % 4 == 0 && ((uintptr_t)f1 & 15) == 0) ? 1 : 0;
+  const int vec2 = (ld2 % 4 == 0 && ((uintptr_t)f2 & 15) == 0) ? 1 : 0;
   dim3 grid(cdiv(w, CT_X), cdiv(h, CT_Y), n);
   hipStream_t s = as_stream(stream);
   int st;
   if (df1) {
     hipLaunchKernelGGL((corr_bwd_kernel<3, 1>), grid, dim3(256), 0, s, dcv, lddcv, f2, ld2, h, w,
-                       c, df1, lddf1, acc1);
+                       c, df1, lddf1, acc1, vec2);
     if ((st = check_launch("corr_bwd_f1"))) return st;
   }
   if (df2) {
     hipLaunchKernelGGL((corr_bwd_kernel<3, -1>), grid, dim3(256), 0, s, dcv, lddcv, f1, ld1, h,
-                       w, c, df2, lddf2, acc2);
+                       w, c, df2, lddf2, acc2, vec1);
     if ((st = check_launch("corr_bwd_f2"))) return st;
   }
   return OF_OK;
@@ -671,22 +652,10 @@ static int warp_bwd_impl(const float* dout, const float* inp, int n, int h, int 
   OF_CHECK_ARG(dout && inp && flow && dflow, "warp bwd: NULL pointer");
   hipStream_t s = as_stream(stream);
   const int64_t npix = (int64_t)n * h * w;
-  const int q = c / 4;
-  const bool vec = c % 4 == 0 && (q == 1 || q == 2 || q == 4 || q == 8 || q == 16 || q == 32 ||
-                                  q == 64) &&
-                   ((uintptr_t)inp & 15) == 0 && ((uintptr_t)dout & 15) == 0 &&
-                   (!dinp || ((uintptr_t)dinp & 15) == 0);
-  if (vec) {
-    const int g = grid_for(npix * q);
-#define OF_WB(QQ)                                                                         \
-  case QQ:                                                                                \
-    hipLaunchKernelGGL(warp_bwd_vec<QQ>, dim3(g), dim3(256), 0, s, dout, inp, n, h, w, c, \
-                       flow, dinp, dflow, absolute);                                      \
-    break;
-    switch (q) {
-      OF_WB(1) OF_WB(2) OF_WB(4) OF_WB(8) OF_WB(16) OF_WB(32) OF_WB(64)
-    }
-#undef OF_WB
+  if (c >= 16) {
+    const int g = grid_for(npix * 64, 256, 16384);
+    hipLaunchKernelGGL(warp_bwd_wave, dim3(g), dim3(256), 0, s, dout, inp, n, h, w, c, flow,
+                       dinp, dflow, absolute);
   } else {
     hipLaunchKernelGGL(warp_bwd_scalar, dim3(grid_for(npix)), dim3(256), 0, s, dout, inp, n, h,
                        w, c, flow, dinp, dflow, absolute);

@@ -4,93 +4,211 @@
 namespace oflow {
 
 // ------------------------------------------------------------------ column reductions --
-// Block = 64 channels x 4 pixel rows; each block owns a contiguous pixel range and writes one
-// partial row; a finalize pass sums partial rows in a fixed order (bitwise reproducible).
-constexpr int CS_PIX_PER_BLOCK = 1024;
+// Per-channel sums over pixels of NHWC data.  Pass 1: RED_BLOCKS-ish workgroups, each owns a
+// contiguous pixel range; threads = (channel quad q) x (pixel row r), float4 loads (16 B/lane,
+// a wave reads whole contiguous pixel rows), 4 pixels in flight per thread; the workgroup
+// writes one partial row.  Pass 2: every channel's partial rows summed in a fixed order by a
+// 64-channel x 4-row workgroup -> bitwise reproducible, no atomics.
+constexpr int RED_TARGET_BLOCKS = 512;
 
-inline int colsum_blocks(int64_t npix) { return (int)cdiv(npix, CS_PIX_PER_BLOCK); }
+struct RedGeo {
+  int qw;       // channel quads per row (<= 64)
+  int rows;     // pixel rows per workgroup (256 / qw)
+  int nblk;     // workgroups along pixels
+  int64_t ppb;  // pixels per workgroup (multiple of rows)
+};
+
+inline RedGeo red_geo(int64_t npix, int c) {
+  RedGeo g;
+  const int cq = (c + 3) / 4;
+  g.qw = 1;
+  while (g.qw < cq && g.qw < 64) g.qw <<= 1;
+  g.rows = 256 / g.qw;
+  const int64_t min_ppb = (int64_t)g.rows * 8;
+  int64_t nb = std::min<int64_t>(RED_TARGET_BLOCKS, cdiv(npix, min_ppb));
+  nb = std::max<int64_t>(nb, 1);
+  g.ppb = round_up(cdiv(npix, nb), g.rows);
+  g.nblk = (int)cdiv(npix, g.ppb);
+  return g;
+}
+
+__device__ __forceinline__ float4 ld4(const float* p, int valid) {
+  // valid = number of the 4 channels that exist (1..4)
+  if (valid >= 4) return *reinterpret_cast<const float4*>(p);
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int e = 0; e < valid; ++e) t[e] = p[e];
+  return make_float4(t[0], t[1], t[2], t[3]);
+}
+
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
+// Sum the `rows` per-row float4 accumulators of a workgroup through LDS; row 0 threads get
+// the total.
+__device__ __forceinline__ float4 rows_reduce(float4 v, int q, int r, int qw, int rows,
+                                             float4* red) {
+  red[r * qw + q] = v;
+  __syncthreads();
+  for (int s = rows / 2; s > 0; s >>= 1) {
+    if (r < s) {
+      float4 o = red[(r + s) * qw + q];
+      add4(v, o);
+      red[r * qw + q] = v;
+    }
+    __syncthreads();
+  }
+  return v;
+}
 
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x,
                                                              int64_t npix, int c, int ld,
-                                                             float* __restrict__ part) {
-  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
-  const int ch = blockIdx.y * 64 + cl;
-  const int64_t p0 = (int64_t)blockIdx.x * CS_PIX_PER_BLOCK;
-  const int64_t p1 = min(npix, p0 + CS_PIX_PER_BLOCK);
-  float s = 0.f;
-  if (ch < c)
-    for (int64_t p = p0 + pr; p < p1; p += 4) s += x[p * ld + ch];
-  __shared__ float red[4][64];
-  red[pr][cl] = s;
+                                                             int qw, int rows, int64_t ppb,
+                                                             int vec, float* __restrict__ part) {
+  __shared__ float4 red[256];
+  const int q = threadIdx.x % qw, r = threadIdx.x / qw;
+  const int ch = (blockIdx.y * qw + q) * 4;
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int64_t p1 = min(npix, p0 + ppb);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int valid = min(4, c - ch);
+  if (valid > 0) {
+    int64_t p = p0 + r;
+    for (; p + 3 * rows < p1; p += 4 * rows) {
+      float4 a = vec ? ld4(x + p * ld + ch, 4) : ld4(x + p * ld + ch, valid);
+      float4 b = vec ? ld4(x + (p + rows) * ld + ch, 4) : ld4(x + (p + rows) * ld + ch, valid);
+      float4 cc = vec ? ld4(x + (p + 2 * rows) * ld + ch, 4)
+                      : ld4(x + (p + 2 * rows) * ld + ch, valid);
+      float4 d = vec ? ld4(x + (p + 3 * rows) * ld + ch, 4)
+                     : ld4(x + (p + 3 * rows) * ld + ch, valid);
+      add4(a, b);
+      add4(cc, d);
+      add4(a, cc);
+      add4(acc, a);
+    }
+    for (; p < p1; p += rows) add4(acc, vec ? ld4(x + p * ld + ch, 4) : ld4(x + p * ld + ch, valid));
+  }
+  acc = rows_reduce(acc, q, r, qw, rows, red);
+  if (r == 0 && valid > 0) {
+    float* o = part + (int64_t)blockIdx.x * c + ch;
+    const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+    for (int e = 0; e < valid; ++e) o[e] = v[e];
+  }
+}
+
+// Sum `nparts` partial rows of `stride` floats (first c channels) in fixed order.
+// grid.x = cdiv(c, 16); 256 threads = 16 channels x 16 row groups (many loads in flight).
+__global__ __launch_bounds__(256) void rows_final_kernel(const float* __restrict__ part,
+                                                         int nparts, int64_t stride, int c,
+                                                         float* __restrict__ out, int accum) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int ch = blockIdx.x * 16 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (ch < c) {
+    int b = g;
+    for (; b + 16 < nparts; b += 32) {
+      s0 += part[(int64_t)b * stride + ch];
+      s1 += part[(int64_t)(b + 16) * stride + ch];
+    }
+    for (; b < nparts; b += 16) s0 += part[(int64_t)b * stride + ch];
+  }
+  red[g][cl] = s0 + s1;
   __syncthreads();
-  if (pr == 0 && ch < c)
-    part[(int64_t)blockIdx.x * c + ch] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+  if (g == 0 && ch < c) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    out[ch] = accum ? out[ch] + t : t;
+  }
 }
 
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part,
-                                                           int nblk, int c,
-                                                           float* __restrict__ out, int accum) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * c + ch];
-  out[ch] = accum ? out[ch] + s : s;
-}
-
-// BN(inference)+residual+act backward: dt = dy*act'(y); dz = dt*g*invstd; dres = dt.
-__global__ __launch_bounds__(256) void bn_relu_bwd_partial(
+// BN(inference)+residual+act backward, fused with its channel reductions:
+// dt = dy*act'(y); dz = dt*gamma*invstd; dres = dt; partial sums of dt and dt*(z-mean)*invstd.
+// Dense [npix][c] tensors, c % 4 == 0.
+__global__ __launch_bounds__(256) void bn_act_bwd_partial(
     int64_t npix, int c, int act, const float* __restrict__ dy, const float* __restrict__ y,
     const float* __restrict__ z, const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ var, float eps, float* __restrict__ dz, float* __restrict__ dres,
-    float* __restrict__ part) {
-  const int cl = threadIdx.x & 63, pr = threadIdx.x >> 6;
-  const int ch = blockIdx.y * 64 + cl;
-  const int64_t p0 = (int64_t)blockIdx.x * CS_PIX_PER_BLOCK;
-  const int64_t p1 = min(npix, p0 + CS_PIX_PER_BLOCK);
-  float sb = 0.f, sg = 0.f;
-  if (ch < c) {
-    const float invstd = rsqrtf(var[ch] + eps);
-    const float sc = gamma[ch] * invstd;
-    const float mu = mean[ch];
-    for (int64_t p = p0 + pr; p < p1; p += 4) {
+    int qw, int rows, int64_t ppb, float* __restrict__ part) {
+  __shared__ float4 red[256];
+  const int q = threadIdx.x % qw, r = threadIdx.x / qw;
+  const int ch = (blockIdx.y * qw + q) * 4;
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int64_t p1 = min(npix, p0 + ppb);
+  float4 sb = make_float4(0.f, 0.f, 0.f, 0.f), sg = sb;
+  const bool live = ch < c;
+  if (live) {
+    const float4 gm = *reinterpret_cast<const float4*>(gamma + ch);
+    const float4 mu = *reinterpret_cast<const float4*>(mean + ch);
+    const float4 vr = *reinterpret_cast<const float4*>(var + ch);
+    const float4 is = make_float4(rsqrtf(vr.x + eps), rsqrtf(vr.y + eps), rsqrtf(vr.z + eps),
+                                  rsqrtf(vr.w + eps));
+    const float4 sc = make_float4(gm.x * is.x, gm.y * is.y, gm.z * is.z, gm.w * is.w);
+    const bool relu = act == OF_ACT_RELU;
+#pragma unroll 2
+    for (int64_t p = p0 + r; p < p1; p += rows) {
       const int64_t o = p * c + ch;
-      const float dt = (act == OF_ACT_NONE || y[o] > 0.f) ? dy[o] : 0.f;
-      dz[o] = dt * sc;
-      if (dres) dres[o] = dt;
-      sb += dt;
-      sg += dt * (z[o] - mu) * invstd;
+      const float4 g = *reinterpret_cast<const float4*>(dy + o);
+      const float4 yy = *reinterpret_cast<const float4*>(y + o);
+      const float4 zz = *reinterpret_cast<const float4*>(z + o);
+      float4 t;
+      t.x = (!relu || yy.x > 0.f) ? g.x : 0.f;
+      t.y = (!relu || yy.y > 0.f) ? g.y : 0.f;
+      t.z = (!relu || yy.z > 0.f) ? g.z : 0.f;
+      t.w = (!relu || yy.w > 0.f) ? g.w : 0.f;
+      *reinterpret_cast<float4*>(dz + o) =
+          make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
+      if (dres) *reinterpret_cast<float4*>(dres + o) = t;
+      add4(sb, t);
+      sg.x += t.x * (zz.x - mu.x) * is.x;
+      sg.y += t.y * (zz.y - mu.y) * is.y;
+      sg.z += t.z * (zz.z - mu.z) * is.z;
+      sg.w += t.w * (zz.w - mu.w) * is.w;
     }
   }
-  __shared__ float red[2][4][64];
-  red[0][pr][cl] = sb;
-  red[1][pr][cl] = sg;
+  sb = rows_reduce(sb, q, r, qw, rows, red);
   __syncthreads();
-  if (pr == 0 && ch < c) {
-    part[((int64_t)blockIdx.x * 2 + 0) * c + ch] =
-        red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-    part[((int64_t)blockIdx.x * 2 + 1) * c + ch] =
-        red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  sg = rows_reduce(sg, q, r, qw, rows, red);
+  if (r == 0 && live) {
+    *reinterpret_cast<float4*>(part + ((int64_t)blockIdx.x * 2 + 0) * c + ch) = sb;
+    *reinterpret_cast<float4*>(part + ((int64_t)blockIdx.x * 2 + 1) * c + ch) = sg;
   }
 }
 
-__global__ __launch_bounds__(256) void bn_relu_bwd_final(const float* __restrict__ part,
-                                                         int nblk, int c,
-                                                         const float* __restrict__ gamma,
-                                                         const float* __restrict__ var,
-                                                         float eps, float* __restrict__ dgamma,
-                                                         float* __restrict__ dbeta,
-                                                         float* __restrict__ dbias, int accum) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
+__global__ __launch_bounds__(256) void bn_act_bwd_final(const float* __restrict__ part,
+                                                        int nblk, int c,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ var,
+                                                        float eps, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta,
+                                                        float* __restrict__ dbias, int accum) {
+  __shared__ float red[2][16][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int ch = blockIdx.x * 16 + cl;
   float sb = 0.f, sg = 0.f;
-  for (int b = 0; b < nblk; ++b) {
-    sb += part[((int64_t)b * 2 + 0) * c + ch];
-    sg += part[((int64_t)b * 2 + 1) * c + ch];
+  if (ch < c) {
+    for (int b = g; b < nblk; b += 16) {
+      sb += part[((int64_t)b * 2 + 0) * c + ch];
+      sg += part[((int64_t)b * 2 + 1) * c + ch];
+    }
   }
-  const float db = sb * gamma[ch] * rsqrtf(var[ch] + eps);
-  if (dbeta) dbeta[ch] = accum ? dbeta[ch] + sb : sb;
-  if (dgamma) dgamma[ch] = accum ? dgamma[ch] + sg : sg;
-  if (dbias) dbias[ch] = accum ? dbias[ch] + db : db;
+  red[0][g][cl] = sb;
+  red[1][g][cl] = sg;
+  __syncthreads();
+  if (g == 0 && ch < c) {
+    sb = 0.f;
+    sg = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      sb += red[0][k][cl];
+      sg += red[1][k][cl];
+    }
+    const float db = sb * gamma[ch] * rsqrtf(var[ch] + eps);
+    if (dbeta) dbeta[ch] = accum ? dbeta[ch] + sb : sb;
+    if (dgamma) dgamma[ch] = accum ? dgamma[ch] + sg : sg;
+    if (dbias) dbias[ch] = accum ? dbias[ch] + db : db;
+  }
 }
 
 // ------------------------------------------------------------------------- max pool ----
@@ -249,26 +367,27 @@ using namespace oflow;
 extern "C" {
 
 size_t of_colsum_workspace(int64_t npix, int c) {
-  return (size_t)colsum_blocks(npix) * c * sizeof(float);
+  return (size_t)red_geo(npix, c).nblk * c * sizeof(float);
 }
 
 int of_colsum(const float* x, int64_t npix, int c, int ld, float* out, int accumulate,
               void* workspace, void* stream) {
-  OF_CHECK_ARG(x && out && workspace && ld >= c && c > 0, "colsum: args");
+  OF_CHECK_ARG(x && out && workspace && ld >= c && c > 0 && npix > 0, "colsum: args");
   hipStream_t s = as_stream(stream);
-  const int nblk = colsum_blocks(npix);
+  const RedGeo g = red_geo(npix, c);
+  const int vec = (c % 4 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15) == 0) ? 1 : 0;
   float* part = static_cast<float*>(workspace);
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(nblk, cdiv(c, 64)), dim3(256), 0, s, x, npix,
-                     c, ld, part);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(g.nblk, cdiv(cdiv(c, 4), g.qw)), dim3(256), 0,
+                     s, x, npix, c, ld, g.qw, g.rows, g.ppb, vec, part);
   int st = check_launch("colsum_partial");
   if (st) return st;
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(c, 256)), dim3(256), 0, s, part, nblk, c,
-                     out, accumulate);
+  hipLaunchKernelGGL(rows_final_kernel, dim3(cdiv(c, 16)), dim3(256), 0, s, part, g.nblk,
+                     (int64_t)c, c, out, accumulate);
   return check_launch("colsum_final");
 }
 
 size_t of_bn_act_bwd_workspace(int64_t npix, int c) {
-  return (size_t)colsum_blocks(npix) * 2 * c * sizeof(float);
+  return (size_t)red_geo(npix, c).nblk * 2 * c * sizeof(float);
 }
 
 int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
@@ -277,16 +396,21 @@ int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
                   int accumulate, void* workspace, void* stream) {
   OF_CHECK_ARG(dy && y && z && gamma && mean && var && dz && workspace, "bn_act_bwd: args");
   OF_CHECK_ARG(act == OF_ACT_NONE || act == OF_ACT_RELU, "bn_act_bwd: act must be none/relu");
+  OF_CHECK_ARG(c % 4 == 0 && npix > 0, "bn_act_bwd: c must be a multiple of 4");
+  OF_CHECK_ARG((((uintptr_t)dy | (uintptr_t)y | (uintptr_t)z | (uintptr_t)dz |
+                 (uintptr_t)dres | (uintptr_t)gamma | (uintptr_t)mean | (uintptr_t)var) & 15) == 0,
+               "bn_act_bwd: 16-byte alignment");
   hipStream_t s = as_stream(stream);
-  const int nblk = colsum_blocks(npix);
+  const RedGeo g = red_geo(npix, c);
   float* part = static_cast<float*>(workspace);
-  hipLaunchKernelGGL(bn_relu_bwd_partial, dim3(nblk, cdiv(c, 64)), dim3(256), 0, s, npix, c, act,
-                     dy, y, z, gamma, mean, var, eps, dz, dres, part);
-  int st = check_launch("bn_relu_bwd_partial");
+  hipLaunchKernelGGL(bn_act_bwd_partial, dim3(g.nblk, cdiv(c / 4, g.qw)), dim3(256), 0, s, npix,
+                     c, act, dy, y, z, gamma, mean, var, eps, dz, dres, g.qw, g.rows, g.ppb,
+                     part);
+  int st = check_launch("bn_act_bwd_partial");
   if (st) return st;
-  hipLaunchKernelGGL(bn_relu_bwd_final, dim3(cdiv(c, 256)), dim3(256), 0, s, part, nblk, c,
+  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c, 16)), dim3(256), 0, s, part, g.nblk, c,
                      gamma, var, eps, dgamma, dbeta, dbias, accumulate);
-  return check_launch("bn_relu_bwd_final");
+  return check_launch("bn_act_bwd_final");
 }
 
 int of_maxpool2_fwd(const float* x, int n, int h, int w, int c, float* y, void* stream) {

@@ -17,6 +17,25 @@ LEAKY_ALPHA = 0.3      # keras LeakyReLU() default (model.py:105)
 BN_EPS = 1e-3          # keras BatchNormalization default (model.py:14)
 
 
+# Bench instrumentation: when TIMING_TAGS is a list, every conv launch appends
+# (layer name, kind) in launch order, matching the hipEvent records of of_timing_read().
+TIMING_TAGS = None
+
+
+def _tag(layer, kind):
+    if TIMING_TAGS is not None:
+        TIMING_TAGS.append((layer.name, kind))
+
+
+def _workspace(nbytes: int, device):
+    """Scratch for one launch: (tensor keeping it alive, pointer, bytes).  The caching
+    allocator is stream-ordered, so the block is only reused after this stream's kernel."""
+    if nbytes <= 0:
+        return None, None, 0
+    t = torch.empty((nbytes + 15) // 4, device=device)
+    return t, C.c_void_p(t.data_ptr()), nbytes
+
+
 def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else C.c_void_p(t.data_ptr())
 
@@ -156,11 +175,13 @@ class _ConvFn(torch.autograd.Function):
         if residual is not None:
             residual = residual.contiguous()
             assert residual.shape == y.shape
+        _tag(layer, 0)
+        wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_fwd_workspace(C.byref(d)), x.device)
         call("of_conv2d_fwd", C.byref(d), _ptr(x), cx, _ptr(wf), _ptr(bias),
              _ptr(bn[0]) if bn else None, _ptr(bn[1]) if bn else None,
              _ptr(bn[2]) if bn else None, _ptr(bn[3]) if bn else None, BN_EPS,
              _ptr(residual), layer.cout, layer.act, layer.alpha,
-             _ptr(z), layer.cout, _ptr(y), layer.cout, _stream())
+             _ptr(z), layer.cout, _ptr(y), layer.cout, wsp, wsb, _stream())
         ctx.layer = layer
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, y, z)
@@ -216,6 +237,7 @@ class _ConvFn(torch.autograd.Function):
             if tbias[0] is not None and tbias[1] != tk[1]:
                 # mixed arena / fresh targets: compute the bias into a temp, then place it
                 tmpb = torch.empty_like(layer.bias)
+                _tag(layer, 2)
                 call("of_conv2d_wgrad", C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
                      _ptr(tk[0]), _ptr(tmpb), tk[1], _ptr(ws), wsb, s)
                 if tbias[1]:
@@ -223,6 +245,7 @@ class _ConvFn(torch.autograd.Function):
                 else:
                     tbias = (tmpb, 0, tmpb)
             else:
+                _tag(layer, 2)
                 call("of_conv2d_wgrad", C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
                      _ptr(tk[0]), _ptr(tbias[0]), tk[1], _ptr(ws), wsb, s)
             ret_k = tk[2] if need_k else None
@@ -233,9 +256,108 @@ class _ConvFn(torch.autograd.Function):
         # ---- input gradient -------------------------------------------------------------
         if need_x:
             dx = torch.empty((n, h, w, cx), device=dy.device)
+            _tag(layer, 1)
+            wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_dgrad_workspace(C.byref(d)),
+                                       dy.device)
             call("of_conv2d_dgrad", C.byref(d), _ptr(dzp), dzp.shape[-1], _ptr(wd), None, 0,
-                 ACT_NONE, 0.0, _ptr(dx), cx, s)
+                 ACT_NONE, 0.0, _ptr(dx), cx, wsp, wsb, s)
         return dx, ret_k, ret_b, ret_g, ret_be, dres, None
+
+
+class _ConvStackFn(torch.autograd.Function):
+    """A chain of plain convs (bias + activation, no BN / residual): the six-conv flow head
+    of ``flow_module`` (model.py:104-114).  The backward is fused across layers: each input
+    gradient kernel multiplies by the producer layer's LeakyReLU derivative in its epilogue
+    (act_src = that layer's saved output), so no separate activation-backward pass runs."""
+
+    @staticmethod
+    def forward(ctx, x, *args):
+        layers = args[-1]
+        n = len(layers)
+        _check_dev(x)
+        x = x.contiguous()
+        s = _stream()
+        acts = [x]
+        for i, layer in enumerate(layers):
+            assert layer.bn is None
+            nb, h, w, cx = acts[-1].shape
+            assert cx == layer.cin_p, "conv %s: %d channels, expected %d" % (layer.name, cx,
+                                                                             layer.cin_p)
+            d = layer.desc(nb, h, w)
+            wf, _ = layer.packed(d)
+            y = torch.empty((nb, d.ho, d.wo, layer.cout), device=x.device)
+            _tag(layer, 0)
+            wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_fwd_workspace(C.byref(d)), x.device)
+            call("of_conv2d_fwd", C.byref(d), _ptr(acts[-1]), cx, _ptr(wf), _ptr(layer.bias),
+                 None, None, None, None, BN_EPS, None, 0, layer.act, layer.alpha, None, 0,
+                 _ptr(y), layer.cout, wsp, wsb, s)
+            if i + 1 < n:
+                assert layers[i + 1].cin_p == layer.cout, "stacked convs need cout % 4 == 0"
+            acts.append(y)
+        ctx.layers = layers
+        ctx.save_for_backward(*acts)
+        return acts[-1]
+
+    @staticmethod
+    def backward(ctx, dy):
+        layers = ctx.layers
+        acts = ctx.saved_tensors
+        s = _stream()
+        n = len(layers)
+        needs = ctx.needs_input_grad
+        g = _pad_channels(dy.contiguous(), _c4(layers[-1].cout))
+        if layers[-1].act != ACT_NONE:
+            gz = torch.empty_like(g)
+            y = _pad_channels(acts[-1], g.shape[-1])
+            call("of_act_bwd", _ptr(g), _ptr(y), layers[-1].act, layers[-1].alpha, _ptr(gz),
+                 g.numel(), s)
+            g = gz
+        dx = None
+        for i in range(n - 1, -1, -1):
+            layer = layers[i]
+            x = acts[i]
+            nb, h, w, cx = x.shape
+            d = layer.desc(nb, h, w)
+            _, wd = layer.packed(d)
+            tk = grad_target(layer.kernel)
+            tb = grad_target(layer.bias)
+            if tk[1] != tb[1]:
+                raise RuntimeError("kernel and bias gradients must both use the arena or not")
+            wsb = _lib.lib().of_conv2d_wgrad_workspace(C.byref(d))
+            ws = torch.empty(wsb // 4 + 1, device=x.device)
+            _tag(layer, 2)
+            call("of_conv2d_wgrad", C.byref(d), _ptr(x), cx, _ptr(g), g.shape[-1], _ptr(tk[0]),
+                 _ptr(tb[0]), tk[1], _ptr(ws), wsb, s)
+            layer._ret = (tk[2], tb[2])
+            _grad_ready(layer.kernel, layer.bias)
+            if i > 0:
+                prev = layers[i - 1]
+                gx = torch.empty((nb, h, w, cx), device=x.device)
+                _tag(layer, 1)
+                wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_dgrad_workspace(C.byref(d)),
+                                           x.device)
+                call("of_conv2d_dgrad", C.byref(d), _ptr(g), g.shape[-1], _ptr(wd), _ptr(x), cx,
+                     prev.act, prev.alpha, _ptr(gx), cx, wsp, wsb, s)
+                g = gx
+            elif needs[0]:
+                dx = torch.empty((nb, h, w, cx), device=x.device)
+                _tag(layer, 1)
+                wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_dgrad_workspace(C.byref(d)),
+                                           x.device)
+                call("of_conv2d_dgrad", C.byref(d), _ptr(g), g.shape[-1], _ptr(wd), None, 0,
+                     ACT_NONE, 0.0, _ptr(dx), cx, wsp, wsb, s)
+        rets = []
+        for layer in layers:
+            rets += list(layer._ret)
+            layer._ret = None
+        return (dx, *rets, None)
+
+
+def conv_stack(x, layers):
+    flat = []
+    for layer in layers:
+        flat += [layer.kernel, layer.bias]
+    return _ConvStackFn.apply(x, *flat, list(layers))
 
 
 # ========================================================================= max pool ====
