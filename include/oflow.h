@@ -63,6 +63,16 @@ int64_t of_conv_wbwd_elems(const of_conv_desc* d);
 int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fwd,
                          float* w_bwd, void* stream);
 
+/* Packing every conv of a model in ONE launch (weights change once per optimizer step):
+ * build the table once on the host with of_conv_pack_table() into a buffer of
+ * of_conv_pack_table_bytes(nconv) bytes, copy it to device memory, then call
+ * of_conv_pack_many(dev_table, total_work, stream) per step; total_work is the 64-bit value at
+ * byte offset 8 of the table. */
+size_t of_conv_pack_table_bytes(int nconv);
+int of_conv_pack_table(int nconv, const of_conv_desc* descs, const float* const* w_hwio,
+                       float* const* w_fwd, float* const* w_bwd, void* host_table);
+int of_conv_pack_many(const void* dev_table, int64_t total_work, void* stream);
+
 /* Forward: z = conv(x, w) + bias;  y = act(BN(z) + residual) with the inference-mode
  * BatchNorm BN(z) = (z - mean) * gamma / sqrt(var + bn_eps) + beta (identity when
  * bn_gamma == NULL); z is also stored when z != NULL (needed for the BN gamma gradient).

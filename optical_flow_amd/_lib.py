@@ -38,6 +38,9 @@ PROTOTYPES = {
     "of_conv_wfwd_elems": (I64, [PD]),
     "of_conv_wbwd_elems": (I64, [PD]),
     "of_conv_pack_weights": (I, [PD, P, P, P, P]),
+    "of_conv_pack_table_bytes": (SZ, [I]),
+    "of_conv_pack_table": (I, [I, PD, C.POINTER(P), C.POINTER(P), C.POINTER(P), P]),
+    "of_conv_pack_many": (I, [P, I64, P]),
     "of_conv2d_fwd_workspace": (SZ, [PD]),
     "of_conv2d_fwd": (I, [PD, P, I, P, P, P, P, P, P, F, P, I, I, F, P, I, P, I, P, SZ, P]),
     "of_conv2d_dgrad_workspace": (SZ, [PD]),

@@ -60,8 +60,8 @@ struct GemmArgs {
   int dt;                 // tap step inside a group (1, or 2 for phase groups)
   int phase;              // dgrad phase-group mode (stride 2)
   int M, N, K;            // wgrad: M = taps*cin_p, K = output pixels
-  const float* A; int lda;
-  const float* B; int ldb; int nb;
+  const float* A; int lda; int64_t a_bytes;
+  const float* B; int ldb; int nb; int64_t b_bytes;
   float* C; int ldc;      // final output (epilogue)
   const float* bias;
   const float* bn_g; const float* bn_b; const float* bn_m; const float* bn_v; float bn_eps;
@@ -134,6 +134,18 @@ __device__ __forceinline__ void column_params(const GemmArgs& a, int n, float& b
   }
 }
 
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;   // buffer offset past num_records: the load returns 0
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ float4 bload4(rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
 __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -141,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
   static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "tile");
   constexpr bool A_KCONTIG = (MODE != MODE_WGRAD);
-  constexpr int SA = A_KCONTIG ? BM + 2 : BM + 4;   // +2: conflict-free transposed b32 writes
+  constexpr int SA = BM + 4;
   constexpr int SB = BN + 4;
   constexpr int A_SLOTS = BM * BK / 4 / 256;
   constexpr int B_QUADS = BK * BN / 4;
@@ -152,7 +164,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   __shared__ float Bs[2][BK * SB];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   // XCD-aware bijective remap: consecutive work ids -> one XCD's L2 (cdna guide T1).
   int wgid;
@@ -181,59 +194,78 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   const int k_end = min(Kg, k_begin + a.k_per_split);
   const int nchunks = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
 
+  const rsrc_t ra_src = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rb_src = make_rsrc(a.B, a.b_bytes);
+
   // ---------------- A loader state ------------------------------------------------------
-  // K-contig (fwd/dgrad): thread -> (row = tid/4 + 64*i, kq = tid%4), 4 channels of one tap.
-  // M-contig (wgrad): thread -> (mq = tid % (BM/4), krow = tid/(BM/4) + i*256/(BM/4)).
-  const int src_h = (MODE == MODE_DGRAD) ? a.ho : a.h;
-  const int src_w = (MODE == MODE_DGRAD) ? a.wo : a.w;
-  int a_py[A_SLOTS], a_px[A_SLOTS], a_b[A_SLOTS];
-  bool a_ok[A_SLOTS];
-  int ks_t = 0, ks_si = 0, ks_r = 0, ks_s = 0, ks_ci = 0;   // fwd/dgrad: per-thread k state
-  int wm_r = 0, wm_s = 0, wm_ci = 0;                         // wgrad: per-thread fixed m
+  // fwd/dgrad: wave w loads k-quad w of every chunk (4 channels of one tap) for rows
+  //   lane + 64*i; the tap walk (t, ci) is wave-uniform (scalar), each row keeps a byte
+  //   offset of its tap-origin pixel and a bitmask of its in-bounds taps, so one chunk costs
+  //   an add and a select per load (out-of-bounds -> past num_records -> 0).
+  // wgrad: thread -> (mq = tid % (BM/4), krow = tid/(BM/4) + i*256/(BM/4)), fixed (tap, ci).
+  int a_off[A_SLOTS];                 // fwd/dgrad: byte offset of tap (0,0) of the row
+  uint64_t a_msk[A_SLOTS];            // fwd/dgrad: in-bounds taps
+  int ks_t = 0, ks_tr = 0, ks_ts = 0, ks_ci = 0;
+  int tap_step = 0;                   // koff(bytes) = tap_sign*(tr*src_w + ts)*lda*4 + ci*4
+  int wm_r = 0, wm_s = 0, wm_ci = 0;  // wgrad: per-thread fixed m
   bool wm_ok = false;
-  int a_oy[A_SLOTS], a_ox[A_SLOTS], a_kb[A_SLOTS];           // wgrad: per-slot pixel state
+  int a_oy[A_SLOTS], a_ox[A_SLOTS], a_b[A_SLOTS], a_kb[A_SLOTS];   // wgrad: pixel state
 
   if constexpr (A_KCONTIG) {
-    const int kq = tid & 3;
+    const int src_h = (MODE == MODE_DGRAD) ? a.ho : a.h;
+    const int src_w = (MODE == MODE_DGRAD) ? a.wo : a.w;
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
-      const int m = m0 + (tid >> 2) + 64 * i;
-      a_ok[i] = m < M;
-      const int mm = a_ok[i] ? m : 0;
+      const int m = m0 + lane + 64 * i;
+      const bool okm = m < M;
+      const int mm = okm ? m : 0;
+      int b, yb, xb;   // tap-origin source pixel (may be outside the image)
       if (MODE == MODE_FWD) {
         const int hw = a.ho * a.wo;
-        const int b = mm / hw, rem = mm - b * hw;
+        b = mm / hw;
+        const int rem = mm - b * hw;
         const int oy = rem / a.wo, ox = rem - oy * a.wo;
-        a_b[i] = b * a.h;
-        a_py[i] = oy * a.stride - a.pt;
-        a_px[i] = ox * a.stride - a.pl;
+        yb = oy * a.stride - a.pt;
+        xb = ox * a.stride - a.pl;
+      } else if (a.phase) {
+        const int hw = G.hc * G.wc;
+        b = mm / hw;
+        const int rem = mm - b * hw;
+        const int u = rem / G.wc, v = rem - u * G.wc;
+        yb = (2 * u + G.ry + a.pt - G.r0) >> 1;
+        xb = (2 * v + G.rx + a.pl - G.s0) >> 1;
       } else {
-        int b, iy, ix;
-        if (a.phase) {
-          const int hw = G.hc * G.wc;
-          b = mm / hw;
-          const int rem = mm - b * hw;
-          const int u = rem / G.wc, v = rem - u * G.wc;
-          iy = 2 * u + G.ry;
-          ix = 2 * v + G.rx;
-        } else {
-          const int hw = a.h * a.w;
-          b = mm / hw;
-          const int rem = mm - b * hw;
-          iy = rem / a.w;
-          ix = rem - iy * a.w;
-        }
-        a_b[i] = b * a.ho;
-        a_py[i] = iy + a.pt;
-        a_px[i] = ix + a.pl;
+        const int hw = a.h * a.w;
+        b = mm / hw;
+        const int rem = mm - b * hw;
+        const int iy = rem / a.w, ix = rem - iy * a.w;
+        yb = iy + a.pt;
+        xb = ix + a.pl;
       }
+      a_off[i] = (int)(((int64_t)(b * src_h + yb) * src_w + xb) * a.lda * 4);
+      uint64_t msk = 0;
+      if (okm) {
+        // taps are row-major over (tr, ts); mask = in-bounds rows x in-bounds columns
+        uint64_t colmask = 0;
+        for (int ts = 0; ts < G.ns; ++ts) {
+          const int sx = (MODE == MODE_FWD) ? xb + ts : xb - ts;
+          if ((unsigned)sx < (unsigned)src_w) colmask |= (uint64_t)1 << ts;
+        }
+        int t = 0;
+        for (int tr = 0; t < G.ntaps; ++tr, t += G.ns) {
+          const int sy = (MODE == MODE_FWD) ? yb + tr : yb - tr;
+          if ((unsigned)sy < (unsigned)src_h) msk |= colmask << t;
+        }
+        if (G.ntaps < 64) msk &= ((uint64_t)1 << G.ntaps) - 1;
+      }
+      a_msk[i] = msk;
     }
-    const int k0 = k_begin + kq * 4;
+    const int k0 = k_begin + wave * 4;
     ks_t = k0 / a.kc;
     ks_ci = k0 - ks_t * a.kc;
-    ks_si = ks_t % G.ns;
-    ks_r = G.r0 + a.dt * (ks_t / G.ns);
-    ks_s = G.s0 + a.dt * ks_si;
+    ks_tr = ks_t / G.ns;
+    ks_ts = ks_t - ks_tr * G.ns;
+    tap_step = (MODE == MODE_FWD ? 1 : -1) * src_w * a.lda * 4;   // bytes per tap row
   } else {
     constexpr int MQ = BM / 4;
     const int mq = tid % MQ;
@@ -264,48 +296,22 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   auto load_a = [&]() {
     if constexpr (A_KCONTIG) {
       const bool tap_ok = ks_t < G.ntaps;
+      const int koff = (ks_tr * tap_step) + (MODE == MODE_FWD ? 1 : -1) * ks_ts * a.lda * 4 +
+                       ks_ci * 4;
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        bool ok = a_ok[i] && tap_ok;
-        int sy, sx;
-        if (MODE == MODE_FWD) {
-          sy = a_py[i] + ks_r;
-          sx = a_px[i] + ks_s;
-        } else {
-          const int ty = a_py[i] - ks_r, tx = a_px[i] - ks_s;
-          if (a.phase) {                 // parity guaranteed by the group
-            sy = ty >> 1;
-            sx = tx >> 1;
-          } else if (a.stride == 1) {
-            sy = ty;
-            sx = tx;
-          } else {                       // generic stride: zero-masked taps
-            ok = ok && ty >= 0 && tx >= 0 && (ty % a.stride) == 0 && (tx % a.stride) == 0;
-            sy = ty / a.stride;
-            sx = tx / a.stride;
-          }
-        }
-        ok = ok && (unsigned)sy < (unsigned)src_h && (unsigned)sx < (unsigned)src_w;
-        if (ok) {
-          const int64_t pix = (int64_t)(a_b[i] + sy) * src_w + sx;
-          v = *reinterpret_cast<const float4*>(a.A + pix * a.lda + ks_ci);
-        }
-        ra[i] = v;
+        const bool ok = tap_ok && ((a_msk[i] >> ks_t) & 1);
+        ra[i] = bload4(ra_src, ok ? (uint32_t)(a_off[i] + koff) : kOOB);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         const int sy = a_oy[i] * a.stride - a.pt + wm_r;
         const int sx = a_ox[i] * a.stride - a.pl + wm_s;
         const bool ok = wm_ok && a_kb[i] < k_end && (unsigned)sy < (unsigned)a.h &&
                         (unsigned)sx < (unsigned)a.w;
-        if (ok) {
-          const int64_t pix = ((int64_t)a_b[i] * a.h + sy) * a.w + sx;
-          v = *reinterpret_cast<const float4*>(a.A + pix * a.lda + wm_ci);
-        }
-        ra[i] = v;
+        const int off = (((a_b[i] * a.h + sy) * a.w + sx) * a.lda + wm_ci) * 4;
+        ra[i] = bload4(ra_src, ok ? (uint32_t)off : kOOB);
       }
     }
   };
@@ -315,22 +321,24 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
       while (ks_ci >= a.kc) {
         ks_ci -= a.kc;
         ++ks_t;
-        if (++ks_si >= G.ns) {
-          ks_si = 0;
-          ks_r += a.dt;
+        if (++ks_ts >= G.ns) {
+          ks_ts = 0;
+          ++ks_tr;
         }
-        ks_s = G.s0 + a.dt * ks_si;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
         a_kb[i] += BK;
         a_ox[i] += BK;
-        while (a_ox[i] >= a.wo) {
-          a_ox[i] -= a.wo;
-          if (++a_oy[i] >= a.ho) {
-            a_oy[i] = 0;
-            ++a_b[i];
+        if (a_ox[i] >= a.wo) {           // row wrap (rare: every wo/BK chunks)
+          const int q = a_ox[i] / a.wo;
+          a_ox[i] -= q * a.wo;
+          a_oy[i] += q;
+          if (a_oy[i] >= a.ho) {
+            const int q2 = a_oy[i] / a.ho;
+            a_oy[i] -= q2 * a.ho;
+            a_b[i] += q2;
           }
         }
       }
@@ -338,10 +346,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   };
   auto store_a = [&](int buf) {
     if constexpr (A_KCONTIG) {
-      const int kq = tid & 3;
+      // 64 consecutive rows of one k per wave-instruction: conflict-free ds_write_b32
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
-        float* p = &As[buf][(kq * 4) * SA + (tid >> 2) + 64 * i];
+        float* p = &As[buf][(wave * 4) * SA + lane + 64 * i];
         p[0] = ra[i].x;
         p[SA] = ra[i].y;
         p[2 * SA] = ra[i].z;
@@ -359,23 +367,28 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   };
 
   // ---------------- B loader --------------------------------------------------------------
-  const float* Bp = a.B + ((MODE == MODE_WGRAD) ? 0 : G.b_off * a.ldb);
+  // per slot a fixed byte offset (row krow, column quad); the chunk adds b_k rows.
+  const int64_t b_base = (MODE == MODE_WGRAD) ? 0 : G.b_off;
+  uint32_t b_off[B_SLOTS];
+  int b_row[B_SLOTS];
+#pragma unroll
+  for (int i = 0; i < B_SLOTS; ++i) {
+    constexpr int NQ = BN / 4;
+    const int slot = tid + 256 * i;
+    const int krow = slot / NQ, nq = slot - krow * NQ;
+    const int n = n0 + 4 * nq;
+    b_row[i] = krow;
+    b_off[i] = (slot < B_QUADS && n < a.nb) ? (uint32_t)(((b_base + krow) * a.ldb + n) * 4)
+                                            : kOOB;
+  }
   int b_k = k_begin;   // first k row of the current chunk
   auto load_b = [&]() {
-    constexpr int NQ = BN / 4;
+    const uint32_t kadd = (uint32_t)b_k * (uint32_t)a.ldb * 4u;
 #pragma unroll
     for (int i = 0; i < B_SLOTS; ++i) {
-      const int slot = tid + 256 * i;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (slot < B_QUADS) {
-        const int krow = slot / NQ, nq = slot - krow * NQ;
-        const int n = n0 + 4 * nq;
-        const int k = b_k + krow;
-        bool ok = n < a.nb;
-        if (MODE == MODE_WGRAD) ok = ok && k < k_end;
-        if (ok) v = *reinterpret_cast<const float4*>(Bp + (int64_t)k * a.ldb + n);
-      }
-      rb[i] = v;
+      bool ok = b_off[i] != kOOB;
+      if (MODE == MODE_WGRAD) ok = ok && (b_k + b_row[i] < k_end);
+      rb[i] = bload4(rb_src, ok ? b_off[i] + kadd : kOOB);
     }
   };
   auto store_b = [&](int buf) {
@@ -498,32 +511,45 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
 }
 
 // Split-K epilogue for fwd/dgrad: sum the K slices' slabs, then the fused epilogue.
+// Workgroup = 32 items x 8 split lanes; item = (slab row, 4 columns); the 8 lanes each sum
+// every 8th slice (many independent loads in flight), then a fixed-order LDS reduction.
+constexpr int EP_ITEMS = 32, EP_LANES = 8;
+
 template <int MODE>
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a) {
+  __shared__ float4 red[EP_LANES][EP_ITEMS];
+  const int it = threadIdx.x % EP_ITEMS, sl = threadIdx.x / EP_ITEMS;
+  const int nq = (a.N + 3) / 4;
   const int64_t rows = (int64_t)(a.tiles_total / a.n_tiles) * a.bm;
-  const int64_t total = rows * a.N;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int n = (int)(idx % a.N);
-    const int64_t srow = idx / a.N;
-    const int tm = (int)(srow / a.bm);
-    int gi = 0;
-    for (int g = 1; g < a.ngroups; ++g)
-      if (tm >= a.grp[g].tiles_begin) gi = g;
-    const Group& G = a.grp[gi];
-    const int m = (int)(srow - (int64_t)G.tiles_begin * a.bm);
-    if (m >= G.M) continue;
-    const float* src = a.slab + srow * a.slab_ld + n;
-    float v0 = 0.f, v1 = 0.f;
-    int z = 0;
-    for (; z + 1 < a.splits; z += 2) {
-      v0 += src[(int64_t)z * a.split_stride];
-      v1 += src[(int64_t)(z + 1) * a.split_stride];
-    }
-    if (z < a.splits) v0 += src[(int64_t)z * a.split_stride];
+  const int64_t item = (int64_t)blockIdx.x * EP_ITEMS + it;
+  const bool live = item < rows * nq;
+  const int q = live ? (int)(item % nq) : 0;
+  const int64_t srow = live ? item / nq : 0;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    const float* src = a.slab + srow * a.slab_ld + 4 * q;
+    for (int z = sl; z < a.splits; z += EP_LANES)
+      add4(acc, *reinterpret_cast<const float4*>(src + (int64_t)z * a.split_stride));
+  }
+  red[sl][it] = acc;
+  __syncthreads();
+  if (sl != 0 || !live) return;
+  for (int k = 1; k < EP_LANES; ++k) add4(acc, red[k][it]);
+  const int tm = (int)(srow / a.bm);
+  int gi = 0;
+  for (int g = 1; g < a.ngroups; ++g)
+    if (tm >= a.grp[g].tiles_begin) gi = g;
+  const Group& G = a.grp[gi];
+  const int m = (int)(srow - (int64_t)G.tiles_begin * a.bm);
+  if (m >= G.M) return;
+  const int64_t row = out_row(a, G, m);
+  const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+  for (int e = 0; e < 4; ++e) {
+    const int n = 4 * q + e;
+    if (n >= a.N) break;
     float bias, scale, shift;
     column_params<MODE>(a, n, bias, scale, shift);
-    epilogue_store<MODE>(a, out_row(a, G, m), n, v0 + v1, bias, scale, shift);
+    epilogue_store<MODE>(a, row, n, v[e], bias, scale, shift);
   }
 }
 
@@ -572,47 +598,101 @@ __global__ void pack_bwd_kernel(const float* __restrict__ w, PackGroups pg, int 
   }
 }
 
+// All convs of a model packed in one launch from a device-resident table.
+struct PackEntry {
+  const float* w;
+  float* wf;
+  float* wd;
+  int taps, kw, cin, cout, cin_p, cout_p, kf, nf, nd;
+  int64_t work_begin;      // cumulative elements (fwd then bwd) before this entry
+  PackGroups pg;
+};
+
+struct PackTableHeader {
+  int nconv;
+  int pad;
+  int64_t total;
+};
+
+__global__ void pack_many_kernel(const char* __restrict__ table) {
+  const PackTableHeader* h = reinterpret_cast<const PackTableHeader*>(table);
+  const PackEntry* e = reinterpret_cast<const PackEntry*>(table + sizeof(PackTableHeader));
+  const int n = h->nconv;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < h->total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (e[mid].work_begin <= idx) lo = mid; else hi = mid - 1;
+    }
+    const PackEntry& E = e[lo];
+    int64_t k = idx - E.work_begin;
+    const int64_t nfwd = (int64_t)E.kf * E.nf;
+    if (k < nfwd) {
+      const int kk = (int)(k / E.nf), nn = (int)(k - (int64_t)kk * E.nf);
+      const int tap = kk / E.cin_p, ci = kk - tap * E.cin_p;
+      float v = 0.f;
+      if (tap < E.taps && ci < E.cin && nn < E.cout)
+        v = E.w[((int64_t)tap * E.cin + ci) * E.cout + nn];
+      E.wf[k] = v;
+    } else {
+      k -= nfwd;
+      const int64_t row = k / E.nd;
+      const int nn = (int)(k - row * E.nd);
+      const PackGroups& pg = E.pg;
+      int g = 0;
+      for (int q = 1; q < pg.ngroups; ++q)
+        if (row >= pg.row_begin[q]) g = q;
+      const int kk = (int)(row - pg.row_begin[g]);
+      const int t = kk / E.cout_p, co = kk - t * E.cout_p;
+      float v = 0.f;
+      if (t < pg.ntaps[g] && co < E.cout && nn < E.cin) {
+        const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
+        const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
+        v = E.w[((int64_t)(r * E.kw + ss) * E.cin + nn) * E.cout + co];
+      }
+      E.wd[k] = v;
+    }
+  }
+}
+
 // dw[tap][ci][co] (HWIO) = sum_z slab[z][tap*kc + ci][co]; optional db[co] = sum_z slab[z][M][co].
-// One thread per (row, 4-column group); 4 slices in flight per iteration.
+// Workgroup = 32 items x 8 split lanes, item = (output row, 4 columns); fixed-order reduction.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws,
                                                            int splits, int64_t split_stride,
                                                            int taps, int kc, int cin, int cout,
                                                            int ldc, float* __restrict__ dw,
                                                            float* __restrict__ db, int accum) {
+  __shared__ float4 red[EP_LANES][EP_ITEMS];
+  const int it = threadIdx.x % EP_ITEMS, sl = threadIdx.x / EP_ITEMS;
   const int cq = (cout + 3) / 4;
   const int rows = taps * cin + (db ? 1 : 0);
-  const int64_t total = (int64_t)rows * cq;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(idx % cq);
-    const int row = (int)(idx / cq);
-    const bool is_bias = row == taps * cin;
-    int64_t m;
-    if (is_bias) {
-      m = (int64_t)taps * kc;
-    } else {
-      const int tap = row / cin, ci = row - tap * cin;
-      m = (int64_t)tap * kc + ci;
-    }
-    const float* src = ws + m * ldc + 4 * q;
-    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
-    int z = 0;
-    for (; z + 3 < splits; z += 4) {
-      add4(s0, *reinterpret_cast<const float4*>(src + (int64_t)z * split_stride));
-      add4(s1, *reinterpret_cast<const float4*>(src + (int64_t)(z + 1) * split_stride));
-      add4(s2, *reinterpret_cast<const float4*>(src + (int64_t)(z + 2) * split_stride));
-      add4(s3, *reinterpret_cast<const float4*>(src + (int64_t)(z + 3) * split_stride));
-    }
-    for (; z < splits; ++z)
-      add4(s0, *reinterpret_cast<const float4*>(src + (int64_t)z * split_stride));
-    add4(s0, s1);
-    add4(s2, s3);
-    add4(s0, s2);
-    const float v[4] = {s0.x, s0.y, s0.z, s0.w};
-    float* dst = is_bias ? db + 4 * q : dw + (int64_t)row * cout + 4 * q;
-    const int nv = min(4, cout - 4 * q);
-    for (int e = 0; e < nv; ++e) dst[e] = accum ? dst[e] + v[e] : v[e];
+  const int64_t item = (int64_t)blockIdx.x * EP_ITEMS + it;
+  const bool live = item < (int64_t)rows * cq;
+  const int q = live ? (int)(item % cq) : 0;
+  const int row = live ? (int)(item / cq) : 0;
+  const bool is_bias = row == taps * cin;
+  int64_t m;
+  if (is_bias) {
+    m = (int64_t)taps * kc;
+  } else {
+    const int tap = row / cin, ci = row - tap * cin;
+    m = (int64_t)tap * kc + ci;
   }
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    const float* src = ws + m * ldc + 4 * q;
+    for (int z = sl; z < splits; z += EP_LANES)
+      add4(acc, *reinterpret_cast<const float4*>(src + (int64_t)z * split_stride));
+  }
+  red[sl][it] = acc;
+  __syncthreads();
+  if (sl != 0 || !live) return;
+  for (int k = 1; k < EP_LANES; ++k) add4(acc, red[k][it]);
+  const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+  float* dst = is_bias ? db + 4 * q : dw + (int64_t)row * cout + 4 * q;
+  const int nv = min(4, cout - 4 * q);
+  for (int e = 0; e < nv; ++e) dst[e] = accum ? dst[e] + v[e] : v[e];
 }
 
 // ------------------------------------------------------------------------------ dispatch --
@@ -666,6 +746,7 @@ int validate(const of_conv_desc* d) {
   OF_CHECK_ARG(d->cin_p >= d->cin && d->cin_p % 4 == 0, "cin_p must be >= cin, multiple of 4");
   OF_CHECK_ARG(d->kh > 0 && d->kw > 0 && d->stride > 0, "conv kernel/stride");
   OF_CHECK_ARG(d->ho > 0 && d->wo > 0, "conv output dims");
+  OF_CHECK_ARG(d->kh * d->kw <= 64, "conv: at most 64 taps (tap bitmasks)");
   return OF_OK;
 }
 
@@ -807,9 +888,9 @@ int launch_gemm(const GemmArgs& a, hipStream_t s) {
   else hipLaunchKernelGGL((conv_gemm_f32<256, 32, 4, 1, MODE>), grid, block, 0, s, a);
   int st = check_launch("conv_gemm_f32");
   if (st || MODE == MODE_WGRAD || a.splits == 1) return st;
-  const int64_t total = slab_rows(a) * a.N;
-  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 8192);
-  hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(blocks), dim3(256), 0, s, a);
+  const int64_t items = slab_rows(a) * cdiv(a.N, 4);
+  hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
+                     a);
   return check_launch("conv_splitk_epilogue");
 }
 
@@ -878,6 +959,54 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
   return OF_OK;
 }
 
+size_t of_conv_pack_table_bytes(int nconv) {
+  return sizeof(PackTableHeader) + (size_t)std::max(nconv, 0) * sizeof(PackEntry);
+}
+
+int of_conv_pack_table(int nconv, const of_conv_desc* descs, const float* const* w_hwio,
+                       float* const* w_fwd, float* const* w_bwd, void* host_table) {
+  OF_CHECK_ARG(nconv > 0 && descs && w_hwio && w_fwd && w_bwd && host_table, "pack table: args");
+  PackTableHeader* h = static_cast<PackTableHeader*>(host_table);
+  PackEntry* e = reinterpret_cast<PackEntry*>(static_cast<char*>(host_table) +
+                                              sizeof(PackTableHeader));
+  int64_t work = 0;
+  for (int i = 0; i < nconv; ++i) {
+    int st = validate(&descs[i]);
+    if (st) return st;
+    OF_CHECK_ARG(w_hwio[i] && w_fwd[i] && w_bwd[i], "pack table: NULL weight pointer");
+    const Geo g = geo(&descs[i]);
+    PackEntry& E = e[i];
+    E = PackEntry{};
+    E.w = w_hwio[i];
+    E.wf = w_fwd[i];
+    E.wd = w_bwd[i];
+    E.taps = g.taps;
+    E.kw = descs[i].kw;
+    E.cin = descs[i].cin;
+    E.cout = descs[i].cout;
+    E.cin_p = g.cin_p;
+    E.cout_p = g.cout_p;
+    E.kf = g.kf;
+    E.nf = g.nf;
+    E.nd = g.nd;
+    E.pg = g.pg;
+    E.work_begin = work;
+    work += (int64_t)g.kf * g.nf + g.kd * g.nd;
+  }
+  h->nconv = nconv;
+  h->pad = 0;
+  h->total = work;
+  return OF_OK;
+}
+
+int of_conv_pack_many(const void* dev_table, int64_t total_work, void* stream) {
+  OF_CHECK_ARG(dev_table && total_work > 0, "pack many: args");
+  const int blocks = (int)std::min<int64_t>(cdiv(total_work, 256), 8192);
+  hipLaunchKernelGGL(pack_many_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+                     static_cast<const char*>(dev_table));
+  return check_launch("pack_many");
+}
+
 size_t of_conv2d_fwd_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
   return fd_workspace(fwd_args(d, geo(d)));
@@ -908,7 +1037,11 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   attach_slab(a, workspace, ws_bytes);
   a.A = x;
   a.lda = ldx;
+  a.a_bytes = (int64_t)d->n * d->h * d->w * ldx * 4;
   a.B = w_fwd;
+  a.b_bytes = (int64_t)g.kf * g.nf * 4;
+  OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX,
+               "conv fwd: tensors must be < 2 GiB (32-bit buffer offsets)");
   a.C = y;
   a.ldc = ldy;
   a.bias = bias;
@@ -943,11 +1076,16 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
   OF_CHECK_ARG(!act_src || ld_act >= d->cin_p, "conv dgrad: ld_act");
   OF_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)w_bwd & 15) == 0,
                "conv dgrad: dy / w must be 16-byte aligned");
+  OF_CHECK_ARG(d->stride == 1 || d->stride == 2, "conv dgrad: stride must be 1 or 2");
   GemmArgs a = dgrad_args(d, g);
   attach_slab(a, workspace, ws_bytes);
   a.A = dy;
   a.lda = lddy;
+  a.a_bytes = (int64_t)d->n * d->ho * d->wo * lddy * 4;
   a.B = w_bwd;
+  a.b_bytes = g.kd * g.nd * 4;
+  OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX,
+               "conv dgrad: tensors must be < 2 GiB (32-bit buffer offsets)");
   a.C = dx;
   a.ldc = lddx;
   a.act_src = act_src;
@@ -987,8 +1125,12 @@ int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float*
   a.M = p.M;
   a.A = x;
   a.lda = ldx;
+  a.a_bytes = (int64_t)d->n * d->h * d->w * ldx * 4;
   a.B = dy;
   a.ldb = lddy;
+  a.b_bytes = (int64_t)a.K * lddy * 4;
+  OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX,
+               "conv wgrad: tensors must be < 2 GiB (32-bit buffer offsets)");
   a.nb = g.cout_p;
   a.slab = static_cast<float*>(workspace);
   a.slab_ld = p.ldc;
@@ -1002,9 +1144,8 @@ int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float*
   st = launch_gemm<MODE_WGRAD>(a, s);
   if (timing_on()) timing_end(s, 2, flops);
   if (st) return st;
-  const int64_t total = ((int64_t)g.taps * d->cin + 1) * cdiv(d->cout, 4);
-  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s,
+  const int64_t items = ((int64_t)g.taps * d->cin + (db ? 1 : 0)) * cdiv(d->cout, 4);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
                      static_cast<const float*>(workspace), p.splits, p.split_stride, g.taps,
                      g.cin_p, d->cin, d->cout, p.ldc, dw, db, accumulate);
   return check_launch("wgrad_reduce");

@@ -269,6 +269,15 @@ class FlowNet:
         self.encoder = Encoder(self.store)
         self.heads = [FlowHead(self.store, level, max_disp) for level in range(4)]
         self.name = "flow_net"
+        self._packer = None
+
+    def conv_layers(self):
+        layers = [self.encoder.conv1]
+        for a, b, p in self.encoder.blocks:
+            layers += [a, b] + ([p] if p is not None else [])
+        for h in self.heads:
+            layers += h.convs
+        return layers
 
     @property
     def trainable_weights(self) -> List[torch.Tensor]:
@@ -282,6 +291,9 @@ class FlowNet:
         """(B, H, W, 6) -> [flow3 (H/2), flow2 (H/4), flow1 (H/8), flow0 (H/16)]."""
         assert batch_imgs.shape[1] == self.height and batch_imgs.shape[2] == self.width
         assert batch_imgs.shape[3] == 6
+        if self._packer is None:
+            self._packer = ops.ConvPacker(self.conv_layers(), lambda: self.store.version)
+        self._packer.ensure()                        # all conv weights packed in one launch
         imgs = ops.split_pair(batch_imgs)            # image1s then image2s (model.py:122-123)
         feats = self.encoder.forward4(imgs)          # shared encoder, both images (P12)
         flows = []

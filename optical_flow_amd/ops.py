@@ -142,6 +142,42 @@ class ConvLayer:
         return _ConvFn.apply(x, self.kernel, self.bias, bn[0], bn[1], residual, self)
 
 
+class ConvPacker:
+    """Packs the GEMM-ready weights of many ConvLayers in ONE kernel launch per optimizer
+    step (of_conv_pack_many over a device-resident table built once)."""
+
+    def __init__(self, layers, version_of):
+        self.layers = list(layers)
+        self.version_of = version_of
+        lib = _lib.lib()
+        n = len(self.layers)
+        descs = (ConvDesc * n)()
+        wp, fp, bp = (C.c_void_p * n)(), (C.c_void_p * n)(), (C.c_void_p * n)()
+        for i, L in enumerate(self.layers):
+            d = L.desc(1, 16, 16)
+            descs[i] = d
+            dev = L.kernel.device
+            L._wf = torch.empty(lib.of_conv_wfwd_elems(C.byref(d)), device=dev)
+            L._wd = torch.empty(lib.of_conv_wbwd_elems(C.byref(d)), device=dev)
+            wp[i], fp[i], bp[i] = L.kernel.data_ptr(), L._wf.data_ptr(), L._wd.data_ptr()
+        nbytes = lib.of_conv_pack_table_bytes(n)
+        host = (C.c_char * nbytes)()
+        call("of_conv_pack_table", n, descs, wp, fp, bp, host)
+        self.total = C.c_int64.from_buffer(host, 8).value
+        self.table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(
+            self.layers[0].kernel.device)
+        self._version = None
+
+    def ensure(self):
+        v = self.version_of()
+        if v == self._version:
+            return
+        call("of_conv_pack_many", C.c_void_p(self.table.data_ptr()), self.total, _stream())
+        for L in self.layers:
+            L._pack_key = (L.kernel.data_ptr(), v)
+        self._version = v
+
+
 def _pad_channels(t: torch.Tensor, cp: int) -> torch.Tensor:
     """Copy an NHWC tensor into a zero-padded one with cp channels (the conv ABI reads
     round_up(C,4) channels)."""
