@@ -33,7 +33,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (spec)
-KIND_NAMES = {0: "conv_gemm_f32<fwd>", 1: "conv_gemm_f32<dgrad>", 2: "conv_gemm_f32<wgrad>"}
+MODE_NAMES = {0: "fwd", 1: "dgrad", 2: "wgrad"}
+TILE_TEMPLATE = {0: "128, 128, 2, 2", 1: "128, 96, 4, 1", 2: "256, 64, 4, 1", 3: "256, 32, 4, 1",
+                 4: "256, 128, 2, 2"}
+
+
+def kernel_symbol(kind):
+    """rocprofv3 name of the conv_gemm_f32 template instance behind a timing kind."""
+    return "void oflow::conv_gemm_f32<%s, %d>(oflow::GemmArgs)" % (TILE_TEMPLATE[kind % 8],
+                                                                    kind // 8)
 
 
 def gflop_per_pair(H, W, max_disp=3):
@@ -175,14 +183,25 @@ def main():
     if dom is not None:
         tf, tm, cnt = per[dom]
         achieved = tf / (tm * 1e-3) / 1e12
-        roof = {"bound": "mfma", "kernel": KIND_NAMES[dom], "achieved": round(achieved, 2),
+        sym = kernel_symbol(dom)
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("kernel") == sym and pmc.get("config") == [H, W, B]:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        allconv = sum(v[0] for v in per.values()) / (sum(v[1] for v in per.values()) * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
                 "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "launches": cnt, "avg_launch_ms": round(tm / cnt, 4),
-                "gflop_per_launch": round(tf / cnt / 1e9, 3),
-                "all_conv": {KIND_NAMES[k]: {"launches": v[2], "ms": round(v[1], 3),
-                                             "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
-                             for k, v in sorted(per.items())}}
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "launches_per_step": cnt // max(args.timing_steps, 1),
+                "avg_launch_ms": round(tm / cnt, 4), "gflop_per_launch": round(tf / cnt / 1e9, 3),
+                "all_conv_gemm_tflops": round(allconv, 2),
+                "per_kernel": {"%s<%s>" % (MODE_NAMES[k // 8], TILE_TEMPLATE[k % 8]):
+                               {"launches": v[2], "ms": round(v[1], 3),
+                                "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
+                               for k, v in sorted(per.items())}}
 
     # ---- CPU baseline + EPE vs the oracle (rank 0 only) ----------------------------------
     cpu = None

@@ -207,6 +207,8 @@ int of_fill(float* y, float v, int64_t n, void* stream);
  * launch records a hipEvent pair on its stream; of_timing_read() returns the count and fills
  * kinds (0 fwd, 1 dgrad, 2 wgrad), flops and elapsed ms (synchronises the events). */
 int of_timing_enable(int on);
+/* Kernel-variant switches for A/B measurements (no keys defined in this build). */
+int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 
 #ifdef __cplusplus

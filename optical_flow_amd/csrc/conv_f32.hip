@@ -752,6 +752,8 @@ int validate(const of_conv_desc* d) {
 
 // Tile configuration by GEMM N: (BM, BN).  Narrow N gets taller M tiles so every wave still
 // owns >= 2 MFMA accumulators and the per-chunk staging cost is amortised.
+// (A 256x128 tile -- 4x2 MFMA tiles per wave, 2 waves/SIMD -- measured 5-10 % slower on
+// dgrad/wgrad and spills on fwd; 128x128 with 4 waves/SIMD is kept.)
 int pick_bn(int N) { return N > 96 ? 128 : N > 64 ? 96 : N > 32 ? 64 : 32; }
 int pick_bm(int N) { return N > 64 ? 128 : 256; }
 
@@ -878,14 +880,19 @@ GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g) {
   return a;
 }
 
+// Timing kinds: mode * 8 + tile config (0: 128x128, 1: 128x96, 2: 256x64, 3: 256x32) -- one
+// per conv_gemm_f32 template instance.
 template <int MODE>
-int launch_gemm(const GemmArgs& a, hipStream_t s) {
+int launch_gemm(const GemmArgs& a, hipStream_t s, double flops) {
   const int bn = pick_bn(a.N);
   dim3 grid(a.tiles_total * a.splits), block(256);
-  if (bn == 128) hipLaunchKernelGGL((conv_gemm_f32<128, 128, 2, 2, MODE>), grid, block, 0, s, a);
-  else if (bn == 96) hipLaunchKernelGGL((conv_gemm_f32<128, 96, 4, 1, MODE>), grid, block, 0, s, a);
-  else if (bn == 64) hipLaunchKernelGGL((conv_gemm_f32<256, 64, 4, 1, MODE>), grid, block, 0, s, a);
+  const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
+  if (timing_on()) timing_begin(s);
+  if (cfg == 0) hipLaunchKernelGGL((conv_gemm_f32<128, 128, 2, 2, MODE>), grid, block, 0, s, a);
+  else if (cfg == 1) hipLaunchKernelGGL((conv_gemm_f32<128, 96, 4, 1, MODE>), grid, block, 0, s, a);
+  else if (cfg == 2) hipLaunchKernelGGL((conv_gemm_f32<256, 64, 4, 1, MODE>), grid, block, 0, s, a);
   else hipLaunchKernelGGL((conv_gemm_f32<256, 32, 4, 1, MODE>), grid, block, 0, s, a);
+  if (timing_on()) timing_end(s, MODE * 8 + cfg, flops);
   int st = check_launch("conv_gemm_f32");
   if (st || MODE == MODE_WGRAD || a.splits == 1) return st;
   const int64_t items = slab_rows(a) * cdiv(a.N, 4);
@@ -957,6 +964,11 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
     if ((st = check_launch("pack_bwd"))) return st;
   }
   return OF_OK;
+}
+
+int of_set_tuning(int key, int value) {
+  (void)value;
+  return fail(OF_EINVAL, "of_set_tuning: unknown key " + std::to_string(key));
 }
 
 size_t of_conv_pack_table_bytes(int nconv) {
@@ -1058,9 +1070,7 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
-  if (timing_on()) timing_begin(s);
-  st = launch_gemm<MODE_FWD>(a, s);
-  if (timing_on()) timing_end(s, 0, flops);
+  st = launch_gemm<MODE_FWD>(a, s, flops);
   return st;
 }
 
@@ -1094,9 +1104,7 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
-  if (timing_on()) timing_begin(s);
-  st = launch_gemm<MODE_DGRAD>(a, s);
-  if (timing_on()) timing_end(s, 1, flops);
+  st = launch_gemm<MODE_DGRAD>(a, s, flops);
   return st;
 }
 
@@ -1140,9 +1148,7 @@ int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float*
   a.colsum = db != nullptr;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
-  if (timing_on()) timing_begin(s);
-  st = launch_gemm<MODE_WGRAD>(a, s);
-  if (timing_on()) timing_end(s, 2, flops);
+  st = launch_gemm<MODE_WGRAD>(a, s, flops);
   if (st) return st;
   const int64_t items = ((int64_t)g.taps * d->cin + (db ? 1 : 0)) * cdiv(d->cout, 4);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,

@@ -339,3 +339,33 @@ def build_flow_net(height, width, pretrained_weights_path=None, max_disp=3, seed
         assert not missing, "pretrained encoder weights missing: %s" % missing[:5]
         net.store.load({n: vals[n] for n in enc_names}, strict=False)
     return net
+
+
+class TwoLayerHead:
+    """Config-1 plumbing model (BASELINE.json configs[0]; build-defined, not in the
+    reference): conv3x3/2 6->32 + LeakyReLU(0.3) -> conv3x3 32->2, one flow at H/2, fed to
+    LossLayer([flow]).  Same HIP kernels as the full net."""
+
+    def __init__(self, height, width, seed=0, device="cuda", values=None):
+        from .params import two_layer_head_spec
+        self.height, self.width = height, width
+        self.store = ParamStore(two_layer_head_spec(), values=values, device=device, seed=seed)
+        P = self.store.params
+        ver = lambda: self.store.version
+        self.convs = [
+            ops.ConvLayer(P["head2/conv0/kernel"], P["head2/conv0/bias"], stride=2,
+                          act=ACT_LEAKY, cin_p=8, version_of=ver, name="head2/conv0"),
+            ops.ConvLayer(P["head2/conv1/kernel"], P["head2/conv1/bias"], stride=1,
+                          act=ACT_NONE, version_of=ver, name="head2/conv1")]
+
+    @property
+    def trainable_weights(self):
+        return self.store.trainable()
+
+    @property
+    def weight_names(self):
+        return [n for n, p in self.store.spec.items() if p.trainable]
+
+    def __call__(self, batch_imgs):
+        x = ops._pad_channels(batch_imgs, 8)      # (B,H,W,6) -> 8 zero-padded channels
+        return [ops.conv_stack(x, self.convs)]

@@ -146,8 +146,12 @@ def warp_features(flow, f2):
     then sampled as (x=ch0, y=ch1) -- the reference's transposed convention (P1, F6)."""
     _, h, w, _ = f2.shape
     ii, jj = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
-    grid = torch.stack([ii, jj], -1).to(flow.dtype).unsqueeze(0)
-    return bilinear_interpolation(f2, grid + flow)
+    grid = torch.stack([ii, jj], -1).to(torch.float32).unsqueeze(0)
+    # The reference forms the sampling coordinates in float32 (model.py:69-71: tf.cast(...,
+    # tf.float32) + flow); floor() of them decides the gather corners, so they are rounded to
+    # float32 here too even when the oracle runs in float64.
+    pts = (grid + flow.to(torch.float32)).to(flow.dtype)
+    return bilinear_interpolation(f2, pts)
 
 
 def resize_bilinear(x, h, w):

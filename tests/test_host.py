@@ -1,0 +1,62 @@
+"""Host-side logic that runs without a GPU: parameter spec, arena layout, FLOP model,
+synthetic data contract."""
+import numpy as np
+import torch
+
+from optical_flow_amd import params as P
+
+
+def test_param_count_and_layout():
+    spec = P.flow_net_spec()
+    train = [p for p in spec if p.trainable]
+    assert sum(p.size for p in train) == 4938760            # 4.94 M params
+    assert P.head_cin(0) == 305 and P.head_cin(1) == 179 and P.head_cin(3) == 115
+    names = [p.name for p in spec]
+    assert len(names) == len(set(names))
+    blocks = list(P.encoder_blocks())
+    assert [b[3] for b in blocks] == [1, 1, 2, 1, 2, 1]
+    assert [b[4] for b in blocks] == [False, False, True, False, True, False]
+
+
+def test_glorot_init_deterministic():
+    a = P.init_params(P.head_spec(3), 0)
+    b = P.init_params(P.head_spec(3), 0)
+    for k in a:
+        assert np.array_equal(a[k], b[k])
+    k = a["flow_module_3/conv0/kernel"]
+    limit = np.sqrt(6.0 / (9 * 115 + 9 * 128))
+    assert k.min() >= -limit and k.max() <= limit
+    assert not a["flow_module_3/conv0/bias"].any()
+
+
+def test_param_store_arena_cpu():
+    from optical_flow_amd.model import ParamStore, backward_order
+    order = backward_order()
+    spec = P.flow_net_spec()
+    assert sorted(order) == sorted(p.name for p in spec if p.trainable)
+    st = ParamStore(spec, device="cpu", order=order)
+    assert st.arena_order[0].startswith("flow_module_3/")       # finest head first
+    assert st.arena_order[-1] == "ResNet18/conv1/kernel"         # stem last
+    for name, off in st.offsets.items():
+        assert off % 4 == 0                                      # 16-byte aligned views
+        assert st.params[name].data_ptr() == st.arena.data_ptr() + 4 * off
+        assert st.params[name]._of_grad.data_ptr() == st.grad_arena.data_ptr() + 4 * off
+    vals = P.init_params(spec, 0)
+    for k, v in vals.items():
+        assert np.array_equal(st.params[k].detach().numpy(), v)
+
+
+def test_flop_model_matches_survey():
+    import bench
+    assert abs(bench.gflop_per_pair(384, 512) - 249.8) < 0.1
+    assert abs(bench.gflop_per_pair(128, 256) - 41.6) < 0.1
+    assert abs(bench.gflop_per_pair(768, 1024) - 999.4) < 0.1
+
+
+def test_synthetic_value_contract():
+    from optical_flow_amd.data import IMAGE_MEANS, synthetic_batch
+    b = synthetic_batch(2, 32, 48, seed=3)
+    assert b.shape == (2, 32, 48, 6) and b.dtype == np.float32
+    assert b.min() > -IMAGE_MEANS.max() - 0.1 and b.max() < 1.0 - IMAGE_MEANS.min() + 0.1
+    assert np.array_equal(b, synthetic_batch(2, 32, 48, seed=3))
+    assert not np.array_equal(b, synthetic_batch(2, 32, 48, seed=3, rank=1))

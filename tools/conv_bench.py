@@ -94,8 +94,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--tune", default=None, help="key=value[,key=value] of_set_tuning")
     args = ap.parse_args()
     _lib.load()
+    if args.tune:
+        for kv in args.tune.split(","):
+            k, v = kv.split("=")
+            _lib.lib().of_set_tuning(int(k), int(v))
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     for sh in SHAPES:
         if args.only and args.only not in sh[0]:
