@@ -139,13 +139,27 @@ int of_maxpool2_bwd(const float* x, const float* dy, int n, int h, int w, int c,
                     void* stream);
 
 /* Cost volume (create_cost_volume, model.py:29-42; P8): out[p][k], k=i*(2d+1)+j =
- * sum_c f1[p][c]*f2[p+(i-d, j-d)][c] with zero padding.  out has ldo >= (2d+1)^2. */
+ * sum_c f1[p][c]*f2[p+(i-d, j-d)][c] with zero padding.  out has ldo >= (2d+1)^2.
+ * Channels are reduced in 64-channel slabs; c > 64 needs of_corr_fwd_workspace() bytes. */
+size_t of_corr_fwd_workspace(int n, int h, int w, int c, int max_disp);
 int of_corr_fwd(const float* f1, int ld1, const float* f2, int ld2, int n, int h, int w,
-                int c, int max_disp, float* out, int ldo, void* stream);
+                int c, int max_disp, float* out, int ldo, void* workspace, size_t ws_bytes,
+                void* stream);
 /* Its gradient: df1 = (accumulate ? df1 : 0) + sum_k dcv*f2_shift; df2 likewise. */
 int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const float* f2,
                 int ld2, int n, int h, int w, int c, int max_disp, float* df1, int lddf1,
                 int acc1, float* df2, int lddf2, int acc2, void* stream);
+/* The flow-module input concat([features1, cost_volume, flow_up]) (model.py:97-102) built in
+ * one launch: cat[p] = [f1[p] (c) | cv[p] (49) | flow[p] (2, if flow) | zeros up to cp].
+ * f1, f2: dense [n][h][w][c]; flow: dense [n][h][w][2] or NULL. */
+int of_corr_concat_fwd(const float* f1, const float* f2, const float* flow, int n, int h, int w,
+                       int c, int max_disp, float* cat, int cp, void* workspace,
+                       size_t ws_bytes, void* stream);
+/* Its gradient from dcat (row stride cp): df1 = dcat[:, :c] + d(cv)/d(f1); df2 = d(cv)/d(f2)
+ * (skipped if NULL); dflow = dcat[:, c+49 : c+51] (skipped if NULL).  All written. */
+int of_corr_concat_bwd(const float* dcat, int cp, const float* f1, const float* f2, int n,
+                       int h, int w, int c, int max_disp, float* df1, float* df2, float* dflow,
+                       void* stream);
 
 /* Bilinear backward warp with the reference index convention (warp_features, model.py:55-73
  * + bilinear_interpolation, transformations.py:85-129; P1, P2):

@@ -54,8 +54,11 @@ PROTOTYPES = {
     "of_bn_act_bwd": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, P, I, P, P]),
     "of_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
     "of_maxpool2_bwd": (I, [P, P, I, I, I, I, P, P]),
-    "of_corr_fwd": (I, [P, I, P, I, I, I, I, I, I, P, I, P]),
+    "of_corr_fwd_workspace": (SZ, [I, I, I, I, I]),
+    "of_corr_fwd": (I, [P, I, P, I, I, I, I, I, I, P, I, P, SZ, P]),
     "of_corr_bwd": (I, [P, I, P, I, P, I, I, I, I, I, I, P, I, I, P, I, I, P]),
+    "of_corr_concat_fwd": (I, [P, P, P, I, I, I, I, I, P, I, P, SZ, P]),
+    "of_corr_concat_bwd": (I, [P, I, P, P, I, I, I, I, I, P, P, P, P]),
     "of_warp_fwd": (I, [P, I, I, I, I, P, P, P]),
     "of_warp_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
     "of_bilinear_fwd": (I, [P, I, I, I, I, P, P, P]),

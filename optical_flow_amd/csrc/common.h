@@ -24,6 +24,38 @@ inline int64_t round_up(int64_t a, int64_t b) { return cdiv(a, b) * b; }
 
 constexpr int kWave = 64;
 
+// Raw buffer loads (CDNA buffer resource, 32-bit byte offsets).  An offset at or past the
+// resource's byte count returns 0 without a branch: padding and halo reads stay straight-line
+// code, so the compiler keeps every load of a staging round in flight (a guarded pointer
+// load instead becomes a branch + s_waitcnt per element).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ float4 bload4(rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+__device__ __forceinline__ float bload1(rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+}
+// Channel quad at byte offset `off` with `n` valid channels (n >= 4: all), zero elsewhere;
+// `ok` false -> zeros.  vec: 16-byte aligned rows (one b128), else four b32.
+__device__ __forceinline__ float4 bload_quad(rsrc_t r, bool ok, uint32_t off, int n, int vec) {
+  if (vec) {
+    float4 v = bload4(r, ok && n > 0 ? off : kOOB);
+    v.y = n > 1 ? v.y : 0.f;
+    v.z = n > 2 ? v.z : 0.f;
+    v.w = n > 3 ? v.w : 0.f;
+    return v;
+  }
+  return make_float4(bload1(r, ok && n > 0 ? off : kOOB), bload1(r, ok && n > 1 ? off + 4 : kOOB),
+                     bload1(r, ok && n > 2 ? off + 8 : kOOB),
+                     bload1(r, ok && n > 3 ? off + 12 : kOOB));
+}
+
 }  // namespace oflow
 
 #define OF_CHECK_ARG(cond, msg)                                   \

@@ -134,18 +134,6 @@ __device__ __forceinline__ void column_params(const GemmArgs& a, int n, float& b
   }
 }
 
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-constexpr uint32_t kOOB = 0x80000000u;   // buffer offset past num_records: the load returns 0
-
-__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes,
-                                           0x00020000);
-}
-
-__device__ __forceinline__ float4 bload4(rsrc_t r, uint32_t voff) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
-}
-
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
 __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;

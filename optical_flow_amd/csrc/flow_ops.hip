@@ -8,166 +8,309 @@ namespace oflow {
 
 // ================================================================ cost volume (K6) =====
 // model.py:29-42: cv[p][i*(2d+1)+j] = sum_c f1[p][c] * f2[p + (i-d, j-d)][c], zero padded.
-// One thread per output pixel of an 8 x 32 tile; channels in chunks of CC staged through LDS
-// (f2 halo tile, pixel stride CC+4 floats -> conflict-free ds_read_b128).
-constexpr int CT_Y = 8, CT_X = 32, CC = 16, CPS = CC + 4;
+//
+// Blocks own a 4 x 16 pixel tile and one 64-channel slab (blockIdx.z = image * slabs + slab).
+// The slab's f2 halo (10 x 22 pixels x 64 channels, 256-B rows: fully coalesced, one load
+// round) sits in LDS; each pixel is worked by 4 adjacent lanes, 16 channels each:
+//   forward : lane partial dots over its 16 channels for all 49 offsets, quad-reduced with
+//             DPP; with more than one slab the partials go to a workspace and a second
+//             kernel sums them (fixed order: deterministic).
+//   backward: lane owns 16 output channels; the 49 coefficients of its pixel come from a
+//             small LDS table (for d/d(f2) gathered with the shift the adjoint needs).
+// LDS pixel stride 68 floats: the b128 reads of a wave's lane groups hit distinct banks.
+constexpr int CT_Y = 4, CT_X = 16, CT_PIX = CT_Y * CT_X;
+constexpr int CSLAB = 64, CSPS = CSLAB + 4;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float quad_sum(float v) {   // sum over the 4 lanes of a quad
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF,
+                                                          0xF, false));   // quad_perm(1,0,3,2)
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF,
+                                                          0xF, false));   // quad_perm(2,3,0,1)
+  return v;
+}
+
+struct CorrFwdArgs {
+  const float* f1;
+  int ld1;
+  const float* f2;
+  int ld2;
+  int h, w, c;
+  float* cv;          // cost volume channel 0 of pixel 0, row stride ldcv
+  int ldcv;
+  int vec;            // float4 global access allowed (strides and bases 16-byte aligned)
+  int slabs;          // ceil(c / 64)
+  float* part;        // slabs > 1: partial sums [slab][n*h*w][49]
+  // Flow-module concat (model.py:97-102), optional: cat row = [f1 | cv | flow | zero pad].
+  float* cat;         // row stride ldcv; cv == cat + c
+  const float* flow;  // (.., 2) or NULL
+};
 
 template <int D>
-__global__ __launch_bounds__(256) void corr_fwd_kernel(const float* __restrict__ f1, int ld1,
-                                                       const float* __restrict__ f2, int ld2,
-                                                       int h, int w, int c,
-                                                       float* __restrict__ out, int ldo,
-                                                       int vec) {
+__global__ __launch_bounds__(256, 2) void corr_fwd_kernel(CorrFwdArgs a) {
   constexpr int ND = 2 * D + 1, NK = ND * ND;
-  constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D;
-  __shared__ float tile[HY * HX * CPS];
-  const int b = blockIdx.z;
+  constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D, NH = HY * HX;
+  constexpr int NQ = NH * (CSLAB / 4), NU = (NQ + 255) / 256;
+  __shared__ float4 lds4[NH * CSPS / 4];
+  float* tile = reinterpret_cast<float*>(lds4);
+  const int h = a.h, w = a.w;
+  const int b = blockIdx.z / a.slabs, slab = blockIdx.z - b * a.slabs;
+  const int c_lo = slab * CSLAB, cs = min(CSLAB, a.c - c_lo);
   const int y0 = blockIdx.y * CT_Y, x0 = blockIdx.x * CT_X;
-  const int ty = threadIdx.x / CT_X, tx = threadIdx.x % CT_X;
+  const int tid = threadIdx.x;
+  const int pix = tid >> 2, qtr = tid & 3;
+  const int ty = pix / CT_X, tx = pix % CT_X;
   const int y = y0 + ty, x = x0 + tx;
   const bool valid = y < h && x < w;
-  float acc[NK];
-#pragma unroll
-  for (int k = 0; k < NK; ++k) acc[k] = 0.f;
   const int64_t img = (int64_t)b * h * w;
-  for (int c0 = 0; c0 < c; c0 += CC) {
-    const int cc = min(CC, c - c0);
-    __syncthreads();
-    // stage f2 halo tile: HY*HX pixels x (CC/4) quads
-    for (int q = threadIdx.x; q < HY * HX * (CC / 4); q += 256) {
-      const int pix = q / (CC / 4), cq = q % (CC / 4);
-      const int hy = pix / HX, hx = pix % HX;
-      const int sy = y0 - D + hy, sx = x0 - D + hx;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if ((unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w && 4 * cq < cc) {
-        const float* src = f2 + (img + (int64_t)sy * w + sx) * ld2 + c0 + 4 * cq;
-        if (vec && 4 * cq + 4 <= cc) {
-          v = *reinterpret_cast<const float4*>(src);
-        } else {
-          float t[4] = {0.f, 0.f, 0.f, 0.f};
-          for (int e = 0; e < cc - 4 * cq; ++e) t[e] = src[e];
-          v = make_float4(t[0], t[1], t[2], t[3]);
-        }
+  const int pl = y * w + x;
+  const rsrc_t r1 = make_rsrc(a.f1 + img * a.ld1, (int64_t)h * w * a.ld1 * 4);
+  const rsrc_t r2 = make_rsrc(a.f2 + img * a.ld2, (int64_t)h * w * a.ld2 * 4);
+  // One load round: the f2 halo slab and this lane's 16 f1 channels.
+  float4 hv[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int q = tid + 256 * u;
+    const int hp = q >> 4, cq = q & 15;
+    const int sy = y0 - D + hp / HX, sx = x0 - D + hp % HX;
+    const bool ok = q < NQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
+    hv[u] = bload_quad(r2, ok, 4 * ((sy * w + sx) * a.ld2 + c_lo + 4 * cq), cs - 4 * cq, a.vec);
+  }
+  f32x2 f[8];
+  float4 fq[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ch = qtr * 16 + 4 * e;
+    fq[e] = bload_quad(r1, valid, 4 * (pl * a.ld1 + c_lo + ch), cs - ch, a.vec);
+    f[2 * e] = f32x2{fq[e].x, fq[e].y};
+    f[2 * e + 1] = f32x2{fq[e].z, fq[e].w};
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int q = tid + 256 * u;
+    if (q < NQ) *reinterpret_cast<float4*>(&tile[(q >> 4) * CSPS + 4 * (q & 15)]) = hv[u];
+  }
+  if (a.cat && valid) {              // f1 slice of the concat row
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ch = qtr * 16 + 4 * e;
+      float* dst = a.cat + (img + pl) * a.ldcv + c_lo + ch;
+      if (a.vec && cs - ch >= 4) {
+        *reinterpret_cast<float4*>(dst) = fq[e];
+      } else {
+        const float t[4] = {fq[e].x, fq[e].y, fq[e].z, fq[e].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k < cs - ch) dst[k] = t[k];
       }
-      *reinterpret_cast<float4*>(&tile[pix * CPS + 4 * cq]) = v;
     }
-    float a[CC];
-    if (valid) {
-      const float* src = f1 + (img + (int64_t)y * w + x) * ld1 + c0;
+  }
+  __syncthreads();
+  // Packed accumulators: (even, odd) channel partial sums per offset, v_pk_fma_f32 only.
+  f32x2 acc[NK];
 #pragma unroll
-      for (int e = 0; e < CC; ++e) a[e] = e < cc ? src[e] : 0.f;
-    } else {
-#pragma unroll
-      for (int e = 0; e < CC; ++e) a[e] = 0.f;
-    }
-    __syncthreads();
+  for (int k = 0; k < NK; ++k) acc[k] = f32x2{0.f, 0.f};
+  // One channel quad per pass (not unrolled): bounds the LDS reads the scheduler can hoist.
+#pragma unroll 1
+  for (int e = 0; e < 4; ++e) {
+    const f32x2 f0 = e == 0 ? f[0] : e == 1 ? f[2] : e == 2 ? f[4] : f[6];
+    const f32x2 f1v = e == 0 ? f[1] : e == 1 ? f[3] : e == 2 ? f[5] : f[7];
+    const float* tb = &tile[(ty * HX + tx) * CSPS + qtr * 16 + 4 * e];
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
-        const float* t = &tile[((ty + i) * HX + tx + j) * CPS];
-        float s = acc[i * ND + j];
-#pragma unroll
-        for (int e = 0; e < CC; e += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(t + e);
-          s = fmaf(a[e], v.x, s);
-          s = fmaf(a[e + 1], v.y, s);
-          s = fmaf(a[e + 2], v.z, s);
-          s = fmaf(a[e + 3], v.w, s);
-        }
-        acc[i * ND + j] = s;
+        const f32x2* t = reinterpret_cast<const f32x2*>(tb + (i * HX + j) * CSPS);
+        acc[i * ND + j] = __builtin_elementwise_fma(f0, t[0], acc[i * ND + j]);
+        acc[i * ND + j] = __builtin_elementwise_fma(f1v, t[1], acc[i * ND + j]);
       }
     }
   }
-  if (valid) {
-    float* o = out + (img + (int64_t)y * w + x) * ldo;
+  float* out;
+  if (a.slabs == 1) {
+    out = a.cv + (img + pl) * a.ldcv;
+  } else {
+    const int64_t npix = (int64_t)(gridDim.z / a.slabs) * h * w;
+    out = a.part + (slab * npix + img + pl) * NK;
+  }
 #pragma unroll
-    for (int k = 0; k < NK; ++k) o[k] = acc[k];
+  for (int k = 0; k < NK; ++k) {
+    const float v = quad_sum(acc[k].x + acc[k].y);
+    if (valid && (k & 3) == qtr) out[k] = v;
+  }
+  if (a.cat && slab == 0 && qtr == 0 && valid) {   // flow and zero channel padding
+    float* row = a.cat + (img + pl) * a.ldcv;
+    int ch = a.c + NK;
+    if (a.flow) {
+      row[ch] = a.flow[2 * (img + pl)];
+      row[ch + 1] = a.flow[2 * (img + pl) + 1];
+      ch += 2;
+    }
+    for (; ch < a.ldcv; ++ch) row[ch] = 0.f;
+  }
+}
+
+// cv[p][k] = sum over slabs of part[slab][p][k] (slab order fixed).
+__global__ __launch_bounds__(256) void corr_slab_sum_kernel(const float* __restrict__ part,
+                                                            int slabs, int64_t n, int nk,
+                                                            float* __restrict__ cv, int ldcv) {
+  const int64_t total = n * nk;
+  for (int64_t q = blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    float s = part[q];
+    for (int t = 1; t < slabs; ++t) s += part[t * total + q];
+    const int64_t p = q / nk;
+    cv[p * ldcv + (q - p * nk)] = s;
   }
 }
 
 // Gradient of the cost volume w.r.t. one input (gather form, no atomics):
-//   SIGN=+1 (df1): df[p][c] = sum_k dcv[p][k]       * src[p + d_k][c]     (src = f2)
-//   SIGN=-1 (df2): df[q][c] = sum_k dcv[q - d_k][k] * src[q - d_k][c]     (src = f1)
+//   SIGN=+1 (df1): df[p][c] = init[p][c] + sum_k g[p][k]       * src[p + d_k][c]   (src = f2)
+//   SIGN=-1 (df2): df[q][c] = init[q][c] + sum_k g[q - d_k][k] * src[q - d_k][c]   (src = f1)
+struct CorrBwdArgs {
+  const float* g;     // d(cost volume), row stride ldg
+  int ldg;
+  const float* src;
+  int lds;
+  int h, w, c;
+  float* df;
+  int lddf;
+  const float* init;  // NULL, or added to the result (row stride ldinit; may alias df)
+  int ldinit;
+  int vec;            // src / df / init float4 access allowed
+  int slabs;
+};
+
 template <int D, int SIGN>
-__global__ __launch_bounds__(256) void corr_bwd_kernel(const float* __restrict__ dcv, int lddcv,
-                                                       const float* __restrict__ src, int lds,
-                                                       int h, int w, int c,
-                                                       float* __restrict__ df, int lddf,
-                                                       int accumulate, int vec) {
+__global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
   constexpr int ND = 2 * D + 1, NK = ND * ND;
-  constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D;
-  __shared__ float tile[HY * HX * CPS];
-  const int b = blockIdx.z;
+  constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D, NH = HY * HX;
+  constexpr int NQ = NH * (CSLAB / 4), NU = (NQ + 255) / 256;
+  // Coefficient loads: d/d(f1) reads each tile pixel's 49 contiguous g values; d/d(f2) reads,
+  // per offset row i, the 7 contiguous g values of the source pixels that map into the tile.
+  constexpr int GROW = HX * ND;                      // per source row, per offset row i
+  constexpr int NGQ = SIGN > 0 ? CT_PIX * NK : ND * CT_Y * GROW;
+  constexpr int NG = (NGQ + 255) / 256;
+  __shared__ float4 lds4[NH * CSPS / 4];
+  __shared__ float G[NK * CT_PIX];
+  float* tile = reinterpret_cast<float*>(lds4);
+  const int h = a.h, w = a.w;
+  const int b = blockIdx.z / a.slabs, slab = blockIdx.z - b * a.slabs;
+  const int c_lo = slab * CSLAB, cs = min(CSLAB, a.c - c_lo);
   const int y0 = blockIdx.y * CT_Y, x0 = blockIdx.x * CT_X;
-  const int ty = threadIdx.x / CT_X, tx = threadIdx.x % CT_X;
+  const int tid = threadIdx.x;
+  const int pix = tid >> 2, qtr = tid & 3;
+  const int ty = pix / CT_X, tx = pix % CT_X;
   const int y = y0 + ty, x = x0 + tx;
   const bool valid = y < h && x < w;
   const int64_t img = (int64_t)b * h * w;
-  float coef[NK];
+  const int pl = y * w + x;
+  const rsrc_t rg = make_rsrc(a.g + img * a.ldg, (int64_t)h * w * a.ldg * 4);
+  const rsrc_t rs = make_rsrc(a.src + img * a.lds, (int64_t)h * w * a.lds * 4);
+  const rsrc_t ri = make_rsrc(a.init ? a.init + img * a.ldinit : nullptr,
+                              a.init ? (int64_t)h * w * a.ldinit * 4 : 0);
+  // One load round: coefficients, the src halo slab, the init values.
+  float gv[NG];
 #pragma unroll
-  for (int i = 0; i < ND; ++i) {
+  for (int u = 0; u < NG; ++u) {
+    const int q = tid + 256 * u;
+    uint32_t off = kOOB;
+    if (SIGN > 0) {
+      const int p = q / NK, k = q - p * NK;
+      const int sy = y0 + p / CT_X, sx = x0 + p % CT_X;
+      if (q < NGQ && sy < h && sx < w) off = 4 * ((sy * w + sx) * a.ldg + k);
+    } else {
+      const int i = q / (CT_Y * GROW), r0 = q - i * (CT_Y * GROW);
+      const int r = r0 / GROW, rem = r0 - r * GROW;
+      const int hx = rem / ND, j = rem - hx * ND;
+      const int sy = y0 + r + D - i, sx = x0 - D + hx;   // source of target row r
+      if (q < NGQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w)
+        off = 4 * ((sy * w + sx) * a.ldg + i * ND + j);
+    }
+    gv[u] = bload1(rg, off);
+  }
+  float4 hv[NU];
 #pragma unroll
-    for (int j = 0; j < ND; ++j) {
-      const int k = i * ND + j;
-      float v = 0.f;
-      if (valid) {
-        if (SIGN > 0) {
-          v = dcv[(img + (int64_t)y * w + x) * lddcv + k];
-        } else {
-          const int sy = y - (i - D), sx = x - (j - D);
-          if ((unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w)
-            v = dcv[(img + (int64_t)sy * w + sx) * lddcv + k];
-        }
-      }
-      coef[k] = v;
+  for (int u = 0; u < NU; ++u) {
+    const int q = tid + 256 * u;
+    const int hp = q >> 4, cq = q & 15;
+    const int sy = y0 - D + hp / HX, sx = x0 - D + hp % HX;
+    const bool ok = q < NQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
+    hv[u] = bload_quad(rs, ok, 4 * ((sy * w + sx) * a.lds + c_lo + 4 * cq), cs - 4 * cq, a.vec);
+  }
+  float acc[16];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ch = qtr * 16 + 4 * e;
+    const float4 v = bload_quad(ri, valid, 4 * (pl * a.ldinit + c_lo + ch), cs - ch, a.vec);
+    acc[4 * e] = v.x;
+    acc[4 * e + 1] = v.y;
+    acc[4 * e + 2] = v.z;
+    acc[4 * e + 3] = v.w;
+  }
+#pragma unroll
+  for (int u = 0; u < NG; ++u) {
+    const int q = tid + 256 * u;
+    if (SIGN > 0) {
+      const int p = q / NK, k = q - p * NK;
+      if (q < NGQ) G[k * CT_PIX + p] = gv[u];
+    } else {
+      const int i = q / (CT_Y * GROW), r0 = q - i * (CT_Y * GROW);
+      const int r = r0 / GROW, rem = r0 - r * GROW;
+      const int hx = rem / ND, j = rem - hx * ND;
+      const int tx2 = hx + j - 2 * D;                  // target column
+      if (q < NGQ && (unsigned)tx2 < (unsigned)CT_X) G[(i * ND + j) * CT_PIX + r * CT_X + tx2] = gv[u];
     }
   }
-  for (int c0 = 0; c0 < c; c0 += CC) {
-    const int cc = min(CC, c - c0);
-    __syncthreads();
-    for (int q = threadIdx.x; q < HY * HX * (CC / 4); q += 256) {
-      const int pix = q / (CC / 4), cq = q % (CC / 4);
-      const int hy = pix / HX, hx = pix % HX;
-      const int sy = y0 - D + hy, sx = x0 - D + hx;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if ((unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w && 4 * cq < cc) {
-        const float* s = src + (img + (int64_t)sy * w + sx) * lds + c0 + 4 * cq;
-        if (vec && 4 * cq + 4 <= cc) {
-          v = *reinterpret_cast<const float4*>(s);
-        } else {
-          float t[4] = {0.f, 0.f, 0.f, 0.f};
-          for (int e = 0; e < cc - 4 * cq; ++e) t[e] = s[e];
-          v = make_float4(t[0], t[1], t[2], t[3]);
-        }
-      }
-      *reinterpret_cast<float4*>(&tile[pix * CPS + 4 * cq]) = v;
-    }
-    __syncthreads();
-    float acc[CC];
 #pragma unroll
-    for (int e = 0; e < CC; ++e) acc[e] = 0.f;
+  for (int u = 0; u < NU; ++u) {
+    const int q = tid + 256 * u;
+    if (q < NQ) *reinterpret_cast<float4*>(&tile[(q >> 4) * CSPS + 4 * (q & 15)]) = hv[u];
+  }
+  __syncthreads();
+  // One channel quad per pass (not unrolled): bounds the LDS reads the scheduler can hoist.
+#pragma unroll 1
+  for (int e = 0; e < 4; ++e) {
+    float4 s4[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    const float* tb = &tile[(ty * HX + tx) * CSPS + qtr * 16 + 4 * e];
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
         const int oy = SIGN > 0 ? i : 2 * D - i;   // tile row of src[p + SIGN*d]
         const int ox = SIGN > 0 ? j : 2 * D - j;
-        const float* t = &tile[((ty + oy) * HX + tx + ox) * CPS];
-        const float cf = coef[i * ND + j];
-#pragma unroll
-        for (int e = 0; e < CC; e += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(t + e);
-          acc[e] = fmaf(cf, v.x, acc[e]);
-          acc[e + 1] = fmaf(cf, v.y, acc[e + 1]);
-          acc[e + 2] = fmaf(cf, v.z, acc[e + 2]);
-          acc[e + 3] = fmaf(cf, v.w, acc[e + 3]);
-        }
+        const float4 v = *reinterpret_cast<const float4*>(tb + (oy * HX + ox) * CSPS);
+        const float cf = G[(i * ND + j) * CT_PIX + pix];
+        float4& sa = s4[(i * ND + j) & 1];   // two chains: halves the FMA dependency depth
+        sa.x = fmaf(cf, v.x, sa.x);
+        sa.y = fmaf(cf, v.y, sa.y);
+        sa.z = fmaf(cf, v.z, sa.z);
+        sa.w = fmaf(cf, v.w, sa.w);
       }
     }
-    if (valid) {
-      float* o = df + (img + (int64_t)y * w + x) * lddf + c0;
-      for (int e = 0; e < cc; ++e) o[e] = accumulate ? o[e] + acc[e] : acc[e];
+    // acc[4e..4e+3] += s4 (register index must stay static: select by e)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q == e) {
+        acc[4 * q] += s4[0].x + s4[1].x;
+        acc[4 * q + 1] += s4[0].y + s4[1].y;
+        acc[4 * q + 2] += s4[0].z + s4[1].z;
+        acc[4 * q + 3] += s4[0].w + s4[1].w;
+      }
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ch = qtr * 16 + 4 * e;
+      float* o = a.df + (img + pl) * a.lddf + c_lo + ch;
+      if (a.vec && cs - ch >= 4) {
+        *reinterpret_cast<float4*>(o) = make_float4(acc[4 * e], acc[4 * e + 1], acc[4 * e + 2],
+                                                    acc[4 * e + 3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k < cs - ch) o[k] = acc[4 * e + k];
+      }
     }
   }
 }
@@ -583,17 +726,61 @@ using namespace oflow;
 
 extern "C" {
 
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static size_t corr_fwd_ws(int n, int h, int w, int c) {
+  const int slabs = (int)cdiv(c, CSLAB);
+  return slabs > 1 ? (size_t)slabs * n * h * w * 49 * sizeof(float) : 0;
+}
+
+static int corr_fwd_launch(CorrFwdArgs a, int n, void* ws, size_t ws_bytes, void* stream) {
+  OF_CHECK_ARG((int64_t)a.h * a.w * std::max(std::max(a.ld1, a.ld2), a.ldcv) < (1LL << 29),
+               "corr: one image must hold < 2^29 elements (32-bit buffer offsets)");
+  a.slabs = (int)cdiv(a.c, CSLAB);
+  const size_t need = corr_fwd_ws(n, a.h, a.w, a.c);
+  OF_CHECK_ARG(ws_bytes >= need && (need == 0 || ws), "corr fwd: workspace too small");
+  a.part = static_cast<float*>(ws);
+  hipStream_t s = as_stream(stream);
+  dim3 grid(cdiv(a.w, CT_X), cdiv(a.h, CT_Y), n * a.slabs);
+  hipLaunchKernelGGL(corr_fwd_kernel<3>, grid, dim3(256), 0, s, a);
+  int st = check_launch("corr_fwd");
+  if (st || a.slabs == 1) return st;
+  const int64_t npix = (int64_t)n * a.h * a.w;
+  hipLaunchKernelGGL(corr_slab_sum_kernel, dim3(grid_for(npix * 49)), dim3(256), 0, s, a.part,
+                     a.slabs, npix, 49, a.cv, a.ldcv);
+  return check_launch("corr_slab_sum");
+}
+
+static int corr_bwd_launch(int sign, CorrBwdArgs a, int n, hipStream_t s) {
+  OF_CHECK_ARG((int64_t)a.h * a.w * std::max(std::max(a.ldg, a.lds), std::max(a.lddf, a.ldinit)) <
+                   (1LL << 29),
+               "corr: one image must hold < 2^29 elements (32-bit buffer offsets)");
+  a.slabs = (int)cdiv(a.c, CSLAB);
+  dim3 grid(cdiv(a.w, CT_X), cdiv(a.h, CT_Y), n * a.slabs);
+  if (sign > 0)
+    hipLaunchKernelGGL((corr_bwd_kernel<3, 1>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((corr_bwd_kernel<3, -1>), grid, dim3(256), 0, s, a);
+  return check_launch(sign > 0 ? "corr_bwd_f1" : "corr_bwd_f2");
+}
+
+size_t of_corr_fwd_workspace(int n, int h, int w, int c, int max_disp) {
+  (void)max_disp;
+  return n > 0 && h > 0 && w > 0 && c > 0 ? corr_fwd_ws(n, h, w, c) : 0;
+}
+
 int of_corr_fwd(const float* f1, int ld1, const float* f2, int ld2, int n, int h, int w, int c,
-                int max_disp, float* out, int ldo, void* stream) {
+                int max_disp, float* out, int ldo, void* workspace, size_t ws_bytes,
+                void* stream) {
   OF_CHECK_ARG(f1 && f2 && out, "corr fwd: NULL pointer");
   OF_CHECK_ARG(max_disp == 3, "corr: only max_disp=3 (the reference default) is compiled");
   OF_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0, "corr fwd: dims");
   OF_CHECK_ARG(ld1 >= c && ld2 >= c && ldo >= 49, "corr fwd: strides");
-  const int vec = (ld2 % 4 == 0 && ((uintptr_t)f2 & 15) == 0) ? 1 : 0;
-  dim3 grid(cdiv(w, CT_X), cdiv(h, CT_Y), n);
-  hipLaunchKernelGGL(corr_fwd_kernel<3>, grid, dim3(256), 0, as_stream(stream), f1, ld1, f2, ld2,
-                     h, w, c, out, ldo, vec);
-  return check_launch("corr_fwd");
+  CorrFwdArgs a{};
+  a.f1 = f1, a.ld1 = ld1, a.f2 = f2, a.ld2 = ld2, a.h = h, a.w = w, a.c = c;
+  a.cv = out, a.ldcv = ldo;
+  a.vec = ld1 % 4 == 0 && ld2 % 4 == 0 && al16(f1) && al16(f2);
+  return corr_fwd_launch(a, n, workspace, ws_bytes, stream);
 }
 
 int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const float* f2, int ld2,
@@ -601,22 +788,63 @@ int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const flo
                 float* df2, int lddf2, int acc2, void* stream) {
   OF_CHECK_ARG(dcv && f1 && f2, "corr bwd: NULL pointer");
   OF_CHECK_ARG(max_disp == 3, "corr: only max_disp=3 (the reference default) is compiled");
-  OF_CHECK_ARG(ld1 >= c && ld2 >= c, "corr bwd: strides");
-  const int vec1 = (ld1 % 4 == 0 && ((uintptr_t)f1 & 15) == 0) ? 1 : 0;
-  const int vec2 = (ld2 % 4 == 0 && ((uintptr_t)f2 & 15) == 0) ? 1 : 0;
-  dim3 grid(cdiv(w, CT_X), cdiv(h, CT_Y), n);
+  OF_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0, "corr bwd: dims");
+  OF_CHECK_ARG(ld1 >= c && ld2 >= c && lddcv >= 49, "corr bwd: strides");
   hipStream_t s = as_stream(stream);
   int st;
   if (df1) {
-    hipLaunchKernelGGL((corr_bwd_kernel<3, 1>), grid, dim3(256), 0, s, dcv, lddcv, f2, ld2, h, w,
-                       c, df1, lddf1, acc1, vec2);
-    if ((st = check_launch("corr_bwd_f1"))) return st;
+    OF_CHECK_ARG(lddf1 >= c, "corr bwd: df1 stride");
+    CorrBwdArgs a{};
+    a.g = dcv, a.ldg = lddcv, a.src = f2, a.lds = ld2, a.h = h, a.w = w, a.c = c;
+    a.df = df1, a.lddf = lddf1, a.init = acc1 ? df1 : nullptr, a.ldinit = lddf1;
+    a.vec = ld2 % 4 == 0 && lddf1 % 4 == 0 && al16(f2) && al16(df1);
+    if ((st = corr_bwd_launch(1, a, n, s))) return st;
   }
   if (df2) {
-    hipLaunchKernelGGL((corr_bwd_kernel<3, -1>), grid, dim3(256), 0, s, dcv, lddcv, f1, ld1, h,
-                       w, c, df2, lddf2, acc2, vec1);
-    if ((st = check_launch("corr_bwd_f2"))) return st;
+    OF_CHECK_ARG(lddf2 >= c, "corr bwd: df2 stride");
+    CorrBwdArgs a{};
+    a.g = dcv, a.ldg = lddcv, a.src = f1, a.lds = ld1, a.h = h, a.w = w, a.c = c;
+    a.df = df2, a.lddf = lddf2, a.init = acc2 ? df2 : nullptr, a.ldinit = lddf2;
+    a.vec = ld1 % 4 == 0 && lddf2 % 4 == 0 && al16(f1) && al16(df2);
+    if ((st = corr_bwd_launch(-1, a, n, s))) return st;
   }
+  return OF_OK;
+}
+
+int of_corr_concat_fwd(const float* f1, const float* f2, const float* flow, int n, int h, int w,
+                       int c, int max_disp, float* cat, int cp, void* workspace, size_t ws_bytes,
+                       void* stream) {
+  OF_CHECK_ARG(f1 && f2 && cat, "corr concat fwd: NULL pointer");
+  OF_CHECK_ARG(max_disp == 3, "corr: only max_disp=3 (the reference default) is compiled");
+  OF_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0, "corr concat fwd: dims");
+  OF_CHECK_ARG(cp >= c + 49 + (flow ? 2 : 0), "corr concat fwd: cp too small");
+  CorrFwdArgs a{};
+  a.f1 = f1, a.ld1 = c, a.f2 = f2, a.ld2 = c, a.h = h, a.w = w, a.c = c;
+  a.cv = cat + c, a.ldcv = cp, a.cat = cat, a.flow = flow;
+  a.vec = c % 4 == 0 && cp % 4 == 0 && al16(f1) && al16(f2) && al16(cat);
+  return corr_fwd_launch(a, n, workspace, ws_bytes, stream);
+}
+
+int of_corr_concat_bwd(const float* dcat, int cp, const float* f1, const float* f2, int n, int h,
+                       int w, int c, int max_disp, float* df1, float* df2, float* dflow,
+                       void* stream) {
+  OF_CHECK_ARG(dcat && f1 && f2 && df1, "corr concat bwd: NULL pointer");
+  OF_CHECK_ARG(max_disp == 3, "corr: only max_disp=3 (the reference default) is compiled");
+  OF_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0, "corr concat bwd: dims");
+  OF_CHECK_ARG(cp >= c + 49 + (dflow ? 2 : 0), "corr concat bwd: cp too small");
+  hipStream_t s = as_stream(stream);
+  const bool vec = c % 4 == 0 && cp % 4 == 0 && al16(f1) && al16(f2) && al16(dcat) && al16(df1);
+  int st;
+  CorrBwdArgs a{};
+  a.g = dcat + c, a.ldg = cp, a.src = f2, a.lds = c, a.h = h, a.w = w, a.c = c;
+  a.df = df1, a.lddf = c, a.init = dcat, a.ldinit = cp, a.vec = vec;
+  if ((st = corr_bwd_launch(1, a, n, s))) return st;
+  if (df2) {
+    a.src = f1, a.df = df2, a.init = nullptr, a.vec = vec && al16(df2);
+    if ((st = corr_bwd_launch(-1, a, n, s))) return st;
+  }
+  if (dflow)
+    return of_copy_strided(dcat + c + 49, cp, dflow, 2, (int64_t)n * h * w, 2, stream);
   return OF_OK;
 }
 

@@ -435,8 +435,9 @@ class _CostVolume(torch.autograd.Function):
         n, h, w, c = f1.shape
         nk = (2 * max_disp + 1) ** 2
         out = torch.empty((n, h, w, nk), device=f1.device)
-        call("of_corr_fwd", _ptr(f1), c, _ptr(f2), c, n, h, w, c, max_disp, _ptr(out), nk,
-             _stream())
+        ws, wp, wb = _workspace(_lib.lib().of_corr_fwd_workspace(n, h, w, c, max_disp), f1.device)
+        call("of_corr_fwd", _ptr(f1), c, _ptr(f2), c, n, h, w, c, max_disp, _ptr(out), nk, wp,
+             wb, _stream())
         ctx.save_for_backward(f1, f2)
         ctx.max_disp = max_disp
         return out
@@ -459,8 +460,9 @@ def cost_volume(f1, f2, max_disp=3):
 
 class _CorrConcat(torch.autograd.Function):
     """The flow-module input ``concat([features1, cost_volume, flow_up])`` (model.py:97-102)
-    built in one zero-padded NHWC buffer of ``cp`` channels: the cost volume kernel writes
-    straight into its channel slice (virtual concat, no separate concat pass)."""
+    built in one zero-padded NHWC buffer of ``cp`` channels by one kernel (f1 copy, cost
+    volume, flow and padding per pixel row); the backward reads the f1 slice of the gradient
+    as the initial value of df1 (no copy or concat passes)."""
 
     @staticmethod
     def forward(ctx, f1, f2w, flow_up, max_disp, cp):
@@ -471,16 +473,10 @@ class _CorrConcat(torch.autograd.Function):
         used = c + nk + (2 if flow_up is not None else 0)
         assert used <= cp
         x = torch.empty((n, h, w, cp), device=f1.device)
-        s = _stream()
-        if used < cp:
-            call("of_fill", _ptr(x), 0.0, x.numel(), s)
-        call("of_copy_strided", _ptr(f1), c, _ptr(x), cp, n * h * w, c, s)
-        call("of_corr_fwd", _ptr(f1), c, _ptr(f2w), c, n, h, w, c, max_disp,
-             C.c_void_p(x.data_ptr() + 4 * c), cp, s)
-        if flow_up is not None:
-            fu = flow_up.contiguous()
-            call("of_copy_strided", _ptr(fu), 2, C.c_void_p(x.data_ptr() + 4 * (c + nk)), cp,
-                 n * h * w, 2, s)
+        fu = flow_up.contiguous() if flow_up is not None else None
+        ws, wp, wb = _workspace(_lib.lib().of_corr_fwd_workspace(n, h, w, c, max_disp), f1.device)
+        call("of_corr_concat_fwd", _ptr(f1), _ptr(f2w), _ptr(fu), n, h, w, c, max_disp, _ptr(x),
+             cp, wp, wb, _stream())
         ctx.save_for_backward(f1, f2w)
         ctx.meta = (max_disp, cp, nk, flow_up is not None)
         return x
@@ -491,17 +487,13 @@ class _CorrConcat(torch.autograd.Function):
         max_disp, cp, nk, has_flow = ctx.meta
         n, h, w, c = f1.shape
         dx = dx.contiguous()
-        s = _stream()
         df1 = torch.empty_like(f1)
-        call("of_copy_strided", _ptr(dx), cp, _ptr(df1), c, n * h * w, c, s)
         df2 = torch.empty_like(f2w) if ctx.needs_input_grad[1] else None
-        call("of_corr_bwd", C.c_void_p(dx.data_ptr() + 4 * c), cp, _ptr(f1), c, _ptr(f2w), c, n,
-             h, w, c, max_disp, _ptr(df1), c, 1, _ptr(df2), c, 0, s)
         dflow = None
         if has_flow and ctx.needs_input_grad[2]:
             dflow = torch.empty((n, h, w, 2), device=dx.device)
-            call("of_copy_strided", C.c_void_p(dx.data_ptr() + 4 * (c + nk)), cp, _ptr(dflow), 2,
-                 n * h * w, 2, s)
+        call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c, max_disp,
+             _ptr(df1), _ptr(df2), _ptr(dflow), _stream())
         return df1, df2, dflow, None, None
 
 

@@ -85,7 +85,7 @@ def test_conv_fwd_bwd(case):
 
 
 # ----------------------------------------------------------------------- cost volume ----
-@pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6)])
+@pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6), (1, 19, 70, 32)])
 def test_cost_volume(shape):
     ops = _ops()
     f1, f2 = rng_tensor(shape, 1), rng_tensor(shape, 2)
@@ -101,22 +101,31 @@ def test_cost_volume(shape):
     assert rel_inf(bd.grad, b.grad) < REL_TOL
 
 
-def test_corr_concat():
+@pytest.mark.parametrize("n,h,w,c,cp,has_flow", [(2, 8, 12, 64, 116, True),
+                                                  (1, 19, 70, 64, 120, True),
+                                                  (2, 24, 32, 256, 308, False),
+                                                  (1, 9, 35, 6, 60, True)])
+def test_corr_concat(n, h, w, c, cp, has_flow):
+    """The fused concat([f1, cost volume, flow]) kernel and its gradient, multi-tile and
+    ragged shapes (tile 8x32 + halo), with and without flow, float4 and scalar paths."""
     ops = _ops()
-    n, h, w, c = 2, 8, 12, 64
     f1, f2, fl = rng_tensor((n, h, w, c), 4), rng_tensor((n, h, w, c), 5), rng_tensor((n, h, w, 2), 6)
     a, b, fo = [f64(t).requires_grad_(True) for t in (f1, f2, fl)]
-    xo = torch.cat([a, R.create_cost_volume(a, b, 3), fo], -1)
+    parts = [a, R.create_cost_volume(a, b, 3)] + ([fo] if has_flow else [])
+    xo = torch.cat(parts, -1)
+    used = xo.shape[-1]
     g = rng_tensor(tuple(xo.shape), 7)
     (xo * f64(g)).sum().backward()
     ad, bd, fd = [dev(t).requires_grad_(True) for t in (f1, f2, fl)]
-    xd = ops.corr_concat(ad, bd, fd, 3, 116)
-    assert rel_inf(xd[..., :115], xo) < REL_TOL
-    assert xd[..., 115:].abs().max().item() == 0
-    gd = torch.zeros((n, h, w, 116), device="cuda")
-    gd[..., :115] = dev(g)
+    xd = ops.corr_concat(ad, bd, fd if has_flow else None, 3, cp)
+    assert rel_inf(xd[..., :used], xo) < REL_TOL
+    assert xd[..., used:].abs().max().item() == 0
+    gd = torch.zeros((n, h, w, cp), device="cuda")
+    gd[..., :used] = dev(g)
+    gd[..., used:] = 1.0        # gradient on the padding must not leak anywhere
     (xd * gd).sum().backward()
-    for d_, o_ in ((ad, a), (bd, b), (fd, fo)):
+    pairs = ((ad, a), (bd, b)) + (((fd, fo),) if has_flow else ())
+    for d_, o_ in pairs:
         assert rel_inf(d_.grad, o_.grad) < REL_TOL
 
 
