@@ -24,6 +24,14 @@ inline int64_t round_up(int64_t a, int64_t b) { return cdiv(a, b) * b; }
 
 constexpr int kWave = 64;
 
+// XCD-aware bijective block remap (cdna guide T1): the hardware deals workgroups to the 8
+// XCDs round-robin; this maps them so that each XCD gets a contiguous range of work ids,
+// i.e. neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 // Raw buffer loads (CDNA buffer resource, 32-bit byte offsets).  An offset at or past the
 // resource's byte count returns 0 without a branch: padding and halo reads stay straight-line
 // code, so the compiler keeps every load of a staging round in flight (a guarded pointer
@@ -42,15 +50,11 @@ __device__ __forceinline__ float bload1(rsrc_t r, uint32_t voff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
 }
 // Channel quad at byte offset `off` with `n` valid channels (n >= 4: all), zero elsewhere;
-// `ok` false -> zeros.  vec: 16-byte aligned rows (one b128), else four b32.
-__device__ __forceinline__ float4 bload_quad(rsrc_t r, bool ok, uint32_t off, int n, int vec) {
-  if (vec) {
-    float4 v = bload4(r, ok && n > 0 ? off : kOOB);
-    v.y = n > 1 ? v.y : 0.f;
-    v.z = n > 2 ? v.z : 0.f;
-    v.w = n > 3 ? v.w : 0.f;
-    return v;
-  }
+// `ok` false -> zeros.  vec: 16-byte aligned rows and whole quads (the caller guarantees
+// n <= 0 or n >= 4), one b128 and no selects on the loaded value -- a select right after
+// the load would force an s_waitcnt there; else four b32, each masked by its offset.
+__device__ __forceinline__ float4 bload_quad(rsrc_t r, bool ok, uint32_t off, int n, bool vec) {
+  if (vec) return bload4(r, ok && n > 0 ? off : kOOB);
   return make_float4(bload1(r, ok && n > 0 ? off : kOOB), bload1(r, ok && n > 1 ? off + 4 : kOOB),
                      bload1(r, ok && n > 2 ? off + 8 : kOOB),
                      bload1(r, ok && n > 3 ? off + 12 : kOOB));

@@ -156,12 +156,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   // XCD-aware bijective remap: consecutive work ids -> one XCD's L2 (cdna guide T1).
-  int wgid;
-  {
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   // work id = split * tiles_total + tile: all tiles of one K slice are consecutive.
   const int split = wgid / a.tiles_total;
   const int tile = wgid - split * a.tiles_total;

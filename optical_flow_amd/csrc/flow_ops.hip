@@ -40,13 +40,14 @@ struct CorrFwdArgs {
   int ldcv;
   int vec;            // float4 global access allowed (strides and bases 16-byte aligned)
   int slabs;          // ceil(c / 64)
+  int tiles_x, tiles_y;
   float* part;        // slabs > 1: partial sums [slab][n*h*w][49]
   // Flow-module concat (model.py:97-102), optional: cat row = [f1 | cv | flow | zero pad].
   float* cat;         // row stride ldcv; cv == cat + c
   const float* flow;  // (.., 2) or NULL
 };
 
-template <int D>
+template <int D, bool VEC>
 __global__ __launch_bounds__(256, 2) void corr_fwd_kernel(CorrFwdArgs a) {
   constexpr int ND = 2 * D + 1, NK = ND * ND;
   constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D, NH = HY * HX;
@@ -54,9 +55,12 @@ __global__ __launch_bounds__(256, 2) void corr_fwd_kernel(CorrFwdArgs a) {
   __shared__ float4 lds4[NH * CSPS / 4];
   float* tile = reinterpret_cast<float*>(lds4);
   const int h = a.h, w = a.w;
-  const int b = blockIdx.z / a.slabs, slab = blockIdx.z - b * a.slabs;
+  // 1-D grid, XCD-aware: neighbouring tiles (shared halo rows) run on one XCD's L2.
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tl = wg % (a.tiles_x * a.tiles_y), z = wg / (a.tiles_x * a.tiles_y);
+  const int b = z / a.slabs, slab = z - b * a.slabs;
   const int c_lo = slab * CSLAB, cs = min(CSLAB, a.c - c_lo);
-  const int y0 = blockIdx.y * CT_Y, x0 = blockIdx.x * CT_X;
+  const int y0 = (tl / a.tiles_x) * CT_Y, x0 = (tl % a.tiles_x) * CT_X;
   const int tid = threadIdx.x;
   const int pix = tid >> 2, qtr = tid & 3;
   const int ty = pix / CT_X, tx = pix % CT_X;
@@ -74,14 +78,14 @@ __global__ __launch_bounds__(256, 2) void corr_fwd_kernel(CorrFwdArgs a) {
     const int hp = q >> 4, cq = q & 15;
     const int sy = y0 - D + hp / HX, sx = x0 - D + hp % HX;
     const bool ok = q < NQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
-    hv[u] = bload_quad(r2, ok, 4 * ((sy * w + sx) * a.ld2 + c_lo + 4 * cq), cs - 4 * cq, a.vec);
+    hv[u] = bload_quad(r2, ok, 4 * ((sy * w + sx) * a.ld2 + c_lo + 4 * cq), cs - 4 * cq, VEC);
   }
   f32x2 f[8];
   float4 fq[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int ch = qtr * 16 + 4 * e;
-    fq[e] = bload_quad(r1, valid, 4 * (pl * a.ld1 + c_lo + ch), cs - ch, a.vec);
+    fq[e] = bload_quad(r1, valid, 4 * (pl * a.ld1 + c_lo + ch), cs - ch, VEC);
     f[2 * e] = f32x2{fq[e].x, fq[e].y};
     f[2 * e + 1] = f32x2{fq[e].z, fq[e].w};
   }
@@ -95,7 +99,7 @@ __global__ __launch_bounds__(256, 2) void corr_fwd_kernel(CorrFwdArgs a) {
     for (int e = 0; e < 4; ++e) {
       const int ch = qtr * 16 + 4 * e;
       float* dst = a.cat + (img + pl) * a.ldcv + c_lo + ch;
-      if (a.vec && cs - ch >= 4) {
+      if (VEC && cs - ch >= 4) {
         *reinterpret_cast<float4*>(dst) = fq[e];
       } else {
         const float t[4] = {fq[e].x, fq[e].y, fq[e].z, fq[e].w};
@@ -126,17 +130,30 @@ __global__ __launch_bounds__(256, 2) void corr_fwd_kernel(CorrFwdArgs a) {
       }
     }
   }
-  float* out;
-  if (a.slabs == 1) {
-    out = a.cv + (img + pl) * a.ldcv;
-  } else {
-    const int64_t npix = (int64_t)(gridDim.z / a.slabs) * h * w;
-    out = a.part + (slab * npix + img + pl) * NK;
-  }
+  // Quad sums -> LDS [pixel][49] (odd stride: conflict-free) -> stores as contiguous runs.
+  __syncthreads();                             // halo tile no longer read
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const float v = quad_sum(acc[k].x + acc[k].y);
-    if (valid && (k & 3) == qtr) out[k] = v;
+    if ((k & 3) == qtr) tile[pix * NK + k] = v;
+  }
+  __syncthreads();
+  {
+    float* out;
+    int64_t ld;
+    if (a.slabs == 1) {
+      out = a.cv;
+      ld = a.ldcv;
+    } else {
+      const int64_t npix = (int64_t)(gridDim.x / (a.tiles_x * a.tiles_y * a.slabs)) * h * w;
+      out = a.part + slab * npix * NK;
+      ld = NK;
+    }
+    for (int q = tid; q < CT_PIX * NK; q += 256) {
+      const int p = q / NK, k = q - p * NK;
+      const int sy = y0 + p / CT_X, sx = x0 + p % CT_X;
+      if (sy < h && sx < w) out[(img + sy * w + sx) * ld + k] = tile[q];
+    }
   }
   if (a.cat && slab == 0 && qtr == 0 && valid) {   // flow and zero channel padding
     float* row = a.cat + (img + pl) * a.ldcv;
@@ -178,9 +195,10 @@ struct CorrBwdArgs {
   int ldinit;
   int vec;            // src / df / init float4 access allowed
   int slabs;
+  int tiles_x, tiles_y;
 };
 
-template <int D, int SIGN>
+template <int D, int SIGN, bool VEC>
 __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
   constexpr int ND = 2 * D + 1, NK = ND * ND;
   constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D, NH = HY * HX;
@@ -194,9 +212,12 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
   __shared__ float G[NK * CT_PIX];
   float* tile = reinterpret_cast<float*>(lds4);
   const int h = a.h, w = a.w;
-  const int b = blockIdx.z / a.slabs, slab = blockIdx.z - b * a.slabs;
+  // 1-D grid, XCD-aware: neighbouring tiles (shared halo rows) run on one XCD's L2.
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tl = wg % (a.tiles_x * a.tiles_y), z = wg / (a.tiles_x * a.tiles_y);
+  const int b = z / a.slabs, slab = z - b * a.slabs;
   const int c_lo = slab * CSLAB, cs = min(CSLAB, a.c - c_lo);
-  const int y0 = blockIdx.y * CT_Y, x0 = blockIdx.x * CT_X;
+  const int y0 = (tl / a.tiles_x) * CT_Y, x0 = (tl % a.tiles_x) * CT_X;
   const int tid = threadIdx.x;
   const int pix = tid >> 2, qtr = tid & 3;
   const int ty = pix / CT_X, tx = pix % CT_X;
@@ -235,13 +256,13 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
     const int hp = q >> 4, cq = q & 15;
     const int sy = y0 - D + hp / HX, sx = x0 - D + hp % HX;
     const bool ok = q < NQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
-    hv[u] = bload_quad(rs, ok, 4 * ((sy * w + sx) * a.lds + c_lo + 4 * cq), cs - 4 * cq, a.vec);
+    hv[u] = bload_quad(rs, ok, 4 * ((sy * w + sx) * a.lds + c_lo + 4 * cq), cs - 4 * cq, VEC);
   }
   float acc[16];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int ch = qtr * 16 + 4 * e;
-    const float4 v = bload_quad(ri, valid, 4 * (pl * a.ldinit + c_lo + ch), cs - ch, a.vec);
+    const float4 v = bload_quad(ri, valid, 4 * (pl * a.ldinit + c_lo + ch), cs - ch, VEC);
     acc[4 * e] = v.x;
     acc[4 * e + 1] = v.y;
     acc[4 * e + 2] = v.z;
@@ -303,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
     for (int e = 0; e < 4; ++e) {
       const int ch = qtr * 16 + 4 * e;
       float* o = a.df + (img + pl) * a.lddf + c_lo + ch;
-      if (a.vec && cs - ch >= 4) {
+      if (VEC && cs - ch >= 4) {
         *reinterpret_cast<float4*>(o) = make_float4(acc[4 * e], acc[4 * e + 1], acc[4 * e + 2],
                                                     acc[4 * e + 3]);
       } else {
@@ -741,8 +762,12 @@ static int corr_fwd_launch(CorrFwdArgs a, int n, void* ws, size_t ws_bytes, void
   OF_CHECK_ARG(ws_bytes >= need && (need == 0 || ws), "corr fwd: workspace too small");
   a.part = static_cast<float*>(ws);
   hipStream_t s = as_stream(stream);
-  dim3 grid(cdiv(a.w, CT_X), cdiv(a.h, CT_Y), n * a.slabs);
-  hipLaunchKernelGGL(corr_fwd_kernel<3>, grid, dim3(256), 0, s, a);
+  a.tiles_x = (int)cdiv(a.w, CT_X), a.tiles_y = (int)cdiv(a.h, CT_Y);
+  const dim3 grid((unsigned)((int64_t)a.tiles_x * a.tiles_y * n * a.slabs));
+  if (a.vec)
+    hipLaunchKernelGGL((corr_fwd_kernel<3, true>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((corr_fwd_kernel<3, false>), grid, dim3(256), 0, s, a);
   int st = check_launch("corr_fwd");
   if (st || a.slabs == 1) return st;
   const int64_t npix = (int64_t)n * a.h * a.w;
@@ -756,11 +781,16 @@ static int corr_bwd_launch(int sign, CorrBwdArgs a, int n, hipStream_t s) {
                    (1LL << 29),
                "corr: one image must hold < 2^29 elements (32-bit buffer offsets)");
   a.slabs = (int)cdiv(a.c, CSLAB);
-  dim3 grid(cdiv(a.w, CT_X), cdiv(a.h, CT_Y), n * a.slabs);
-  if (sign > 0)
-    hipLaunchKernelGGL((corr_bwd_kernel<3, 1>), grid, dim3(256), 0, s, a);
+  a.tiles_x = (int)cdiv(a.w, CT_X), a.tiles_y = (int)cdiv(a.h, CT_Y);
+  const dim3 grid((unsigned)((int64_t)a.tiles_x * a.tiles_y * n * a.slabs));
+  if (sign > 0 && a.vec)
+    hipLaunchKernelGGL((corr_bwd_kernel<3, 1, true>), grid, dim3(256), 0, s, a);
+  else if (sign > 0)
+    hipLaunchKernelGGL((corr_bwd_kernel<3, 1, false>), grid, dim3(256), 0, s, a);
+  else if (a.vec)
+    hipLaunchKernelGGL((corr_bwd_kernel<3, -1, true>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((corr_bwd_kernel<3, -1>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((corr_bwd_kernel<3, -1, false>), grid, dim3(256), 0, s, a);
   return check_launch(sign > 0 ? "corr_bwd_f1" : "corr_bwd_f2");
 }
 
@@ -779,7 +809,7 @@ int of_corr_fwd(const float* f1, int ld1, const float* f2, int ld2, int n, int h
   CorrFwdArgs a{};
   a.f1 = f1, a.ld1 = ld1, a.f2 = f2, a.ld2 = ld2, a.h = h, a.w = w, a.c = c;
   a.cv = out, a.ldcv = ldo;
-  a.vec = ld1 % 4 == 0 && ld2 % 4 == 0 && al16(f1) && al16(f2);
+  a.vec = c % 4 == 0 && ld1 % 4 == 0 && ld2 % 4 == 0 && al16(f1) && al16(f2);
   return corr_fwd_launch(a, n, workspace, ws_bytes, stream);
 }
 
@@ -797,7 +827,7 @@ int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const flo
     CorrBwdArgs a{};
     a.g = dcv, a.ldg = lddcv, a.src = f2, a.lds = ld2, a.h = h, a.w = w, a.c = c;
     a.df = df1, a.lddf = lddf1, a.init = acc1 ? df1 : nullptr, a.ldinit = lddf1;
-    a.vec = ld2 % 4 == 0 && lddf1 % 4 == 0 && al16(f2) && al16(df1);
+    a.vec = c % 4 == 0 && ld2 % 4 == 0 && lddf1 % 4 == 0 && al16(f2) && al16(df1);
     if ((st = corr_bwd_launch(1, a, n, s))) return st;
   }
   if (df2) {
@@ -805,7 +835,7 @@ int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const flo
     CorrBwdArgs a{};
     a.g = dcv, a.ldg = lddcv, a.src = f1, a.lds = ld1, a.h = h, a.w = w, a.c = c;
     a.df = df2, a.lddf = lddf2, a.init = acc2 ? df2 : nullptr, a.ldinit = lddf2;
-    a.vec = ld1 % 4 == 0 && lddf2 % 4 == 0 && al16(f1) && al16(df2);
+    a.vec = c % 4 == 0 && ld1 % 4 == 0 && lddf2 % 4 == 0 && al16(f1) && al16(df2);
     if ((st = corr_bwd_launch(-1, a, n, s))) return st;
   }
   return OF_OK;

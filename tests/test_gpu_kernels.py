@@ -104,10 +104,15 @@ def test_cost_volume(shape):
 @pytest.mark.parametrize("n,h,w,c,cp,has_flow", [(2, 8, 12, 64, 116, True),
                                                   (1, 19, 70, 64, 120, True),
                                                   (2, 24, 32, 256, 308, False),
-                                                  (1, 9, 35, 6, 60, True)])
+                                                  (1, 9, 35, 6, 60, True),
+                                                  # h >= 96: the strip-sweep kernels
+                                                  (1, 100, 40, 64, 116, True),
+                                                  (2, 97, 33, 128, 180, True),
+                                                  (1, 96, 20, 6, 60, False)])
 def test_corr_concat(n, h, w, c, cp, has_flow):
-    """The fused concat([f1, cost volume, flow]) kernel and its gradient, multi-tile and
-    ragged shapes (tile 8x32 + halo), with and without flow, float4 and scalar paths."""
+    """The fused concat([f1, cost volume, flow]) kernel and its gradient: 2-D tile kernels
+    (h < 96) and strip sweeps (h >= 96), multi-tile and ragged shapes, 1 and 2 channel
+    slabs, with and without flow, float4 and scalar paths."""
     ops = _ops()
     f1, f2, fl = rng_tensor((n, h, w, c), 4), rng_tensor((n, h, w, c), 5), rng_tensor((n, h, w, 2), 6)
     a, b, fo = [f64(t).requires_grad_(True) for t in (f1, f2, fl)]
