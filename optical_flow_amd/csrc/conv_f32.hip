@@ -27,6 +27,7 @@
 // the producer layer's activation derivative (dgrad).  Work-group ids are remapped so that
 // consecutive tiles (and all tiles of one K slice) run on one XCD and share its L2.
 #include "common.h"
+#include "conv_narrow.h"
 
 #include <algorithm>
 
@@ -1027,6 +1028,8 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   OF_CHECK_ARG(!z || ldz >= d->cout, "conv fwd: ldz");
   OF_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_fwd & 15) == 0,
                "conv fwd: x / w must be 16-byte aligned");
+  if (narrow_ok(d) && !bn_gamma && !residual && !z)   // 2-channel flow layers: VALU path
+    return narrow_fwd(d, x, ldx, w_fwd, bias, act, alpha, y, ldy, as_stream(stream));
   Geo g = geo(d);
   GemmArgs a = fwd_args(d, g);
   attach_slab(a, workspace, ws_bytes);
@@ -1070,6 +1073,9 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
   OF_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)w_bwd & 15) == 0,
                "conv dgrad: dy / w must be 16-byte aligned");
   OF_CHECK_ARG(d->stride == 1 || d->stride == 2, "conv dgrad: stride must be 1 or 2");
+  if (narrow_ok(d))
+    return narrow_dgrad(d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, dx, lddx,
+                        as_stream(stream));
   GemmArgs a = dgrad_args(d, g);
   attach_slab(a, workspace, ws_bytes);
   a.A = dy;
@@ -1093,6 +1099,7 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
 
 size_t of_conv2d_wgrad_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
+  if (narrow_ok(d)) return narrow_wgrad_ws(d);
   WgradPlan p = wgrad_plan(d);
   return (size_t)p.splits * p.split_stride * sizeof(float);
 }
@@ -1107,6 +1114,8 @@ int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float*
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv wgrad: lddy");
   OF_CHECK_ARG(ws_bytes >= of_conv2d_wgrad_workspace(d), "conv wgrad: workspace too small");
+  if (narrow_ok(d))
+    return narrow_wgrad(d, x, ldx, dy, lddy, dw, db, accumulate, workspace, as_stream(stream));
   WgradPlan p = wgrad_plan(d);
   GemmArgs a = base_args(d);
   a.kc = g.cin_p;

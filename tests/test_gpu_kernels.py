@@ -19,7 +19,11 @@ CONV_CASES = [
     # (n, h, w, cin, cout, k, stride, act, bn, residual)
     (2, 16, 24, 16, 32, 3, 1, "leaky", False, False),
     (2, 16, 24, 115, 128, 3, 1, "leaky", False, False),     # decoder c0 (cin padded)
-    (1, 12, 16, 32, 2, 3, 1, "none", False, False),         # flow conv (cout 2)
+    (1, 12, 16, 32, 2, 3, 1, "none", False, False),         # flow conv (cout 2): narrow path
+    (2, 33, 70, 32, 2, 3, 1, "none", False, False),         # narrow, ragged, many slices
+    (1, 10, 20, 64, 3, 3, 1, "relu", False, False),         # narrow, 16 lanes per pixel
+    (2, 8, 8, 3, 2, 3, 1, "leaky", False, False),           # narrow, 1 lane per pixel
+    (1, 9, 9, 12, 2, 3, 1, "leaky", False, False),          # cin_p 12: GEMM fallback
     (2, 16, 16, 64, 96, 3, 1, "leaky", False, False),       # cout 96 tile
     (2, 32, 48, 3, 64, 7, 2, "relu", True, False),          # conv1 7x7/2 + BN + ReLU
     (2, 16, 16, 64, 128, 3, 2, "relu", True, False),        # stride-2 block conv
