@@ -35,11 +35,16 @@ sys.path.insert(0, ROOT)
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (spec)
 MODE_NAMES = {0: "fwd", 1: "dgrad", 2: "wgrad"}
 TILE_TEMPLATE = {0: "128, 128, 2, 2", 1: "128, 96, 4, 1", 2: "256, 64, 4, 1", 3: "256, 32, 4, 1",
-                 4: "256, 128, 2, 2"}
+                 7: "narrow"}
+NARROW_SYMBOLS = {0: "oflow::narrow_fwd_kernel(oflow::NarrowArgs)",
+                  1: "oflow::narrow_dgrad_kernel(oflow::NarrowArgs)",
+                  2: "oflow::narrow_wgrad_kernel(oflow::NarrowArgs)"}
 
 
 def kernel_symbol(kind):
     """rocprofv3 name of the conv_gemm_f32 template instance behind a timing kind."""
+    if kind % 8 == 7:
+        return NARROW_SYMBOLS[kind // 8]
     return "void oflow::conv_gemm_f32<%s, %d>(oflow::GemmArgs)" % (TILE_TEMPLATE[kind % 8],
                                                                     kind // 8)
 

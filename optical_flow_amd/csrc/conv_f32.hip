@@ -1003,6 +1003,13 @@ int of_conv_pack_many(const void* dev_table, int64_t total_work, void* stream) {
   return check_launch("pack_many");
 }
 
+// Timing kind of the narrow (VALU) path; GEMM kinds are MODE * 8 + tile config (0..3).
+constexpr int KIND_NARROW = 7;
+
+double conv_flops(const of_conv_desc* d) {
+  return 2.0 * d->n * d->ho * d->wo * (double)d->cout * d->kh * d->kw * d->cin;
+}
+
 size_t of_conv2d_fwd_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
   return fd_workspace(fwd_args(d, geo(d)));
@@ -1028,8 +1035,13 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   OF_CHECK_ARG(!z || ldz >= d->cout, "conv fwd: ldz");
   OF_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_fwd & 15) == 0,
                "conv fwd: x / w must be 16-byte aligned");
-  if (narrow_ok(d) && !bn_gamma && !residual && !z)   // 2-channel flow layers: VALU path
-    return narrow_fwd(d, x, ldx, w_fwd, bias, act, alpha, y, ldy, as_stream(stream));
+  if (narrow_ok(d) && !bn_gamma && !residual && !z) {   // 2-channel flow layers: VALU path
+    hipStream_t s = as_stream(stream);
+    if (timing_on()) timing_begin(s);
+    st = narrow_fwd(d, x, ldx, w_fwd, bias, act, alpha, y, ldy, s);
+    if (timing_on()) timing_end(s, MODE_FWD * 8 + KIND_NARROW, conv_flops(d));
+    return st;
+  }
   Geo g = geo(d);
   GemmArgs a = fwd_args(d, g);
   attach_slab(a, workspace, ws_bytes);
@@ -1073,9 +1085,13 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
   OF_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)w_bwd & 15) == 0,
                "conv dgrad: dy / w must be 16-byte aligned");
   OF_CHECK_ARG(d->stride == 1 || d->stride == 2, "conv dgrad: stride must be 1 or 2");
-  if (narrow_ok(d))
-    return narrow_dgrad(d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, dx, lddx,
-                        as_stream(stream));
+  if (narrow_ok(d)) {
+    hipStream_t s = as_stream(stream);
+    if (timing_on()) timing_begin(s);
+    st = narrow_dgrad(d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, dx, lddx, s);
+    if (timing_on()) timing_end(s, MODE_DGRAD * 8 + KIND_NARROW, conv_flops(d));
+    return st;
+  }
   GemmArgs a = dgrad_args(d, g);
   attach_slab(a, workspace, ws_bytes);
   a.A = dy;
@@ -1114,8 +1130,13 @@ int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float*
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv wgrad: lddy");
   OF_CHECK_ARG(ws_bytes >= of_conv2d_wgrad_workspace(d), "conv wgrad: workspace too small");
-  if (narrow_ok(d))
-    return narrow_wgrad(d, x, ldx, dy, lddy, dw, db, accumulate, workspace, as_stream(stream));
+  if (narrow_ok(d)) {
+    hipStream_t s = as_stream(stream);
+    if (timing_on()) timing_begin(s);
+    st = narrow_wgrad(d, x, ldx, dy, lddy, dw, db, accumulate, workspace, s);
+    if (timing_on()) timing_end(s, MODE_WGRAD * 8 + KIND_NARROW, conv_flops(d));
+    return st;
+  }
   WgradPlan p = wgrad_plan(d);
   GemmArgs a = base_args(d);
   a.kc = g.cin_p;
