@@ -41,12 +41,27 @@ NARROW_SYMBOLS = {0: "oflow::narrow_fwd_kernel(oflow::NarrowArgs)",
                   2: "oflow::narrow_wgrad_kernel(oflow::NarrowArgs)"}
 
 
+BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def kind_parts(kind):
+    """timing kind -> (mode, tile config, bf16): f32 GEMMs mode*8+cfg, narrow cfg 7, bf16
+    GEMMs 64 + mode*8 + cfg (optical_flow_amd/csrc/conv_f32.hip)."""
+    return (kind % 64) // 8, kind % 8, kind >= 64
+
+
+def kind_name(kind):
+    mode, cfg, bf = kind_parts(kind)
+    return "%s%s<%s>" % (MODE_NAMES[mode], "_bf16" if bf else "", TILE_TEMPLATE[cfg])
+
+
 def kernel_symbol(kind):
-    """rocprofv3 name of the conv_gemm_f32 template instance behind a timing kind."""
-    if kind % 8 == 7:
-        return NARROW_SYMBOLS[kind // 8]
-    return "void oflow::conv_gemm_f32<%s, %d>(oflow::GemmArgs)" % (TILE_TEMPLATE[kind % 8],
-                                                                    kind // 8)
+    """rocprofv3 name of the conv kernel instance behind a timing kind."""
+    mode, cfg, bf = kind_parts(kind)
+    if cfg == 7:
+        return NARROW_SYMBOLS[mode]
+    return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (
+        "bf16" if bf else "f32", TILE_TEMPLATE[cfg], mode)
 
 
 def gflop_per_pair(H, W, max_disp=3):
@@ -80,16 +95,22 @@ def gflop_per_pair(H, W, max_disp=3):
     return (2 * macs + 3 * corr) / 1e9
 
 
-def cpu_baseline(pair_np, vals, steps=2):
+def cpu_baseline(pair_np, vals, steps=2, precision="fp32"):
     """Oracle train_step (torch CPU fp32, reference semantics) on one pair; returns
-    (pairs/s, threads, flows_at_init, loss_at_init)."""
+    (pairs/s, threads, flows_at_init, loss_at_init).  With precision "bf16" the reference
+    outputs come from the oracle with the build's bf16 operand rounding; the timed steps are
+    always the fp32 reference semantics."""
     from oracle import ref_flow as R
     from optical_flow_amd.params import encoder_blocks
     threads = torch.get_num_threads()
     p = {k: torch.tensor(v) for k, v in vals.items()}
     blocks = list(encoder_blocks())
     x = torch.tensor(pair_np)
-    loss0, flows0, _ = R.train_step(x, p, blocks, None)      # warm-up + reference outputs
+    R.set_conv_precision(precision)
+    try:
+        loss0, flows0, _ = R.train_step(x, p, blocks, None)  # warm-up + reference outputs
+    finally:
+        R.set_conv_precision("fp32")
     opt = R.KerasAdam()
     t0 = time.time()
     n = 0
@@ -113,6 +134,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--timing-steps", type=int, default=2)
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                    help="fp32: config 2 (headline); bf16: configs 3-5 conv contractions on "
+                         "bf16 MFMA with fp32 accumulation")
     args = ap.parse_args()
 
     from optical_flow_amd import _lib, ops
@@ -128,7 +152,7 @@ def main():
     _lib.load()
     H, W, B = args.height, args.width, args.batch
     vals = init_params(flow_net_spec(), 0)                 # identical weights on every rank
-    net = FlowNet(H, W, values=vals)
+    net = FlowNet(H, W, values=vals, precision=args.precision)
     trainer = Trainer(net, KerasAdam(net.store), LossLayer())
     batch = torch.from_numpy(synthetic_batch(B, H, W, seed=1234, rank=rank)).cuda()
 
@@ -197,13 +221,14 @@ def main():
             if pmc.get("kernel") == sym and pmc.get("config") == [H, W, B]:
                 traffic = pmc.get("hbm_bytes_per_launch")
         allconv = sum(v[0] for v in per.values()) / (sum(v[1] for v in per.values()) * 1e-3) / 1e12
+        peak = BF16_MFMA_PEAK_TFLOPS if kind_parts(dom)[2] else FP32_MFMA_PEAK_TFLOPS
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
-                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": traffic,
                 "launches_per_step": cnt // max(args.timing_steps, 1),
                 "avg_launch_ms": round(tm / cnt, 4), "gflop_per_launch": round(tf / cnt / 1e9, 3),
                 "all_conv_gemm_tflops": round(allconv, 2),
-                "per_kernel": {"%s<%s>" % (MODE_NAMES[k // 8], TILE_TEMPLATE[k % 8]):
+                "per_kernel": {kind_name(k):
                                {"launches": v[2], "ms": round(v[1], 3),
                                 "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
                                for k, v in sorted(per.items())}}
@@ -213,7 +238,8 @@ def main():
     parity = None
     if rank == 0 and not args.no_cpu_baseline:
         pair = batch[:1].cpu().numpy()
-        cps, threads, flows_ref, loss_ref = cpu_baseline(pair, vals, args.cpu_steps)
+        cps, threads, flows_ref, loss_ref = cpu_baseline(pair, vals, args.cpu_steps,
+                                                         args.precision)
         cpu = {"value": round(cps, 4), "unit": "image-pairs/s", "cores": threads,
                "kind": "port",
                "sample": "%d oracle train steps (torch-CPU fp32 restatement of the reference "
@@ -224,8 +250,9 @@ def main():
                zip(flows_hip, flows_ref)]
         parity = {"epe": [round(e, 6) for e in epe], "flow_rel_inf": [float("%.3e" % r) for r in rel],
                   "loss_rel": float("%.3e" % (abs(loss_hip - loss_ref) / abs(loss_ref))),
-                  "note": "HIP fp32 vs CPU oracle fp32, same pair and initial weights, flows "
-                          "[H/2, H/4, H/8, H/16]"}
+                  "note": "HIP %s vs CPU oracle (%s operand rounding), same pair and initial "
+                          "weights, flows [H/2, H/4, H/8, H/16]" % (args.precision,
+                                                                    args.precision)}
 
     gfp = gflop_per_pair(H, W)
     if rank == 0:
@@ -240,7 +267,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if args.precision == "fp32" else "bf16",
             "data": "synthetic (U[0,1)-mean pairs, image2 = shifted image1 + noise; resident in HBM)",
             "config": {"workload": "full model.py encoder-decoder + loss.py photometric loss, "
                                    "train step (fwd+bwd+Keras Adam)",

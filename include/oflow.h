@@ -111,6 +111,36 @@ int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float*
                     float* dw, float* db, int accumulate, void* workspace, size_t ws_bytes,
                     void* stream);
 
+/* bf16 MFMA variants (BASELINE configs 3-5: "bf16 with MFMA direct-conv path"): same
+ * geometry, epilogues and error behaviour as of_conv2d_{fwd,dgrad,wgrad}; activations stay
+ * fp32 in memory and are rounded to bf16 (RNE) while staged, weights are the bf16 images of
+ * of_conv_pack_weights_bf16 (of_conv_w{fwd,bwd}16_elems bf16 elements each), accumulation is
+ * fp32.  of_conv_path(d) == 1 marks the narrow (cout <= 4) layers, which stay on the f32
+ * VALU kernels in every precision. */
+int of_conv_path(const of_conv_desc* d);
+int64_t of_conv_wfwd16_elems(const of_conv_desc* d);
+int64_t of_conv_wbwd16_elems(const of_conv_desc* d);
+int of_conv_pack_weights_bf16(const of_conv_desc* d, const float* w_hwio, void* w16_fwd,
+                              void* w16_bwd, void* stream);
+/* of_conv_pack_table with a per-conv precision flag (bf16[i] != 0: bf16 images). */
+int of_conv_pack_table_ex(int nconv, const of_conv_desc* descs, const float* const* w_hwio,
+                          void* const* w_fwd, void* const* w_bwd, const int* bf16,
+                          void* host_table);
+size_t of_conv2d_fwd_bf16_workspace(const of_conv_desc* d);
+int of_conv2d_fwd_bf16(const of_conv_desc* d, const float* x, int ldx, const void* w16_fwd,
+                       const float* bias, const float* bn_gamma, const float* bn_beta,
+                       const float* bn_mean, const float* bn_var, float bn_eps,
+                       const float* residual, int ldr, int act, float alpha, float* z, int ldz,
+                       float* y, int ldy, void* workspace, size_t ws_bytes, void* stream);
+size_t of_conv2d_wgrad_bf16_workspace(const of_conv_desc* d);
+int of_conv2d_wgrad_bf16(const of_conv_desc* d, const float* x, int ldx, const float* dy,
+                         int lddy, float* dw, float* db, int accumulate, void* workspace,
+                         size_t ws_bytes, void* stream);
+size_t of_conv2d_dgrad_bf16_workspace(const of_conv_desc* d);
+int of_conv2d_dgrad_bf16(const of_conv_desc* d, const float* dy, int lddy, const void* w16_bwd,
+                         const float* act_src, int ld_act, int act, float alpha, float* dx,
+                         int lddx, void* workspace, size_t ws_bytes, void* stream);
+
 /* Activation backward: dz = dy * act'(y) over n elements (y = forward output). */
 int of_act_bwd(const float* dy, const float* y, int act, float alpha, float* dz, int64_t n,
                void* stream);

@@ -47,6 +47,18 @@ PROTOTYPES = {
     "of_conv2d_dgrad": (I, [PD, P, I, P, P, I, I, F, P, I, P, SZ, P]),
     "of_conv2d_wgrad_workspace": (SZ, [PD]),
     "of_conv2d_wgrad": (I, [PD, P, I, P, I, P, P, I, P, SZ, P]),
+    "of_conv_path": (I, [PD]),
+    "of_conv_wfwd16_elems": (I64, [PD]),
+    "of_conv_wbwd16_elems": (I64, [PD]),
+    "of_conv_pack_weights_bf16": (I, [PD, P, P, P, P]),
+    "of_conv_pack_table_ex": (I, [I, PD, C.POINTER(P), C.POINTER(P), C.POINTER(P),
+                                  C.POINTER(I), P]),
+    "of_conv2d_fwd_bf16_workspace": (SZ, [PD]),
+    "of_conv2d_fwd_bf16": (I, [PD, P, I, P, P, P, P, P, P, F, P, I, I, F, P, I, P, I, P, SZ, P]),
+    "of_conv2d_wgrad_bf16_workspace": (SZ, [PD]),
+    "of_conv2d_wgrad_bf16": (I, [PD, P, I, P, I, P, P, I, P, SZ, P]),
+    "of_conv2d_dgrad_bf16_workspace": (SZ, [PD]),
+    "of_conv2d_dgrad_bf16": (I, [PD, P, I, P, P, I, I, F, P, I, P, SZ, P]),
     "of_act_bwd": (I, [P, P, I, F, P, I64, P]),
     "of_colsum_workspace": (SZ, [I64, I]),
     "of_colsum": (I, [P, I64, I, I, P, I, P, P]),

@@ -494,6 +494,505 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   }
 }
 
+// ===================================================================== bf16 MFMA variant ===
+// fwd / dgrad with bf16 operands (fp32 activations converted while staging, RNE; bf16 packed
+// weights), fp32 accumulation: v_mfma_f32_32x32x16_bf16, 16x the f32-MFMA rate per clock.
+// Same implicit-GEMM geometry, split-K and epilogues as conv_gemm_f32.  Differences:
+//   * K chunk 32 (two MFMA k-steps); LDS operand images are [row][k] with k contiguous
+//     (80-byte rows: the ds_read_b128 fragment reads of a wave are conflict-free);
+//   * wave w stages k-octet w of every chunk: two channel quads, each with its own tap walk
+//     (kc need only be a multiple of 4);
+//   * packed weights are bf16 [n][k] (k contiguous, K padded to 32 per group).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int BKH = 32;                  // bf16 chunk
+constexpr int SROW16 = 5;                // LDS row stride in 16-byte units (40 bf16 = 80 B)
+
+__device__ __forceinline__ uint4 pack_bf16x8(const float4& lo, const float4& hi) {
+  bf16x8 v;
+  v[0] = (__bf16)lo.x;
+  v[1] = (__bf16)lo.y;
+  v[2] = (__bf16)lo.z;
+  v[3] = (__bf16)lo.w;
+  v[4] = (__bf16)hi.x;
+  v[5] = (__bf16)hi.y;
+  v[6] = (__bf16)hi.z;
+  v[7] = (__bf16)hi.w;
+  return __builtin_bit_cast(uint4, v);
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
+__global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
+  static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "bf16: fwd / dgrad");
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  static_assert(TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "tile");
+  constexpr int A_SLOTS = BM / 64;               // rows per lane
+  constexpr int B_OCTS = BN * (BKH / 8);         // 16-byte octets of the B chunk
+  constexpr int B_SLOTS = (B_OCTS + 255) / 256;
+  static_assert(A_SLOTS >= 1, "BM >= 64");
+
+  __shared__ uint4 As[2][BM * SROW16];
+  __shared__ uint4 Bs[2][BN * SROW16];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_n = tile % a.n_tiles;
+  const int tile_mg = tile / a.n_tiles;
+  int gi = 0;
+#pragma unroll
+  for (int g = 1; g < MAX_GROUPS; ++g)
+    if (g < a.ngroups && tile_mg >= a.grp[g].tiles_begin) gi = g;
+  const Group& G = a.grp[gi];
+  const int tile_m = tile_mg - G.tiles_begin;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int M = G.M;
+
+  const int k_begin = split * a.k_per_split;
+  const int k_end = min(G.K, k_begin + a.k_per_split);
+  const int nchunks = k_end > k_begin ? (k_end - k_begin + BKH - 1) / BKH : 0;
+
+  const rsrc_t ra_src = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rb_src = make_rsrc(a.B, a.b_bytes);
+
+  // ---------------- A rows (same geometry as the f32 kernel) --------------------------------
+  const int src_h = (MODE == MODE_DGRAD) ? a.ho : a.h;
+  const int src_w = (MODE == MODE_DGRAD) ? a.wo : a.w;
+  int a_off[A_SLOTS];
+  uint64_t a_msk[A_SLOTS];
+#pragma unroll
+  for (int i = 0; i < A_SLOTS; ++i) {
+    const int m = m0 + lane + 64 * i;
+    const bool okm = m < M;
+    const int mm = okm ? m : 0;
+    int b, yb, xb;
+    if (MODE == MODE_FWD) {
+      const int hw = a.ho * a.wo;
+      b = mm / hw;
+      const int rem = mm - b * hw;
+      const int oy = rem / a.wo, ox = rem - oy * a.wo;
+      yb = oy * a.stride - a.pt;
+      xb = ox * a.stride - a.pl;
+    } else if (a.phase) {
+      const int hw = G.hc * G.wc;
+      b = mm / hw;
+      const int rem = mm - b * hw;
+      const int u = rem / G.wc, v = rem - u * G.wc;
+      yb = (2 * u + G.ry + a.pt - G.r0) >> 1;
+      xb = (2 * v + G.rx + a.pl - G.s0) >> 1;
+    } else {
+      const int hw = a.h * a.w;
+      b = mm / hw;
+      const int rem = mm - b * hw;
+      const int iy = rem / a.w, ix = rem - iy * a.w;
+      yb = iy + a.pt;
+      xb = ix + a.pl;
+    }
+    a_off[i] = (int)(((int64_t)(b * src_h + yb) * src_w + xb) * a.lda * 4);
+    uint64_t msk = 0;
+    if (okm) {
+      uint64_t colmask = 0;
+      for (int ts = 0; ts < G.ns; ++ts) {
+        const int sx = (MODE == MODE_FWD) ? xb + ts : xb - ts;
+        if ((unsigned)sx < (unsigned)src_w) colmask |= (uint64_t)1 << ts;
+      }
+      int t = 0;
+      for (int tr = 0; t < G.ntaps; ++tr, t += G.ns) {
+        const int sy = (MODE == MODE_FWD) ? yb + tr : yb - tr;
+        if ((unsigned)sy < (unsigned)src_h) msk |= colmask << t;
+      }
+      if (G.ntaps < 64) msk &= ((uint64_t)1 << G.ntaps) - 1;
+    }
+    a_msk[i] = msk;
+  }
+  // Two wave-uniform tap walkers: channel quads 2w and 2w+1 of the chunk.
+  int ks_t[2], ks_tr[2], ks_ts[2], ks_ci[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k0 = k_begin + wave * 8 + 4 * h;
+    ks_t[h] = k0 / a.kc;
+    ks_ci[h] = k0 - ks_t[h] * a.kc;
+    ks_tr[h] = ks_t[h] / G.ns;
+    ks_ts[h] = ks_t[h] - ks_tr[h] * G.ns;
+  }
+  const int sgn = MODE == MODE_FWD ? 1 : -1;
+  const int tap_step = sgn * src_w * a.lda * 4;
+
+  float4 ra[A_SLOTS][2];
+  uint4 rb[B_SLOTS];
+
+  auto load_a = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool tap_ok = ks_t[h] < G.ntaps;
+      const int koff = ks_tr[h] * tap_step + sgn * ks_ts[h] * a.lda * 4 + ks_ci[h] * 4;
+#pragma unroll
+      for (int i = 0; i < A_SLOTS; ++i) {
+        const bool ok = tap_ok && ((a_msk[i] >> ks_t[h]) & 1);
+        ra[i][h] = bload4(ra_src, ok ? (uint32_t)(a_off[i] + koff) : kOOB);
+      }
+    }
+  };
+  auto advance_a = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      ks_ci[h] += BKH;
+      while (ks_ci[h] >= a.kc) {
+        ks_ci[h] -= a.kc;
+        ++ks_t[h];
+        if (++ks_ts[h] >= G.ns) {
+          ks_ts[h] = 0;
+          ++ks_tr[h];
+        }
+      }
+    }
+  };
+  auto store_a = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_SLOTS; ++i)
+      As[buf][(lane + 64 * i) * SROW16 + wave] = pack_bf16x8(ra[i][0], ra[i][1]);
+  };
+
+  // ---------------- B (packed bf16 weights [n][k]) -------------------------------------------
+  uint32_t b_off[B_SLOTS];
+#pragma unroll
+  for (int i = 0; i < B_SLOTS; ++i) {
+    const int slot = tid + 256 * i;
+    const int row = slot >> 2, oct = slot & 3;
+    const int n = n0 + row;
+    b_off[i] = (slot < B_OCTS && n < a.nb) ? (uint32_t)((((int64_t)n * a.ldb) + G.b_off + 8 * oct) * 2)
+                                           : kOOB;
+  }
+  int b_k = k_begin;
+  auto load_b = [&]() {
+#pragma unroll
+    for (int i = 0; i < B_SLOTS; ++i)
+      rb[i] = __builtin_bit_cast(uint4, bload4(rb_src, b_off[i] != kOOB ? b_off[i] + 2u * b_k : kOOB));
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < B_SLOTS; ++i) {
+      const int slot = tid + 256 * i;
+      if (slot < B_OCTS) Bs[buf][(slot >> 2) * SROW16 + (slot & 3)] = rb[i];
+    }
+  };
+
+  // ---------------- main loop --------------------------------------------------------------
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int wm0 = (wave / WAVES_N) * WM;
+  const int wn0 = (wave % WAVES_N) * WN;
+  const int lrow = lane & 31, lk = lane >> 5;
+
+  if (nchunks > 0) {
+    load_a();
+    load_b();
+    store_a(0);
+    store_b(0);
+  }
+  __syncthreads();
+
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      advance_a();
+      b_k += BKH;
+      load_a();
+      load_b();
+    }
+#pragma unroll
+    for (int st = 0; st < BKH / 16; ++st) {
+      bf16x8 av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        av[i] = __builtin_bit_cast(bf16x8, As[buf][(wm0 + 32 * i + lrow) * SROW16 + 2 * st + lk]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bv[j] = __builtin_bit_cast(bf16x8, Bs[buf][(wn0 + 32 * j + lrow) * SROW16 + 2 * st + lk]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      store_a(buf ^ 1);
+      store_b(buf ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue (as conv_gemm_f32) ----------------------------------------------
+  if (a.splits > 1) {
+    float* S = a.slab + (int64_t)split * a.split_stride;
+    const int row_base = G.tiles_begin * BM;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn0 + 32 * j + lrow;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (m < M) S[(int64_t)(row_base + m) * a.slab_ld + n] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + 32 * j + lrow;
+    if (n >= a.N) continue;
+    float bias, scale, shift;
+    column_params<MODE>(a, n, bias, scale, shift);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (m >= M) continue;
+        epilogue_store<MODE>(a, out_row(a, G, m), n, acc[i][j][r], bias, scale, shift);
+      }
+    }
+  }
+}
+
+// Weight gradient on bf16 MFMA: C[m=(tap,ci)][n=co] = sum_{k=output pixel} x[pix(k,tap)][ci] *
+// dy[k][co], both operands rounded to bf16 while staged, fp32 accumulation into the split-K
+// slabs (reduced by wgrad_reduce_kernel, as the f32 path).  The MFMA operands need 8
+// consecutive pixels per lane, while NHWC keeps channels contiguous: each staging slot loads
+// a 4-channel x 8-pixel block (8 float4, coalesced across the lanes of a pixel) and writes
+// it transposed as 4 rows of 8 bf16 (ds_write_b128) into the same [row][k] images the
+// fwd/dgrad kernel reads.  Chunk = 32 pixels; slots = BM + BN (4 rows x 8 pixels each).
+// The bias gradient (column sums of dy) is accumulated in fp32 from the staged values.
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_bf16(GemmArgs a) {
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  constexpr int NSLOT = BM + BN;
+  constexpr int SPT = (NSLOT + 255) / 256;
+  __shared__ uint4 As[2][BM * SROW16];
+  __shared__ uint4 Bs[2][BN * SROW16];
+  __shared__ float csum[4][BN];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_n = tile % a.n_tiles;
+  const int tile_m = tile / a.n_tiles;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int M = a.M;
+  const int k_begin = split * a.k_per_split;
+  const int k_end = min(a.K, k_begin + a.k_per_split);
+  const int nchunks = k_end > k_begin ? (k_end - k_begin + BKH - 1) / BKH : 0;
+  const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
+  const bool do_colsum = a.colsum && tile_m == 0;
+
+  // ---- per-slot fixed state
+  bool s_isa[SPT], s_ok[SPT];
+  int s_row[SPT], s_oc[SPT], s_col[SPT];          // LDS row, k-octet, channel offset
+  int s_r[SPT], s_s[SPT];                         // A: tap
+  int s_b[SPT], s_oy[SPT], s_ox[SPT];             // first pixel of the slot's octet
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int sl = tid + 256 * j;
+    const bool live = sl < NSLOT;
+    const bool isa = sl < BM;
+    const int q = isa ? sl : sl - BM;
+    const int nq = isa ? BM / 4 : BN / 4;
+    const int rq = q % nq, oc = q / nq;
+    s_isa[j] = isa;
+    s_row[j] = 4 * rq;
+    s_oc[j] = live ? oc : -1;
+    if (isa) {
+      const int m = m0 + 4 * rq;
+      s_ok[j] = live && m < M;
+      const int mm = m < M ? m : 0;
+      const int tap = mm / a.kc;
+      s_col[j] = mm - tap * a.kc;
+      s_r[j] = tap / a.kw;
+      s_s[j] = tap - s_r[j] * a.kw;
+    } else {
+      const int n = n0 + 4 * rq;
+      s_ok[j] = live && n < a.nb;
+      s_col[j] = n;
+      s_r[j] = s_s[j] = 0;
+    }
+    const int k = k_begin + 8 * oc;
+    const int hw = a.ho * a.wo;
+    const int kk = k < a.K ? k : 0;
+    s_b[j] = kk / hw;
+    const int rem = kk - s_b[j] * hw;
+    s_oy[j] = rem / a.wo;
+    s_ox[j] = rem - s_oy[j] * a.wo;
+  }
+  float4 stg[SPT][8];
+  float4 colacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int kc0 = k_begin;   // first pixel of the current chunk
+
+  auto load = [&]() {
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      int b = s_b[j], oy = s_oy[j], ox = s_ox[j];
+      const int kbase = kc0 + 8 * s_oc[j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool okk = s_ok[j] && s_oc[j] >= 0 && kbase + e < k_end;
+        uint32_t off = kOOB;
+        if (s_isa[j]) {
+          const int sy = oy * a.stride - a.pt + s_r[j], sx = ox * a.stride - a.pl + s_s[j];
+          if (okk && (unsigned)sy < (unsigned)a.h && (unsigned)sx < (unsigned)a.w)
+            off = (uint32_t)((((b * a.h + sy) * a.w + sx) * a.lda + s_col[j]) * 4);
+          stg[j][e] = bload4(rx, off);
+        } else {
+          if (okk) off = (uint32_t)(((kbase + e) * a.ldb + s_col[j]) * 4);
+          stg[j][e] = bload4(rd, off);
+        }
+        if (++ox >= a.wo) {
+          ox = 0;
+          if (++oy >= a.ho) {
+            oy = 0;
+            ++b;
+          }
+        }
+      }
+    }
+  };
+  auto advance = [&]() {
+    kc0 += BKH;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      s_ox[j] += BKH;
+      while (s_ox[j] >= a.wo) {
+        s_ox[j] -= a.wo;
+        if (++s_oy[j] >= a.ho) {
+          s_oy[j] = 0;
+          ++s_b[j];
+        }
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      if (s_oc[j] < 0) continue;
+      float4 t[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = stg[j][e];
+      // rows (channel c of the quad) of 8 pixels each
+      const uint4 r0 = pack_bf16x8(make_float4(t[0].x, t[1].x, t[2].x, t[3].x),
+                                   make_float4(t[4].x, t[5].x, t[6].x, t[7].x));
+      const uint4 r1 = pack_bf16x8(make_float4(t[0].y, t[1].y, t[2].y, t[3].y),
+                                   make_float4(t[4].y, t[5].y, t[6].y, t[7].y));
+      const uint4 r2 = pack_bf16x8(make_float4(t[0].z, t[1].z, t[2].z, t[3].z),
+                                   make_float4(t[4].z, t[5].z, t[6].z, t[7].z));
+      const uint4 r3 = pack_bf16x8(make_float4(t[0].w, t[1].w, t[2].w, t[3].w),
+                                   make_float4(t[4].w, t[5].w, t[6].w, t[7].w));
+      uint4* img = s_isa[j] ? As[buf] : Bs[buf];
+      const int base = s_row[j] * SROW16 + s_oc[j];
+      img[base] = r0;
+      img[base + SROW16] = r1;
+      img[base + 2 * SROW16] = r2;
+      img[base + 3 * SROW16] = r3;
+      if (!s_isa[j] && do_colsum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) add4(colacc, t[e]);
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int wm0 = (wave / WAVES_N) * WM;
+  const int wn0 = (wave % WAVES_N) * WN;
+  const int lrow = lane & 31, lk = lane >> 5;
+
+  if (nchunks > 0) {
+    load();
+    store(0);
+  }
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      advance();
+      load();
+    }
+#pragma unroll
+    for (int st = 0; st < BKH / 16; ++st) {
+      bf16x8 av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        av[i] = __builtin_bit_cast(bf16x8, As[buf][(wm0 + 32 * i + lrow) * SROW16 + 2 * st + lk]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bv[j] = __builtin_bit_cast(bf16x8, Bs[buf][(wn0 + 32 * j + lrow) * SROW16 + 2 * st + lk]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- raw partial sums into this K slice's slab (+ bias column sums in row M)
+  float* S = a.slab + (int64_t)split * a.split_stride;
+  if (do_colsum) {
+    // B-slot threads hold 4 columns x their k-octet; 4 octets per column quad
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      if (!s_isa[j] && s_oc[j] >= 0) {
+        const int cq = s_row[j];
+        csum[s_oc[j]][cq] = colacc.x;
+        csum[s_oc[j]][cq + 1] = colacc.y;
+        csum[s_oc[j]][cq + 2] = colacc.z;
+        csum[s_oc[j]][cq + 3] = colacc.w;
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N)
+      S[(int64_t)M * a.slab_ld + n0 + tid] = csum[0][tid] + csum[1][tid] + csum[2][tid] + csum[3][tid];
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + 32 * j + lrow;
+    if (n >= a.N) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (m < M) S[(int64_t)m * a.slab_ld + n] = acc[i][j][r];
+      }
+  }
+}
+
 // Split-K epilogue for fwd/dgrad: sum the K slices' slabs, then the fused epilogue.
 // Workgroup = 32 items x 8 split lanes; item = (slab row, 4 columns); the 8 lanes each sum
 // every 8th slice (many independent loads in flight), then a fixed-order LDS reduction.
@@ -557,7 +1056,8 @@ struct PackGroups {
   int ngroups;
   int dt;
   int r0[MAX_GROUPS], s0[MAX_GROUPS], ns[MAX_GROUPS], ntaps[MAX_GROUPS];
-  int64_t row_begin[MAX_GROUPS + 1];
+  int64_t row_begin[MAX_GROUPS + 1];     // f32 packing: group row blocks padded to BK
+  int64_t row_begin16[MAX_GROUPS + 1];   // bf16 packing: group k blocks padded to BKH
 };
 
 __global__ void pack_bwd_kernel(const float* __restrict__ w, PackGroups pg, int kw, int cin,
@@ -585,9 +1085,12 @@ __global__ void pack_bwd_kernel(const float* __restrict__ w, PackGroups pg, int 
 // All convs of a model packed in one launch from a device-resident table.
 struct PackEntry {
   const float* w;
-  float* wf;
+  float* wf;               // f32 packing; bf16 packing: __bf16 buffers
   float* wd;
   int taps, kw, cin, cout, cin_p, cout_p, kf, nf, nd;
+  int bf16;                // 1: transposed bf16 images [n][k] (conv_gemm_bf16)
+  int kf16;
+  int64_t kd16;
   int64_t work_begin;      // cumulative elements (fwd then bwd) before this entry
   PackGroups pg;
 };
@@ -597,6 +1100,65 @@ struct PackTableHeader {
   int pad;
   int64_t total;
 };
+
+// One packed element of entry E (f32: fwd rows [k][n] then bwd rows; bf16: transposed).
+__device__ void pack_elem(const PackEntry& E, int64_t k) {
+  if (E.bf16) {
+    const int64_t nfwd16 = (int64_t)E.cout_p * E.kf16;
+    if (k < nfwd16) {                       // W16_f[n][tap*cin_p + ci]
+      const int n = (int)(k / E.kf16), kk = (int)(k - (int64_t)n * E.kf16);
+      const int tap = kk / E.cin_p, ci = kk - tap * E.cin_p;
+      float v = 0.f;
+      if (tap < E.taps && ci < E.cin && n < E.cout)
+        v = E.w[((int64_t)tap * E.cin + ci) * E.cout + n];
+      reinterpret_cast<__bf16*>(E.wf)[k] = (__bf16)v;
+    } else {                                // W16_d[ci][group k block: t*cout_p + co]
+      k -= nfwd16;
+      const int ci = (int)(k / E.kd16);
+      const int64_t kc = k - (int64_t)ci * E.kd16;
+      const PackGroups& pg = E.pg;
+      int g = 0;
+      for (int q = 1; q < pg.ngroups; ++q)
+        if (kc >= pg.row_begin16[q]) g = q;
+      const int kk = (int)(kc - pg.row_begin16[g]);
+      const int t = kk / E.cout_p, co = kk - t * E.cout_p;
+      float v = 0.f;
+      if (t < pg.ntaps[g] && co < E.cout && ci < E.cin) {
+        const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
+        const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
+        v = E.w[((int64_t)(r * E.kw + ss) * E.cin + ci) * E.cout + co];
+      }
+      reinterpret_cast<__bf16*>(E.wd)[k] = (__bf16)v;
+    }
+    return;
+  }
+  const int64_t nfwd = (int64_t)E.kf * E.nf;
+  if (k < nfwd) {
+    const int kk = (int)(k / E.nf), nn = (int)(k - (int64_t)kk * E.nf);
+    const int tap = kk / E.cin_p, ci = kk - tap * E.cin_p;
+    float v = 0.f;
+    if (tap < E.taps && ci < E.cin && nn < E.cout)
+      v = E.w[((int64_t)tap * E.cin + ci) * E.cout + nn];
+    E.wf[k] = v;
+  } else {
+    k -= nfwd;
+    const int64_t row = k / E.nd;
+    const int nn = (int)(k - row * E.nd);
+    const PackGroups& pg = E.pg;
+    int g = 0;
+    for (int q = 1; q < pg.ngroups; ++q)
+      if (row >= pg.row_begin[q]) g = q;
+    const int kk = (int)(row - pg.row_begin[g]);
+    const int t = kk / E.cout_p, co = kk - t * E.cout_p;
+    float v = 0.f;
+    if (t < pg.ntaps[g] && co < E.cout && nn < E.cin) {
+      const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
+      const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
+      v = E.w[((int64_t)(r * E.kw + ss) * E.cin + nn) * E.cout + co];
+    }
+    E.wd[k] = v;
+  }
+}
 
 __global__ void pack_many_kernel(const char* __restrict__ table) {
   const PackTableHeader* h = reinterpret_cast<const PackTableHeader*>(table);
@@ -609,35 +1171,14 @@ __global__ void pack_many_kernel(const char* __restrict__ table) {
       const int mid = (lo + hi + 1) >> 1;
       if (e[mid].work_begin <= idx) lo = mid; else hi = mid - 1;
     }
-    const PackEntry& E = e[lo];
-    int64_t k = idx - E.work_begin;
-    const int64_t nfwd = (int64_t)E.kf * E.nf;
-    if (k < nfwd) {
-      const int kk = (int)(k / E.nf), nn = (int)(k - (int64_t)kk * E.nf);
-      const int tap = kk / E.cin_p, ci = kk - tap * E.cin_p;
-      float v = 0.f;
-      if (tap < E.taps && ci < E.cin && nn < E.cout)
-        v = E.w[((int64_t)tap * E.cin + ci) * E.cout + nn];
-      E.wf[k] = v;
-    } else {
-      k -= nfwd;
-      const int64_t row = k / E.nd;
-      const int nn = (int)(k - row * E.nd);
-      const PackGroups& pg = E.pg;
-      int g = 0;
-      for (int q = 1; q < pg.ngroups; ++q)
-        if (row >= pg.row_begin[q]) g = q;
-      const int kk = (int)(row - pg.row_begin[g]);
-      const int t = kk / E.cout_p, co = kk - t * E.cout_p;
-      float v = 0.f;
-      if (t < pg.ntaps[g] && co < E.cout && nn < E.cin) {
-        const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
-        const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
-        v = E.w[((int64_t)(r * E.kw + ss) * E.cin + nn) * E.cout + co];
-      }
-      E.wd[k] = v;
-    }
+    pack_elem(e[lo], idx - e[lo].work_begin);
   }
+}
+
+__global__ void pack_one_kernel(PackEntry E, int64_t total) {
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x)
+    pack_elem(E, idx);
 }
 
 // dw[tap][ci][co] (HWIO) = sum_z slab[z][tap*kc + ci][co]; optional db[co] = sum_z slab[z][M][co].
@@ -687,6 +1228,8 @@ struct Geo {
   bool phase;            // dgrad as stride-2 phase groups
   PackGroups pg;
   int64_t kd;            // packed bwd rows
+  int kf16;              // bf16: fwd K (padded to BKH) = row length of W16_f [cout_p][kf16]
+  int64_t kd16;          // bf16: dgrad K over all groups = row length of W16_d [cin_p][kd16]
 };
 
 Geo geo(const of_conv_desc* d) {
@@ -700,6 +1243,7 @@ Geo geo(const of_conv_desc* d) {
   g.phase = d->stride == 2;
   PackGroups& pg = g.pg;
   pg.row_begin[0] = 0;
+  pg.row_begin16[0] = 0;
   if (g.phase) {
     pg.ngroups = 4;
     pg.dt = 2;
@@ -711,6 +1255,8 @@ Geo geo(const of_conv_desc* d) {
       pg.ns[c] = std::max(ns, 1);
       pg.ntaps[c] = nr * ns;
       pg.row_begin[c + 1] = pg.row_begin[c] + round_up((int64_t)pg.ntaps[c] * g.cout_p, BK);
+      pg.row_begin16[c + 1] =
+          pg.row_begin16[c] + round_up((int64_t)pg.ntaps[c] * g.cout_p, BKH);
     }
   } else {
     pg.ngroups = 1;
@@ -719,8 +1265,11 @@ Geo geo(const of_conv_desc* d) {
     pg.ns[0] = d->kw;
     pg.ntaps[0] = g.taps;
     pg.row_begin[1] = round_up((int64_t)g.taps * g.cout_p, BK);
+    pg.row_begin16[1] = round_up((int64_t)g.taps * g.cout_p, BKH);
   }
   g.kd = pg.row_begin[pg.ngroups];
+  g.kf16 = (int)round_up((int64_t)g.taps * g.cin_p, BKH);
+  g.kd16 = pg.row_begin16[pg.ngroups];
   return g;
 }
 
@@ -773,15 +1322,15 @@ void single_group(GemmArgs& a, const of_conv_desc* d, int M, int K) {
 }
 
 // fwd/dgrad split-K: split when the tile grid cannot fill the chip.
-void plan_splits(GemmArgs& a, int kmax) {
+void plan_splits(GemmArgs& a, int kmax, int bk = BK) {
   a.splits = 1;
-  a.k_per_split = (int)round_up(kmax, BK);
+  a.k_per_split = (int)round_up(kmax, bk);
   if (a.tiles_total >= 2 * kCUs) return;
-  const int nchunks = (int)cdiv(kmax, BK);
+  const int nchunks = (int)cdiv(kmax, bk);
   int s = std::max(1, (4 * kCUs) / a.tiles_total);
-  s = std::min(s, std::max(1, nchunks / 12));
+  s = std::min(s, std::max(1, nchunks / (bk == BK ? 12 : 6)));
   if (s <= 1) return;
-  a.k_per_split = (int)round_up(cdiv(kmax, s), BK);
+  a.k_per_split = (int)round_up(cdiv(kmax, s), bk);
   a.splits = (int)cdiv(kmax, a.k_per_split);
 }
 
@@ -793,7 +1342,7 @@ size_t fd_workspace(const GemmArgs& a) {
 }
 
 // Attach the split-K slab; without (enough) workspace fall back to one K slice.
-void attach_slab(GemmArgs& a, void* ws, size_t ws_bytes) {
+void attach_slab(GemmArgs& a, void* ws, size_t ws_bytes, int bk = BK) {
   if (a.splits > 1 && ws && ws_bytes >= fd_workspace(a)) {
     a.slab = static_cast<float*>(ws);
     a.slab_ld = (int)round_up(a.N, 4);
@@ -803,26 +1352,28 @@ void attach_slab(GemmArgs& a, void* ws, size_t ws_bytes) {
   int kmax = 0;
   for (int g = 0; g < a.ngroups; ++g) kmax = std::max(kmax, a.grp[g].K);
   a.splits = 1;
-  a.k_per_split = (int)round_up(kmax, BK);
+  a.k_per_split = (int)round_up(kmax, bk);
 }
 
-GemmArgs fwd_args(const of_conv_desc* d, const Geo& g) {
+// bf16: K in units of k padded to BKH, B = W16_f [cout_p rows][kf16] (row length ldb).
+GemmArgs fwd_args(const of_conv_desc* d, const Geo& g, bool bf16 = false) {
   GemmArgs a = base_args(d);
   a.kc = g.cin_p;
   a.N = d->cout;
   a.M = d->n * d->ho * d->wo;
-  single_group(a, d, a.M, g.kf);
-  plan_splits(a, g.kf);
-  a.ldb = g.nf;
-  a.nb = g.nf;
+  const int K = bf16 ? g.kf16 : g.kf;
+  single_group(a, d, a.M, K);
+  plan_splits(a, K, bf16 ? BKH : BK);
+  a.ldb = bf16 ? g.kf16 : g.nf;
+  a.nb = bf16 ? d->cout : g.nf;
   return a;
 }
 
-GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g) {
+GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g, bool bf16 = false) {
   GemmArgs a = base_args(d);
   a.kc = g.cout_p;
   a.N = g.cin_p;
-  a.ldb = g.nd;
+  a.ldb = bf16 ? (int)g.kd16 : g.nd;
   a.nb = g.nd;
   int kmax = 0;
   if (g.phase) {
@@ -849,18 +1400,19 @@ GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g) {
       G.s0 = g.pg.s0[c];
       G.ns = g.pg.ns[c];
       G.ntaps = g.pg.ntaps[c];
-      G.K = (int)(g.pg.row_begin[c + 1] - g.pg.row_begin[c]);
-      G.b_off = g.pg.row_begin[c];
+      const int64_t* rb = bf16 ? g.pg.row_begin16 : g.pg.row_begin;
+      G.K = (int)(rb[c + 1] - rb[c]);
+      G.b_off = rb[c];
       kmax = std::max(kmax, G.K);
     }
     a.tiles_total = tiles * a.n_tiles;
     a.M = d->n * d->h * d->w;
   } else {
     a.M = d->n * d->h * d->w;
-    single_group(a, d, a.M, (int)g.kd);
-    kmax = (int)g.kd;
+    kmax = (int)(bf16 ? g.kd16 : g.kd);
+    single_group(a, d, a.M, kmax);
   }
-  plan_splits(a, kmax);
+  plan_splits(a, kmax, bf16 ? BKH : BK);
   return a;
 }
 
@@ -885,23 +1437,44 @@ int launch_gemm(const GemmArgs& a, hipStream_t s, double flops) {
   return check_launch("conv_splitk_epilogue");
 }
 
+// bf16 instances: timing kinds 64 + mode * 8 + tile config.
+template <int MODE>
+int launch_gemm_bf16(const GemmArgs& a, hipStream_t s, double flops) {
+  const int bn = pick_bn(a.N);
+  dim3 grid(a.tiles_total * a.splits), block(256);
+  const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
+  if (timing_on()) timing_begin(s);
+  if (cfg == 0) hipLaunchKernelGGL((conv_gemm_bf16<128, 128, 2, 2, MODE>), grid, block, 0, s, a);
+  else if (cfg == 1) hipLaunchKernelGGL((conv_gemm_bf16<128, 96, 4, 1, MODE>), grid, block, 0, s, a);
+  else if (cfg == 2) hipLaunchKernelGGL((conv_gemm_bf16<256, 64, 4, 1, MODE>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((conv_gemm_bf16<256, 32, 4, 1, MODE>), grid, block, 0, s, a);
+  if (timing_on()) timing_end(s, 64 + MODE * 8 + cfg, flops);
+  int st = check_launch("conv_gemm_bf16");
+  if (st || a.splits == 1) return st;
+  const int64_t items = slab_rows(a) * cdiv(a.N, 4);
+  hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
+                     a);
+  return check_launch("conv_splitk_epilogue");
+}
+
 struct WgradPlan {
   int splits, k_per_split, M, ldc;
   int64_t split_stride;
 };
 
-WgradPlan wgrad_plan(const of_conv_desc* d) {
+WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false) {
   Geo g = geo(d);
   WgradPlan p;
   p.M = g.taps * g.cin_p;
   p.ldc = g.cout_p;
+  const int bk = bf16 ? BKH : BK;
   const int K = d->n * d->ho * d->wo;
   const int tiles = (int)(cdiv(p.M, pick_bm(d->cout)) * cdiv(d->cout, pick_bn(d->cout)));
   // Fill up to 4 workgroups per CU without overshooting a multiple of the CU count (an
   // overshoot leaves a few CUs with one extra long-running workgroup: a tail).
   int splits = std::max(1, (4 * kCUs) / tiles);
-  splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * BK)));
-  p.k_per_split = (int)round_up(cdiv(K, splits), BK);
+  splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * bk)));
+  p.k_per_split = (int)round_up(cdiv(K, splits), bk);
   p.splits = (int)cdiv(K, p.k_per_split);
   p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
   return p;
@@ -924,6 +1497,58 @@ int64_t of_conv_wbwd_elems(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return -1;
   Geo g = geo(d);
   return g.kd * g.nd;
+}
+
+int64_t of_conv_wfwd16_elems(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return -1;
+  Geo g = geo(d);
+  return (int64_t)g.cout_p * g.kf16;
+}
+
+int64_t of_conv_wbwd16_elems(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return -1;
+  Geo g = geo(d);
+  return g.kd16 * g.nd;
+}
+
+static PackEntry pack_entry(const of_conv_desc* d, const float* w, void* wf, void* wd,
+                            int bf16) {
+  const Geo g = geo(d);
+  PackEntry E{};
+  E.w = w;
+  E.wf = static_cast<float*>(wf);
+  E.wd = static_cast<float*>(wd);
+  E.taps = g.taps;
+  E.kw = d->kw;
+  E.cin = d->cin;
+  E.cout = d->cout;
+  E.cin_p = g.cin_p;
+  E.cout_p = g.cout_p;
+  E.kf = g.kf;
+  E.nf = g.nf;
+  E.nd = g.nd;
+  E.bf16 = bf16;
+  E.kf16 = g.kf16;
+  E.kd16 = g.kd16;
+  E.pg = g.pg;
+  return E;
+}
+
+static int64_t pack_work(const of_conv_desc* d, int bf16) {
+  const Geo g = geo(d);
+  return bf16 ? (int64_t)g.cout_p * g.kf16 + g.kd16 * g.nd : (int64_t)g.kf * g.nf + g.kd * g.nd;
+}
+
+int of_conv_pack_weights_bf16(const of_conv_desc* d, const float* w_hwio, void* w16_fwd,
+                              void* w16_bwd, void* stream) {
+  int st = validate(d);
+  if (st) return st;
+  OF_CHECK_ARG(w_hwio && w16_fwd && w16_bwd, "pack bf16: NULL pointer");
+  const int64_t total = pack_work(d, 1);
+  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+  hipLaunchKernelGGL(pack_one_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+                     pack_entry(d, w_hwio, w16_fwd, w16_bwd, 1), total);
+  return check_launch("pack_bf16");
 }
 
 int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fwd,
@@ -959,8 +1584,9 @@ size_t of_conv_pack_table_bytes(int nconv) {
   return sizeof(PackTableHeader) + (size_t)std::max(nconv, 0) * sizeof(PackEntry);
 }
 
-int of_conv_pack_table(int nconv, const of_conv_desc* descs, const float* const* w_hwio,
-                       float* const* w_fwd, float* const* w_bwd, void* host_table) {
+int of_conv_pack_table_ex(int nconv, const of_conv_desc* descs, const float* const* w_hwio,
+                          void* const* w_fwd, void* const* w_bwd, const int* bf16,
+                          void* host_table) {
   OF_CHECK_ARG(nconv > 0 && descs && w_hwio && w_fwd && w_bwd && host_table, "pack table: args");
   PackTableHeader* h = static_cast<PackTableHeader*>(host_table);
   PackEntry* e = reinterpret_cast<PackEntry*>(static_cast<char*>(host_table) +
@@ -970,29 +1596,21 @@ int of_conv_pack_table(int nconv, const of_conv_desc* descs, const float* const*
     int st = validate(&descs[i]);
     if (st) return st;
     OF_CHECK_ARG(w_hwio[i] && w_fwd[i] && w_bwd[i], "pack table: NULL weight pointer");
-    const Geo g = geo(&descs[i]);
-    PackEntry& E = e[i];
-    E = PackEntry{};
-    E.w = w_hwio[i];
-    E.wf = w_fwd[i];
-    E.wd = w_bwd[i];
-    E.taps = g.taps;
-    E.kw = descs[i].kw;
-    E.cin = descs[i].cin;
-    E.cout = descs[i].cout;
-    E.cin_p = g.cin_p;
-    E.cout_p = g.cout_p;
-    E.kf = g.kf;
-    E.nf = g.nf;
-    E.nd = g.nd;
-    E.pg = g.pg;
-    E.work_begin = work;
-    work += (int64_t)g.kf * g.nf + g.kd * g.nd;
+    const int b16 = bf16 ? (bf16[i] != 0) : 0;
+    e[i] = pack_entry(&descs[i], w_hwio[i], w_fwd[i], w_bwd[i], b16);
+    e[i].work_begin = work;
+    work += pack_work(&descs[i], b16);
   }
   h->nconv = nconv;
   h->pad = 0;
   h->total = work;
   return OF_OK;
+}
+
+int of_conv_pack_table(int nconv, const of_conv_desc* descs, const float* const* w_hwio,
+                       float* const* w_fwd, float* const* w_bwd, void* host_table) {
+  return of_conv_pack_table_ex(nconv, descs, w_hwio, reinterpret_cast<void* const*>(w_fwd),
+                               reinterpret_cast<void* const*>(w_bwd), nullptr, host_table);
 }
 
 int of_conv_pack_many(const void* dev_table, int64_t total_work, void* stream) {
@@ -1020,11 +1638,27 @@ size_t of_conv2d_dgrad_workspace(const of_conv_desc* d) {
   return fd_workspace(dgrad_args(d, geo(d)));
 }
 
-int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w_fwd,
-                  const float* bias, const float* bn_gamma, const float* bn_beta,
-                  const float* bn_mean, const float* bn_var, float bn_eps,
-                  const float* residual, int ldr, int act, float alpha, float* z, int ldz,
-                  float* y, int ldy, void* workspace, size_t ws_bytes, void* stream) {
+size_t of_conv2d_fwd_bf16_workspace(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return 0;
+  return fd_workspace(fwd_args(d, geo(d), true));
+}
+
+size_t of_conv2d_dgrad_bf16_workspace(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return 0;
+  return fd_workspace(dgrad_args(d, geo(d), true));
+}
+
+int of_conv_path(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return -1;
+  return narrow_ok(d) ? 1 : 0;
+}
+
+static int conv_fwd_impl(bool bf16, const of_conv_desc* d, const float* x, int ldx,
+                         const void* w_fwd, const float* bias, const float* bn_gamma,
+                         const float* bn_beta, const float* bn_mean, const float* bn_var,
+                         float bn_eps, const float* residual, int ldr, int act, float alpha,
+                         float* z, int ldz, float* y, int ldy, void* workspace, size_t ws_bytes,
+                         void* stream) {
   int st = validate(d);
   if (st) return st;
   OF_CHECK_ARG(x && w_fwd && y, "conv fwd: NULL pointer");
@@ -1035,21 +1669,21 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   OF_CHECK_ARG(!z || ldz >= d->cout, "conv fwd: ldz");
   OF_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_fwd & 15) == 0,
                "conv fwd: x / w must be 16-byte aligned");
-  if (narrow_ok(d) && !bn_gamma && !residual && !z) {   // 2-channel flow layers: VALU path
+  if (!bf16 && narrow_ok(d) && !bn_gamma && !residual && !z) {   // 2-channel layers: VALU
     hipStream_t s = as_stream(stream);
     if (timing_on()) timing_begin(s);
-    st = narrow_fwd(d, x, ldx, w_fwd, bias, act, alpha, y, ldy, s);
+    st = narrow_fwd(d, x, ldx, static_cast<const float*>(w_fwd), bias, act, alpha, y, ldy, s);
     if (timing_on()) timing_end(s, MODE_FWD * 8 + KIND_NARROW, conv_flops(d));
     return st;
   }
   Geo g = geo(d);
-  GemmArgs a = fwd_args(d, g);
-  attach_slab(a, workspace, ws_bytes);
+  GemmArgs a = fwd_args(d, g, bf16);
+  attach_slab(a, workspace, ws_bytes, bf16 ? BKH : BK);
   a.A = x;
   a.lda = ldx;
   a.a_bytes = (int64_t)d->n * d->h * d->w * ldx * 4;
-  a.B = w_fwd;
-  a.b_bytes = (int64_t)g.kf * g.nf * 4;
+  a.B = static_cast<const float*>(w_fwd);
+  a.b_bytes = bf16 ? (int64_t)g.cout_p * g.kf16 * 2 : (int64_t)g.kf * g.nf * 4;
   OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX,
                "conv fwd: tensors must be < 2 GiB (32-bit buffer offsets)");
   a.C = y;
@@ -1068,13 +1702,34 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
-  st = launch_gemm<MODE_FWD>(a, s, flops);
+  st = bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops) : launch_gemm<MODE_FWD>(a, s, flops);
   return st;
 }
 
-int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
-                    const float* act_src, int ld_act, int act, float alpha, float* dx,
-                    int lddx, void* workspace, size_t ws_bytes, void* stream) {
+int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w_fwd,
+                  const float* bias, const float* bn_gamma, const float* bn_beta,
+                  const float* bn_mean, const float* bn_var, float bn_eps,
+                  const float* residual, int ldr, int act, float alpha, float* z, int ldz,
+                  float* y, int ldy, void* workspace, size_t ws_bytes, void* stream) {
+  return conv_fwd_impl(false, d, x, ldx, w_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
+                       bn_eps, residual, ldr, act, alpha, z, ldz, y, ldy, workspace, ws_bytes,
+                       stream);
+}
+
+int of_conv2d_fwd_bf16(const of_conv_desc* d, const float* x, int ldx, const void* w16_fwd,
+                       const float* bias, const float* bn_gamma, const float* bn_beta,
+                       const float* bn_mean, const float* bn_var, float bn_eps,
+                       const float* residual, int ldr, int act, float alpha, float* z, int ldz,
+                       float* y, int ldy, void* workspace, size_t ws_bytes, void* stream) {
+  return conv_fwd_impl(true, d, x, ldx, w16_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
+                       bn_eps, residual, ldr, act, alpha, z, ldz, y, ldy, workspace, ws_bytes,
+                       stream);
+}
+
+static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, int lddy,
+                           const void* w_bwd, const float* act_src, int ld_act, int act,
+                           float alpha, float* dx, int lddx, void* workspace, size_t ws_bytes,
+                           void* stream) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
@@ -1085,20 +1740,21 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
   OF_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)w_bwd & 15) == 0,
                "conv dgrad: dy / w must be 16-byte aligned");
   OF_CHECK_ARG(d->stride == 1 || d->stride == 2, "conv dgrad: stride must be 1 or 2");
-  if (narrow_ok(d)) {
+  if (!bf16 && narrow_ok(d)) {
     hipStream_t s = as_stream(stream);
     if (timing_on()) timing_begin(s);
-    st = narrow_dgrad(d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, dx, lddx, s);
+    st = narrow_dgrad(d, dy, lddy, static_cast<const float*>(w_bwd), act_src, ld_act, act,
+                      alpha, dx, lddx, s);
     if (timing_on()) timing_end(s, MODE_DGRAD * 8 + KIND_NARROW, conv_flops(d));
     return st;
   }
-  GemmArgs a = dgrad_args(d, g);
-  attach_slab(a, workspace, ws_bytes);
+  GemmArgs a = dgrad_args(d, g, bf16);
+  attach_slab(a, workspace, ws_bytes, bf16 ? BKH : BK);
   a.A = dy;
   a.lda = lddy;
   a.a_bytes = (int64_t)d->n * d->ho * d->wo * lddy * 4;
-  a.B = w_bwd;
-  a.b_bytes = g.kd * g.nd * 4;
+  a.B = static_cast<const float*>(w_bwd);
+  a.b_bytes = bf16 ? g.kd16 * g.nd * 2 : g.kd * g.nd * 4;
   OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX,
                "conv dgrad: tensors must be < 2 GiB (32-bit buffer offsets)");
   a.C = dx;
@@ -1109,8 +1765,22 @@ int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const floa
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
-  st = launch_gemm<MODE_DGRAD>(a, s, flops);
+  st = bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops) : launch_gemm<MODE_DGRAD>(a, s, flops);
   return st;
+}
+
+int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
+                    const float* act_src, int ld_act, int act, float alpha, float* dx,
+                    int lddx, void* workspace, size_t ws_bytes, void* stream) {
+  return conv_dgrad_impl(false, d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, dx, lddx,
+                         workspace, ws_bytes, stream);
+}
+
+int of_conv2d_dgrad_bf16(const of_conv_desc* d, const float* dy, int lddy, const void* w16_bwd,
+                         const float* act_src, int ld_act, int act, float alpha, float* dx,
+                         int lddx, void* workspace, size_t ws_bytes, void* stream) {
+  return conv_dgrad_impl(true, d, dy, lddy, w16_bwd, act_src, ld_act, act, alpha, dx, lddx,
+                         workspace, ws_bytes, stream);
 }
 
 size_t of_conv2d_wgrad_workspace(const of_conv_desc* d) {
@@ -1120,24 +1790,33 @@ size_t of_conv2d_wgrad_workspace(const of_conv_desc* d) {
   return (size_t)p.splits * p.split_stride * sizeof(float);
 }
 
-int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float* dy, int lddy,
-                    float* dw, float* db, int accumulate, void* workspace, size_t ws_bytes,
-                    void* stream) {
+size_t of_conv2d_wgrad_bf16_workspace(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return 0;
+  if (narrow_ok(d)) return narrow_wgrad_ws(d);
+  WgradPlan p = wgrad_plan(d, true);
+  return (size_t)p.splits * p.split_stride * sizeof(float);
+}
+
+static int conv_wgrad_impl(bool bf16, const of_conv_desc* d, const float* x, int ldx,
+                           const float* dy, int lddy, float* dw, float* db, int accumulate,
+                           void* workspace, size_t ws_bytes, void* stream) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
   OF_CHECK_ARG(x && dy && dw && workspace, "conv wgrad: NULL pointer");
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv wgrad: lddy");
-  OF_CHECK_ARG(ws_bytes >= of_conv2d_wgrad_workspace(d), "conv wgrad: workspace too small");
   if (narrow_ok(d)) {
+    OF_CHECK_ARG(ws_bytes >= narrow_wgrad_ws(d), "conv wgrad: workspace too small");
     hipStream_t s = as_stream(stream);
     if (timing_on()) timing_begin(s);
     st = narrow_wgrad(d, x, ldx, dy, lddy, dw, db, accumulate, workspace, s);
     if (timing_on()) timing_end(s, MODE_WGRAD * 8 + KIND_NARROW, conv_flops(d));
     return st;
   }
-  WgradPlan p = wgrad_plan(d);
+  WgradPlan p = wgrad_plan(d, bf16);
+  OF_CHECK_ARG(ws_bytes >= (size_t)p.splits * p.split_stride * sizeof(float),
+               "conv wgrad: workspace too small");
   GemmArgs a = base_args(d);
   a.kc = g.cin_p;
   a.N = d->cout;
@@ -1161,13 +1840,40 @@ int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float*
   a.colsum = db != nullptr;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
-  st = launch_gemm<MODE_WGRAD>(a, s, flops);
+  if (bf16) {
+    const int bn = pick_bn(a.N);
+    const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
+    dim3 grid(a.tiles_total * a.splits), block(256);
+    if (timing_on()) timing_begin(s);
+    if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_bf16<128, 128, 2, 2>), grid, block, 0, s, a);
+    else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_bf16<128, 96, 4, 1>), grid, block, 0, s, a);
+    else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_bf16<256, 64, 4, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_bf16<256, 32, 4, 1>), grid, block, 0, s, a);
+    if (timing_on()) timing_end(s, 64 + MODE_WGRAD * 8 + cfg, flops);
+    st = check_launch("conv_wgrad_bf16");
+  } else {
+    st = launch_gemm<MODE_WGRAD>(a, s, flops);
+  }
   if (st) return st;
   const int64_t items = ((int64_t)g.taps * d->cin + (db ? 1 : 0)) * cdiv(d->cout, 4);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
                      static_cast<const float*>(workspace), p.splits, p.split_stride, g.taps,
                      g.cin_p, d->cin, d->cout, p.ldc, dw, db, accumulate);
   return check_launch("wgrad_reduce");
+}
+
+int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float* dy, int lddy,
+                    float* dw, float* db, int accumulate, void* workspace, size_t ws_bytes,
+                    void* stream) {
+  return conv_wgrad_impl(false, d, x, ldx, dy, lddy, dw, db, accumulate, workspace, ws_bytes,
+                         stream);
+}
+
+int of_conv2d_wgrad_bf16(const of_conv_desc* d, const float* x, int ldx, const float* dy,
+                         int lddy, float* dw, float* db, int accumulate, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  return conv_wgrad_impl(true, d, x, ldx, dy, lddy, dw, db, accumulate, workspace, ws_bytes,
+                         stream);
 }
 
 }  // extern "C"

@@ -261,7 +261,8 @@ def flow_module(features1, features2, previous_flow, max_disp, head: Optional[Fl
 class FlowNet:
     """The Keras ``Model`` returned by build_flow_net (model.py:119-143)."""
 
-    def __init__(self, height, width, max_disp=3, seed=0, device="cuda", values=None):
+    def __init__(self, height, width, max_disp=3, seed=0, device="cuda", values=None,
+                 precision="fp32"):
         assert height % 16 == 0 and width % 16 == 0, "H and W must be divisible by 16 (P17)"
         self.height, self.width, self.max_disp = height, width, max_disp
         self.store = ParamStore(flow_net_spec(max_disp), values=values, device=device,
@@ -269,6 +270,19 @@ class FlowNet:
         self.encoder = Encoder(self.store)
         self.heads = [FlowHead(self.store, level, max_disp) for level in range(4)]
         self.name = "flow_net"
+        self._packer = None
+        self.set_precision(precision)
+
+    def set_precision(self, precision):
+        """"fp32" (config 2) or "bf16" (configs 3-5: conv fwd / dgrad on bf16 MFMA, fp32
+        accumulation, fp32 activations, weights, gradients and Adam state)."""
+        assert precision in ("fp32", "bf16"), precision
+        self.precision = precision
+        for L in self.conv_layers():
+            L.precision = precision
+            L._bf16 = None
+            L._wf = L._wd = None
+            L._pack_key = None
         self._packer = None
 
     def conv_layers(self):
@@ -326,11 +340,11 @@ class FlowNet:
 
 
 def build_flow_net(height, width, pretrained_weights_path=None, max_disp=3, seed=0,
-                   device="cuda"):
+                   device="cuda", precision="fp32"):
     """model.py:119-143.  ``pretrained_weights_path``: an .npz of encoder weights named as in
     params.encoder_spec() (Keras-checkpoint import is out of scope, SURVEY.md §8 f); the
     reference asserts every encoder object is matched (model.py:129) -- so does this."""
-    net = FlowNet(height, width, max_disp, seed=seed, device=device)
+    net = FlowNet(height, width, max_disp, seed=seed, device=device, precision=precision)
     if pretrained_weights_path is not None:
         with np.load(pretrained_weights_path, allow_pickle=False) as z:
             vals = {k: z[k] for k in z.files}

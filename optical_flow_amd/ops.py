@@ -101,7 +101,7 @@ class ConvLayer:
     parameters (HWIO kernel, bias, BN vectors) and its per-step packed weights."""
 
     def __init__(self, kernel, bias, stride=1, act=ACT_NONE, alpha=LEAKY_ALPHA, bn=None,
-                 cin_p=None, version_of=None, name=""):
+                 cin_p=None, version_of=None, name="", precision="fp32"):
         self.kernel, self.bias = kernel, bias
         kh, kw, cin, cout = kernel.shape
         self.kh, self.kw, self.cin, self.cout = kh, kw, cin, cout
@@ -110,9 +110,12 @@ class ConvLayer:
         self.bn = bn                      # (gamma, beta, moving_mean, moving_variance) or None
         self.version_of = version_of      # callable -> int, bumps when the weights change
         self.name = name
+        assert precision in ("fp32", "bf16"), precision
+        self.precision = precision        # "bf16": fwd / dgrad on bf16 MFMA (configs 3-5)
         self._pack_key = None
         self._wf = self._wd = None
         self._descs = {}
+        self._bf16 = None
 
     def desc(self, n, h, w) -> ConvDesc:
         key = (n, h, w)
@@ -125,17 +128,54 @@ class ConvLayer:
             self._descs[key] = d
         return d
 
+    def bf16(self, d: ConvDesc = None) -> bool:
+        """True when fwd/dgrad run the bf16 MFMA kernels (bf16 precision, GEMM-path layer)."""
+        if self._bf16 is None:
+            d = d or self.desc(1, 16, 16)
+            self._bf16 = (self.precision == "bf16" and
+                          _lib.lib().of_conv_path(C.byref(d)) == 0)
+        return self._bf16
+
+    def alloc_packed(self, d: ConvDesc):
+        lib = _lib.lib()
+        dev = self.kernel.device
+        if self.bf16(d):
+            self._wf = torch.empty(lib.of_conv_wfwd16_elems(C.byref(d)), device=dev,
+                                   dtype=torch.bfloat16)
+            self._wd = torch.empty(lib.of_conv_wbwd16_elems(C.byref(d)), device=dev,
+                                   dtype=torch.bfloat16)
+        else:
+            self._wf = torch.empty(lib.of_conv_wfwd_elems(C.byref(d)), device=dev)
+            self._wd = torch.empty(lib.of_conv_wbwd_elems(C.byref(d)), device=dev)
+
     def packed(self, d: ConvDesc):
         key = (self.kernel.data_ptr(), self.version_of() if self.version_of else None)
         if self._wf is None:
-            lib = _lib.lib()
-            self._wf = torch.empty(lib.of_conv_wfwd_elems(C.byref(d)), device=self.kernel.device)
-            self._wd = torch.empty(lib.of_conv_wbwd_elems(C.byref(d)), device=self.kernel.device)
+            self.alloc_packed(d)
         if key != self._pack_key or self.version_of is None:
-            call("of_conv_pack_weights", C.byref(d), _ptr(self.kernel), _ptr(self._wf),
-                 _ptr(self._wd), _stream())
+            call("of_conv_pack_weights_bf16" if self.bf16(d) else "of_conv_pack_weights",
+                 C.byref(d), _ptr(self.kernel), _ptr(self._wf), _ptr(self._wd), _stream())
             self._pack_key = key
         return self._wf, self._wd
+
+    def fwd_entry(self, d):
+        """(C entry point, workspace bytes) of the forward conv for this layer's precision."""
+        lib = _lib.lib()
+        if self.bf16(d):
+            return "of_conv2d_fwd_bf16", lib.of_conv2d_fwd_bf16_workspace(C.byref(d))
+        return "of_conv2d_fwd", lib.of_conv2d_fwd_workspace(C.byref(d))
+
+    def wgrad_entry(self, d):
+        lib = _lib.lib()
+        if self.bf16(d):
+            return "of_conv2d_wgrad_bf16", lib.of_conv2d_wgrad_bf16_workspace(C.byref(d))
+        return "of_conv2d_wgrad", lib.of_conv2d_wgrad_workspace(C.byref(d))
+
+    def dgrad_entry(self, d):
+        lib = _lib.lib()
+        if self.bf16(d):
+            return "of_conv2d_dgrad_bf16", lib.of_conv2d_dgrad_bf16_workspace(C.byref(d))
+        return "of_conv2d_dgrad", lib.of_conv2d_dgrad_workspace(C.byref(d))
 
     def __call__(self, x, residual=None):
         bn = self.bn or (None, None, None, None)
@@ -153,16 +193,16 @@ class ConvPacker:
         n = len(self.layers)
         descs = (ConvDesc * n)()
         wp, fp, bp = (C.c_void_p * n)(), (C.c_void_p * n)(), (C.c_void_p * n)()
+        flags = (C.c_int * n)()
         for i, L in enumerate(self.layers):
             d = L.desc(1, 16, 16)
             descs[i] = d
-            dev = L.kernel.device
-            L._wf = torch.empty(lib.of_conv_wfwd_elems(C.byref(d)), device=dev)
-            L._wd = torch.empty(lib.of_conv_wbwd_elems(C.byref(d)), device=dev)
+            L.alloc_packed(d)
+            flags[i] = 1 if L.bf16(d) else 0
             wp[i], fp[i], bp[i] = L.kernel.data_ptr(), L._wf.data_ptr(), L._wd.data_ptr()
         nbytes = lib.of_conv_pack_table_bytes(n)
         host = (C.c_char * nbytes)()
-        call("of_conv_pack_table", n, descs, wp, fp, bp, host)
+        call("of_conv_pack_table_ex", n, descs, wp, fp, bp, flags, host)
         self.total = C.c_int64.from_buffer(host, 8).value
         self.table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(
             self.layers[0].kernel.device)
@@ -212,8 +252,9 @@ class _ConvFn(torch.autograd.Function):
             residual = residual.contiguous()
             assert residual.shape == y.shape
         _tag(layer, 0)
-        wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_fwd_workspace(C.byref(d)), x.device)
-        call("of_conv2d_fwd", C.byref(d), _ptr(x), cx, _ptr(wf), _ptr(bias),
+        entry, wsz = layer.fwd_entry(d)
+        wsk, wsp, wsb = _workspace(wsz, x.device)
+        call(entry, C.byref(d), _ptr(x), cx, _ptr(wf), _ptr(bias),
              _ptr(bn[0]) if bn else None, _ptr(bn[1]) if bn else None,
              _ptr(bn[2]) if bn else None, _ptr(bn[3]) if bn else None, BN_EPS,
              _ptr(residual), layer.cout, layer.act, layer.alpha,
@@ -268,13 +309,13 @@ class _ConvFn(torch.autograd.Function):
         if need_k or (need_b and not bias_done):
             tk = grad_target(layer.kernel)
             tbias = grad_target(layer.bias) if (need_b and not bias_done) else (None, 0, None)
-            wsb = _lib.lib().of_conv2d_wgrad_workspace(C.byref(d))
+            went, wsb = layer.wgrad_entry(d)
             ws = torch.empty(wsb // 4 + 1, device=dy.device)
             if tbias[0] is not None and tbias[1] != tk[1]:
                 # mixed arena / fresh targets: compute the bias into a temp, then place it
                 tmpb = torch.empty_like(layer.bias)
                 _tag(layer, 2)
-                call("of_conv2d_wgrad", C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
+                call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
                      _ptr(tk[0]), _ptr(tmpb), tk[1], _ptr(ws), wsb, s)
                 if tbias[1]:
                     call("of_add_inplace", _ptr(tbias[0]), _ptr(tmpb), tmpb.numel(), s)
@@ -282,7 +323,7 @@ class _ConvFn(torch.autograd.Function):
                     tbias = (tmpb, 0, tmpb)
             else:
                 _tag(layer, 2)
-                call("of_conv2d_wgrad", C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
+                call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
                      _ptr(tk[0]), _ptr(tbias[0]), tk[1], _ptr(ws), wsb, s)
             ret_k = tk[2] if need_k else None
             if need_b and not bias_done:
@@ -293,9 +334,9 @@ class _ConvFn(torch.autograd.Function):
         if need_x:
             dx = torch.empty((n, h, w, cx), device=dy.device)
             _tag(layer, 1)
-            wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_dgrad_workspace(C.byref(d)),
-                                       dy.device)
-            call("of_conv2d_dgrad", C.byref(d), _ptr(dzp), dzp.shape[-1], _ptr(wd), None, 0,
+            entry, wsz = layer.dgrad_entry(d)
+            wsk, wsp, wsb = _workspace(wsz, dy.device)
+            call(entry, C.byref(d), _ptr(dzp), dzp.shape[-1], _ptr(wd), None, 0,
                  ACT_NONE, 0.0, _ptr(dx), cx, wsp, wsb, s)
         return dx, ret_k, ret_b, ret_g, ret_be, dres, None
 
@@ -323,8 +364,9 @@ class _ConvStackFn(torch.autograd.Function):
             wf, _ = layer.packed(d)
             y = torch.empty((nb, d.ho, d.wo, layer.cout), device=x.device)
             _tag(layer, 0)
-            wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_fwd_workspace(C.byref(d)), x.device)
-            call("of_conv2d_fwd", C.byref(d), _ptr(acts[-1]), cx, _ptr(wf), _ptr(layer.bias),
+            entry, wsz = layer.fwd_entry(d)
+            wsk, wsp, wsb = _workspace(wsz, x.device)
+            call(entry, C.byref(d), _ptr(acts[-1]), cx, _ptr(wf), _ptr(layer.bias),
                  None, None, None, None, BN_EPS, None, 0, layer.act, layer.alpha, None, 0,
                  _ptr(y), layer.cout, wsp, wsb, s)
             if i + 1 < n:
@@ -359,10 +401,10 @@ class _ConvStackFn(torch.autograd.Function):
             tb = grad_target(layer.bias)
             if tk[1] != tb[1]:
                 raise RuntimeError("kernel and bias gradients must both use the arena or not")
-            wsb = _lib.lib().of_conv2d_wgrad_workspace(C.byref(d))
+            went, wsb = layer.wgrad_entry(d)
             ws = torch.empty(wsb // 4 + 1, device=x.device)
             _tag(layer, 2)
-            call("of_conv2d_wgrad", C.byref(d), _ptr(x), cx, _ptr(g), g.shape[-1], _ptr(tk[0]),
+            call(went, C.byref(d), _ptr(x), cx, _ptr(g), g.shape[-1], _ptr(tk[0]),
                  _ptr(tb[0]), tk[1], _ptr(ws), wsb, s)
             layer._ret = (tk[2], tb[2])
             _grad_ready(layer.kernel, layer.bias)
@@ -370,17 +412,17 @@ class _ConvStackFn(torch.autograd.Function):
                 prev = layers[i - 1]
                 gx = torch.empty((nb, h, w, cx), device=x.device)
                 _tag(layer, 1)
-                wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_dgrad_workspace(C.byref(d)),
-                                           x.device)
-                call("of_conv2d_dgrad", C.byref(d), _ptr(g), g.shape[-1], _ptr(wd), _ptr(x), cx,
+                entry, wsz = layer.dgrad_entry(d)
+                wsk, wsp, wsb = _workspace(wsz, x.device)
+                call(entry, C.byref(d), _ptr(g), g.shape[-1], _ptr(wd), _ptr(x), cx,
                      prev.act, prev.alpha, _ptr(gx), cx, wsp, wsb, s)
                 g = gx
             elif needs[0]:
                 dx = torch.empty((nb, h, w, cx), device=x.device)
                 _tag(layer, 1)
-                wsk, wsp, wsb = _workspace(_lib.lib().of_conv2d_dgrad_workspace(C.byref(d)),
-                                           x.device)
-                call("of_conv2d_dgrad", C.byref(d), _ptr(g), g.shape[-1], _ptr(wd), None, 0,
+                entry, wsz = layer.dgrad_entry(d)
+                wsk, wsp, wsb = _workspace(wsz, x.device)
+                call(entry, C.byref(d), _ptr(g), g.shape[-1], _ptr(wd), None, 0,
                      ACT_NONE, 0.0, _ptr(dx), cx, wsp, wsb, s)
         rets = []
         for layer in layers:

@@ -37,8 +37,62 @@ def same_pads(n: int, k: int, s: int):
     return total // 2, total - total // 2
 
 
+# Conv operand precision of the build under test: "fp32" (config 2) or "bf16" (configs 3-5:
+# forward, input-gradient and weight-gradient contractions on bf16-rounded operands, fp32
+# accumulation; the bias gradient and the narrow cout <= 4 layers stay fp32 -- the HIP
+# build's policy).
+CONV_PRECISION = "fp32"
+
+
+def set_conv_precision(p):
+    global CONV_PRECISION
+    assert p in ("fp32", "bf16"), p
+    CONV_PRECISION = p
+
+
+def bf16_round(t):
+    """Round to bf16 (round-to-nearest-even) and back to t's dtype."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def _narrow(w, stride):
+    """The build's narrow-conv rule (conv_narrow.hip narrow_ok): those stay fp32."""
+    kh, kw, cin, cout = w.shape
+    nq = (cin + 3) // 4
+    return cout <= 4 and stride == 1 and kh == 3 and kw == 3 and nq in (1, 2, 4, 8, 16)
+
+
+class _Bf16Conv(torch.autograd.Function):
+    """conv2d_same with bf16-rounded operands (x, w, and dz for both gradients), exact bias
+    gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride):
+        ctx.save_for_backward(x, w)
+        ctx.stride = stride
+        return _conv2d_same_exact(bf16_round(x), bf16_round(w), b, stride)
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, w = [t.detach() for t in ctx.saved_tensors]
+        with torch.enable_grad():
+            xv = x.clone().requires_grad_(True)
+            (_conv2d_same_exact(xv, bf16_round(w), None, ctx.stride) * bf16_round(dz)).sum().backward()
+            wv = w.clone().requires_grad_(True)
+            (_conv2d_same_exact(bf16_round(x), wv, None, ctx.stride) *
+             bf16_round(dz)).sum().backward()
+        db = dz.sum(dim=(0, 1, 2)) if ctx.needs_input_grad[2] else None
+        return xv.grad, wv.grad, db, None
+
+
 def conv2d_same(x, w, b, stride=1):
     """layers.Conv2D(padding='same') on NHWC x, HWIO w (model.py:12,104-114)."""
+    if CONV_PRECISION == "bf16" and not _narrow(w, stride):
+        return _Bf16Conv.apply(x, w, b, stride)
+    return _conv2d_same_exact(x, w, b, stride)
+
+
+def _conv2d_same_exact(x, w, b, stride=1):
     kh, kw = w.shape[0], w.shape[1]
     pt, pb = same_pads(x.shape[1], kh, stride)
     pl, pr = same_pads(x.shape[2], kw, stride)

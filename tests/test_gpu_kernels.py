@@ -88,6 +88,56 @@ def test_conv_fwd_bwd(case):
         assert rel_inf(resd.grad, reso.grad) < REL_TOL, "residual grad"
 
 
+BF16_CASES = [c for c in CONV_CASES if c[4] > 4]
+
+
+@pytest.mark.parametrize("case", BF16_CASES, ids=lambda c: "x".join(map(str, c[:7])) + c[7])
+def test_conv_bf16(case):
+    """bf16 MFMA fwd/dgrad (configs 3-5) against the float64 oracle on bf16-rounded operands."""
+    ops = _ops()
+    from optical_flow_amd._lib import ACT_LEAKY, ACT_NONE, ACT_RELU
+    n, h, w, cin, cout, k, s, act, use_bn, use_res = case
+    seed = hash(case) % 1000 + 17
+    x = rng_tensor((n, h, w, cin), seed)
+    wt = rng_tensor((k, k, cin, cout), seed + 1, scale=(2.0 / (k * k * cin)) ** 0.5)
+    b = rng_tensor((cout,), seed + 2, scale=0.1)
+    g = rng_tensor((cout,), seed + 3, lo=0.5, hi=1.5)
+    be = rng_tensor((cout,), seed + 4, scale=0.1)
+    mu = rng_tensor((cout,), seed + 5, scale=0.1)
+    var = rng_tensor((cout,), seed + 6, lo=0.5, hi=1.5)
+    xo, wo_, bo = [f64(t).requires_grad_(True) for t in (x, wt, b)]
+    yo = R._Bf16Conv.apply(xo, wo_, bo, s)
+    p = {"bn/gamma": f64(g), "bn/beta": f64(be), "bn/moving_mean": f64(mu),
+         "bn/moving_variance": f64(var)}
+    if use_bn:
+        yo = R.batchnorm_inference(yo, p, "bn")
+    res = rng_tensor(tuple(yo.shape), seed + 7) if use_res else None
+    if use_res:
+        yo = yo + f64(res)
+    yo = {"relu": torch.relu, "leaky": R.leaky_relu, "none": lambda t: t}[act](yo)
+    gy = rng_tensor(tuple(yo.shape), seed + 8)
+    (yo * f64(gy)).sum().backward()
+    cin_p = (cin + 3) // 4 * 4
+    xd = torch.zeros((n, h, w, cin_p), device="cuda")
+    xd[..., :cin] = dev(x)
+    wd, bd = [dev(t).requires_grad_(True) for t in (wt, b)]
+    layer = ops.ConvLayer(wd, bd, stride=s,
+                          act={"relu": ACT_RELU, "leaky": ACT_LEAKY, "none": ACT_NONE}[act],
+                          bn=(dev(g), dev(be), dev(mu), dev(var)) if use_bn else None,
+                          cin_p=cin_p, precision="bf16")
+    assert layer.bf16()
+    xd.requires_grad_(True)
+    yd = layer(xd, residual=dev(res) if use_res else None)
+    assert rel_inf(yd, yo) < REL_TOL, "forward"
+    (yd * dev(gy)).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_inf(xd.grad[..., :cin], xo.grad) < REL_TOL, "dgrad"
+    if cin < cin_p:
+        assert xd.grad[..., cin:].abs().max().item() == 0.0, "padded channels must get 0 grad"
+    assert rel_l2(wd.grad, wo_.grad) < REL_TOL, "wgrad"
+    assert rel_l2(bd.grad, bo.grad) < REL_TOL, "bias grad"
+
+
 # ----------------------------------------------------------------------- cost volume ----
 @pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6), (1, 19, 70, 32)])
 def test_cost_volume(shape):

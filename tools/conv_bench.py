@@ -34,7 +34,7 @@ SHAPES = [
 ]
 
 
-def bench_one(name, n, h, w, cin, cout, k, s, reps):
+def bench_one(name, n, h, w, cin, cout, k, s, reps, precision="fp32"):
     dev = "cuda"
     cin_p = (cin + 3) // 4 * 4
     x = torch.randn(n, h, w, cin_p, device=dev)
@@ -42,7 +42,8 @@ def bench_one(name, n, h, w, cin, cout, k, s, reps):
         x[..., cin:] = 0
     wt = torch.randn(k, k, cin, cout, device=dev) * (2.0 / (k * k * cin)) ** 0.5
     b = torch.randn(cout, device=dev) * 0.1
-    layer = ops.ConvLayer(wt, b, stride=s, act=ACT_LEAKY, cin_p=cin_p, name=name)
+    layer = ops.ConvLayer(wt, b, stride=s, act=ACT_LEAKY, cin_p=cin_p, name=name,
+                          precision=precision)
     d = layer.desc(n, h, w)
     wf, wd = layer.packed(d)
     cout_p = (cout + 3) // 4 * 4
@@ -51,26 +52,26 @@ def bench_one(name, n, h, w, cin, cout, k, s, reps):
     dx = torch.empty_like(x)
     dw = torch.empty_like(wt)
     db = torch.empty_like(b)
-    wsb = _lib.lib().of_conv2d_wgrad_workspace(C.byref(d))
+    went, wsb = layer.wgrad_entry(d)
     ws = torch.empty(wsb // 4 + 1, device=dev)
     st = ops._stream()
-    fws = _lib.lib().of_conv2d_fwd_workspace(C.byref(d))
-    dws = _lib.lib().of_conv2d_dgrad_workspace(C.byref(d))
+    fent, fws = layer.fwd_entry(d)
+    dent, dws = layer.dgrad_entry(d)
     fwt = torch.empty(fws // 4 + 4, device=dev)
     dwt = torch.empty(dws // 4 + 4, device=dev)
     P = ops._ptr
     flops = 2.0 * n * d.ho * d.wo * cout * k * k * cin
 
     def fwd():
-        call("of_conv2d_fwd", C.byref(d), P(x), cin_p, P(wf), P(b), None, None, None, None,
+        call(fent, C.byref(d), P(x), cin_p, P(wf), P(b), None, None, None, None,
              1e-3, None, 0, ACT_LEAKY, 0.3, None, 0, P(y), cout, P(fwt), fws, st)
 
     def dgrad():
-        call("of_conv2d_dgrad", C.byref(d), P(dy), cout_p, P(wd), P(x), cin_p, ACT_LEAKY, 0.3,
+        call(dent, C.byref(d), P(dy), cout_p, P(wd), P(x), cin_p, ACT_LEAKY, 0.3,
              P(dx), cin_p, P(dwt), dws, st)
 
     def wgrad():
-        call("of_conv2d_wgrad", C.byref(d), P(x), cin_p, P(dy), cout_p, P(dw), P(db), 0, P(ws),
+        call(went, C.byref(d), P(x), cin_p, P(dy), cout_p, P(dw), P(db), 0, P(ws),
              wsb, st)
 
     out = {}
@@ -95,6 +96,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default=None)
     ap.add_argument("--tune", default=None, help="key=value[,key=value] of_set_tuning")
+    ap.add_argument("--bf16", action="store_true", help="bf16 MFMA fwd/dgrad/wgrad")
     args = ap.parse_args()
     _lib.load()
     if args.tune:
@@ -105,7 +107,7 @@ def main():
     for sh in SHAPES:
         if args.only and args.only not in sh[0]:
             continue
-        flops, out = bench_one(*sh, args.reps)
+        flops, out = bench_one(*sh, args.reps, "bf16" if args.bf16 else "fp32")
         line = "%-10s %7.2f GF " % (sh[0], flops / 1e9)
         for p, (ms, tf) in out.items():
             line += " %s %7.3f ms %6.1f TF |" % (p, ms, tf)
