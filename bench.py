@@ -45,23 +45,31 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md; no spar
 
 
 def kind_parts(kind):
-    """timing kind -> (mode, tile config, bf16): f32 GEMMs mode*8+cfg, narrow cfg 7, bf16
-    GEMMs 64 + mode*8 + cfg (optical_flow_amd/csrc/conv_f32.hip)."""
-    return (kind % 64) // 8, kind % 8, kind >= 64
+    """timing kind -> (mode, tile config, family): f32 GEMMs mode*8+cfg (narrow VALU cfg 7),
+    bf16 implicit GEMMs 64 + mode*8 + cfg, bf16 halo-tiled 3x3 96 + mode*8 + cfg
+    (optical_flow_amd/csrc/conv_f32.hip)."""
+    fam = "tile_bf16" if kind >= 96 else "bf16" if kind >= 64 else "f32"
+    return (kind % 32) // 8, kind % 8, fam
+
+
+TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1"}
 
 
 def kind_name(kind):
-    mode, cfg, bf = kind_parts(kind)
-    return "%s%s<%s>" % (MODE_NAMES[mode], "_bf16" if bf else "", TILE_TEMPLATE[cfg])
+    mode, cfg, fam = kind_parts(kind)
+    sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16"}[fam]
+    return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (TILE_BN if fam == "tile_bf16"
+                                                 else TILE_TEMPLATE)[cfg])
 
 
 def kernel_symbol(kind):
     """rocprofv3 name of the conv kernel instance behind a timing kind."""
-    mode, cfg, bf = kind_parts(kind)
+    mode, cfg, fam = kind_parts(kind)
     if cfg == 7:
         return NARROW_SYMBOLS[mode]
-    return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (
-        "bf16" if bf else "f32", TILE_TEMPLATE[cfg], mode)
+    if fam == "tile_bf16":
+        return "void oflow::conv_tile_bf16<%s, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode)
+    return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_TEMPLATE[cfg], mode)
 
 
 def gflop_per_pair(H, W, max_disp=3):
@@ -221,7 +229,7 @@ def main():
             if pmc.get("kernel") == sym and pmc.get("config") == [H, W, B]:
                 traffic = pmc.get("hbm_bytes_per_launch")
         allconv = sum(v[0] for v in per.values()) / (sum(v[1] for v in per.values()) * 1e-3) / 1e12
-        peak = BF16_MFMA_PEAK_TFLOPS if kind_parts(dom)[2] else FP32_MFMA_PEAK_TFLOPS
+        peak = FP32_MFMA_PEAK_TFLOPS if kind_parts(dom)[2] == "f32" else BF16_MFMA_PEAK_TFLOPS
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,

@@ -770,6 +770,204 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
   }
 }
 
+// ---- bf16, 3x3 stride 1: 2-D output tiles with an LDS-staged input halo -----------------
+// The implicit-GEMM kernels above re-read the input once per tap (9x for 3x3) through L2;
+// with bf16 MFMA that traffic, not the MFMA, bounds them.  Here a workgroup owns an 8 x 16
+// output-pixel tile (BM = 128 GEMM rows) and, per 32-channel chunk, stages the 10 x 18 input
+// halo once (fp32 -> bf16) and takes all 9 taps' A fragments from it at shifted positions;
+// the 3 taps of one kernel row share a B stage (3 x BN x 32 bf16, double-buffered).
+// fwd:   out(oy, ox) += in(oy + r - pt, ox + s - pl) . W[r][s]
+// dgrad: out(iy, ix) += dy(iy + pt - r, ix + pl - s) . W[r][s]^T
+// GEMM K = channel chunks: a.K = chunks, a.k_per_split = chunks per K slice.
+constexpr int TT_H = 8, TT_W = 16;
+
+template <int BN, int WAVES_M, int WAVES_N, int MODE>
+__global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
+  constexpr int BM = TT_H * TT_W, KS = 3;
+  constexpr int HH = TT_H + KS - 1, HW = TT_W + KS - 1, HP = HH * HW;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  static_assert(WAVES_M * WAVES_N == 4 && TM >= 1 && TN >= 1, "tile");
+  constexpr int HQ = HP * 8, HS = (HQ + 255) / 256;          // halo quads (32 ch)
+  constexpr int BOCT = KS * BN * 4, BSL = (BOCT + 255) / 256; // B octets per kernel row
+  __shared__ uint4 Ah[HP * SROW16];
+  __shared__ uint4 Bs[2][KS * BN * SROW16];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_n = tile % a.n_tiles;
+  const int tile_m = tile / a.n_tiles;
+  const int n0 = tile_n * BN;
+  const int OH = MODE == MODE_FWD ? a.ho : a.h, OW = MODE == MODE_FWD ? a.wo : a.w;
+  const int SH = MODE == MODE_FWD ? a.h : a.ho, SW = MODE == MODE_FWD ? a.w : a.wo;
+  const int tiles_x = (OW + TT_W - 1) / TT_W, tiles_y = (OH + TT_H - 1) / TT_H;
+  const int b = tile_m / (tiles_x * tiles_y);
+  const int trem = tile_m - b * tiles_x * tiles_y;
+  const int oy0 = (trem / tiles_x) * TT_H, ox0 = (trem % tiles_x) * TT_W;
+  const int hy0 = MODE == MODE_FWD ? oy0 - a.pt : oy0 + a.pt - (KS - 1);
+  const int hx0 = MODE == MODE_FWD ? ox0 - a.pl : ox0 + a.pl - (KS - 1);
+  const int c_begin = split * a.k_per_split;
+  const int c_end = min(a.K, c_begin + a.k_per_split);
+  const int steps = c_end > c_begin ? (c_end - c_begin) * KS : 0;
+
+  const rsrc_t ra_src = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rb_src = make_rsrc(a.B, a.b_bytes);
+
+  // ---- halo slots: quad (q & 7) of halo pixel (q >> 3)
+  int h_off[HS];
+  unsigned h_ok = 0;
+  const int hcq = tid & 7;
+#pragma unroll
+  for (int j = 0; j < HS; ++j) {
+    const int q = tid + 256 * j;
+    const int hp = q >> 3;
+    const int sy = hy0 + hp / HW, sx = hx0 + hp % HW;
+    const bool ok = q < HQ && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+    h_off[j] = ok ? (((b * SH + sy) * SW + sx) * a.lda + 4 * hcq) * 4 : 0;
+    h_ok |= (ok ? 1u : 0u) << j;
+  }
+  float4 hv[HS];
+  auto load_halo = [&](int c) {
+    const bool cok = 32 * c + 4 * hcq < a.kc;
+#pragma unroll
+    for (int j = 0; j < HS; ++j)
+      hv[j] = bload4(ra_src, cok && ((h_ok >> j) & 1) ? (uint32_t)(h_off[j] + 128 * c) : kOOB);
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int j = 0; j < HS; ++j) {
+      const int q = tid + 256 * j;
+      if (q < HQ) {
+        bf16x8 t;   // low 4 used: one quad -> 8 bytes
+        const float4 v = hv[j];
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 u;
+        u[0] = (__bf16)v.x;
+        u[1] = (__bf16)v.y;
+        u[2] = (__bf16)v.z;
+        u[3] = (__bf16)v.w;
+        (void)t;
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<char*>(Ah) + (q >> 3) * (SROW16 * 16) +
+                                   8 * (q & 7)) = u;
+      }
+    }
+  };
+  // ---- B slots: (tap s of the kernel row, weight row, octet)
+  uint4 rb[BSL];
+  auto load_b = [&](int c, int r) {
+#pragma unroll
+    for (int j = 0; j < BSL; ++j) {
+      const int o = tid + 256 * j;
+      const int s = o / (BN * 4), rem = o - s * (BN * 4);
+      const int n = n0 + (rem >> 2), oct = rem & 3;
+      const bool ok = o < BOCT && n < a.nb;
+      const int k = (r * KS + s) * a.kc + 32 * c + 8 * oct;
+      rb[j] = __builtin_bit_cast(uint4,
+                                 bload4(rb_src, ok ? (uint32_t)(((int64_t)n * a.ldb + k) * 2) : kOOB));
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < BSL; ++j) {
+      const int o = tid + 256 * j;
+      if (o < BOCT) {
+        const int s = o / (BN * 4), rem = o - s * (BN * 4);
+        Bs[buf][(s * BN + (rem >> 2)) * SROW16 + (rem & 3)] = rb[j];
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int wm0 = (wave / WAVES_N) * WM;
+  const int wn0 = (wave % WAVES_N) * WN;
+  const int lrow = lane & 31, lk = lane >> 5;
+  int a_hp[TM];   // halo pixel of this lane's A row at tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wm0 + 32 * i + lrow;
+    const int ty = m / TT_W, tx = m % TT_W;
+    a_hp[i] = MODE == MODE_FWD ? ty * HW + tx : (ty + KS - 1) * HW + tx + KS - 1;
+  }
+
+  if (steps > 0) {
+    load_halo(c_begin);
+    load_b(c_begin, 0);
+    store_halo();
+    store_b(0);
+  }
+  __syncthreads();
+  for (int q = 0; q < steps; ++q) {
+    const int r = q % KS, buf = q & 1;
+    const bool more = q + 1 < steps;
+    const int nq = q + 1;
+    const int nc = c_begin + nq / KS, nr = nq % KS;
+    if (more) {
+      load_b(nc, nr);
+      if (nr == 0) load_halo(nc);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int dh = MODE == MODE_FWD ? r * HW + s : -(r * HW + s);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 av[TM], bv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          av[i] = __builtin_bit_cast(bf16x8, Ah[(a_hp[i] + dh) * SROW16 + 2 * st + lk]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bv[j] = __builtin_bit_cast(
+              bf16x8, Bs[buf][(s * BN + wn0 + 32 * j + lrow) * SROW16 + 2 * st + lk]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store_b(buf ^ 1);
+      if (nr == 0) store_halo();
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue
+  const int64_t img = (int64_t)b * OH * OW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + 32 * j + lrow;
+    if (n >= a.N) continue;
+    float bias = 0.f, scale = 1.f, shift = 0.f;
+    if (a.splits == 1) column_params<MODE>(a, n, bias, scale, shift);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
+        const int oy = oy0 + m / TT_W, ox = ox0 + m % TT_W;
+        if (oy >= OH || ox >= OW) continue;
+        const int64_t row = img + (int64_t)oy * OW + ox;
+        if (a.splits > 1)
+          a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n] = acc[i][j][rr];
+        else
+          epilogue_store<MODE>(a, row, n, acc[i][j][rr], bias, scale, shift);
+      }
+    }
+  }
+}
+
 // Weight gradient on bf16 MFMA: C[m=(tap,ci)][n=co] = sum_{k=output pixel} x[pix(k,tap)][ci] *
 // dy[k][co], both operands rounded to bf16 while staged, fp32 accumulation into the split-K
 // slabs (reduced by wgrad_reduce_kernel, as the f32 path).  The MFMA operands need 8
@@ -1457,6 +1655,61 @@ int launch_gemm_bf16(const GemmArgs& a, hipStream_t s, double flops) {
   return check_launch("conv_splitk_epilogue");
 }
 
+// bf16 3x3 stride-1 fwd / dgrad: halo-tiled kernel (conv_tile_bf16).
+bool tile_ok(const of_conv_desc* d) { return d->kh == 3 && d->kw == 3 && d->stride == 1; }
+
+GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode) {
+  GemmArgs a = base_args(d);
+  const bool fwd = mode == MODE_FWD;
+  a.kc = fwd ? g.cin_p : g.cout_p;
+  a.N = fwd ? d->cout : g.cin_p;
+  a.nb = fwd ? d->cout : g.nd;
+  a.ldb = fwd ? g.kf16 : (int)g.kd16;
+  const int OH = fwd ? d->ho : d->h, OW = fwd ? d->wo : d->w;
+  const int m_tiles = d->n * (int)cdiv(OH, TT_H) * (int)cdiv(OW, TT_W);
+  a.bm = TT_H * TT_W;
+  a.ngroups = 1;
+  Group& G = a.grp[0];
+  G = Group{};
+  G.M = d->n * OH * OW;
+  G.m_tiles = m_tiles;
+  G.ns = 3;
+  G.ntaps = 9;
+  a.M = G.M;
+  a.n_tiles = (int)cdiv(a.N, pick_bn(a.N));
+  a.tiles_total = m_tiles * a.n_tiles;
+  a.K = (int)cdiv(a.kc, 32);                       // channel chunks
+  G.K = a.K;
+  a.splits = 1;
+  a.k_per_split = a.K;
+  if (a.tiles_total < 2 * kCUs) {
+    int sp = std::max(1, (4 * kCUs) / a.tiles_total);
+    sp = std::min(sp, std::max(1, a.K / 2));       // >= 2 chunks (6 tap rows) per slice
+    a.k_per_split = (int)cdiv(a.K, sp);
+    a.splits = (int)cdiv(a.K, a.k_per_split);
+  }
+  return a;
+}
+
+template <int MODE>
+int launch_tile_bf16(const GemmArgs& a, hipStream_t s, double flops) {
+  const int bn = pick_bn(a.N);
+  dim3 grid(a.tiles_total * a.splits), block(256);
+  const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
+  if (timing_on()) timing_begin(s);
+  if (cfg == 0) hipLaunchKernelGGL((conv_tile_bf16<128, 2, 2, MODE>), grid, block, 0, s, a);
+  else if (cfg == 1) hipLaunchKernelGGL((conv_tile_bf16<96, 4, 1, MODE>), grid, block, 0, s, a);
+  else if (cfg == 2) hipLaunchKernelGGL((conv_tile_bf16<64, 2, 2, MODE>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((conv_tile_bf16<32, 4, 1, MODE>), grid, block, 0, s, a);
+  if (timing_on()) timing_end(s, 64 + 32 + MODE * 8 + cfg, flops);
+  int st = check_launch("conv_tile_bf16");
+  if (st || a.splits == 1) return st;
+  const int64_t items = slab_rows(a) * cdiv(a.N, 4);
+  hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
+                     a);
+  return check_launch("conv_splitk_epilogue");
+}
+
 struct WgradPlan {
   int splits, k_per_split, M, ldc;
   int64_t split_stride;
@@ -1640,12 +1893,13 @@ size_t of_conv2d_dgrad_workspace(const of_conv_desc* d) {
 
 size_t of_conv2d_fwd_bf16_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
-  return fd_workspace(fwd_args(d, geo(d), true));
+  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_FWD) : fwd_args(d, geo(d), true));
 }
 
 size_t of_conv2d_dgrad_bf16_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
-  return fd_workspace(dgrad_args(d, geo(d), true));
+  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_DGRAD)
+                                 : dgrad_args(d, geo(d), true));
 }
 
 int of_conv_path(const of_conv_desc* d) {
@@ -1677,8 +1931,9 @@ static int conv_fwd_impl(bool bf16, const of_conv_desc* d, const float* x, int l
     return st;
   }
   Geo g = geo(d);
-  GemmArgs a = fwd_args(d, g, bf16);
-  attach_slab(a, workspace, ws_bytes, bf16 ? BKH : BK);
+  const bool tile = bf16 && tile_ok(d);
+  GemmArgs a = tile ? tile_args(d, g, MODE_FWD) : fwd_args(d, g, bf16);
+  attach_slab(a, workspace, ws_bytes, tile ? 1 : bf16 ? BKH : BK);
   a.A = x;
   a.lda = ldx;
   a.a_bytes = (int64_t)d->n * d->h * d->w * ldx * 4;
@@ -1702,7 +1957,9 @@ static int conv_fwd_impl(bool bf16, const of_conv_desc* d, const float* x, int l
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
-  st = bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops) : launch_gemm<MODE_FWD>(a, s, flops);
+  st = tile   ? launch_tile_bf16<MODE_FWD>(a, s, flops)
+       : bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops)
+              : launch_gemm<MODE_FWD>(a, s, flops);
   return st;
 }
 
@@ -1748,8 +2005,9 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
     if (timing_on()) timing_end(s, MODE_DGRAD * 8 + KIND_NARROW, conv_flops(d));
     return st;
   }
-  GemmArgs a = dgrad_args(d, g, bf16);
-  attach_slab(a, workspace, ws_bytes, bf16 ? BKH : BK);
+  const bool tile = bf16 && tile_ok(d);
+  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD) : dgrad_args(d, g, bf16);
+  attach_slab(a, workspace, ws_bytes, tile ? 1 : bf16 ? BKH : BK);
   a.A = dy;
   a.lda = lddy;
   a.a_bytes = (int64_t)d->n * d->ho * d->wo * lddy * 4;
@@ -1765,7 +2023,9 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
-  st = bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops) : launch_gemm<MODE_DGRAD>(a, s, flops);
+  st = tile   ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
+       : bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops)
+              : launch_gemm<MODE_DGRAD>(a, s, flops);
   return st;
 }
 

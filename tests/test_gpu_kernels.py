@@ -88,7 +88,10 @@ def test_conv_fwd_bwd(case):
         assert rel_inf(resd.grad, reso.grad) < REL_TOL, "residual grad"
 
 
-BF16_CASES = [c for c in CONV_CASES if c[4] > 4]
+BF16_CASES = [c for c in CONV_CASES if c[4] > 4] + [
+    (1, 13, 35, 48, 64, 3, 1, "leaky", False, False),    # halo tiles: ragged, partial chunk
+    (1, 8, 16, 256, 128, 3, 1, "relu", True, False),     # halo tiles: split over channels
+]
 
 
 @pytest.mark.parametrize("case", BF16_CASES, ids=lambda c: "x".join(map(str, c[:7])) + c[7])
