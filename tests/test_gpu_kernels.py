@@ -24,6 +24,10 @@ CONV_CASES = [
     (1, 10, 20, 64, 3, 3, 1, "relu", False, False),         # narrow, 16 lanes per pixel
     (2, 8, 8, 3, 2, 3, 1, "leaky", False, False),           # narrow, 1 lane per pixel
     (1, 9, 9, 12, 2, 3, 1, "leaky", False, False),          # cin_p 12: GEMM fallback
+    # smoke() level 1 (64x128 image, batch 1): 32-pixel layers, deep split-K
+    (1, 4, 8, 179, 128, 3, 1, "leaky", False, False),
+    (1, 4, 8, 128, 96, 3, 1, "leaky", False, False),
+    (1, 4, 8, 32, 2, 3, 1, "none", False, False),
     (2, 16, 16, 64, 96, 3, 1, "leaky", False, False),       # cout 96 tile
     (2, 32, 48, 3, 64, 7, 2, "relu", True, False),          # conv1 7x7/2 + BN + ReLU
     (2, 16, 16, 64, 128, 3, 2, "relu", True, False),        # stride-2 block conv
@@ -165,7 +169,9 @@ def test_cost_volume(shape):
                                                   # h >= 96: the strip-sweep kernels
                                                   (1, 100, 40, 64, 116, True),
                                                   (2, 97, 33, 128, 180, True),
-                                                  (1, 96, 20, 6, 60, False)])
+                                                  (1, 96, 20, 6, 60, False),
+                                                  (1, 4, 8, 128, 180, True),
+                                                  (1, 2, 4, 256, 308, False)])
 def test_corr_concat(n, h, w, c, cp, has_flow):
     """The fused concat([f1, cost volume, flow]) kernel and its gradient: 2-D tile kernels
     (h < 96) and strip sweeps (h >= 96), multi-tile and ragged shapes, 1 and 2 channel
@@ -193,7 +199,8 @@ def test_corr_concat(n, h, w, c, cp, has_flow):
 
 # ------------------------------------------------------------------------------ warp ----
 @pytest.mark.parametrize("shape,flow_scale", [((2, 12, 20, 64), 3.0), ((2, 16, 16, 128), 1.5),
-                                              ((1, 10, 14, 3), 4.0), ((2, 8, 24, 32), 20.0)])
+                                              ((1, 10, 14, 3), 4.0), ((2, 8, 24, 32), 20.0),
+                                              ((1, 4, 8, 128), 0.5)])
 def test_warp(shape, flow_scale):
     ops = _ops()
     n, h, w, c = shape
@@ -229,7 +236,7 @@ def test_bilinear_interpolation_absolute():
 
 
 # -------------------------------------------------------------------------- upscale -----
-@pytest.mark.parametrize("shape", [(2, 6, 8, 2), (1, 24, 32, 2), (2, 5, 7, 3)])
+@pytest.mark.parametrize("shape", [(2, 6, 8, 2), (1, 24, 32, 2), (2, 5, 7, 3), (1, 2, 4, 2)])
 def test_upscale(shape):
     ops = _ops()
     x = rng_tensor(shape, 31)
@@ -260,7 +267,7 @@ def test_maxpool():
 
 
 # ------------------------------------------------------------------- photometric loss ---
-@pytest.mark.parametrize("size", [(2, 64, 96), (1, 128, 256)])
+@pytest.mark.parametrize("size", [(2, 64, 96), (1, 128, 256), (1, 64, 128)])
 def test_photometric_loss(size):
     from optical_flow_amd.loss import LossLayer
     from optical_flow_amd.data import synthetic_batch
