@@ -69,6 +69,8 @@ def kernel_symbol(kind):
         return NARROW_SYMBOLS[mode]
     if fam == "tile_bf16":
         return "void oflow::conv_tile_bf16<%s, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode)
+    if fam == "bf16" and mode == 2:
+        return "void oflow::conv_wgrad_bf16<%s>(oflow::GemmArgs)" % TILE_TEMPLATE[cfg]
     return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_TEMPLATE[cfg], mode)
 
 

@@ -1,0 +1,45 @@
+"""Write a profile summary (markdown) from a bench JSON line and the rocprofv3 kernel_stats.csv
+of the same bench command.
+
+python tools/make_summary.py <bench.log> <kernel_stats.csv> <command> [top]  > profiles/....md
+"""
+import csv
+import json
+import sys
+
+
+def main():
+    log, stats, cmd = sys.argv[1:4]
+    top = int(sys.argv[4]) if len(sys.argv) > 4 else 30
+    line = [ln for ln in open(log) if ln.startswith("{")][-1]
+    b = json.loads(line)
+    rf = b["roofline"]
+    rows = list(csv.DictReader(open(stats)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    dom = [r for r in rows if r["Name"] == rf["kernel"]]
+    prof_avg = float(dom[0]["AverageNs"]) / 1e6 if dom else float("nan")
+    print("# Profile summary: `%s` (MI355X, gfx950, ROCm 7.2)\n" % cmd)
+    print("rocprofv3 command: `rocprofv3 --kernel-trace --stats --output-format csv -- %s` "
+          "(warm-up + timed + instrumented steps of one bench run).\n" % cmd)
+    print("Bench line (un-profiled run): **%.1f %s**, %.2f ms/step, dtype %s, model %.1f TFLOP/s."
+          % (b["value"], b["unit"], b["ms_per_step"], b["dtype"], b.get("model_tflops", 0)))
+    print("Dominant kernel `%s`: %.1f %s achieved = %.1f %% of the %.1f %s peak; hipEvent average "
+          "%.4f ms per launch vs rocprof average %.4f ms.\n"
+          % (rf["kernel"], rf["achieved"], rf["unit"], 100 * rf["frac"], rf["peak"], rf["unit"],
+             rf["avg_launch_ms"], prof_avg))
+    print("| kernel | calls | total ms | % of GPU time | avg ms |")
+    print("|---|---|---|---|---|")
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
+        print("| `%s` | %s | %.2f | %.1f | %.4f |" % (
+            r["Name"][:90], r["Calls"], float(r["TotalDurationNs"]) / 1e6,
+            100 * float(r["TotalDurationNs"]) / tot, float(r["AverageNs"]) / 1e6))
+    print("\nPer-kernel hipEvent table from the bench (ms per step):\n")
+    print("| instance | launches/step | ms/step | TFLOP/s |")
+    print("|---|---|---|---|")
+    for k, v in rf.get("per_kernel", {}).items():
+        print("| %s | %d | %.3f | %.1f |" % (k, v["launches"] // max(1, b["steps"] // b["steps"]),
+                                            v["ms"], v["tflops"]))
+
+
+if __name__ == "__main__":
+    main()
