@@ -55,9 +55,14 @@ def kind_parts(kind):
 TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1"}
 
 
+WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>
+
+
 def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16"}[fam]
+    if fam == "tile_bf16" and mode == 2:
+        return "wgrad_tile_bf16<%s>" % WGT_WAVES[cfg]
     return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (TILE_BN if fam == "tile_bf16"
                                                  else TILE_TEMPLATE)[cfg])
 
@@ -67,6 +72,8 @@ def kernel_symbol(kind):
     mode, cfg, fam = kind_parts(kind)
     if cfg == 7:
         return NARROW_SYMBOLS[mode]
+    if fam == "tile_bf16" and mode == 2:
+        return "void oflow::conv_wgrad_tile_bf16<%s>(oflow::GemmArgs)" % WGT_WAVES[cfg]
     if fam == "tile_bf16":
         return "void oflow::conv_tile_bf16<%s, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode)
     if fam == "bf16" and mode == 2:

@@ -11,7 +11,8 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboflow.so")
+# OFLOW_LIB: an alternative build of the same library (A/B experiments with tools/ab_build.sh)
+LIB_PATH = os.environ.get("OFLOW_LIB") or os.path.join(HERE, "liboflow.so")
 
 OF_OK, OF_EINVAL, OF_EHIP, OF_EUNSUPPORTED = 0, 1, 2, 3
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2

@@ -101,21 +101,41 @@ __device__ __forceinline__ int64_t out_row(const GemmArgs& a, const Group& g, in
   return ((int64_t)b * a.h + 2 * u + g.ry) * a.w + 2 * v + g.rx;
 }
 
-// Fused epilogue for one element (fwd / dgrad), v = the full K sum.
+// The epilogue's second input for one element: the residual (fwd) or the producer's output
+// whose activation derivative scales dx (dgrad).  Call sites gather all of a lane's values
+// before the first store: interleaved, every load would wait behind the previous store (the
+// compiler cannot prove a.C does not alias them).
+template <int MODE>
+__device__ __forceinline__ float epilogue_aux(const GemmArgs& a, int64_t row, int n) {
+  if (MODE == MODE_FWD) return a.res ? a.res[row * a.ldr + n] : 0.f;
+  if (MODE == MODE_DGRAD) return a.act_src ? a.act_src[row * a.ld_act + n] : 1.f;
+  return 0.f;
+}
+
+// Aux values gathered ahead of the stores: the whole 16-value MFMA fragment for dgrad (the
+// decoder's act_src on every layer); 4 for fwd, whose residual only the encoder has and whose
+// epilogue registers set the kernels' occupancy.
+#ifndef OF_EPG_FWD
+#define OF_EPG_FWD 4
+#endif
+#ifndef OF_EPG_DGRAD
+#define OF_EPG_DGRAD 16
+#endif
+template <int MODE>
+constexpr int EP_GATHER = MODE == MODE_DGRAD ? OF_EPG_DGRAD : OF_EPG_FWD;
+
+// Fused epilogue for one element (fwd / dgrad), v = the full K sum, aux = epilogue_aux.
 template <int MODE>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int64_t row, int n, float v,
-                                               float bias, float scale, float shift) {
+                                               float bias, float scale, float shift, float aux) {
   if (MODE == MODE_FWD) {
     v += bias;
     if (a.z) a.z[row * a.ldz + n] = v;
     if (a.bn_g) v = v * scale + shift;
-    if (a.res) v += a.res[row * a.ldr + n];
+    v += aux;
     v = act_fwd(v, a.act, a.alpha);
   } else if (MODE == MODE_DGRAD) {
-    if (a.act_src) {
-      const float s = a.act_src[row * a.ld_act + n];
-      v *= s > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
-    }
+    v *= aux > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
   }
   a.C[row * a.ldc + n] = v;
 }
@@ -485,10 +505,20 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (m >= M) continue;
-        epilogue_store<MODE>(a, out_row(a, G, m), n, acc[i][j][r], bias, scale, shift);
+      for (int r0 = 0; r0 < 16; r0 += EP_GATHER<MODE>) {
+        float aux[EP_GATHER<MODE>];
+#pragma unroll
+        for (int r = r0; r < r0 + EP_GATHER<MODE>; ++r) {
+          const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          aux[r - r0] = m < M ? epilogue_aux<MODE>(a, out_row(a, G, m), n) : 0.f;
+        }
+#pragma unroll
+        for (int r = r0; r < r0 + EP_GATHER<MODE>; ++r) {
+          const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (m >= M) continue;
+          epilogue_store<MODE>(a, out_row(a, G, m), n, acc[i][j][r], bias, scale, shift,
+                               aux[r - r0]);
+        }
       }
     }
   }
@@ -761,10 +791,20 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (m >= M) continue;
-        epilogue_store<MODE>(a, out_row(a, G, m), n, acc[i][j][r], bias, scale, shift);
+      for (int r0 = 0; r0 < 16; r0 += EP_GATHER<MODE>) {
+        float aux[EP_GATHER<MODE>];
+#pragma unroll
+        for (int r = r0; r < r0 + EP_GATHER<MODE>; ++r) {
+          const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          aux[r - r0] = m < M ? epilogue_aux<MODE>(a, out_row(a, G, m), n) : 0.f;
+        }
+#pragma unroll
+        for (int r = r0; r < r0 + EP_GATHER<MODE>; ++r) {
+          const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (m >= M) continue;
+          epilogue_store<MODE>(a, out_row(a, G, m), n, acc[i][j][r], bias, scale, shift,
+                               aux[r - r0]);
+        }
       }
     }
   }
@@ -953,6 +993,14 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
     if (a.splits == 1) column_params<MODE>(a, n, bias, scale, shift);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      float aux[16];
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
+        const int oy = oy0 + m / TT_W, ox = ox0 + m % TT_W;
+        aux[rr] = a.splits == 1 && oy < OH && ox < OW
+                      ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : 0.f;
+      }
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
@@ -962,7 +1010,7 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
         if (a.splits > 1)
           a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n] = acc[i][j][rr];
         else
-          epilogue_store<MODE>(a, row, n, acc[i][j][rr], bias, scale, shift);
+          epilogue_store<MODE>(a, row, n, acc[i][j][rr], bias, scale, shift, aux[rr]);
       }
     }
   }
@@ -1191,6 +1239,208 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_bf16(GemmArgs a) {
   }
 }
 
+// ---- bf16 weight gradient, 3x3 stride 1: all 9 taps from one staged halo ---------------
+// dW[r][s][ci][co] = sum_p x(p + (r, s) - pad)[ci] . dy(p)[co].  A workgroup owns CIB input x
+// COB output channels for ALL 9 taps (wave = 32 ci x 32 co x 9 taps = 9 accumulators) and
+// walks 8 x 16 output-pixel tiles of its K slice: per tile it stages dy [co][128 px] once and
+// the x halo (10 rows x 18 px) once, as three copies shifted by s = 0, 1, 2 pixels so every
+// tap's A fragment (8 consecutive pixels of one channel) is an aligned 16-byte LDS read.
+// Against the implicit GEMM (each tap a separate GEMM row block re-reading x and dy through
+// L2) this cuts global traffic per MFMA by ~3.5x.  Both LDS images are double-buffered, one
+// barrier per tile; the fp32 -> bf16 rounding and the [pixel][ch] -> [ch][pixel] transpose
+// happen in the staging registers.  XOR swizzles keep the ds_read_b128 fragments
+// conflict-free: x rows (s, hy, ci) of 2 octets swap the octets of ci & 8; dy rows of 16
+// octets XOR the octet with co & 15.  K slice = a range of pixel tiles (a.K tiles in all).
+// Output: the same split-K slabs as conv_wgrad_bf16 (rows tap * kc + ci, bias row M).
+template <int WAVES_CI, int WAVES_CO>
+__global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
+  constexpr int CIB = 32 * WAVES_CI, COB = 32 * WAVES_CO, KS = 3, HH = TT_H + KS - 1;
+  static_assert(WAVES_CI * WAVES_CO == 4 && COB >= 64, "4 waves, COB >= 64");
+  static_assert(TT_H == 8 && TT_W == 16, "tile = 8 rows x 16 px");
+  constexpr int XQ = HH * (CIB / 4) * 2, XS = (XQ + 255) / 256;   // (hy, ci quad, half)
+  constexpr int DQ = 16 * (COB / 4), DS = DQ / 256;               // (octet, co quad)
+  static_assert(DQ % 256 == 0, "dy items");
+  constexpr int NG = 256 / (COB / 4);                              // colsum groups
+  __shared__ uint4 Xs[2][KS * HH * CIB * 2];
+  __shared__ uint4 Ds[2][COB * 16];
+  __shared__ float csum[NG][COB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_co = tile % a.n_tiles;
+  const int tile_ci = tile / a.n_tiles;
+  const int ci0 = tile_ci * CIB, co0 = tile_co * COB;
+  const int t_begin = split * a.k_per_split;
+  const int t_end = min(a.K, t_begin + a.k_per_split);
+  const int steps = max(0, t_end - t_begin);
+  const int tiles_x = (a.wo + TT_W - 1) / TT_W, tiles_y = (a.ho + TT_H - 1) / TT_H;
+  const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
+  const bool do_colsum = a.colsum && tile_ci == 0;
+
+  // x items: channel quad fastest (coalesced 16-B lanes of one pixel)
+  const int xcq = tid % (CIB / 4);
+  const bool xc_ok = ci0 + 4 * xcq < a.kc;
+  // dy items: co quad fixed per thread across its DS items
+  const int dcq = tid % (COB / 4);
+  const bool dc_ok = co0 + 4 * dcq < a.nb;
+
+  float4 xv[XS][10];
+  float4 dv[DS][8];
+  float4 colacc = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  auto load = [&](int t) {
+    const int b = t / (tiles_x * tiles_y);
+    const int trem = t - b * tiles_x * tiles_y;
+    const int oy0 = (trem / tiles_x) * TT_H, ox0 = (trem % tiles_x) * TT_W;
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int q = tid + 256 * j;
+      const int half = (q / (CIB / 4)) & 1, hy = q / (CIB / 2);
+      const int iy = oy0 - a.pt + hy;
+      const bool rok = q < XQ && xc_ok && (unsigned)iy < (unsigned)a.h;
+      const int ix0 = ox0 - a.pl + 8 * half;
+      const int base = ((b * a.h + iy) * a.w + ix0) * a.lda + ci0 + 4 * xcq;
+#pragma unroll
+      for (int e = 0; e < 10; ++e) {
+        const bool ok = rok && (unsigned)(ix0 + e) < (unsigned)a.w;
+        xv[j][e] = bload4(rx, ok ? (uint32_t)((base + e * a.lda) * 4) : kOOB);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < DS; ++j) {
+      const int o = (tid + 256 * j) / (COB / 4);
+      const int oy = oy0 + (o >> 1), ox = ox0 + 8 * (o & 1);
+      const bool rok = dc_ok && oy < a.ho;
+      const int base = ((b * a.ho + oy) * a.wo + ox) * a.ldb + co0 + 4 * dcq;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = rok && ox + e < a.wo;
+        dv[j][e] = bload4(rd, ok ? (uint32_t)((base + e * a.ldb) * 4) : kOOB);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int q = tid + 256 * j;
+      if (q < XQ) {
+        const int half = (q / (CIB / 4)) & 1, hy = q / (CIB / 2);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const float4* v = &xv[j][s];
+          const uint4 r0 = pack_bf16x8(make_float4(v[0].x, v[1].x, v[2].x, v[3].x),
+                                       make_float4(v[4].x, v[5].x, v[6].x, v[7].x));
+          const uint4 r1 = pack_bf16x8(make_float4(v[0].y, v[1].y, v[2].y, v[3].y),
+                                       make_float4(v[4].y, v[5].y, v[6].y, v[7].y));
+          const uint4 r2 = pack_bf16x8(make_float4(v[0].z, v[1].z, v[2].z, v[3].z),
+                                       make_float4(v[4].z, v[5].z, v[6].z, v[7].z));
+          const uint4 r3 = pack_bf16x8(make_float4(v[0].w, v[1].w, v[2].w, v[3].w),
+                                       make_float4(v[4].w, v[5].w, v[6].w, v[7].w));
+          const int ci = 4 * xcq;                     // ci & 8 is the same for the quad
+          const int oct = half ^ ((ci >> 3) & 1);
+          uint4* row = &Xs[buf][((s * HH + hy) * CIB + ci) * 2 + oct];
+          row[0] = r0;
+          row[2] = r1;
+          row[4] = r2;
+          row[6] = r3;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < DS; ++j) {
+      const int o = (tid + 256 * j) / (COB / 4);
+      const float4* v = dv[j];
+      const uint4 r0 = pack_bf16x8(make_float4(v[0].x, v[1].x, v[2].x, v[3].x),
+                                   make_float4(v[4].x, v[5].x, v[6].x, v[7].x));
+      const uint4 r1 = pack_bf16x8(make_float4(v[0].y, v[1].y, v[2].y, v[3].y),
+                                   make_float4(v[4].y, v[5].y, v[6].y, v[7].y));
+      const uint4 r2 = pack_bf16x8(make_float4(v[0].z, v[1].z, v[2].z, v[3].z),
+                                   make_float4(v[4].z, v[5].z, v[6].z, v[7].z));
+      const uint4 r3 = pack_bf16x8(make_float4(v[0].w, v[1].w, v[2].w, v[3].w),
+                                   make_float4(v[4].w, v[5].w, v[6].w, v[7].w));
+      const int co = 4 * dcq;
+      Ds[buf][(co + 0) * 16 + (o ^ ((co + 0) & 15))] = r0;
+      Ds[buf][(co + 1) * 16 + (o ^ ((co + 1) & 15))] = r1;
+      Ds[buf][(co + 2) * 16 + (o ^ ((co + 2) & 15))] = r2;
+      Ds[buf][(co + 3) * 16 + (o ^ ((co + 3) & 15))] = r3;
+      if (do_colsum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) add4(colacc, v[e]);
+      }
+    }
+  };
+
+  f32x16 acc[KS * KS];
+#pragma unroll
+  for (int t = 0; t < KS * KS; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const int wci0 = (wave / WAVES_CO) * 32;
+  const int wco0 = (wave % WAVES_CO) * 32;
+  const int lrow = lane & 31, lk = lane >> 5;
+  const int a_base = (wci0 + lrow) * 2 + (lk ^ ((lrow >> 3) & 1));
+  const int b_base = (wco0 + lrow) * 16;
+
+  if (steps > 0) {
+    load(t_begin);
+    store(0);
+  }
+  __syncthreads();
+  for (int i = 0; i < steps; ++i) {
+    const int buf = i & 1;
+    const bool more = i + 1 < steps;
+    if (more) load(t_begin + i + 1);
+#pragma unroll
+    for (int kk = 0; kk < TT_H; ++kk) {
+      const bf16x8 bv = __builtin_bit_cast(bf16x8, Ds[buf][b_base + ((2 * kk + lk) ^ (lrow & 15))]);
+#pragma unroll
+      for (int r = 0; r < KS; ++r)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8 av = __builtin_bit_cast(
+              bf16x8, Xs[buf][(s * HH + kk + r) * CIB * 2 + a_base]);
+          acc[r * KS + s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[r * KS + s], 0, 0, 0);
+        }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- raw partial sums into this K slice's slab (+ bias column sums in row M)
+  float* S = a.slab + (int64_t)split * a.split_stride;
+  if (do_colsum) {
+    if (DS > 0) {
+      const int g = tid / (COB / 4);
+      csum[g][4 * dcq] = colacc.x;
+      csum[g][4 * dcq + 1] = colacc.y;
+      csum[g][4 * dcq + 2] = colacc.z;
+      csum[g][4 * dcq + 3] = colacc.w;
+    }
+    __syncthreads();
+    if (tid < COB && co0 + tid < a.N) {
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) v += csum[g][tid];
+      S[(int64_t)a.M * a.slab_ld + co0 + tid] = v;
+    }
+  }
+  const int n = co0 + wco0 + lrow;
+  if (n < a.N) {
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = ci0 + wci0 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (ci < a.kc) S[((int64_t)t * a.kc + ci) * a.slab_ld + n] = acc[t][r];
+      }
+  }
+}
+
 // Split-K epilogue for fwd/dgrad: sum the K slices' slabs, then the fused epilogue.
 // Workgroup = 32 items x 8 split lanes; item = (slab row, 4 columns); the 8 lanes each sum
 // every 8th slice (many independent loads in flight), then a fixed-order LDS reduction.
@@ -1225,12 +1475,16 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a) {
   if (m >= G.M) return;
   const int64_t row = out_row(a, G, m);
   const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+  float aux[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) aux[e] = 4 * q + e < a.N ? epilogue_aux<MODE>(a, row, 4 * q + e) : 0.f;
+#pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int n = 4 * q + e;
     if (n >= a.N) break;
     float bias, scale, shift;
     column_params<MODE>(a, n, bias, scale, shift);
-    epilogue_store<MODE>(a, row, n, v[e], bias, scale, shift);
+    epilogue_store<MODE>(a, row, n, v[e], bias, scale, shift, aux[e]);
   }
 }
 
@@ -1715,11 +1969,31 @@ struct WgradPlan {
   int64_t split_stride;
 };
 
+// bf16 3x3 stride-1 wgrad on conv_wgrad_tile_bf16: block channel tiles (CIB x COB).
+bool wgt_ok(const of_conv_desc* d) { return tile_ok(d); }
+int wgt_cfg(const of_conv_desc* d) { return d->cout > 64 ? 0 : 2; }   // <1,4> : <2,2>
+void wgt_blocks(const of_conv_desc* d, int& cib, int& cob) {
+  cib = wgt_cfg(d) == 0 ? 32 : 64;
+  cob = wgt_cfg(d) == 0 ? 128 : 64;
+}
+
 WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false) {
   Geo g = geo(d);
   WgradPlan p;
   p.M = g.taps * g.cin_p;
   p.ldc = g.cout_p;
+  p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
+  if (bf16 && wgt_ok(d)) {
+    // K = 8 x 16 pixel tiles; one workgroup per CU (LDS-bound occupancy), equal slices
+    int cib, cob;
+    wgt_blocks(d, cib, cob);
+    const int chan_tiles = (int)(cdiv(g.cin_p, cib) * cdiv(d->cout, cob));
+    const int T = d->n * (int)cdiv(d->ho, TT_H) * (int)cdiv(d->wo, TT_W);
+    int splits = std::max(1, std::min(T, kCUs / chan_tiles));
+    p.k_per_split = (int)cdiv(T, splits);
+    p.splits = (int)cdiv(T, p.k_per_split);
+    return p;
+  }
   const int bk = bf16 ? BKH : BK;
   const int K = d->n * d->ho * d->wo;
   const int tiles = (int)(cdiv(p.M, pick_bm(d->cout)) * cdiv(d->cout, pick_bn(d->cout)));
@@ -1729,7 +2003,6 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false) {
   splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * bk)));
   p.k_per_split = (int)round_up(cdiv(K, splits), bk);
   p.splits = (int)cdiv(K, p.k_per_split);
-  p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
   return p;
 }
 
@@ -2100,7 +2373,20 @@ static int conv_wgrad_impl(bool bf16, const of_conv_desc* d, const float* x, int
   a.colsum = db != nullptr;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
-  if (bf16) {
+  if (bf16 && wgt_ok(d)) {
+    int cib, cob;
+    wgt_blocks(d, cib, cob);
+    a.K = d->n * (int)cdiv(d->ho, TT_H) * (int)cdiv(d->wo, TT_W);
+    a.n_tiles = (int)cdiv(d->cout, cob);
+    a.tiles_total = (int)cdiv(g.cin_p, cib) * a.n_tiles;
+    const int cfg = wgt_cfg(d);
+    dim3 grid(a.tiles_total * a.splits), block(256);
+    if (timing_on()) timing_begin(s);
+    if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_bf16<1, 4>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_tile_bf16<2, 2>), grid, block, 0, s, a);
+    if (timing_on()) timing_end(s, 96 + MODE_WGRAD * 8 + cfg, flops);
+    st = check_launch("conv_wgrad_tile_bf16");
+  } else if (bf16) {
     const int bn = pick_bn(a.N);
     const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
     dim3 grid(a.tiles_total * a.splits), block(256);

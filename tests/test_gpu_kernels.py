@@ -95,6 +95,9 @@ def test_conv_fwd_bwd(case):
 BF16_CASES = [c for c in CONV_CASES if c[4] > 4] + [
     (1, 13, 35, 48, 64, 3, 1, "leaky", False, False),    # halo tiles: ragged, partial chunk
     (1, 8, 16, 256, 128, 3, 1, "relu", True, False),     # halo tiles: split over channels
+    (2, 40, 70, 64, 64, 3, 1, "leaky", False, False),    # wgrad tiles <2,2>: ragged, splits
+    (1, 24, 48, 128, 96, 3, 1, "leaky", False, False),   # wgrad tiles <1,4>: partial co tile
+    (1, 17, 20, 64, 32, 3, 1, "leaky", False, False),    # wgrad tiles <2,2>: cout 32
 ]
 
 
