@@ -187,7 +187,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss, _ = trainer.train_step(batch, args.warmup + i)
+        loss, flows = trainer.train_step(batch, args.warmup + i)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -199,6 +199,8 @@ def main():
     pairs = world * B * args.steps
     value = pairs / elapsed
     final_loss = float(loss)
+    # the warp backward's atomics depend on where the flows send samples (clipped borders)
+    flow_abs = [[round(float(f.abs().mean()), 4), round(float(f.abs().max()), 3)] for f in flows]
 
     # ---- dominant-kernel roofline (instrumented extra steps, outside the timed region) ----
     lib = _lib.lib()
@@ -294,6 +296,7 @@ def main():
             "model_tflops": round(gfp * value / 1e3, 2),
             "conv_ms_per_step": round(conv_ms_step, 3),
             "final_loss": final_loss,
+            "flow_abs_mean_max": flow_abs,
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,

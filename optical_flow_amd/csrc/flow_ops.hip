@@ -468,6 +468,111 @@ __global__ __launch_bounds__(256) void warp_bwd_wave(const float* __restrict__ d
   }
 }
 
+// Backward with per-workgroup pre-aggregation of the border scatter (grid + flow,
+// c % 64 == 0).  The reference's sampler clips (P2), so samples that leave the image pile onto
+// its border pixels, and the transposed grid (P1) sends every column j >= h to row h-1: with
+// flows pointing off the image (the coarse levels reach tens of pixels in training) per-pixel
+// atomics serialise on a few addresses, 4-17x slower (tools/flow_bench.py --flow-offset).
+// A workgroup owns an 8 x 8 output tile, one wave per pixel with lanes over 64 channels (as
+// warp_bwd_wave).  Corners inside the image go straight to global atomics (their adders are
+// naturally spread); corners ON the border go through a 64-slot direct-mapped LDS cache of
+// destination pixels: a corner whose slot is free or already holds its destination is added
+// there (ds_add_f32), a collision falls back to a global atomic, and the cache is flushed with
+// one 256-B atomic wave-instruction per destination: a clipped run of the tile's pixels leaves
+// the workgroup as one add per destination instead of one per pixel and corner.
+constexpr int WH_T = 8, WH_SLOTS = 64, WH_WAVES = 16;
+
+__global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __restrict__ dout,
+                                                    const float* __restrict__ inp, int n, int h,
+                                                    int w, int c,
+                                                    const float* __restrict__ flow,
+                                                    float* __restrict__ dinp,
+                                                    float* __restrict__ dflow) {
+  __shared__ float data[WH_SLOTS * 64];
+  __shared__ int tag[WH_SLOTS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_i = (h + WH_T - 1) / WH_T, tiles_j = (w + WH_T - 1) / WH_T;
+  const int passes = c / 64;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int cc = (bid % passes) * 64;                  // this workgroup's 64 channels
+  const int tile = bid / passes;
+  const int b = tile / (tiles_i * tiles_j);
+  const int rem = tile - b * tiles_i * tiles_j;
+  const int i0 = (rem / tiles_j) * WH_T, j0 = (rem % tiles_j) * WH_T;
+  const int64_t img = (int64_t)b * h * w;
+
+  {
+    const int e = cc + lane;
+    if (dinp) {
+      for (int k = tid; k < WH_SLOTS * 64; k += 64 * WH_WAVES) data[k] = 0.f;
+      if (tid < WH_SLOTS) tag[tid] = -1;
+    }
+    __syncthreads();
+    for (int pr = wave; pr < WH_T * WH_T; pr += WH_WAVES) {
+      const int i = i0 + pr / WH_T, j = j0 + pr % WH_T;
+      if (i >= h || j >= w) continue;                 // wave-uniform
+      const int64_t p = img + (int64_t)i * w + j;
+      const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
+      const float x = (float)i + f.x, y = (float)j + f.y;
+      const int xi = (int)fmaxf(fminf(floorf(x), 2147483520.f), -2147483520.f);
+      const int yi = (int)fmaxf(fminf(floorf(y), 2147483520.f), -2147483520.f);
+      const int x0 = min(max(xi, 0), w - 1), x1 = min(max(xi + 1, 0), w - 1);
+      const int y0 = min(max(yi, 0), h - 1), y1 = min(max(yi + 1, 0), h - 1);
+      const float a = (float)x1 - x, bq = (float)y1 - y;
+      const float g = dout[p * c + e];
+      const int ys[4] = {y0, y1, y0, y1}, xs[4] = {x0, x0, x1, x1};
+      float pv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pv[k] = inp[(img + (int64_t)ys[k] * w + xs[k]) * c + e];
+      float gx = -g * (bq * (pv[0] - pv[2]) + (1.f - bq) * (pv[1] - pv[3]));
+      float gy = -g * (a * (pv[0] - pv[1]) + (1.f - a) * (pv[2] - pv[3]));
+      if (dinp) {
+        const float wt[4] = {a * bq, a * (1.f - bq), (1.f - a) * bq, (1.f - a) * (1.f - bq)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int yy = ys[k], xx = xs[k];
+          const int d = yy * w + xx;
+          bool cached = false;
+          int sl = 0;
+          if (yy == 0 || yy == h - 1 || xx == 0 || xx == w - 1) {   // wave-uniform
+            sl = (xx * 7 + yy * 13) & (WH_SLOTS - 1);
+            int t = 0;
+            if (lane == 0) t = atomicCAS(&tag[sl], -1, d);
+            t = __builtin_amdgcn_readfirstlane(t);
+            cached = t == -1 || t == d;
+          }
+          if (cached)
+            atomicAdd(&data[sl * 64 + lane], wt[k] * g);
+          else
+            atomicAdd(dinp + (img + d) * c + e, wt[k] * g);
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        gx += __shfl_xor(gx, o, 64);
+        gy += __shfl_xor(gy, o, 64);
+      }
+      if (lane == 0) {
+        if (passes == 1) {
+          *reinterpret_cast<float2*>(dflow + 2 * p) = make_float2(gx, gy);
+        } else {                                       // dflow zeroed by the launcher
+          atomicAdd(dflow + 2 * p, gx);
+          atomicAdd(dflow + 2 * p + 1, gy);
+        }
+      }
+    }
+    if (dinp) {
+      __syncthreads();
+      for (int sl = wave; sl < WH_SLOTS; sl += WH_WAVES) {
+        const int d = tag[sl];
+        if (d >= 0) atomicAdd(dinp + (img + d) * c + e, data[sl * 64 + lane]);
+      }
+      __syncthreads();
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void warp_bwd_scalar(const float* __restrict__ dout,
                                                        const float* __restrict__ inp, int n,
                                                        int h, int w, int c,
@@ -910,7 +1015,15 @@ static int warp_bwd_impl(const float* dout, const float* inp, int n, int h, int 
   OF_CHECK_ARG(dout && inp && flow && dflow, "warp bwd: NULL pointer");
   hipStream_t s = as_stream(stream);
   const int64_t npix = (int64_t)n * h * w;
-  if (c >= 16) {
+  if (!absolute && c % 64 == 0 && (int64_t)h * w < INT32_MAX) {
+    const int64_t blocks =
+        (int64_t)n * ((h + WH_T - 1) / WH_T) * ((w + WH_T - 1) / WH_T) * (c / 64);
+    OF_CHECK_ARG(blocks < INT32_MAX, "warp bwd: too many tiles");
+    if (c > 64 && hipMemsetAsync(dflow, 0, (size_t)npix * 2 * sizeof(float), s) != hipSuccess)
+      return check_launch("warp_bwd: dflow memset");
+    hipLaunchKernelGGL(warp_bwd_agg, dim3((unsigned)blocks), dim3(64 * WH_WAVES), 0, s, dout,
+                       inp, n, h, w, c, flow, dinp, dflow);
+  } else if (c >= 16) {
     const int g = grid_for(npix * 64, 256, 16384);
     hipLaunchKernelGGL(warp_bwd_wave, dim3(g), dim3(256), 0, s, dout, inp, n, h, w, c, flow,
                        dinp, dflow, absolute);

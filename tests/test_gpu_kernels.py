@@ -204,7 +204,7 @@ def test_corr_concat(n, h, w, c, cp, has_flow):
 @pytest.mark.parametrize("shape,flow_scale", [((2, 12, 20, 64), 3.0), ((2, 16, 16, 128), 1.5),
                                               ((1, 10, 14, 3), 4.0), ((2, 8, 24, 32), 20.0),
                                               ((1, 4, 8, 128), 0.5), ((1, 40, 70, 64), 1.0),
-                                              ((2, 70, 40, 32), 6.0)])
+                                              ((2, 70, 40, 32), 6.0), ((2, 30, 50, 64), 40.0)])
 def test_warp(shape, flow_scale):
     ops = _ops()
     n, h, w, c = shape

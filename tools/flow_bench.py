@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--flow-scale", type=float, default=2.0,
                     help="std of the random flows in pixels (at init the net's are ~0.1)")
+    ap.add_argument("--flow-offset", type=float, default=0.0,
+                    help="constant added to both flow channels (large: clipped samples)")
     args = ap.parse_args()
     _lib.load()
     n = args.batch
@@ -48,7 +50,7 @@ def main():
     for lvl, h, w, c, cp, has_flow in LEVELS:
         f1 = torch.randn(n, h, w, c, device="cuda")
         f2 = torch.randn(n, h, w, c, device="cuda")
-        fl = torch.randn(n, h, w, 2, device="cuda") * args.flow_scale if has_flow else None
+        fl = torch.randn(n, h, w, 2, device="cuda") * args.flow_scale + args.flow_offset if has_flow else None
         cat = torch.empty(n, h, w, cp, device="cuda")
         dcat = torch.randn(n, h, w, cp, device="cuda")
         df1, df2 = torch.empty_like(f1), torch.empty_like(f2)
