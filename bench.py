@@ -46,9 +46,11 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md; no spar
 
 def kind_parts(kind):
     """timing kind -> (mode, tile config, family): f32 GEMMs mode*8+cfg (narrow VALU cfg 7),
+    f32 halo-tiled wgrad 32 + mode*8 + cfg,
     bf16 implicit GEMMs 64 + mode*8 + cfg, bf16 halo-tiled 3x3 96 + mode*8 + cfg
     (optical_flow_amd/csrc/conv_f32.hip)."""
-    fam = "tile_bf16" if kind >= 96 else "bf16" if kind >= 64 else "f32"
+    fam = ("tile_bf16" if kind >= 96 else "bf16" if kind >= 64 else
+           "tile_f32" if kind >= 32 else "f32")
     return (kind % 32) // 8, kind % 8, fam
 
 
@@ -60,9 +62,9 @@ WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>
 
 def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
-    sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16"}[fam]
-    if fam == "tile_bf16" and mode == 2:
-        return "wgrad_tile_bf16<%s>" % WGT_WAVES[cfg]
+    sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32"}[fam]
+    if fam in ("tile_bf16", "tile_f32") and mode == 2:
+        return "wgrad%s<%s>" % (sfx, WGT_WAVES[cfg])
     return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (TILE_BN if fam == "tile_bf16"
                                                  else TILE_TEMPLATE)[cfg])
 
@@ -72,8 +74,8 @@ def kernel_symbol(kind):
     mode, cfg, fam = kind_parts(kind)
     if cfg == 7:
         return NARROW_SYMBOLS[mode]
-    if fam == "tile_bf16" and mode == 2:
-        return "void oflow::conv_wgrad_tile_bf16<%s>(oflow::GemmArgs)" % WGT_WAVES[cfg]
+    if fam in ("tile_bf16", "tile_f32") and mode == 2:
+        return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (fam, WGT_WAVES[cfg])
     if fam == "tile_bf16":
         return "void oflow::conv_tile_bf16<%s, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode)
     if fam == "bf16" and mode == 2:
@@ -240,7 +242,8 @@ def main():
             if pmc.get("kernel") == sym and pmc.get("config") == [H, W, B]:
                 traffic = pmc.get("hbm_bytes_per_launch")
         allconv = sum(v[0] for v in per.values()) / (sum(v[1] for v in per.values()) * 1e-3) / 1e12
-        peak = FP32_MFMA_PEAK_TFLOPS if kind_parts(dom)[2] == "f32" else BF16_MFMA_PEAK_TFLOPS
+        peak = (FP32_MFMA_PEAK_TFLOPS if kind_parts(dom)[2] in ("f32", "tile_f32")
+                else BF16_MFMA_PEAK_TFLOPS)
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,

@@ -136,6 +136,16 @@ size_t of_conv2d_wgrad_bf16_workspace(const of_conv_desc* d);
 int of_conv2d_wgrad_bf16(const of_conv_desc* d, const float* x, int ldx, const float* dy,
                          int lddy, float* dw, float* db, int accumulate, void* workspace,
                          size_t ws_bytes, void* stream);
+/* Input gradient plus an added gradient: dx = dgrad(dy) + add (add may alias dx).  The
+ * residual block's two input-gradient branches (conv_a and the shortcut, AddV2 in the
+ * resnet block of model.py:18-22) sum in this epilogue instead of a separate add pass.
+ * Same workspace as of_conv2d_dgrad; not for Cout <= 4 layers. */
+int of_conv2d_dgrad_add(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
+                        const float* add, int ld_add, float* dx, int lddx, void* workspace,
+                        size_t ws_bytes, void* stream);
+int of_conv2d_dgrad_add_bf16(const of_conv_desc* d, const float* dy, int lddy,
+                             const void* w16_bwd, const float* add, int ld_add, float* dx,
+                             int lddx, void* workspace, size_t ws_bytes, void* stream);
 size_t of_conv2d_dgrad_bf16_workspace(const of_conv_desc* d);
 int of_conv2d_dgrad_bf16(const of_conv_desc* d, const float* dy, int lddy, const void* w16_bwd,
                          const float* act_src, int ld_act, int act, float alpha, float* dx,

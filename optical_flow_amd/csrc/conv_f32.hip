@@ -105,11 +105,17 @@ __device__ __forceinline__ int64_t out_row(const GemmArgs& a, const Group& g, in
 // whose activation derivative scales dx (dgrad).  Call sites gather all of a lane's values
 // before the first store: interleaved, every load would wait behind the previous store (the
 // compiler cannot prove a.C does not alias them).
+// dgrad: s = the producer's output (activation derivative), r = a gradient to add (the
+// residual branch's, so the autograd sum of the two input gradients needs no extra pass).
+struct EpAux {
+  float s, r;
+};
 template <int MODE>
-__device__ __forceinline__ float epilogue_aux(const GemmArgs& a, int64_t row, int n) {
-  if (MODE == MODE_FWD) return a.res ? a.res[row * a.ldr + n] : 0.f;
-  if (MODE == MODE_DGRAD) return a.act_src ? a.act_src[row * a.ld_act + n] : 1.f;
-  return 0.f;
+__device__ __forceinline__ EpAux epilogue_aux(const GemmArgs& a, int64_t row, int n) {
+  if (MODE == MODE_FWD) return {a.res ? a.res[row * a.ldr + n] : 0.f, 0.f};
+  if (MODE == MODE_DGRAD)
+    return {a.act_src ? a.act_src[row * a.ld_act + n] : 1.f, a.res ? a.res[row * a.ldr + n] : 0.f};
+  return {0.f, 0.f};
 }
 
 // Aux values gathered ahead of the stores: the whole 16-value MFMA fragment for dgrad (the
@@ -119,7 +125,7 @@ __device__ __forceinline__ float epilogue_aux(const GemmArgs& a, int64_t row, in
 #define OF_EPG_FWD 4
 #endif
 #ifndef OF_EPG_DGRAD
-#define OF_EPG_DGRAD 16
+#define OF_EPG_DGRAD 8
 #endif
 template <int MODE>
 constexpr int EP_GATHER = MODE == MODE_DGRAD ? OF_EPG_DGRAD : OF_EPG_FWD;
@@ -127,15 +133,16 @@ constexpr int EP_GATHER = MODE == MODE_DGRAD ? OF_EPG_DGRAD : OF_EPG_FWD;
 // Fused epilogue for one element (fwd / dgrad), v = the full K sum, aux = epilogue_aux.
 template <int MODE>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int64_t row, int n, float v,
-                                               float bias, float scale, float shift, float aux) {
+                                               float bias, float scale, float shift, EpAux aux) {
   if (MODE == MODE_FWD) {
     v += bias;
     if (a.z) a.z[row * a.ldz + n] = v;
     if (a.bn_g) v = v * scale + shift;
-    v += aux;
+    v += aux.s;
     v = act_fwd(v, a.act, a.alpha);
   } else if (MODE == MODE_DGRAD) {
-    v *= aux > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
+    v *= aux.s > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
+    v += aux.r;
   }
   a.C[row * a.ldc + n] = v;
 }
@@ -506,11 +513,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r0 = 0; r0 < 16; r0 += EP_GATHER<MODE>) {
-        float aux[EP_GATHER<MODE>];
+        EpAux aux[EP_GATHER<MODE>];
 #pragma unroll
         for (int r = r0; r < r0 + EP_GATHER<MODE>; ++r) {
           const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          aux[r - r0] = m < M ? epilogue_aux<MODE>(a, out_row(a, G, m), n) : 0.f;
+          aux[r - r0] = m < M ? epilogue_aux<MODE>(a, out_row(a, G, m), n) : EpAux{0.f, 0.f};
         }
 #pragma unroll
         for (int r = r0; r < r0 + EP_GATHER<MODE>; ++r) {
@@ -792,11 +799,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r0 = 0; r0 < 16; r0 += EP_GATHER<MODE>) {
-        float aux[EP_GATHER<MODE>];
+        EpAux aux[EP_GATHER<MODE>];
 #pragma unroll
         for (int r = r0; r < r0 + EP_GATHER<MODE>; ++r) {
           const int m = m0 + wm0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          aux[r - r0] = m < M ? epilogue_aux<MODE>(a, out_row(a, G, m), n) : 0.f;
+          aux[r - r0] = m < M ? epilogue_aux<MODE>(a, out_row(a, G, m), n) : EpAux{0.f, 0.f};
         }
 #pragma unroll
         for (int r = r0; r < r0 + EP_GATHER<MODE>; ++r) {
@@ -993,13 +1000,13 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
     if (a.splits == 1) column_params<MODE>(a, n, bias, scale, shift);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      float aux[16];
+      EpAux aux[16];
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
         const int oy = oy0 + m / TT_W, ox = ox0 + m % TT_W;
         aux[rr] = a.splits == 1 && oy < OH && ox < OW
-                      ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : 0.f;
+                      ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : EpAux{0.f, 0.f};
       }
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
@@ -1441,6 +1448,151 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
   }
 }
 
+// ---- fp32 weight gradient, 3x3 stride 1: all 9 taps from one staged halo ----------------
+// dW[r][s][ci][co] = sum_p x(p + (r, s) - pad)[ci] . dy(p)[co] on v_mfma_f32_32x32x2_f32, the
+// fp32 counterpart of conv_wgrad_tile_bf16: a workgroup owns CIB x COB channels for all 9
+// taps (wave = 32 ci x 32 co x 9 accumulators) and walks 8 x 16 output-pixel tiles; per tile
+// it stages the x halo (10 x 18 px x CIB, pixel-major as in HBM) and dy (128 px x COB) once,
+// and every tap reads its A fragments from the halo at a shifted pixel.  fp32 fragments are
+// single dwords, so a shift needs no aligned copies: lanes 0-31 read 32 consecutive channels
+// of one pixel, lanes 32-63 of the next (conflict-free ds_read_b32).  One LDS image, register
+// prefetch of the next tile during the MFMAs.  Output: the split-K slabs of the GEMM path.
+template <int WAVES_CI, int WAVES_CO>
+__global__ __launch_bounds__(256, 1) void conv_wgrad_tile_f32(GemmArgs a) {
+  constexpr int CIB = 32 * WAVES_CI, COB = 32 * WAVES_CO, KS = 3;
+  constexpr int HH = TT_H + KS - 1, HW = TT_W + KS - 1, HP = HH * HW;
+  static_assert(WAVES_CI * WAVES_CO == 4 && COB >= 64, "4 waves, COB >= 64");
+  constexpr int XQ = HP * (CIB / 4), XS = (XQ + 255) / 256;      // (halo px, ci quad)
+  constexpr int DQ = TT_H * TT_W * (COB / 4), DS = DQ / 256;     // (px, co quad)
+  static_assert(DQ % 256 == 0, "dy items");
+  constexpr int NG = 256 / (COB / 4);
+  __shared__ float4 Xs4[HP * CIB / 4];
+  __shared__ float4 Ds4[TT_H * TT_W * COB / 4];
+  __shared__ float csum[NG][COB];
+  const float* Xs = reinterpret_cast<const float*>(Xs4);
+  const float* Dsf = reinterpret_cast<const float*>(Ds4);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_co = tile % a.n_tiles;
+  const int tile_ci = tile / a.n_tiles;
+  const int ci0 = tile_ci * CIB, co0 = tile_co * COB;
+  const int t_begin = split * a.k_per_split;
+  const int t_end = min(a.K, t_begin + a.k_per_split);
+  const int steps = max(0, t_end - t_begin);
+  const int tiles_x = (a.wo + TT_W - 1) / TT_W, tiles_y = (a.ho + TT_H - 1) / TT_H;
+  const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
+  const bool do_colsum = a.colsum && tile_ci == 0;
+  const int xcq = tid % (CIB / 4);
+  const bool xc_ok = ci0 + 4 * xcq < a.kc;
+  const int dcq = tid % (COB / 4);
+  const bool dc_ok = co0 + 4 * dcq < a.nb;
+
+  float4 xv[XS], dv[DS];
+  float4 colacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load = [&](int t) {
+    const int b = t / (tiles_x * tiles_y);
+    const int trem = t - b * tiles_x * tiles_y;
+    const int oy0 = (trem / tiles_x) * TT_H, ox0 = (trem % tiles_x) * TT_W;
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int q = tid + 256 * j;
+      const int hp = q / (CIB / 4);
+      const int iy = oy0 - a.pt + hp / HW, ix = ox0 - a.pl + hp % HW;
+      const bool ok = q < XQ && xc_ok && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+      xv[j] = bload4(rx, ok ? (uint32_t)((((b * a.h + iy) * a.w + ix) * a.lda + ci0 + 4 * xcq) * 4)
+                            : kOOB);
+    }
+#pragma unroll
+    for (int j = 0; j < DS; ++j) {
+      const int px = (tid + 256 * j) / (COB / 4);
+      const int oy = oy0 + px / TT_W, ox = ox0 + px % TT_W;
+      const bool ok = dc_ok && oy < a.ho && ox < a.wo;
+      dv[j] = bload4(rd, ok ? (uint32_t)((((b * a.ho + oy) * a.wo + ox) * a.ldb + co0 + 4 * dcq) * 4)
+                            : kOOB);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int q = tid + 256 * j;
+      if (q < XQ) Xs4[q] = xv[j];          // [halo px][CIB] with quads contiguous
+    }
+#pragma unroll
+    for (int j = 0; j < DS; ++j) {
+      Ds4[tid + 256 * j] = dv[j];           // [px][COB]
+      if (do_colsum) add4(colacc, dv[j]);
+    }
+  };
+
+  f32x16 acc[KS * KS];
+#pragma unroll
+  for (int t = 0; t < KS * KS; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const int wci0 = (wave / WAVES_CO) * 32;
+  const int wco0 = (wave % WAVES_CO) * 32;
+  const int lrow = lane & 31, lk = lane >> 5;
+
+  if (steps > 0) {
+    load(t_begin);
+    store();
+  }
+  __syncthreads();
+  for (int i = 0; i < steps; ++i) {
+    const bool more = i + 1 < steps;
+    if (more) load(t_begin + i + 1);
+#pragma unroll 2
+    for (int k2 = 0; k2 < TT_H * TT_W / 2; ++k2) {
+      const int p = 2 * k2 + lk;                        // this lane's pixel of the pair
+      const float bv = Dsf[p * COB + wco0 + lrow];
+      const float* xa = Xs + ((p / TT_W) * HW + p % TT_W) * CIB + wci0 + lrow;
+#pragma unroll
+      for (int r = 0; r < KS; ++r)
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          acc[r * KS + s] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[(r * HW + s) * CIB], bv,
+                                                                 acc[r * KS + s], 0, 0, 0);
+    }
+    if (more) {
+      __syncthreads();
+      store();
+    }
+    __syncthreads();
+  }
+
+  float* S = a.slab + (int64_t)split * a.split_stride;
+  if (do_colsum) {
+    const int g = tid / (COB / 4);
+    csum[g][4 * dcq] = colacc.x;
+    csum[g][4 * dcq + 1] = colacc.y;
+    csum[g][4 * dcq + 2] = colacc.z;
+    csum[g][4 * dcq + 3] = colacc.w;
+    __syncthreads();
+    if (tid < COB && co0 + tid < a.N) {
+      float v = 0.f;
+#pragma unroll
+      for (int g2 = 0; g2 < NG; ++g2) v += csum[g2][tid];
+      S[(int64_t)a.M * a.slab_ld + co0 + tid] = v;
+    }
+  }
+  const int n = co0 + wco0 + lrow;
+  if (n < a.N) {
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = ci0 + wci0 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (ci < a.kc) S[((int64_t)t * a.kc + ci) * a.slab_ld + n] = acc[t][r];
+      }
+  }
+}
+
 // Split-K epilogue for fwd/dgrad: sum the K slices' slabs, then the fused epilogue.
 // Workgroup = 32 items x 8 split lanes; item = (slab row, 4 columns); the 8 lanes each sum
 // every 8th slice (many independent loads in flight), then a fixed-order LDS reduction.
@@ -1475,9 +1627,10 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a) {
   if (m >= G.M) return;
   const int64_t row = out_row(a, G, m);
   const float v[4] = {acc.x, acc.y, acc.z, acc.w};
-  float aux[4];
+  EpAux aux[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) aux[e] = 4 * q + e < a.N ? epilogue_aux<MODE>(a, row, 4 * q + e) : 0.f;
+  for (int e = 0; e < 4; ++e)
+    aux[e] = 4 * q + e < a.N ? epilogue_aux<MODE>(a, row, 4 * q + e) : EpAux{0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int n = 4 * q + e;
@@ -1970,7 +2123,15 @@ struct WgradPlan {
 };
 
 // bf16 3x3 stride-1 wgrad on conv_wgrad_tile_bf16: block channel tiles (CIB x COB).
-bool wgt_ok(const of_conv_desc* d) { return tile_ok(d); }
+// bf16: every 3x3 stride-1 layer.  fp32 (MFMA-bound either way): where the implicit GEMM
+// loses to its N = 64 tiles or to many small split-K slabs (measured, tools/conv_bench.py):
+// Cout = 64, or Cout % 128 == 0 on up to 8 x 96 x 128 output pixels.
+bool wgt_ok(const of_conv_desc* d, bool bf16) {
+  if (!tile_ok(d)) return false;
+  if (bf16) return true;
+  const int64_t npix = (int64_t)d->n * d->ho * d->wo;
+  return d->cout == 64 || (d->cout % 128 == 0 && npix <= 8 * 96 * 128);
+}
 int wgt_cfg(const of_conv_desc* d) { return d->cout > 64 ? 0 : 2; }   // <1,4> : <2,2>
 void wgt_blocks(const of_conv_desc* d, int& cib, int& cob) {
   cib = wgt_cfg(d) == 0 ? 32 : 64;
@@ -1983,7 +2144,7 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false) {
   p.M = g.taps * g.cin_p;
   p.ldc = g.cout_p;
   p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
-  if (bf16 && wgt_ok(d)) {
+  if (wgt_ok(d, bf16)) {
     // K = 8 x 16 pixel tiles; one workgroup per CU (LDS-bound occupancy), equal slices
     int cib, cob;
     wgt_blocks(d, cib, cob);
@@ -2258,8 +2419,8 @@ int of_conv2d_fwd_bf16(const of_conv_desc* d, const float* x, int ldx, const voi
 
 static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, int lddy,
                            const void* w_bwd, const float* act_src, int ld_act, int act,
-                           float alpha, float* dx, int lddx, void* workspace, size_t ws_bytes,
-                           void* stream) {
+                           float alpha, const float* add, int ld_add, float* dx, int lddx,
+                           void* workspace, size_t ws_bytes, void* stream) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
@@ -2267,10 +2428,12 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv dgrad: lddy (>= round_up(cout,4))");
   OF_CHECK_ARG(lddx >= d->cin_p, "conv dgrad: lddx");
   OF_CHECK_ARG(!act_src || ld_act >= d->cin_p, "conv dgrad: ld_act");
+  OF_CHECK_ARG(!add || ld_add >= d->cin_p, "conv dgrad: ld_add");
   OF_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)w_bwd & 15) == 0,
                "conv dgrad: dy / w must be 16-byte aligned");
   OF_CHECK_ARG(d->stride == 1 || d->stride == 2, "conv dgrad: stride must be 1 or 2");
   if (!bf16 && narrow_ok(d)) {
+    OF_CHECK_ARG(!add, "conv dgrad: the Cout <= 4 kernels take no added gradient");
     hipStream_t s = as_stream(stream);
     if (timing_on()) timing_begin(s);
     st = narrow_dgrad(d, dy, lddy, static_cast<const float*>(w_bwd), act_src, ld_act, act,
@@ -2294,6 +2457,8 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
   a.ld_act = ld_act;
   a.act = act;
   a.alpha = alpha;
+  a.res = add;
+  a.ldr = ld_add;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   st = tile   ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
@@ -2305,15 +2470,29 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
 int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
                     const float* act_src, int ld_act, int act, float alpha, float* dx,
                     int lddx, void* workspace, size_t ws_bytes, void* stream) {
-  return conv_dgrad_impl(false, d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, dx, lddx,
-                         workspace, ws_bytes, stream);
+  return conv_dgrad_impl(false, d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, nullptr, 0,
+                         dx, lddx, workspace, ws_bytes, stream);
+}
+
+int of_conv2d_dgrad_add(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
+                        const float* add, int ld_add, float* dx, int lddx, void* workspace,
+                        size_t ws_bytes, void* stream) {
+  return conv_dgrad_impl(false, d, dy, lddy, w_bwd, nullptr, 0, OF_ACT_NONE, 0.f, add, ld_add,
+                         dx, lddx, workspace, ws_bytes, stream);
 }
 
 int of_conv2d_dgrad_bf16(const of_conv_desc* d, const float* dy, int lddy, const void* w16_bwd,
                          const float* act_src, int ld_act, int act, float alpha, float* dx,
                          int lddx, void* workspace, size_t ws_bytes, void* stream) {
-  return conv_dgrad_impl(true, d, dy, lddy, w16_bwd, act_src, ld_act, act, alpha, dx, lddx,
-                         workspace, ws_bytes, stream);
+  return conv_dgrad_impl(true, d, dy, lddy, w16_bwd, act_src, ld_act, act, alpha, nullptr, 0,
+                         dx, lddx, workspace, ws_bytes, stream);
+}
+
+int of_conv2d_dgrad_add_bf16(const of_conv_desc* d, const float* dy, int lddy,
+                             const void* w16_bwd, const float* add, int ld_add, float* dx,
+                             int lddx, void* workspace, size_t ws_bytes, void* stream) {
+  return conv_dgrad_impl(true, d, dy, lddy, w16_bwd, nullptr, 0, OF_ACT_NONE, 0.f, add, ld_add,
+                         dx, lddx, workspace, ws_bytes, stream);
 }
 
 size_t of_conv2d_wgrad_workspace(const of_conv_desc* d) {
@@ -2373,7 +2552,7 @@ static int conv_wgrad_impl(bool bf16, const of_conv_desc* d, const float* x, int
   a.colsum = db != nullptr;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
-  if (bf16 && wgt_ok(d)) {
+  if (wgt_ok(d, bf16)) {
     int cib, cob;
     wgt_blocks(d, cib, cob);
     a.K = d->n * (int)cdiv(d->ho, TT_H) * (int)cdiv(d->wo, TT_W);
@@ -2382,10 +2561,15 @@ static int conv_wgrad_impl(bool bf16, const of_conv_desc* d, const float* x, int
     const int cfg = wgt_cfg(d);
     dim3 grid(a.tiles_total * a.splits), block(256);
     if (timing_on()) timing_begin(s);
-    if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_bf16<1, 4>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((conv_wgrad_tile_bf16<2, 2>), grid, block, 0, s, a);
-    if (timing_on()) timing_end(s, 96 + MODE_WGRAD * 8 + cfg, flops);
-    st = check_launch("conv_wgrad_tile_bf16");
+    if (bf16) {
+      if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_bf16<1, 4>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((conv_wgrad_tile_bf16<2, 2>), grid, block, 0, s, a);
+    } else {
+      if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_f32<1, 4>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((conv_wgrad_tile_f32<2, 2>), grid, block, 0, s, a);
+    }
+    if (timing_on()) timing_end(s, (bf16 ? 96 : 32) + MODE_WGRAD * 8 + cfg, flops);
+    st = check_launch("conv_wgrad_tile");
   } else if (bf16) {
     const int bn = pick_bn(a.N);
     const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;

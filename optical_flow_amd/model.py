@@ -123,6 +123,9 @@ def backward_order(max_disp=3) -> List[str]:
 
 
 # ========================================================================= encoder ======
+# OFLOW_PER_LAYER_BLOCKS=1: run the residual blocks as separate conv nodes (A/B timing only)
+_PER_LAYER_BLOCKS = os.environ.get("OFLOW_PER_LAYER_BLOCKS", "0") == "1"
+
 class Encoder:
     """reset18_encoder (model.py:10-26): conv1 7x7/2 + BN + ReLU -> out0 (H/2, 64);
     max-pool; three resnet_layer_simple stages -> H/4 x64, H/8 x128, H/16 x256.
@@ -162,9 +165,11 @@ class Encoder:
         outs = [x]
         x = ops.maxpool2(x)
         for i, (a, b, p) in enumerate(self.blocks):
-            y = a(x)
-            sc = p(x) if p is not None else x
-            x = b(y, residual=sc)
+            if _PER_LAYER_BLOCKS:       # A/B switch: one autograd node per conv
+                y = a(x)
+                x = b(y, residual=p(x) if p is not None else x)
+            else:
+                x = ops.res_block(x, a, b, p)
             if i % 2 == 1:
                 outs.append(x)
         return outs

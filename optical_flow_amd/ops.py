@@ -171,6 +171,13 @@ class ConvLayer:
             return "of_conv2d_wgrad_bf16", lib.of_conv2d_wgrad_bf16_workspace(C.byref(d))
         return "of_conv2d_wgrad", lib.of_conv2d_wgrad_workspace(C.byref(d))
 
+    def dgrad_add_entry(self, d):
+        """(C entry point, workspace bytes) of the input gradient with an added gradient."""
+        lib = _lib.lib()
+        if self.bf16(d):
+            return "of_conv2d_dgrad_add_bf16", lib.of_conv2d_dgrad_bf16_workspace(C.byref(d))
+        return "of_conv2d_dgrad_add", lib.of_conv2d_dgrad_workspace(C.byref(d))
+
     def dgrad_entry(self, d):
         lib = _lib.lib()
         if self.bf16(d):
@@ -232,113 +239,189 @@ def _pad_channels(t: torch.Tensor, cp: int) -> torch.Tensor:
     return out
 
 
+def _conv_forward(layer: "ConvLayer", x, residual=None):
+    """Conv2D + BiasAdd [+ FusedBatchNorm(inference)] [+ AddV2 residual] [+ Relu/LeakyRelu]:
+    one fused kernel.  Returns (y, z); z = the pre-BN conv output (BN layers only)."""
+    _check_dev(x, residual)
+    n, h, w, cx = x.shape
+    assert cx == layer.cin_p, "conv %s: input has %d channels, expected %d (cin_p)" % (
+        layer.name, cx, layer.cin_p)
+    d = layer.desc(n, h, w)
+    wf, _ = layer.packed(d)
+    y = torch.empty((n, d.ho, d.wo, layer.cout), device=x.device)
+    z = torch.empty_like(y) if layer.bn is not None else None
+    bn = layer.bn
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == y.shape
+    _tag(layer, 0)
+    entry, wsz = layer.fwd_entry(d)
+    wsk, wsp, wsb = _workspace(wsz, x.device)
+    call(entry, C.byref(d), _ptr(x), cx, _ptr(wf), _ptr(layer.bias),
+         _ptr(bn[0]) if bn else None, _ptr(bn[1]) if bn else None,
+         _ptr(bn[2]) if bn else None, _ptr(bn[3]) if bn else None, BN_EPS,
+         _ptr(residual), layer.cout, layer.act, layer.alpha,
+         _ptr(z), layer.cout, _ptr(y), layer.cout, wsp, wsb, _stream())
+    return y, z
+
+
+def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx_out=None):
+    """Backward of _conv_forward: BN/activation backward (with the residual gradient), weight
+    and bias gradients, input gradient.  needs = (x, kernel, bias, gamma, beta, residual).
+    add: a gradient summed into dx by the input-gradient kernel's epilogue (dx_out may be
+    that same buffer).  Returns (dx, d_kernel, d_bias, d_gamma, d_beta, d_residual) with None
+    for gradients written straight into the gradient arena."""
+    n, h, w, cx = x.shape
+    d = layer.desc(n, h, w)
+    _, wd = layer.packed(d)
+    dy = dy.contiguous()
+    s = _stream()
+    need_x, need_k, need_b, need_g, need_be, need_res = needs
+    ret_k = ret_b = ret_g = ret_be = dres = dx = None
+    npix = n * d.ho * d.wo
+    # ---- pre-activation gradient dz -----------------------------------------------------
+    if layer.bn is not None:
+        gamma, beta, mean, var = layer.bn
+        dz = torch.empty_like(dy)
+        dres = torch.empty_like(dy) if (has_res and need_res) else None
+        tg = grad_target(gamma) if need_g else (None, 0, None)
+        tb = grad_target(beta) if need_be else (None, 0, None)
+        tbias = grad_target(layer.bias) if need_b else (None, 0, None)
+        ret_g, ret_be, ret_b = tg[2], tb[2], tbias[2]
+        acc = tg[1] if need_g else (tb[1] if need_be else tbias[1])
+        # per-target accumulate flags must agree (all arena or all fresh)
+        assert all(t[0] is None or t[1] == acc for t in (tg, tb, tbias))
+        ws = torch.empty(_lib.lib().of_bn_act_bwd_workspace(npix, layer.cout) // 4 + 1,
+                         device=dy.device)
+        call("of_bn_act_bwd", npix, layer.cout, layer.act, _ptr(dy), _ptr(y), _ptr(z),
+             _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, _ptr(dz), _ptr(dres),
+             _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
+        bias_done = True
+    else:
+        if layer.act != ACT_NONE:
+            dz = torch.empty_like(dy)
+            call("of_act_bwd", _ptr(dy), _ptr(y), layer.act, layer.alpha, _ptr(dz),
+                 dy.numel(), s)
+        else:
+            dz = dy
+        if has_res and need_res:
+            dres = dz
+        bias_done = False
+    dzp = _pad_channels(dz, _c4(layer.cout))
+    # ---- weight (+bias) gradient --------------------------------------------------------
+    if need_k or (need_b and not bias_done):
+        tk = grad_target(layer.kernel)
+        tbias = grad_target(layer.bias) if (need_b and not bias_done) else (None, 0, None)
+        went, wsb = layer.wgrad_entry(d)
+        ws = torch.empty(wsb // 4 + 1, device=dy.device)
+        if tbias[0] is not None and tbias[1] != tk[1]:
+            # mixed arena / fresh targets: compute the bias into a temp, then place it
+            tmpb = torch.empty_like(layer.bias)
+            _tag(layer, 2)
+            call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
+                 _ptr(tk[0]), _ptr(tmpb), tk[1], _ptr(ws), wsb, s)
+            if tbias[1]:
+                call("of_add_inplace", _ptr(tbias[0]), _ptr(tmpb), tmpb.numel(), s)
+            else:
+                tbias = (tmpb, 0, tmpb)
+        else:
+            _tag(layer, 2)
+            call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
+                 _ptr(tk[0]), _ptr(tbias[0]), tk[1], _ptr(ws), wsb, s)
+        ret_k = tk[2] if need_k else None
+        if need_b and not bias_done:
+            ret_b = tbias[2]
+    _grad_ready(layer.kernel if need_k else None, layer.bias if need_b else None,
+                *(layer.bn[:2] if layer.bn is not None else ()))
+    # ---- input gradient -----------------------------------------------------------------
+    if need_x:
+        dx = dx_out if dx_out is not None else torch.empty((n, h, w, cx), device=dy.device)
+        _tag(layer, 1)
+        if add is not None:
+            add = add.contiguous()
+            assert add.shape == dx.shape
+            entry, wsz = layer.dgrad_add_entry(d)
+            wsk, wsp, wsb = _workspace(wsz, dy.device)
+            call(entry, C.byref(d), _ptr(dzp), dzp.shape[-1], _ptr(wd), _ptr(add), cx,
+                 _ptr(dx), cx, wsp, wsb, s)
+        else:
+            entry, wsz = layer.dgrad_entry(d)
+            wsk, wsp, wsb = _workspace(wsz, dy.device)
+            call(entry, C.byref(d), _ptr(dzp), dzp.shape[-1], _ptr(wd), None, 0,
+                 ACT_NONE, 0.0, _ptr(dx), cx, wsp, wsb, s)
+    return dx, ret_k, ret_b, ret_g, ret_be, dres
+
+
 class _ConvFn(torch.autograd.Function):
     """Conv2D + BiasAdd [+ FusedBatchNorm(inference)] [+ AddV2 residual] [+ Relu/LeakyRelu]
     forward; Conv2DBackpropInput / Conv2DBackpropFilter / BiasAddGrad / BN grads backward."""
 
     @staticmethod
     def forward(ctx, x, kernel, bias, gamma, beta, residual, layer: ConvLayer):
-        _check_dev(x, kernel, bias, residual)
-        n, h, w, cx = x.shape
-        assert cx == layer.cin_p, "conv %s: input has %d channels, expected %d (cin_p)" % (
-            layer.name, cx, layer.cin_p)
-        x = x.contiguous()
-        d = layer.desc(n, h, w)
-        wf, _ = layer.packed(d)
-        y = torch.empty((n, d.ho, d.wo, layer.cout), device=x.device)
-        z = torch.empty_like(y) if layer.bn is not None else None
-        bn = layer.bn
-        if residual is not None:
-            residual = residual.contiguous()
-            assert residual.shape == y.shape
-        _tag(layer, 0)
-        entry, wsz = layer.fwd_entry(d)
-        wsk, wsp, wsb = _workspace(wsz, x.device)
-        call(entry, C.byref(d), _ptr(x), cx, _ptr(wf), _ptr(bias),
-             _ptr(bn[0]) if bn else None, _ptr(bn[1]) if bn else None,
-             _ptr(bn[2]) if bn else None, _ptr(bn[3]) if bn else None, BN_EPS,
-             _ptr(residual), layer.cout, layer.act, layer.alpha,
-             _ptr(z), layer.cout, _ptr(y), layer.cout, wsp, wsb, _stream())
+        _check_dev(kernel, bias)
+        y, z = _conv_forward(layer, x.contiguous(), residual)
         ctx.layer = layer
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y, z)
+        ctx.save_for_backward(x.contiguous(), y, z)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        layer: ConvLayer = ctx.layer
         x, y, z = ctx.saved_tensors
-        n, h, w, cx = x.shape
-        d = layer.desc(n, h, w)
-        _, wd = layer.packed(d)
-        dy = dy.contiguous()
-        s = _stream()
-        need_x, need_k, need_b, need_g, need_be, need_res = ctx.needs_input_grad[:6]
-        ret_k = ret_b = ret_g = ret_be = dres = dx = None
-        npix = n * d.ho * d.wo
-        # ---- pre-activation gradient dz -------------------------------------------------
-        if layer.bn is not None:
-            gamma, beta, mean, var = layer.bn
-            dz = torch.empty_like(dy)
-            dres = torch.empty_like(dy) if (ctx.has_res and need_res) else None
-            tg = grad_target(gamma) if need_g else (None, 0, None)
-            tb = grad_target(beta) if need_be else (None, 0, None)
-            tbias = grad_target(layer.bias) if need_b else (None, 0, None)
-            ret_g, ret_be, ret_b = tg[2], tb[2], tbias[2]
-            acc = tg[1] if need_g else (tb[1] if need_be else tbias[1])
-            # per-target accumulate flags must agree (all arena or all fresh)
-            assert all(t[0] is None or t[1] == acc for t in (tg, tb, tbias))
-            ws = torch.empty(_lib.lib().of_bn_act_bwd_workspace(npix, layer.cout) // 4 + 1,
-                             device=dy.device)
-            call("of_bn_act_bwd", npix, layer.cout, layer.act, _ptr(dy), _ptr(y), _ptr(z),
-                 _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, _ptr(dz), _ptr(dres),
-                 _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
-            bias_done = True
+        out = _conv_backward(ctx.layer, x, y, z, dy, ctx.has_res, ctx.needs_input_grad[:6])
+        return (*out, None)
+
+
+class _ResBlockFn(torch.autograd.Function):
+    """One residual block of the encoder (resnet_layer_simple, model.py:18,20,22; assumed
+    basic block): y = ReLU(BN_b(conv_b(ReLU(BN_a(conv_a(x))))) + shortcut),
+    shortcut = x or BN_p(proj(x)).  One autograd node so that the input gradient's two
+    branches are summed by the conv_a input-gradient epilogue (of_conv2d_dgrad_add) rather
+    than by an extra elementwise pass."""
+
+    @staticmethod
+    def forward(ctx, x, *args):
+        a, b, p = args[-1]
+        x = x.contiguous()
+        ya, za = _conv_forward(a, x)
+        yp = zp = None
+        sc = x
+        if p is not None:
+            yp, zp = _conv_forward(p, x)
+            sc = yp
+        y, zb = _conv_forward(b, ya, residual=sc)
+        ctx.block = (a, b, p)
+        ctx.save_for_backward(x, ya, za, y, zb, yp, zp)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, ya, za, y, zb, yp, zp = ctx.saved_tensors
+        a, b, p = ctx.block
+        need = ctx.needs_input_grad
+        need_x = need[0]
+        nb = lambda k: tuple(need[1 + 4 * k:5 + 4 * k])     # kernel, bias, gamma, beta of layer k
+        dya, *gb = _conv_backward(b, ya, y, zb, dy, True, (True, *nb(1), True))
+        dres = gb[-1]
+        gb = gb[:-1]
+        if p is not None:
+            dxp, *gp = _conv_backward(p, x, yp, zp, dres, False, (need_x, *nb(2), False))
+            gp = gp[:-1]
+            add, dx_out = dxp, dxp
         else:
-            if layer.act != ACT_NONE:
-                dz = torch.empty_like(dy)
-                call("of_act_bwd", _ptr(dy), _ptr(y), layer.act, layer.alpha, _ptr(dz),
-                     dy.numel(), s)
-            else:
-                dz = dy
-            if ctx.has_res and need_res:
-                dres = dz
-            bias_done = False
-        dzp = _pad_channels(dz, _c4(layer.cout))
-        # ---- weight (+bias) gradient ----------------------------------------------------
-        if need_k or (need_b and not bias_done):
-            tk = grad_target(layer.kernel)
-            tbias = grad_target(layer.bias) if (need_b and not bias_done) else (None, 0, None)
-            went, wsb = layer.wgrad_entry(d)
-            ws = torch.empty(wsb // 4 + 1, device=dy.device)
-            if tbias[0] is not None and tbias[1] != tk[1]:
-                # mixed arena / fresh targets: compute the bias into a temp, then place it
-                tmpb = torch.empty_like(layer.bias)
-                _tag(layer, 2)
-                call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
-                     _ptr(tk[0]), _ptr(tmpb), tk[1], _ptr(ws), wsb, s)
-                if tbias[1]:
-                    call("of_add_inplace", _ptr(tbias[0]), _ptr(tmpb), tmpb.numel(), s)
-                else:
-                    tbias = (tmpb, 0, tmpb)
-            else:
-                _tag(layer, 2)
-                call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
-                     _ptr(tk[0]), _ptr(tbias[0]), tk[1], _ptr(ws), wsb, s)
-            ret_k = tk[2] if need_k else None
-            if need_b and not bias_done:
-                ret_b = tbias[2]
-        _grad_ready(layer.kernel if need_k else None, layer.bias if need_b else None,
-                    *(layer.bn[:2] if layer.bn is not None else ()))
-        # ---- input gradient -------------------------------------------------------------
-        if need_x:
-            dx = torch.empty((n, h, w, cx), device=dy.device)
-            _tag(layer, 1)
-            entry, wsz = layer.dgrad_entry(d)
-            wsk, wsp, wsb = _workspace(wsz, dy.device)
-            call(entry, C.byref(d), _ptr(dzp), dzp.shape[-1], _ptr(wd), None, 0,
-                 ACT_NONE, 0.0, _ptr(dx), cx, wsp, wsb, s)
-        return dx, ret_k, ret_b, ret_g, ret_be, dres, None
+            gp = []
+            add, dx_out = dres, None
+        dx, *ga = _conv_backward(a, x, ya, za, dya, False, (need_x, *nb(0), False),
+                                 add=add if need_x else None, dx_out=dx_out)
+        ga = ga[:-1]
+        return (dx, *ga, *gb, *gp, None)
+
+
+def res_block(x, a: ConvLayer, b: ConvLayer, p: Optional[ConvLayer] = None):
+    params = []
+    for L in (a, b) + ((p,) if p is not None else ()):
+        params += [L.kernel, L.bias, L.bn[0], L.bn[1]]
+    return _ResBlockFn.apply(x, *params, (a, b, p))
 
 
 class _ConvStackFn(torch.autograd.Function):

@@ -24,6 +24,7 @@ CONV_CASES = [
     (1, 10, 20, 64, 3, 3, 1, "relu", False, False),         # narrow, 16 lanes per pixel
     (2, 8, 8, 3, 2, 3, 1, "leaky", False, False),           # narrow, 1 lane per pixel
     (1, 9, 9, 12, 2, 3, 1, "leaky", False, False),          # cin_p 12: GEMM fallback
+    (2, 20, 36, 64, 64, 3, 1, "relu", True, True),          # wgrad tiles <2,2> (fp32 too)
     # smoke() level 1 (64x128 image, batch 1): 32-pixel layers, deep split-K
     (1, 4, 8, 179, 128, 3, 1, "leaky", False, False),
     (1, 4, 8, 128, 96, 3, 1, "leaky", False, False),
