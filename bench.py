@@ -83,7 +83,7 @@ def kernel_symbol(kind):
     return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_TEMPLATE[cfg], mode)
 
 
-def gflop_per_pair(H, W, max_disp=3):
+def gflop_per_pair(H, W, max_disp=3, levels=4):
     """Algorithmic training FLOPs per image pair (SURVEY.md §8 d): every conv's fwd + dgrad +
     wgrad (2 FLOP/MAC, logical channels, TF-'same' output sizes) minus the stem dgrad, plus
     3x the cost-volume forward."""
@@ -93,7 +93,7 @@ def gflop_per_pair(H, W, max_disp=3):
     stem = 2 * h * w * 7 * 7 * 3 * 64             # both Siamese branches
     macs += 2 * stem                               # fwd + wgrad (no input grad for images)
     hh, ww = h // 2, w // 2
-    for prefix, cin, cout, stride, proj in encoder_blocks():
+    for prefix, cin, cout, stride, proj in encoder_blocks(levels):
         ho, wo = hh // stride, ww // stride
         m = 2 * ho * wo                            # two branches
         macs += 3 * m * 9 * cin * cout             # conv_a
@@ -102,19 +102,19 @@ def gflop_per_pair(H, W, max_disp=3):
             macs += 3 * m * cin * cout
         hh, ww = ho, wo
     corr = 0.0
-    for level in range(4):
-        s = 16 >> level
+    for level in range(levels):
+        s = (1 << levels) >> level
         ph, pw = H // s, W // s
-        cin = head_cin(level, max_disp)
+        cin = head_cin(level, max_disp, levels)
         for cout in HEAD_WIDTHS:
             macs += 3 * ph * pw * 9 * cin * cout
             cin = cout
-        c = ENC_CHANNELS[3 - level]
+        c = ENC_CHANNELS[levels - 1 - level]
         corr += 2.0 * ph * pw * (2 * max_disp + 1) ** 2 * c
     return (2 * macs + 3 * corr) / 1e9
 
 
-def cpu_baseline(pair_np, vals, steps=2, precision="fp32"):
+def cpu_baseline(pair_np, vals, steps=2, precision="fp32", levels=4):
     """Oracle train_step (torch CPU fp32, reference semantics) on one pair; returns
     (pairs/s, threads, flows_at_init, loss_at_init).  With precision "bf16" the reference
     outputs come from the oracle with the build's bf16 operand rounding; the timed steps are
@@ -123,7 +123,7 @@ def cpu_baseline(pair_np, vals, steps=2, precision="fp32"):
     from optical_flow_amd.params import encoder_blocks
     threads = torch.get_num_threads()
     p = {k: torch.tensor(v) for k, v in vals.items()}
-    blocks = list(encoder_blocks())
+    blocks = list(encoder_blocks(levels))
     x = torch.tensor(pair_np)
     R.set_conv_precision(precision)
     try:
@@ -153,6 +153,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--timing-steps", type=int, default=2)
+    ap.add_argument("--levels", type=int, choices=[4, 5], default=4,
+                    help="5: the reference's commented-out 5th pyramid level (model.py:24-25)")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="fp32: config 2 (headline); bf16: configs 3-5 conv contractions on "
                          "bf16 MFMA with fp32 accumulation")
@@ -170,8 +172,8 @@ def main():
     torch.cuda.set_device(local)
     _lib.load()
     H, W, B = args.height, args.width, args.batch
-    vals = init_params(flow_net_spec(), 0)                 # identical weights on every rank
-    net = FlowNet(H, W, values=vals, precision=args.precision)
+    vals = init_params(flow_net_spec(levels=args.levels), 0)   # identical weights on all ranks
+    net = FlowNet(H, W, values=vals, precision=args.precision, levels=args.levels)
     trainer = Trainer(net, KerasAdam(net.store), LossLayer())
     batch = torch.from_numpy(synthetic_batch(B, H, W, seed=1234, rank=rank)).cuda()
 
@@ -261,7 +263,7 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         pair = batch[:1].cpu().numpy()
         cps, threads, flows_ref, loss_ref = cpu_baseline(pair, vals, args.cpu_steps,
-                                                         args.precision)
+                                                         args.precision, args.levels)
         cpu = {"value": round(cps, 4), "unit": "image-pairs/s", "cores": threads,
                "kind": "port",
                "sample": "%d oracle train steps (torch-CPU fp32 restatement of the reference "
@@ -273,10 +275,10 @@ def main():
         parity = {"epe": [round(e, 6) for e in epe], "flow_rel_inf": [float("%.3e" % r) for r in rel],
                   "loss_rel": float("%.3e" % (abs(loss_hip - loss_ref) / abs(loss_ref))),
                   "note": "HIP %s vs CPU oracle (%s operand rounding), same pair and initial "
-                          "weights, flows [H/2, H/4, H/8, H/16]" % (args.precision,
-                                                                    args.precision)}
+                          "weights, flows [H/2 ... H/%d]" % (args.precision, args.precision,
+                                                             2 ** args.levels)}
 
-    gfp = gflop_per_pair(H, W)
+    gfp = gflop_per_pair(H, W, levels=args.levels)
     if rank == 0:
         out = {
             "metric": "image-pairs/sec training, %dx%d batch=%d per GPU" % (H, W, B),
@@ -294,7 +296,9 @@ def main():
             "config": {"workload": "full model.py encoder-decoder + loss.py photometric loss, "
                                    "train step (fwd+bwd+Keras Adam)",
                        "height": H, "width": W, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": "dp%d" % world, "params": 4938760},
+                       "parallelism": "dp%d" % world,
+                       "params": sum(p.numel() for p in net.trainable_weights),
+                       **({"levels": args.levels} if args.levels != 4 else {})},
             "algorithmic_gflop_per_pair": round(gfp, 2),
             "model_tflops": round(gfp * value / 1e3, 2),
             "conv_ms_per_step": round(conv_ms_step, 3),

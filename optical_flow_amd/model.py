@@ -113,12 +113,12 @@ class ParamStore:
                            if p.trainable)
 
 
-def backward_order(max_disp=3) -> List[str]:
+def backward_order(max_disp=3, levels=4) -> List[str]:
     """Arena order = gradient completion order of the backward pass."""
     names = []
-    for level in (3, 2, 1, 0):
-        names += [p.name for p in head_spec(level, max_disp) if p.trainable]
-    names += [p.name for p in reversed(encoder_spec()) if p.trainable]
+    for level in reversed(range(levels)):
+        names += [p.name for p in head_spec(level, max_disp, levels) if p.trainable]
+    names += [p.name for p in reversed(encoder_spec(levels)) if p.trainable]
     return names
 
 
@@ -131,9 +131,10 @@ class Encoder:
     max-pool; three resnet_layer_simple stages -> H/4 x64, H/8 x128, H/16 x256.
     The stage body is the assumed standard basic block (params.py)."""
 
-    def __init__(self, store: ParamStore, name="ResNet18"):
+    def __init__(self, store: ParamStore, name="ResNet18", levels=4):
         self.store = store
         self.name = name
+        self.levels = levels
         ver = lambda: store.version
         P = store.params
 
@@ -145,7 +146,7 @@ class Encoder:
                                    act=ACT_RELU, bn=bn("ResNet18/layer1_bn"), cin_p=4,
                                    version_of=ver, name="conv1")
         self.blocks = []
-        for prefix, cin, cout, stride, proj in encoder_blocks():
+        for prefix, cin, cout, stride, proj in encoder_blocks(levels):
             a = ops.ConvLayer(P[prefix + "/conv_a/kernel"], P[prefix + "/conv_a/bias"],
                               stride=stride, act=ACT_RELU, bn=bn(prefix + "/bn_a"),
                               version_of=ver, name=prefix + "/conv_a")
@@ -214,10 +215,10 @@ class FlowHead:
     """The six 3x3 convs a ``flow_module`` call creates (model.py:104-114): 128, 128, 96, 64,
     32 with LeakyReLU(0.3), then a linear 2-channel flow conv."""
 
-    def __init__(self, store: ParamStore, level: int, max_disp: int = 3):
+    def __init__(self, store: ParamStore, level: int, max_disp: int = 3, levels: int = 4):
         self.level = level
         self.max_disp = max_disp
-        self.cin = head_cin(level, max_disp)
+        self.cin = head_cin(level, max_disp, levels)
         self.cp = ops._c4(self.cin)
         P = store.params
         ver = lambda: store.version
@@ -267,13 +268,19 @@ class FlowNet:
     """The Keras ``Model`` returned by build_flow_net (model.py:119-143)."""
 
     def __init__(self, height, width, max_disp=3, seed=0, device="cuda", values=None,
-                 precision="fp32"):
-        assert height % 16 == 0 and width % 16 == 0, "H and W must be divisible by 16 (P17)"
+                 precision="fp32", levels=4):
+        """levels=5 enables the reference's commented-out 5th pyramid level (model.py:24-25,
+        138, 141): encoder stage 5 (512 channels at H/32) and flow4 at H/2."""
+        assert levels in (4, 5), levels
+        m = 2 ** levels
+        assert height % m == 0 and width % m == 0, \
+            "H and W must be divisible by %d with %d levels (P17)" % (m, levels)
         self.height, self.width, self.max_disp = height, width, max_disp
-        self.store = ParamStore(flow_net_spec(max_disp), values=values, device=device,
-                                order=backward_order(max_disp), seed=seed)
-        self.encoder = Encoder(self.store)
-        self.heads = [FlowHead(self.store, level, max_disp) for level in range(4)]
+        self.levels = levels
+        self.store = ParamStore(flow_net_spec(max_disp, levels), values=values, device=device,
+                                order=backward_order(max_disp, levels), seed=seed)
+        self.encoder = Encoder(self.store, levels=levels)
+        self.heads = [FlowHead(self.store, level, max_disp, levels) for level in range(levels)]
         self.name = "flow_net"
         self._packer = None
         self.set_precision(precision)
@@ -307,7 +314,8 @@ class FlowNet:
         return [n for n, p in self.store.spec.items() if p.trainable]
 
     def __call__(self, batch_imgs):
-        """(B, H, W, 6) -> [flow3 (H/2), flow2 (H/4), flow1 (H/8), flow0 (H/16)]."""
+        """(B, H, W, 6) -> [flow3 (H/2), flow2 (H/4), flow1 (H/8), flow0 (H/16)] (levels=4;
+        levels=5 prepends flow4 at H/2, so flow0 is at H/32)."""
         assert batch_imgs.shape[1] == self.height and batch_imgs.shape[2] == self.width
         assert batch_imgs.shape[3] == 6
         if self._packer is None:
@@ -317,8 +325,9 @@ class FlowNet:
         feats = self.encoder.forward4(imgs)          # shared encoder, both images (P12)
         flows = []
         prev = None
-        for level in range(4):
-            f1, f2 = ops.halves(feats[3 - level])
+        L = self.levels
+        for level in range(L):
+            f1, f2 = ops.halves(feats[L - 1 - level])
             prev = self.heads[level](f1, f2, prev)
             flows.append(prev)
         return flows[::-1]
@@ -345,15 +354,16 @@ class FlowNet:
 
 
 def build_flow_net(height, width, pretrained_weights_path=None, max_disp=3, seed=0,
-                   device="cuda", precision="fp32"):
+                   device="cuda", precision="fp32", levels=4):
     """model.py:119-143.  ``pretrained_weights_path``: an .npz of encoder weights named as in
     params.encoder_spec() (Keras-checkpoint import is out of scope, SURVEY.md §8 f); the
     reference asserts every encoder object is matched (model.py:129) -- so does this."""
-    net = FlowNet(height, width, max_disp, seed=seed, device=device, precision=precision)
+    net = FlowNet(height, width, max_disp, seed=seed, device=device, precision=precision,
+                  levels=levels)
     if pretrained_weights_path is not None:
         with np.load(pretrained_weights_path, allow_pickle=False) as z:
             vals = {k: z[k] for k in z.files}
-        enc_names = [p.name for p in encoder_spec()]
+        enc_names = [p.name for p in encoder_spec(levels)]
         missing = [n for n in enc_names if n not in vals]
         assert not missing, "pretrained encoder weights missing: %s" % missing[:5]
         net.store.load({n: vals[n] for n in enc_names}, strict=False)

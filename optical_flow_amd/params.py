@@ -26,8 +26,11 @@ from typing import List, Tuple
 import numpy as np
 
 HEAD_WIDTHS = (128, 128, 96, 64, 32, 2)          # model.py:104-114
-ENC_STAGES = ((2, False, 64), (3, True, 128), (4, True, 256))   # model.py:18-23
-ENC_CHANNELS = (64, 64, 128, 256)                # outputs at H/2, H/4, H/8, H/16
+# model.py:18-23; the 5th entry is the commented-out stage 5 (model.py:24-25), enabled by
+# levels=5 (SURVEY.md §8 f row 3: flow4 at H/2 and a 512-channel encoder output at H/32)
+ENC_STAGES = ((2, False, 64), (3, True, 128), (4, True, 256), (5, True, 512))
+ENC_CHANNELS = (64, 64, 128, 256, 512)           # outputs at H/2, H/4, H/8, H/16, H/32
+LEVELS = (4, 5)
 
 
 @dataclass(frozen=True)
@@ -56,10 +59,11 @@ def _bn(prefix, c):
             PSpec(prefix + "/moving_variance", (c,), "var")]
 
 
-def encoder_blocks():
+def encoder_blocks(levels: int = 4):
     """Yield (prefix, cin, cout, stride, has_proj) for every residual block, in order."""
+    assert levels in LEVELS, levels
     cin = 64
-    for idx, down, cout in ENC_STAGES:
+    for idx, down, cout in ENC_STAGES[:levels - 1]:
         for j in range(2):
             stride = 2 if (down and j == 0) else 1
             proj = (j == 0 and (down or cin != cout))
@@ -67,9 +71,9 @@ def encoder_blocks():
             cin = cout
 
 
-def encoder_spec() -> List[PSpec]:
+def encoder_spec(levels: int = 4) -> List[PSpec]:
     s = _conv("ResNet18/conv1", 7, 3, 64) + _bn("ResNet18/layer1_bn", 64)
-    for prefix, cin, cout, stride, proj in encoder_blocks():
+    for prefix, cin, cout, stride, proj in encoder_blocks(levels):
         s += _conv(prefix + "/conv_a", 3, cin, cout) + _bn(prefix + "/bn_a", cout)
         s += _conv(prefix + "/conv_b", 3, cout, cout) + _bn(prefix + "/bn_b", cout)
         if proj:
@@ -77,26 +81,26 @@ def encoder_spec() -> List[PSpec]:
     return s
 
 
-def head_cin(level: int, max_disp: int = 3) -> int:
-    """Input channels of the first head conv at pyramid level (0 = coarsest, H/16)."""
-    c = ENC_CHANNELS[3 - level]
+def head_cin(level: int, max_disp: int = 3, levels: int = 4) -> int:
+    """Input channels of the first head conv at pyramid level (0 = coarsest, H/2^levels)."""
+    c = ENC_CHANNELS[levels - 1 - level]
     ncv = (2 * max_disp + 1) ** 2
     return c + ncv + (2 if level > 0 else 0)      # model.py:100-102 (P9)
 
 
-def head_spec(level: int, max_disp: int = 3) -> List[PSpec]:
+def head_spec(level: int, max_disp: int = 3, levels: int = 4) -> List[PSpec]:
     s = []
-    cin = head_cin(level, max_disp)
+    cin = head_cin(level, max_disp, levels)
     for i, cout in enumerate(HEAD_WIDTHS):
         s += _conv("flow_module_%d/conv%d" % (level, i), 3, cin, cout)
         cin = cout
     return s
 
 
-def flow_net_spec(max_disp: int = 3) -> List[PSpec]:
-    s = encoder_spec()
-    for level in range(4):
-        s += head_spec(level, max_disp)
+def flow_net_spec(max_disp: int = 3, levels: int = 4) -> List[PSpec]:
+    s = encoder_spec(levels)
+    for level in range(levels):
+        s += head_spec(level, max_disp, levels)
     return s
 
 

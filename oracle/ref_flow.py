@@ -255,8 +255,9 @@ def flow_net(batch_imgs, p, blocks, max_disp=3):
     e2 = encoder(img2, p, blocks)
     flows = []
     prev = None
-    for level in range(4):
-        prev = flow_module(e1[3 - level], e2[3 - level], prev, max_disp, p,
+    n = len(e1)                  # 4, or 5 with the commented-out stage 5 (model.py:24-25,138)
+    for level in range(n):
+        prev = flow_module(e1[n - 1 - level], e2[n - 1 - level], prev, max_disp, p,
                            "flow_module_%d" % level)
         flows.append(prev)
     return flows[::-1]

@@ -112,3 +112,30 @@ def test_flow_net_bf16():
     print("bf16 median grad rel_l2 %.2e" % errs[len(errs) // 2][0])
     assert errs[len(errs) // 2][0] < BF16_GRAD_MEDIAN
     assert errs[0][0] < BF16_GRAD_WORST, errs[0]
+
+
+def test_flow_net_5_levels():
+    """levels=5: the reference's commented-out stage 5 + flow4 (model.py:24-25,138,141)."""
+    from optical_flow_amd.data import synthetic_batch
+    from optical_flow_amd.loss import LossLayer
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params, perturb_params
+    H, W, B = 64, 128, 2
+    vals = perturb_params(init_params(flow_net_spec(levels=5), 3), 4)
+    net = FlowNet(H, W, values=vals, levels=5)
+    batch = synthetic_batch(B, H, W, seed=77)
+    p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+    loss_o, flows_o, grads_o = R.train_step(torch.tensor(batch, dtype=torch.float64), p,
+                                            list(encoder_blocks(5)), None)
+    net.store.zero_grad()
+    bd = dev(torch.from_numpy(batch))
+    flows = net(bd)
+    loss = LossLayer()(bd, flows)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert len(flows) == 5 and flows[-1].shape == (B, H // 32, W // 32, 2)
+    for k in range(5):
+        assert rel_inf(flows[k], flows_o[k]) < REL_TOL
+    assert abs(loss.item() - loss_o.item()) / abs(loss_o.item()) < REL_TOL
+    worst = max(rel_l2(g, grads_o[n]) for n, g in net.store.grads().items())
+    assert worst < REL_TOL, worst

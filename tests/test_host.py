@@ -60,3 +60,15 @@ def test_synthetic_value_contract():
     assert b.min() > -IMAGE_MEANS.max() - 0.1 and b.max() < 1.0 - IMAGE_MEANS.min() + 0.1
     assert np.array_equal(b, synthetic_batch(2, 32, 48, seed=3))
     assert not np.array_equal(b, synthetic_batch(2, 32, 48, seed=3, rank=1))
+
+
+def test_five_level_spec():
+    """levels=5 adds encoder stage 5 (512 ch, H/32) and a fifth flow head (model.py:24-25)."""
+    from optical_flow_amd import params as P
+    assert P.head_cin(0, levels=5) == 512 + 49
+    assert P.head_cin(1, levels=5) == 256 + 49 + 2 and P.head_cin(4, levels=5) == 64 + 49 + 2
+    blocks = list(P.encoder_blocks(5))
+    assert len(blocks) == 8 and blocks[-2][2] == 512 and blocks[-2][3] == 2 and blocks[-2][4]
+    names = {p.name for p in P.flow_net_spec(levels=5)}
+    assert "flow_module_4/conv5/kernel" in names and "ResNet18/res5_1/conv_b/kernel" in names
+    assert "flow_module_4/conv0/kernel" not in {p.name for p in P.flow_net_spec()}
