@@ -10,6 +10,7 @@ The 1/world average is folded into the Adam launch (grad_scale).
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Dict, List, Optional
 
 import torch
@@ -57,11 +58,17 @@ class GradBucketReducer:
         if self._pending[bi] == 0:
             self._launch(bi)
 
-    def _launch(self, bi):
+    def _launch(self, bi, in_backward=True):
         lo, hi = self.ranges[bi]
         view = self.store.grad_arena[lo:hi]
-        self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
-                                           async_op=True))
+        # A bucket's gradients are written on the current stream (BN / bias reductions) and on
+        # the wgrad side stream (ops.side_stream): during the backward the all-reduce is
+        # enqueued on the side stream once it has waited for the current one, so RCCL is
+        # ordered after both without stalling the input-gradient chain.
+        side = in_backward and view.is_cuda and ops.SIDE_STREAM_WGRAD
+        with torch.cuda.stream(ops.side_stream()) if side else contextlib.nullcontext():
+            self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
         self._launched[bi] = True
 
     def begin(self):
@@ -78,7 +85,7 @@ class GradBucketReducer:
         if self.world > 1:
             for bi in range(len(self.buckets)):
                 if not self._launched[bi]:
-                    self._launch(bi)
+                    self._launch(bi, in_backward=False)
             for w in self._works:
                 w.wait()
         self._works = []

@@ -219,7 +219,10 @@ class FlowHead:
         self.level = level
         self.max_disp = max_disp
         self.cin = head_cin(level, max_disp, levels)
-        self.cp = ops._c4(self.cin)
+        # Concat row padded to a multiple of 8 channels: 115 -> 120, not 116.  A 116-float
+        # (464-byte) row runs the level-3/2 c0 convs 12-15 % slower than a 120-float one in
+        # both precisions (profiles/r1_conv_bench*.txt); the zero channels cost 3.5 % MACs.
+        self.cp = (self.cin + 7) // 8 * 8
         P = store.params
         ver = lambda: store.version
         self.convs = []

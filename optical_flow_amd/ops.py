@@ -5,6 +5,7 @@ Tensors are NHWC float32 on the GPU.  Each Function cites the reference op it re
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from typing import Optional
 
@@ -81,6 +82,45 @@ def _grad_ready(*params):
         for p in params:
             if p is not None:
                 _GRAD_READY_HOOK(p)
+
+
+# ------------------------------------------------------- weight-gradient side stream ----
+# The weight gradient of a conv is off the backward's critical path (nothing downstream reads
+# it until the optimizer / all-reduce), so wgrad launches whose target is the gradient arena
+# run on a second HIP stream, ordered after the kernel that produced their dy.  Small-grid
+# layers (coarse flow levels, encoder stages 3-4) and the tail waves of large ones then share
+# the chip with the input-gradient chain.  The current stream joins the side stream at the
+# end of the autograd backward (engine callback), so .backward() returning still means every
+# gradient kernel is ordered before whatever the caller enqueues next.
+SIDE_STREAM_WGRAD = True
+_SIDE = {}
+_side_armed = False
+
+
+def _side_join():
+    global _side_armed
+    _side_armed = False
+    for dev, s in _SIDE.items():
+        torch.cuda.current_stream(dev).wait_stream(s)
+
+
+def side_stream(*tensors):
+    """The wgrad side stream of the current device, ordered after all work enqueued so far on
+    the current stream; ``tensors`` (read by the side stream's kernels) are marked in use by
+    it for the caching allocator."""
+    global _side_armed
+    cur = torch.cuda.current_stream()
+    s = _SIDE.get(cur.device)
+    if s is None:
+        s = _SIDE[cur.device] = torch.cuda.Stream(cur.device)
+    s.wait_stream(cur)
+    for t in tensors:
+        if t is not None:
+            t.record_stream(s)
+    if not _side_armed:
+        _side_armed = True
+        torch.autograd.Variable._execution_engine.queue_callback(_side_join)
+    return s
 
 
 def grad_target(param: torch.Tensor):
@@ -313,21 +353,24 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
         tk = grad_target(layer.kernel)
         tbias = grad_target(layer.bias) if (need_b and not bias_done) else (None, 0, None)
         went, wsb = layer.wgrad_entry(d)
-        ws = torch.empty(wsb // 4 + 1, device=dy.device)
-        if tbias[0] is not None and tbias[1] != tk[1]:
-            # mixed arena / fresh targets: compute the bias into a temp, then place it
-            tmpb = torch.empty_like(layer.bias)
-            _tag(layer, 2)
-            call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
-                 _ptr(tk[0]), _ptr(tmpb), tk[1], _ptr(ws), wsb, s)
-            if tbias[1]:
-                call("of_add_inplace", _ptr(tbias[0]), _ptr(tmpb), tmpb.numel(), s)
+        side = SIDE_STREAM_WGRAD and tk[1] == 1 and (tbias[0] is None or tbias[1] == 1)
+        with torch.cuda.stream(side_stream(x, dzp)) if side else contextlib.nullcontext():
+            ss = _stream()
+            ws = torch.empty(wsb // 4 + 1, device=dy.device)
+            if tbias[0] is not None and tbias[1] != tk[1]:
+                # mixed arena / fresh targets: compute the bias into a temp, then place it
+                tmpb = torch.empty_like(layer.bias)
+                _tag(layer, 2)
+                call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
+                     _ptr(tk[0]), _ptr(tmpb), tk[1], _ptr(ws), wsb, ss)
+                if tbias[1]:
+                    call("of_add_inplace", _ptr(tbias[0]), _ptr(tmpb), tmpb.numel(), ss)
+                else:
+                    tbias = (tmpb, 0, tmpb)
             else:
-                tbias = (tmpb, 0, tmpb)
-        else:
-            _tag(layer, 2)
-            call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
-                 _ptr(tk[0]), _ptr(tbias[0]), tk[1], _ptr(ws), wsb, s)
+                _tag(layer, 2)
+                call(went, C.byref(d), _ptr(x), cx, _ptr(dzp), dzp.shape[-1],
+                     _ptr(tk[0]), _ptr(tbias[0]), tk[1], _ptr(ws), wsb, ss)
         ret_k = tk[2] if need_k else None
         if need_b and not bias_done:
             ret_b = tbias[2]
@@ -485,10 +528,12 @@ class _ConvStackFn(torch.autograd.Function):
             if tk[1] != tb[1]:
                 raise RuntimeError("kernel and bias gradients must both use the arena or not")
             went, wsb = layer.wgrad_entry(d)
-            ws = torch.empty(wsb // 4 + 1, device=x.device)
-            _tag(layer, 2)
-            call(went, C.byref(d), _ptr(x), cx, _ptr(g), g.shape[-1], _ptr(tk[0]),
-                 _ptr(tb[0]), tk[1], _ptr(ws), wsb, s)
+            side = SIDE_STREAM_WGRAD and tk[1] == 1
+            with torch.cuda.stream(side_stream(x, g)) if side else contextlib.nullcontext():
+                ws = torch.empty(wsb // 4 + 1, device=x.device)
+                _tag(layer, 2)
+                call(went, C.byref(d), _ptr(x), cx, _ptr(g), g.shape[-1], _ptr(tk[0]),
+                     _ptr(tb[0]), tk[1], _ptr(ws), wsb, _stream())
             layer._ret = (tk[2], tb[2])
             _grad_ready(layer.kernel, layer.bias)
             if i > 0:

@@ -97,14 +97,22 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--tune", default=None, help="key=value[,key=value] of_set_tuning")
     ap.add_argument("--bf16", action="store_true", help="bf16 MFMA fwd/dgrad/wgrad")
+    ap.add_argument("--shapes", default=None,
+                    help="extra shapes 'name:n,h,w,cin,cout,k,s;...' benched instead of SHAPES")
     args = ap.parse_args()
+    shapes = SHAPES
+    if args.shapes:
+        shapes = []
+        for item in args.shapes.split(";"):
+            nm, dims = item.split(":")
+            shapes.append((nm, *[int(v) for v in dims.split(",")]))
     _lib.load()
     if args.tune:
         for kv in args.tune.split(","):
             k, v = kv.split("=")
             _lib.lib().of_set_tuning(int(k), int(v))
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
-    for sh in SHAPES:
+    for sh in shapes:
         if args.only and args.only not in sh[0]:
             continue
         flops, out = bench_one(*sh, args.reps, "bf16" if args.bf16 else "fp32")
