@@ -158,12 +158,17 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
                     help="fp32: config 2 (headline); bf16: configs 3-5 conv contractions on "
                          "bf16 MFMA with fp32 accumulation")
+    ap.add_argument("--tune", default=None, help="key=value[,...] of_set_tuning (experiments)")
     ap.add_argument("--side-stream", type=int, choices=[0, 1], default=1,
                     help="1: weight-gradient kernels on a second HIP stream (ops.side_stream)")
     args = ap.parse_args()
 
     from optical_flow_amd import _lib, ops
     ops.SIDE_STREAM_WGRAD = bool(args.side_stream)
+    if args.tune:
+        for kv in args.tune.split(","):
+            k, v = kv.split("=")
+            _lib.lib().of_set_tuning(int(k), int(v))
     from optical_flow_amd.data import synthetic_batch
     from optical_flow_amd.dist import init_from_env
     from optical_flow_amd.loss import LossLayer

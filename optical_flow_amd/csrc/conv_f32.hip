@@ -1926,14 +1926,17 @@ void single_group(GemmArgs& a, const of_conv_desc* d, int M, int K) {
   a.tiles_total = g.m_tiles * a.n_tiles;
 }
 
-// fwd/dgrad split-K: split when the tile grid cannot fill the chip.
+// fwd/dgrad split-K: split when the tile grid cannot fill the chip.  Target: g_split_wgs
+// workgroups per CU (of_set_tuning key 1), slices of at least g_split_min_chunks chunks (key 2).
+static int g_split_wgs = 4;
+static int g_split_min_chunks = 12;
 void plan_splits(GemmArgs& a, int kmax, int bk = BK) {
   a.splits = 1;
   a.k_per_split = (int)round_up(kmax, bk);
   if (a.tiles_total >= 2 * kCUs) return;
   const int nchunks = (int)cdiv(kmax, bk);
-  int s = std::max(1, (4 * kCUs) / a.tiles_total);
-  s = std::min(s, std::max(1, nchunks / (bk == BK ? 12 : 6)));
+  int s = std::max(1, (g_split_wgs * kCUs) / a.tiles_total);
+  s = std::min(s, std::max(1, nchunks / (bk == BK ? g_split_min_chunks : g_split_min_chunks / 2)));
   if (s <= 1) return;
   a.k_per_split = (int)round_up(cdiv(kmax, s), bk);
   a.splits = (int)cdiv(kmax, a.k_per_split);
@@ -2263,8 +2266,9 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
 }
 
 int of_set_tuning(int key, int value) {
-  (void)value;
-  return fail(OF_EINVAL, "of_set_tuning: unknown key " + std::to_string(key));
+  if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }
+  if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
+  return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
 size_t of_conv_pack_table_bytes(int nconv) {
