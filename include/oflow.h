@@ -261,9 +261,67 @@ int of_fill(float* y, float v, int64_t n, void* stream);
  * launch records a hipEvent pair on its stream; of_timing_read() returns the count and fills
  * kinds (0 fwd, 1 dgrad, 2 wgrad), flops and elapsed ms (synchronises the events). */
 int of_timing_enable(int on);
-/* Kernel-variant switches for A/B measurements (no keys defined in this build). */
+/* Kernel-variant switches for A/B measurements: key 1 = fwd/dgrad split-K target workgroups
+ * per CU (1-16, default 4), key 2 = minimum 16-deep K chunks per split slice (2-64, default 12). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
+
+/* ==== SURVEY.md §8 f row 1: the KITTI data path (data_reader.py) ========================== */
+
+/* One decoded frame inside a raw batch buffer: 8-bit BGR, h x w x 3, at byte `offset` from the
+ * start of the buffer.  A raw batch = of_image_desc[2*batch] (frame 2i = image1 of pair i,
+ * 2i+1 = image2, swaps already applied) padded to 256 bytes, then the frames. */
+typedef struct of_image_desc {
+  int64_t offset;
+  int32_t h, w;
+} of_image_desc;
+
+/* PNG header: size, channels and bit depth (no pixel decode). */
+int of_png_info(const char* path, int* h, int* w, int* channels, int* depth);
+/* cv2.imread(path) (data_reader.py:53-54; IMREAD_COLOR): 8-bit BGR h x w x 3 into out
+ * (cap bytes).  Gray is replicated, palettes expanded, alpha dropped, 16-bit -> high byte. */
+int of_png_read_bgr(const char* path, uint8_t* out, int64_t cap, int* h, int* w);
+/* Write an 8-bit image (c = 1 gray, 3 BGR, 4 BGRA) as PNG.  flags = filter | (level+1) << 8:
+ * filter 0-4 fixed, 5 adaptive, 6 cycle by row; level bits 0 -> zlib level 6. */
+int of_png_write(const char* path, const uint8_t* img, int h, int w, int c, int flags);
+/* Largest height / width over n PNG headers, read by nthreads threads. */
+int of_png_scan(int n, const char* const* paths, int nthreads, int* max_h, int* max_w);
+
+/* AsyncReader (data_reader.py:81-124): nworkers decode threads fill nslots batch slots of raw
+ * frames (each frame <= max_h x max_w) in shuffled order with a p=0.5 pair swap, seeded;
+ * nbatches = npairs / batch (remainder dropped), reshuffled at each epoch wrap.  pinned != 0
+ * allocates the slots with hipHostMalloc (needed by of_reader_next). */
+typedef struct of_reader of_reader;
+int of_reader_create(int npairs, const char* const* path1, const char* const* path2, int batch,
+                     int nworkers, int nslots, int max_h, int max_w, uint64_t seed, int pinned,
+                     of_reader** out);
+int64_t of_reader_raw_bytes(const of_reader* r);
+int of_reader_nbatches(const of_reader* r);
+/* get_batch() (data_reader.py:121-124): waits for the next batch in order, copies its raw
+ * frames into dev_raw (cap >= of_reader_raw_bytes) on `stream`, then runs
+ * of_preprocess_pairs into out (batch, out_h, out_w, 6) on the same stream.  pair_index /
+ * swapped (may be NULL) receive the batch's pair ids and swap flags.  The slot is refilled
+ * with the next batch once that copy has completed. */
+int of_reader_next(of_reader* r, void* dev_raw, int64_t cap, float* out, int out_h, int out_w,
+                   int32_t* pair_index, int32_t* swapped, void* stream);
+/* The same hand-out without a GPU: the raw batch is copied to host memory dst. */
+int of_reader_next_host(of_reader* r, void* dst, int64_t cap, int32_t* pair_index,
+                        int32_t* swapped);
+int of_reader_destroy(of_reader* r);
+
+/* read_item's cv2.resize(img, (out_w, out_h)) (INTER_LINEAR, 8-bit fixed point) + /255 - mean
+ * (data_reader.py:56-63) + packing into (npairs, out_h, out_w, 6) float32 (:36-41), from a
+ * raw batch already in device memory. */
+int of_preprocess_pairs(const void* dev_raw, int npairs, int out_h, int out_w, float* out,
+                        void* stream);
+
+/* ==== SURVEY.md §8 f row 4: flow pictures (drawing.py) ==================================== */
+
+/* draw_optical_flow_color (drawing.py:45-53) for n flows (n, h, w, 2) -> (n, h, w, 3) BGR
+ * bytes; ws: 2*n floats of workspace (per-image magnitude min/max). */
+int of_flow_color(const float* flow, int n, int h, int w, uint8_t* bgr, float* ws, void* stream);
+/* draw_optical_flow_intensity (drawing.py:37-42): min(sqrt(u^2 + u^2) / 20, 1) per pixel. */
+int of_flow_intensity(const float* flow, int64_t npix, float* out, void* stream);
 
 #ifdef __cplusplus
 }

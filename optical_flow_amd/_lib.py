@@ -93,6 +93,21 @@ PROTOTYPES = {
     "of_timing_enable": (I, [I]),
     "of_set_tuning": (I, [I, I]),
     "of_timing_read": (I, [I, C.POINTER(I), C.POINTER(C.c_double), C.POINTER(F)]),
+    # data path (SURVEY §8 f row 1) and flow pictures (row 4)
+    "of_png_info": (I, [C.c_char_p, C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "of_png_read_bgr": (I, [C.c_char_p, P, I64, C.POINTER(I), C.POINTER(I)]),
+    "of_png_write": (I, [C.c_char_p, P, I, I, I, I]),
+    "of_png_scan": (I, [I, C.POINTER(C.c_char_p), I, C.POINTER(I), C.POINTER(I)]),
+    "of_reader_create": (I, [I, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), I, I, I, I, I,
+                             C.c_uint64, I, C.POINTER(P)]),
+    "of_reader_raw_bytes": (I64, [P]),
+    "of_reader_nbatches": (I, [P]),
+    "of_reader_next": (I, [P, P, I64, P, I, I, C.POINTER(C.c_int32), C.POINTER(C.c_int32), P]),
+    "of_reader_next_host": (I, [P, P, I64, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "of_reader_destroy": (I, [P]),
+    "of_preprocess_pairs": (I, [P, I, I, I, P, P]),
+    "of_flow_color": (I, [P, I, I, I, P, P, P]),
+    "of_flow_intensity": (I, [P, I64, P, P]),
 }
 
 

@@ -1,0 +1,246 @@
+"""KITTI data path (SURVEY.md §8 f row 1): the reference ``data_reader.py`` with the same names
+and argument meaning, on the native reader (``reader.cpp``: PNG decode threads, pinned batch
+slots) and the HIP preprocess kernel (``image_ops.hip``: cv2-style resize + normalise + pair
+packing in HBM).
+
+Differences from the reference, by design:
+  - ``get_batch()`` returns the ``(B, H, W, 6)`` float32 batch already on the GPU (the
+    reference returns numpy and ``train.py:75`` converts it); the host->device copy moves the
+    8-bit frames at their native size, on a side HIP stream.
+  - Batches come out in submission order and the shuffle / pair swaps are seeded
+    (``ReaderOpts.seed``), so a run is reproducible; the reference's Pool queue delivers in
+    completion order with unseeded ``random`` / ``np.random``.
+  - Worker threads in one process instead of a ``multiprocessing.Pool`` (no cv2 fork issue to
+    work around: ``data_reader.py:104-106``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call
+
+image_means = (np.array([123.0, 117.0, 104.0]) / 255.0).reshape(1, 1, 3)   # data_reader.py:7-9
+
+
+def read_kitti(kitti_path: str) -> List[List[str]]:
+    """data_reader.py:12-32: per day / drive, temporal pairs (image_02 frame i, i+1) then
+    stereo pairs (image_02 / image_03 frame i).  Days and drives in os.listdir order, frames
+    sorted; entries of a day ending in '.txt' (the calibration files) are skipped."""
+    path_pairs = []
+    for day in os.listdir(os.path.join(kitti_path)):
+        for drive in os.listdir(os.path.join(kitti_path, day)):
+            if drive[-4:] == '.txt':
+                continue
+            images_dir_l = os.path.join(kitti_path, day, drive, 'image_02', 'data')
+            images_dir_r = os.path.join(kitti_path, day, drive, 'image_03', 'data')
+            assert os.path.isdir(images_dir_l)
+            assert os.path.isdir(images_dir_r)
+            frames = os.listdir(images_dir_l)
+            frames.sort()
+            for i in range(len(frames) - 1):
+                path_pairs.append([os.path.join(images_dir_l, frames[i]),
+                                   os.path.join(images_dir_l, frames[i + 1])])
+            for i in range(len(frames)):
+                assert os.path.isfile(os.path.join(images_dir_r, frames[i]))
+                path_pairs.append([os.path.join(images_dir_l, frames[i]),
+                                   os.path.join(images_dir_r, frames[i])])
+    print('Total number of KITTI pairs: ' + str(len(path_pairs)))
+    return path_pairs
+
+
+class ReaderOpts:
+    """data_reader.py:72-78, plus the build's knobs: seed (shuffle + swaps), nslots (batches
+    decoded ahead), pairs (an explicit pair list instead of scanning kitti_path), max_h /
+    max_w (frame size bound; scanned from the PNG headers when None)."""
+
+    def __init__(self, kitti_path, batch_size, img_height, img_width, nworkers, seed=0,
+                 nslots=3, pairs=None, max_h=None, max_w=None):
+        self.kitti_path = kitti_path
+        self.batch_size = batch_size
+        self.img_height = img_height
+        self.img_width = img_width
+        self.nworkers = nworkers
+        self.seed = seed
+        self.nslots = nslots
+        self.pairs = pairs
+        self.max_h = max_h
+        self.max_w = max_w
+
+
+def _cstrings(paths: Sequence[str]):
+    arr = (C.c_char_p * len(paths))()
+    arr[:] = [os.fsencode(p) for p in paths]
+    return arr
+
+
+def png_size(path: str):
+    """(h, w) from the PNG header."""
+    h, w = C.c_int(), C.c_int()
+    call("of_png_info", os.fsencode(path), C.byref(h), C.byref(w), None, None)
+    return h.value, w.value
+
+
+def imread_bgr(path: str) -> np.ndarray:
+    """cv2.imread(path) (IMREAD_COLOR) on the native PNG decoder: (h, w, 3) uint8 BGR."""
+    h, w = png_size(path)
+    out = np.empty((h, w, 3), np.uint8)
+    hh, ww = C.c_int(), C.c_int()
+    call("of_png_read_bgr", os.fsencode(path), out.ctypes.data_as(C.c_void_p), out.nbytes,
+         C.byref(hh), C.byref(ww))
+    return out
+
+
+def imwrite(path: str, img: np.ndarray, filt: int = 5, level: int = 6):
+    """Write an 8-bit gray / BGR / BGRA image as PNG (cv2.imwrite's channel convention)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    c = 1 if img.ndim == 2 else img.shape[2]
+    call("of_png_write", os.fsencode(path), img.ctypes.data_as(C.c_void_p), img.shape[0],
+         img.shape[1], c, filt | ((level + 1) << 8))
+
+
+def split_raw(raw: np.ndarray, batch: int):
+    """Decode a raw batch buffer (of_image_desc header + frames) into [(img1, img2), ...]."""
+    desc = raw[:16 * 2 * batch].view(np.int64).reshape(2 * batch, 2)
+    frames = []
+    for k in range(2 * batch):
+        off = int(desc[k, 0])
+        hw = desc[k, 1:2].view(np.int32)
+        h, w = int(hw[0]), int(hw[1])
+        frames.append(raw[off:off + h * w * 3].reshape(h, w, 3))
+    return [(frames[2 * i], frames[2 * i + 1]) for i in range(batch)]
+
+
+class AsyncReader:
+    """data_reader.py:81-124.  ``get_batch()`` -> (B, H, W, 6) float32 CUDA tensor, ordered on
+    the current stream; ``next_raw()`` is the GPU-free hand-out (raw frames, pair ids, swap
+    flags) used by the CPU tests and by ``pinned=False`` readers."""
+
+    def __init__(self, opts: ReaderOpts, pinned: Optional[bool] = None):
+        self.opts = opts
+        self.data_info = opts.pairs if opts.pairs is not None else read_kitti(opts.kitti_path)
+        self.nbatches = len(self.data_info) // opts.batch_size
+        assert self.nbatches > 0, "fewer pairs than one batch"
+        if pinned is None:
+            pinned = torch.cuda.is_available()
+        self.pinned = bool(pinned)
+        p1 = _cstrings([p[0] for p in self.data_info])
+        p2 = _cstrings([p[1] for p in self.data_info])
+        max_h, max_w = opts.max_h, opts.max_w
+        if max_h is None or max_w is None:
+            mh, mw = C.c_int(), C.c_int()
+            both = _cstrings([p for pair in self.data_info for p in pair])
+            call("of_png_scan", len(both), both, max(1, opts.nworkers), C.byref(mh), C.byref(mw))
+            max_h, max_w = mh.value, mw.value
+        self.max_h, self.max_w = max_h, max_w
+        r = C.c_void_p()
+        call("of_reader_create", len(self.data_info), p1, p2, opts.batch_size, opts.nworkers,
+             opts.nslots, max_h, max_w, C.c_uint64(opts.seed), int(self.pinned), C.byref(r))
+        self._r = r
+        self.raw_bytes = _lib.lib().of_reader_raw_bytes(r)
+        self._raw_dev = None
+        self._copy_stream = None
+        self.last_pairs = np.zeros(opts.batch_size, np.int32)
+        self.last_swapped = np.zeros(opts.batch_size, np.int32)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc_val, exc_tb):
+        self.close()
+
+    def close(self):
+        if self._r is not None:
+            torch.cuda.synchronize() if (self.pinned and torch.cuda.is_available()) else None
+            call("of_reader_destroy", self._r)
+            self._r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _meta(self):
+        i32 = C.POINTER(C.c_int32)
+        return self.last_pairs.ctypes.data_as(i32), self.last_swapped.ctypes.data_as(i32)
+
+    def next_raw(self) -> np.ndarray:
+        raw = np.empty(self.raw_bytes, np.uint8)
+        call("of_reader_next_host", self._r, raw.ctypes.data_as(C.c_void_p), raw.nbytes,
+             *self._meta())
+        return raw
+
+    def get_batch(self) -> torch.Tensor:
+        assert self.pinned, "get_batch needs a reader with pinned slots (GPU present)"
+        o = self.opts
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream()
+            self._raw_dev = torch.empty(self.raw_bytes, dtype=torch.uint8, device="cuda")
+        compute = torch.cuda.current_stream()
+        cs = self._copy_stream
+        # the raw buffer is reused: order this copy after the previous preprocess (same
+        # stream) -- and after the compute stream's use of nothing else (raw is private)
+        with torch.cuda.stream(cs):
+            out = torch.empty((o.batch_size, o.img_height, o.img_width, 6), device="cuda")
+            call("of_reader_next", self._r, C.c_void_p(self._raw_dev.data_ptr()), self.raw_bytes,
+                 C.c_void_p(out.data_ptr()), o.img_height, o.img_width, *self._meta(),
+                 C.c_void_p(cs.cuda_stream))
+        compute.wait_stream(cs)
+        out.record_stream(compute)
+        return out
+
+
+def preprocess_frames(frames, out_h: int, out_w: int) -> torch.Tensor:
+    """read_batch (data_reader.py:35-42) for frames already decoded to host memory:
+    [(img1_bgr_u8, img2_bgr_u8), ...] -> (B, out_h, out_w, 6) CUDA tensor (one upload of the
+    raw frames, then of_preprocess_pairs)."""
+    n = len(frames)
+    header = -(-16 * 2 * n // 256) * 256
+    offs, sizes, total = [], [], header
+    for pair in frames:
+        for img in pair:
+            assert img.dtype == np.uint8 and img.ndim == 3 and img.shape[2] == 3
+            offs.append(total)
+            sizes.append(img.shape[:2])
+            total += -(-img.nbytes // 256) * 256
+    raw = np.zeros(total, np.uint8)
+    desc = raw[:16 * 2 * n].view(np.int64).reshape(2 * n, 2)
+    for k, ((h, w), off) in enumerate(zip(sizes, offs)):
+        desc[k, 0] = off
+        desc[k, 1:2].view(np.int32)[:] = (h, w)
+        img = frames[k // 2][k % 2]
+        raw[off:off + img.nbytes] = np.ascontiguousarray(img).reshape(-1)
+    dev = torch.from_numpy(raw).cuda()
+    out = torch.empty((n, out_h, out_w, 6), device="cuda")
+    call("of_preprocess_pairs", C.c_void_p(dev.data_ptr()), n, out_h, out_w,
+         C.c_void_p(out.data_ptr()), C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    return out
+
+
+def read_item(item_info, opts: ReaderOpts, swap: Optional[bool] = None):
+    """data_reader.py:45-64 for one pair: (image1, image2), each (H, W, 3) float32 on the GPU.
+    swap=None draws the p=0.5 order swap like the reference."""
+    if swap is None:
+        swap = bool(np.random.rand() >= 0.5)
+    path1, path2 = (item_info[1], item_info[0]) if swap else (item_info[0], item_info[1])
+    batch = preprocess_frames([(imread_bgr(path1), imread_bgr(path2))], opts.img_height,
+                              opts.img_width)
+    return batch[0, :, :, :3], batch[0, :, :, 3:]
+
+
+def read_batch(batch_info, opts: ReaderOpts, swaps: Optional[Sequence[bool]] = None):
+    """data_reader.py:35-42 synchronously: (B, H, W, 6) float32 on the GPU."""
+    frames = []
+    for i, item in enumerate(batch_info):
+        sw = bool(np.random.rand() >= 0.5) if swaps is None else bool(swaps[i])
+        a, b = (item[1], item[0]) if sw else (item[0], item[1])
+        frames.append((imread_bgr(a), imread_bgr(b)))
+    out = torch.zeros((opts.batch_size, opts.img_height, opts.img_width, 6), device="cuda")
+    out[:len(frames)] = preprocess_frames(frames, opts.img_height, opts.img_width)
+    return out
