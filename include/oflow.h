@@ -315,6 +315,12 @@ int of_reader_destroy(of_reader* r);
 int of_preprocess_pairs(const void* dev_raw, int npairs, int out_h, int out_w, float* out,
                         void* stream);
 
+/* ==== SURVEY.md §8 f row 2: TensorFlow checkpoint bundles (save_weights / load_weights) ===== */
+
+/* CRC32C (Castagnoli) of n bytes, continuing from crc (0 to start; unmasked).  The bundle's
+ * table blocks and tensor entries carry masked CRC32C values (optical_flow_amd/checkpoint.py). */
+uint32_t of_crc32c(const void* data, int64_t n, uint32_t crc);
+
 /* ==== SURVEY.md §8 f row 4: flow pictures (drawing.py) ==================================== */
 
 /* draw_optical_flow_color (drawing.py:45-53) for n flows (n, h, w, 2) -> (n, h, w, 3) BGR

@@ -108,6 +108,7 @@ PROTOTYPES = {
     "of_preprocess_pairs": (I, [P, I, I, I, P, P]),
     "of_flow_color": (I, [P, I, I, I, P, P, P]),
     "of_flow_intensity": (I, [P, I64, P, P]),
+    "of_crc32c": (C.c_uint32, [P, I64, C.c_uint32]),   # checkpoint bundles (row 2)
 }
 
 

@@ -355,3 +355,41 @@ int of_png_write(const char* path, const uint8_t* img, int h, int w, int c, int 
 }
 
 }  // extern "C"
+
+// ---- CRC32C (Castagnoli), for the TensorFlow checkpoint bundle (SURVEY.md §8 f row 2) ----
+// Slicing-by-8 over the reflected polynomial 0x82F63B78; `crc` is the running (unmasked)
+// value, 0 to start.
+namespace {
+struct Crc32cTables {
+  uint32_t t[8][256];
+  Crc32cTables() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xff];
+  }
+};
+const Crc32cTables& crc_tables() {
+  static const Crc32cTables tabs;
+  return tabs;
+}
+}  // namespace
+
+extern "C" uint32_t of_crc32c(const void* data, int64_t n, uint32_t crc) {
+  const auto& T = crc_tables().t;
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  uint32_t c = ~crc;
+  for (; n >= 8; n -= 8, p += 8) {
+    uint32_t lo, hi;
+    memcpy(&lo, p, 4);
+    memcpy(&hi, p + 4, 4);
+    lo ^= c;
+    c = T[7][lo & 0xff] ^ T[6][(lo >> 8) & 0xff] ^ T[5][(lo >> 16) & 0xff] ^ T[4][lo >> 24] ^
+        T[3][hi & 0xff] ^ T[2][(hi >> 8) & 0xff] ^ T[1][(hi >> 16) & 0xff] ^ T[0][hi >> 24];
+  }
+  for (; n > 0; --n, ++p) c = (c >> 8) ^ T[0][(c ^ *p) & 0xff];
+  return ~c;
+}

@@ -344,13 +344,33 @@ class FlowNet:
             print_fn("  %-44s %-18s %s" % (n, str(p.shape), "" if p.trainable else "(non-trainable)"))
         print_fn("Trainable params: %d" % total)
 
-    def save_weights(self, path):
+    def save_weights(self, path, save_format=None):
+        """Keras Model.save_weights (train.py:88): a path without an .h5 / .npz suffix
+        writes a TensorFlow checkpoint (prefix.index + prefix.data-00000-of-00001 + the
+        directory's 'checkpoint' file) with Keras object-based keys (checkpoint.py, SURVEY.md
+        §8 f row 2); '.npz' writes a numpy archive of the parameter names."""
+        fmt = save_format or ("npz" if path.endswith(".npz") else
+                              "h5" if path.endswith((".h5", ".keras")) else "tf")
+        if fmt == "h5":
+            raise NotImplementedError("HDF5 weights need h5py, which is not installed; use the "
+                                      "TensorFlow checkpoint format (no suffix)")
         d = os.path.dirname(path)
         if d:
             os.makedirs(d, exist_ok=True)
-        np.savez(path if path.endswith(".npz") else path + ".npz", **self.store.state())
+        if fmt == "npz":
+            np.savez(path if path.endswith(".npz") else path + ".npz", **self.store.state())
+        else:
+            from .checkpoint import save_keras_checkpoint
+            save_keras_checkpoint(path, self.store.state(), levels=self.levels)
 
     def load_weights(self, path, strict=True):
+        """Keras Model.load_weights: a TF checkpoint prefix (or its directory) or an .npz."""
+        if os.path.exists(path + ".index") or os.path.isdir(path):
+            from .checkpoint import load_keras_checkpoint
+            shapes = {n: p.shape for n, p in self.store.spec.items()}
+            self.store.load(load_keras_checkpoint(path, levels=self.levels, expect_shapes=shapes),
+                            strict=strict)
+            return
         p = path if os.path.exists(path) else path + ".npz"
         with np.load(p, allow_pickle=False) as z:
             self.store.load({k: z[k] for k in z.files}, strict=strict)
@@ -358,15 +378,23 @@ class FlowNet:
 
 def build_flow_net(height, width, pretrained_weights_path=None, max_disp=3, seed=0,
                    device="cuda", precision="fp32", levels=4):
-    """model.py:119-143.  ``pretrained_weights_path``: an .npz of encoder weights named as in
-    params.encoder_spec() (Keras-checkpoint import is out of scope, SURVEY.md §8 f); the
-    reference asserts every encoder object is matched (model.py:129) -- so does this."""
+    """model.py:119-143.  ``pretrained_weights_path``: the stand-alone ResNet18 encoder's
+    weights, as a TF checkpoint (Keras object-based keys, checkpoint.py) or an .npz of
+    encoder parameter names; like the reference (model.py:128-129) every encoder weight must
+    be matched."""
     net = FlowNet(height, width, max_disp, seed=seed, device=device, precision=precision,
                   levels=levels)
     if pretrained_weights_path is not None:
-        with np.load(pretrained_weights_path, allow_pickle=False) as z:
-            vals = {k: z[k] for k in z.files}
         enc_names = [p.name for p in encoder_spec(levels)]
+        if (os.path.exists(pretrained_weights_path + ".index")
+                or os.path.isdir(pretrained_weights_path)):
+            from .checkpoint import load_keras_checkpoint
+            shapes = {p.name: p.shape for p in encoder_spec(levels)}
+            vals = load_keras_checkpoint(pretrained_weights_path, levels=levels,
+                                         encoder_only=True, expect_shapes=shapes)
+        else:
+            with np.load(pretrained_weights_path, allow_pickle=False) as z:
+                vals = {k: z[k] for k in z.files}
         missing = [n for n in enc_names if n not in vals]
         assert not missing, "pretrained encoder weights missing: %s" % missing[:5]
         net.store.load({n: vals[n] for n in enc_names}, strict=False)

@@ -1,13 +1,17 @@
-"""Mirror of the reference ``train.py`` driver (train.py:1-88) on synthetic pairs.
+"""Mirror of the reference ``train.py`` driver (train.py:1-88).
 
 ``train_step(batch_imgs, step_count)`` keeps the reference's shape (train.py:47-61): forward
 through the flow net, the photometric loss, gradients of the trainable weights, one Keras-Adam
-update; returns ``(loss_value, flows)``.  Differences that are out of scope:
-no KITTI reader (synthetic pairs with the reference value contract, data.py), no TensorBoard
-writer (a JSONL step log instead), no cv2 display.  Data parallelism (one process per GPU,
-RCCL all-reduce of gradient buckets overlapped with the backward) is build-added.
+update; returns ``(loss_value, flows)``.  Data: ``--kitti PATH`` reads KITTI raw pairs
+through the native AsyncReader (data_reader.py; batches land in HBM already resized and
+normalised), otherwise synthetic pairs with the reference value contract (data.py).
+``--display-dir`` writes the every-10-batches display_training pictures (train.py:80-81) as
+PNGs.  No TensorBoard writer (a JSONL step log instead).  Data parallelism (one process per
+GPU, RCCL all-reduce of gradient buckets overlapped with the backward) is build-added; with
+KITTI each rank reads its own seeded shuffle.
 
 Run:  python -m optical_flow_amd.train --height 384 --width 512 --batch 8 --steps 20
+      python -m optical_flow_amd.train --kitti /data/kitti_raw --epochs 20
 """
 from __future__ import annotations
 
@@ -94,6 +98,9 @@ def main(argv=None):
     ap.add_argument("--save-dir", default=None)
     ap.add_argument("--log", default=None, help="JSONL step log")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--kitti", default=None, help="KITTI raw root (train.py:20)")
+    ap.add_argument("--nworkers", type=int, default=6)      # train.py:22
+    ap.add_argument("--display-dir", default=None, help="PNG flow pictures every 10 batches")
     args = ap.parse_args(argv)
 
     rank, world, local = init_from_env()
@@ -104,21 +111,33 @@ def main(argv=None):
     opt = KerasAdam(net.store, learning_rate=args.lr)
     trainer = Trainer(net, opt)
     log = open(args.log, "a") if (args.log and rank == 0) else None
+    reader = None
+    if args.kitti:
+        from .data_reader import AsyncReader, ReaderOpts
+        reader = AsyncReader(ReaderOpts(args.kitti, args.batch, args.height, args.width,
+                                        args.nworkers, seed=args.seed + rank))
+    nbatches = reader.nbatches if reader is not None else args.steps
     step = 0
     for epoch in range(args.epochs):
         if epoch == args.lr_drop_epoch:
             opt.learning_rate = args.lr * 0.1
         t0 = time.time()
-        for b in range(args.steps):
-            batch = torch.from_numpy(synthetic_batch(args.batch, args.height, args.width,
-                                                     seed=1234 + step, rank=rank)).cuda()
+        for b in range(nbatches):
+            if reader is not None:
+                batch = reader.get_batch()
+            else:
+                batch = torch.from_numpy(synthetic_batch(args.batch, args.height, args.width,
+                                                         seed=1234 + step, rank=rank)).cuda()
             loss, flows = trainer.train_step(batch, step)
             lv = float(loss)
             if rank == 0:
-                sys.stdout.write("\rbatch %d/%d, loss: %.2e    " % (b + 1, args.steps, lv))
+                sys.stdout.write("\rbatch %d/%d, loss: %.2e    " % (b + 1, nbatches, lv))
                 sys.stdout.flush()
                 if log:
                     log.write(json.dumps({"step": step, "loss": lv, "t": time.time() - t0}) + "\n")
+                if args.display_dir and (b + 1) % 10 == 0:
+                    from .drawing import display_training
+                    display_training(batch, flows, args.display_dir, step)
             step += 1
         if rank == 0:
             print("\nEpoch computed in %.3fs" % (time.time() - t0))
@@ -126,6 +145,8 @@ def main(argv=None):
                 net.save_weights(os.path.join(args.save_dir, "flow_net_%d" % epoch, "weights"))
     if log:
         log.close()
+    if reader is not None:
+        reader.close()
 
 
 if __name__ == "__main__":

@@ -119,3 +119,21 @@ def test_display_training_writes_pngs(tmp_path):
     c = np.asarray(Image.open(tmp_path / "flow_color_000007.png"))[..., ::-1]
     assert a.shape == (128, 256, 3)
     np.testing.assert_array_equal(c, color)
+
+
+def test_train_driver_on_kitti_tree(tmp_path):
+    """train.py's loop shape on a KITTI-shaped tree: AsyncReader batches -> train_step ->
+    display pictures every 10 batches (train.py:64-82)."""
+    from test_data_path import make_kitti
+    from optical_flow_amd.train import main
+    root = tmp_path / "kitti"
+    make_kitti(str(root), days=(("2011_09_26", 2),), frames=6, size=(40, 130))
+    disp = tmp_path / "disp"
+    log = tmp_path / "log.jsonl"
+    main(["--kitti", str(root), "--height", "32", "--width", "64", "--batch", "2",
+          "--epochs", "1", "--nworkers", "2", "--display-dir", str(disp), "--log", str(log)])
+    lines = [l for l in open(log).read().splitlines() if l]
+    assert len(lines) == (2 * (5 + 6)) // 2                     # nbatches = 22 pairs // 2
+    import json
+    assert all(np.isfinite(json.loads(l)["loss"]) for l in lines)
+    assert sorted(os.listdir(disp))[:2] == ["flow_arrows_000009.png", "flow_arrows_000019.png"]

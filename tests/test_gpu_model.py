@@ -2,6 +2,8 @@
 weights and image pairs: the 4 flow fields, the loss, every trainable-weight gradient, and a
 short Keras-Adam trajectory.  Tolerance 1e-3 relative (BASELINE.json north star); EPE between
 the HIP flows and the oracle flows is reported."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -139,3 +141,33 @@ def test_flow_net_5_levels():
     assert abs(loss.item() - loss_o.item()) / abs(loss_o.item()) < REL_TOL
     worst = max(rel_l2(g, grads_o[n]) for n, g in net.store.grads().items())
     assert worst < REL_TOL, worst
+
+
+def test_save_load_weights_tf_checkpoint(tmp_path):
+    """train.py:88 save_weights -> TF checkpoint (SURVEY §8 f row 2); load_weights into a
+    differently-seeded net reproduces the flows bit for bit; build_flow_net's
+    pretrained_weights_path takes an encoder-only checkpoint (model.py:127-129)."""
+    from optical_flow_amd import checkpoint as K
+    from optical_flow_amd.model import build_flow_net
+    from optical_flow_amd.params import encoder_spec
+    net, vals, batch, _ = _setup(64, 128, 1, seed=4)
+    prefix = str(tmp_path / "flow_net_0" / "weights")
+    net.save_weights(prefix)
+    assert os.path.exists(prefix + ".index") and os.path.exists(prefix + K.DATA_SUFFIX)
+    other = build_flow_net(64, 128, None, seed=9)
+    other.load_weights(prefix)
+    for n, v in net.store.state().items():
+        np.testing.assert_array_equal(other.store.state()[n], v)
+    bd = dev(torch.from_numpy(batch))
+    with torch.no_grad():
+        for a, b in zip(net(bd), other(bd)):
+            assert torch.equal(a, b)
+    enc = {p.name: vals[p.name] for p in encoder_spec()}
+    K.save_keras_checkpoint(str(tmp_path / "resnet18" / "ckpt"), enc, encoder_only=True)
+    pre = build_flow_net(64, 128, str(tmp_path / "resnet18" / "ckpt"), seed=9)
+    st = pre.store.state()
+    for n in enc:
+        np.testing.assert_array_equal(st[n], enc[n])
+    fresh = build_flow_net(64, 128, None, seed=9).store.state()
+    np.testing.assert_array_equal(st["flow_module_0/conv0/kernel"],
+                                  fresh["flow_module_0/conv0/kernel"])   # heads not loaded
