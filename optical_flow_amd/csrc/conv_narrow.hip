@@ -216,26 +216,252 @@ __global__ __launch_bounds__(256) void narrow_wgrad_kernel(NarrowArgs a) {
   }
 }
 
+// Sum the per-slice partials in a fixed order: block (tap, 64 consecutive partial columns);
+// lane = column (coalesced 256-byte rows), wave w sums slices w, w+4, ...; the 4 wave sums
+// are combined in LDS in wave order.  Column k < cin_p*4 is (ci = k/4, co = k%4) -> HWIO
+// dW[tap][ci][co]; tap 0's columns cin_p*4 + co hold the bias sums.
 __global__ __launch_bounds__(256) void narrow_wgrad_final_kernel(NarrowArgs a) {
-  const int taps = a.kh * a.kw, row = a.cin_p * 4 + 4;
-  const int total = taps * a.cin * a.cout + a.cout;
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
-    float sum = 0.f;
-    float* dst;
-    if (e < taps * a.cin * a.cout) {
-      const int t = e / (a.cin * a.cout), rem = e - t * a.cin * a.cout;
-      const int ci = rem / a.cout, co = rem - ci * a.cout;
-      const float* src = a.part + (int64_t)t * a.nslice * row + ci * 4 + co;
-      for (int sl = 0; sl < a.nslice; ++sl) sum += src[(int64_t)sl * row];
-      dst = a.dw + e;                    // HWIO: ((tap * cin + ci) * cout + co)
-    } else {
-      if (!a.db) continue;
-      const int co = e - taps * a.cin * a.cout;
-      const float* src = a.part + a.cin_p * 4 + co;   // tap 0 holds the bias sums
-      for (int sl = 0; sl < a.nslice; ++sl) sum += src[(int64_t)sl * row];
-      dst = a.db + co;
+  __shared__ float ws[4][64];
+  const int tap = blockIdx.x, row = a.cin_p * 4 + 4;
+  const int k = blockIdx.y * 64 + (threadIdx.x & 63), wave = threadIdx.x >> 6;
+  float sum = 0.f;
+  if (k < row) {
+    const float* src = a.part + (int64_t)tap * a.nslice * row + k;
+#pragma unroll 8
+    for (int sl = wave; sl < a.nslice; sl += 4) sum += src[(int64_t)sl * row];
+  }
+  ws[wave][threadIdx.x & 63] = sum;
+  __syncthreads();
+  if (wave != 0 || k >= row) return;
+  const int j = threadIdx.x & 63;
+  sum = ((ws[0][j] + ws[1][j]) + ws[2][j]) + ws[3][j];
+  float* dst = nullptr;
+  if (k < a.cin_p * 4) {
+    const int ci = k >> 2, co = k & 3;
+    if (ci < a.cin && co < a.cout) dst = a.dw + ((int64_t)tap * a.cin + ci) * a.cout + co;
+  } else if (tap == 0 && a.db && k - a.cin_p * 4 < a.cout) {
+    dst = a.db + (k - a.cin_p * 4);
+  }
+  if (dst) *dst = a.accumulate ? *dst + sum : sum;
+}
+
+// ---- halo-tiled variants for cin_p == 32 (every flow head's last conv, 32 -> 2) ------------
+// A workgroup owns an 8 x 32 pixel tile; the (8+2) x (32+2) x 32-channel input halo is
+// staged in LDS once (each input pixel leaves L2 ~1.3x instead of 9x), each lane keeps
+// its channel quad's 9 x 4 x CO weights in registers, so the inner loop is one conflict-free
+// ds_read_b128 + 4*CO FMAs per tap.  Lanes: 8 per pixel (channel quads), 32 pixels per row.
+constexpr int NT_W = 32, NT_H = 8, NT_HW = NT_W + 2, NT_HH = NT_H + 2, NT_Q = 8;
+
+template <int CO>
+__device__ __forceinline__ void load_wf(const float* wf, int q, float (&w)[NK3][4][CO]) {
+  const float4* W4 = reinterpret_cast<const float4*>(wf);
+#pragma unroll
+  for (int t = 0; t < NK3; ++t)
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+      const float4 v = W4[t * 32 + 4 * q + ci];     // W_f row (tap, ci): 4 output channels
+      w[t][ci][0] = v.x;
+      w[t][ci][1] = v.y;
+      if (CO > 2) { w[t][ci][CO > 2 ? 2 : 0] = v.z; w[t][ci][CO > 2 ? 3 : 0] = v.w; }
     }
-    *dst = a.accumulate ? *dst + sum : sum;
+}
+
+__device__ __forceinline__ void stage_halo32(float4* halo, const NarrowArgs& a, int b, int y0,
+                                             int x0) {
+  const rsrc_t rx = make_rsrc(a.x + (int64_t)b * a.h * a.w * a.ldx, (int64_t)a.h * a.w * a.ldx * 4);
+  for (int i = threadIdx.x; i < NT_HH * NT_HW * NT_Q; i += 256) {
+    const int qq = i & 7, pix = i >> 3, hy = pix / NT_HW, hx = pix - hy * NT_HW;
+    const int iy = y0 + hy, ix = x0 + hx;
+    const bool ok = (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    halo[i] = bload4(rx, ok ? 4u * ((iy * a.w + ix) * a.ldx + 4 * qq) : kOOB);
+  }
+}
+
+template <int CO>
+__global__ __launch_bounds__(256) void narrow_fwd_tile(NarrowArgs a) {
+  __shared__ float4 halo[NT_HH * NT_HW * NT_Q];          // 43.5 KB
+  const int q = threadIdx.x & 7, col = threadIdx.x >> 3;
+  const int tx0 = blockIdx.x * NT_W, ty0 = blockIdx.y * NT_H, b = blockIdx.z;
+  float w[NK3][4][CO];
+  load_wf<CO>(a.wt, q, w);
+  stage_halo32(halo, a, b, ty0 - a.pt, tx0 - a.pl);
+  __syncthreads();
+  float bias[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) bias[c] = (a.bias && c < a.cout) ? a.bias[c] : 0.f;
+  const int ox = tx0 + col;
+  for (int r = 0; r < NT_H; ++r) {
+    float acc[CO];
+#pragma unroll
+    for (int c = 0; c < CO; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int t = 0; t < NK3; ++t) {
+      const float4 xv = halo[((r + t / 3) * NT_HW + col + t % 3) * NT_Q + q];
+#pragma unroll
+      for (int c = 0; c < CO; ++c)
+        acc[c] = fmaf(xv.w, w[t][3][c], fmaf(xv.z, w[t][2][c], fmaf(xv.y, w[t][1][c],
+                 fmaf(xv.x, w[t][0][c], acc[c]))));
+    }
+#pragma unroll
+    for (int c = 0; c < CO; ++c) acc[c] = lane_sum(acc[c], 3);
+    const int oy = ty0 + r;
+    if (q < CO && q < a.cout && oy < a.ho && ox < a.wo) {
+      float v = acc[0], bv = bias[0];
+#pragma unroll
+      for (int c = 1; c < CO; ++c) {
+        v = q == c ? acc[c] : v;
+        bv = q == c ? bias[c] : bv;
+      }
+      v += bv;
+      if (a.act == OF_ACT_RELU) v = v > 0.f ? v : 0.f;
+      if (a.act == OF_ACT_LEAKY) v = v > 0.f ? v : a.alpha * v;
+      a.out[(((int64_t)b * a.ho + oy) * a.wo + ox) * a.ldo + q] = v;
+    }
+  }
+}
+
+// dx[iy][ix][4q..4q+3] = sum_t sum_co dy[iy - r + pt][ix - s + pl][co] * W[t][4q..][co]
+template <int CO>
+__global__ __launch_bounds__(256) void narrow_dgrad_tile(NarrowArgs a) {
+  __shared__ float dyh[NT_HH * NT_HW * CO];
+  const int q = threadIdx.x & 7, col = threadIdx.x >> 3;
+  const int tx0 = blockIdx.x * NT_W, ty0 = blockIdx.y * NT_H, b = blockIdx.z;
+  float4 w[NK3][CO];
+  const float4* W4 = reinterpret_cast<const float4*>(a.wt);   // W_d [(t*4 + co)][32]
+#pragma unroll
+  for (int t = 0; t < NK3; ++t)
+#pragma unroll
+    for (int c = 0; c < CO; ++c) w[t][c] = W4[(t * 4 + c) * 8 + q];
+  const rsrc_t rd =
+      make_rsrc(a.dy + (int64_t)b * a.ho * a.wo * a.lddy, (int64_t)a.ho * a.wo * a.lddy * 4);
+  const int y0 = ty0 + a.pt - 2, x0 = tx0 + a.pl - 2;       // dy halo origin
+  for (int i = threadIdx.x; i < NT_HH * NT_HW * CO; i += 256) {
+    const int c = i % CO, pix = i / CO, hy = pix / NT_HW, hx = pix - hy * NT_HW;
+    const int oy = y0 + hy, ox = x0 + hx;
+    const bool ok = c < a.cout && (unsigned)oy < (unsigned)a.ho && (unsigned)ox < (unsigned)a.wo;
+    dyh[i] = bload1(rd, ok ? 4u * ((oy * a.wo + ox) * a.lddy + c) : kOOB);
+  }
+  __syncthreads();
+  const int ix = tx0 + col;
+  const float neg = a.act == OF_ACT_LEAKY ? a.alpha : 0.f;
+  for (int r = 0; r < NT_H; ++r) {
+    const int iy = ty0 + r;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int t = 0; t < NK3; ++t) {
+      const float* d = &dyh[((r + 2 - t / 3) * NT_HW + col + 2 - t % 3) * CO];
+#pragma unroll
+      for (int c = 0; c < CO; ++c) acc = fma4(d[c], w[t][c], acc);
+    }
+    if (iy < a.h && ix < a.w) {
+      const int64_t p = ((int64_t)b * a.h + iy) * a.w + ix;
+      if (a.act_src) {
+        const float4 sv = *reinterpret_cast<const float4*>(a.act_src + p * a.ld_act + 4 * q);
+        acc.x *= sv.x > 0.f ? 1.f : neg;
+        acc.y *= sv.y > 0.f ? 1.f : neg;
+        acc.z *= sv.z > 0.f ? 1.f : neg;
+        acc.w *= sv.w > 0.f ? 1.f : neg;
+      }
+      *reinterpret_cast<float4*>(a.out + p * a.ldo + 4 * q) = acc;
+    }
+  }
+}
+
+// Per-block partials of dW[t][ci][co] (+ bias sums) over a grid-stride set of 8 x 32 tiles,
+// written in narrow_wgrad_kernel's partial layout (slice = block), summed by
+// narrow_wgrad_final_kernel in a fixed order.
+template <int CO>
+__global__ __launch_bounds__(256) void narrow_wgrad_tile(NarrowArgs a, int tiles_x, int tiles_y) {
+  __shared__ float4 halo[NT_HH * NT_HW * NT_Q];
+  __shared__ float dyt[NT_H * NT_W * CO];
+  const int q = threadIdx.x & 7, col = threadIdx.x >> 3;
+  float acc[NK3][4][CO];
+#pragma unroll
+  for (int t = 0; t < NK3; ++t)
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci)
+#pragma unroll
+      for (int c = 0; c < CO; ++c) acc[t][ci][c] = 0.f;
+  float bacc[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) bacc[c] = 0.f;
+  const int ntiles = tiles_x * tiles_y * a.n;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / (tiles_x * tiles_y), rem = tile - b * tiles_x * tiles_y;
+    const int ty0 = (rem / tiles_x) * NT_H, tx0 = (rem % tiles_x) * NT_W;
+    __syncthreads();                                   // previous tile's LDS reads done
+    stage_halo32(halo, a, b, ty0 - a.pt, tx0 - a.pl);
+    const rsrc_t rd =
+        make_rsrc(a.dy + (int64_t)b * a.ho * a.wo * a.lddy, (int64_t)a.ho * a.wo * a.lddy * 4);
+    for (int i = threadIdx.x; i < NT_H * NT_W * CO; i += 256) {
+      const int c = i % CO, pix = i / CO, hy = pix / NT_W, hx = pix - hy * NT_W;
+      const int oy = ty0 + hy, ox = tx0 + hx;
+      const bool ok = c < a.cout && oy < a.ho && ox < a.wo;
+      dyt[i] = bload1(rd, ok ? 4u * ((oy * a.wo + ox) * a.lddy + c) : kOOB);
+    }
+    __syncthreads();
+    for (int r = 0; r < NT_H; ++r) {
+      float d[CO];
+#pragma unroll
+      for (int c = 0; c < CO; ++c) d[c] = dyt[(r * NT_W + col) * CO + c];
+#pragma unroll
+      for (int c = 0; c < CO; ++c) bacc[c] += d[c];
+#pragma unroll
+      for (int t = 0; t < NK3; ++t) {
+        const float4 xv = halo[((r + t / 3) * NT_HW + col + t % 3) * NT_Q + q];
+#pragma unroll
+        for (int c = 0; c < CO; ++c) {
+          acc[t][0][c] = fmaf(xv.x, d[c], acc[t][0][c]);
+          acc[t][1][c] = fmaf(xv.y, d[c], acc[t][1][c]);
+          acc[t][2][c] = fmaf(xv.z, d[c], acc[t][2][c]);
+          acc[t][3][c] = fmaf(xv.w, d[c], acc[t][3][c]);
+        }
+      }
+    }
+  }
+  // reduce over the 8 pixel columns of a wave (lane bits 3..5), then over the 4 waves
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(halo);          // [4 waves][8 q][9*4*CO + CO]
+  constexpr int ROW = NK3 * 4 * CO + CO;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < NK3; ++t)
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci)
+#pragma unroll
+      for (int c = 0; c < CO; ++c) {
+        float v = acc[t][ci][c];
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (lane < 8) red[(wave * 8 + q) * ROW + (t * 4 + ci) * CO + c] = v;
+      }
+#pragma unroll
+  for (int c = 0; c < CO; ++c) {
+    float v = bacc[c];
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane < 8) red[(wave * 8 + q) * ROW + NK3 * 4 * CO + c] = v;
+  }
+  __syncthreads();
+  const int row = a.cin_p * 4 + 4;                       // narrow_wgrad_final's layout
+  for (int e = threadIdx.x; e < NK3 * 32 * 4 + 4; e += 256) {
+    float sum = 0.f;
+    int t, slot;
+    if (e < NK3 * 32 * 4) {
+      t = e / 128;
+      const int ci = (e % 128) >> 2, co = e & 3;
+      slot = co < CO ? ((ci >> 2) * ROW + (t * 4 + (ci & 3)) * CO + co) : -1;
+      if (slot >= 0)
+        for (int wv = 0; wv < 4; ++wv) sum += red[wv * 8 * ROW + slot];
+      a.part[((int64_t)t * a.nslice + blockIdx.x) * row + (e % 128)] = sum;
+    } else {
+      const int co = e - NK3 * 128;
+      if (co < CO)                                       // bias: counted once per pixel (q = 0)
+        for (int wv = 0; wv < 4; ++wv) sum += red[(wv * 8) * ROW + NK3 * 4 * CO + co];
+      a.part[(int64_t)blockIdx.x * row + a.cin_p * 4 + co] = sum;   // tap 0 holds the bias
+    }
   }
 }
 
@@ -252,7 +478,13 @@ static NarrowArgs base(const of_conv_desc* d) {
   return a;
 }
 
+static bool narrow_tiled(const of_conv_desc* d) { return d->cin_p == 32 && d->cout <= 4; }
+static int tiles_x(const of_conv_desc* d) { return (int)cdiv(d->wo, NT_W); }
+static int tiles_y(const of_conv_desc* d) { return (int)cdiv(d->ho, NT_H); }
+
 static int wgrad_slices(const of_conv_desc* d) {
+  if (narrow_tiled(d))   // one partial per block; 3 blocks per CU, grid-stride over the tiles
+    return (int)std::min<int64_t>((int64_t)tiles_x(d) * tiles_y(d) * d->n, 768);
   const int64_t npix = (int64_t)d->n * d->ho * d->wo;
   const int taps = d->kh * d->kw;
   // ~4 blocks per CU in total (measured: more slices lose to the per-block reduction)
@@ -270,6 +502,12 @@ int narrow_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w_fw
   a.x = x, a.ldx = ldx, a.wt = w_fwd, a.bias = bias, a.out = y, a.ldo = ldy, a.act = act,
   a.alpha = alpha;
   OF_CHECK_ARG((int64_t)d->h * d->w * ldx < (1LL << 29), "narrow conv: image too large");
+  if (narrow_tiled(d) && ldx % 4 == 0) {
+    const dim3 grid(tiles_x(d), tiles_y(d), d->n);
+    if (d->cout <= 2) hipLaunchKernelGGL(narrow_fwd_tile<2>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(narrow_fwd_tile<4>, grid, dim3(256), 0, s, a);
+    return check_launch("narrow_fwd_tile");
+  }
   const int64_t npix = (int64_t)d->n * d->ho * d->wo;
   const int ppb = 256 >> a.lg;
   const size_t lds = (size_t)d->kh * d->kw * d->cin_p * sizeof(float4);
@@ -287,6 +525,12 @@ int narrow_dgrad(const of_conv_desc* d, const float* dy, int lddy, const float* 
   OF_CHECK_ARG(lddx % 4 == 0 && (!act_src || ld_act % 4 == 0) && ((uintptr_t)dx & 15) == 0 &&
                    (!act_src || ((uintptr_t)act_src & 15) == 0),
                "narrow conv dgrad: dx / act_src rows must be float4 aligned");
+  if (narrow_tiled(d)) {   // stride 1, 'same': the input grid is the output grid
+    const dim3 grid((unsigned)cdiv(d->w, NT_W), (unsigned)cdiv(d->h, NT_H), d->n);
+    if (d->cout <= 2) hipLaunchKernelGGL(narrow_dgrad_tile<2>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(narrow_dgrad_tile<4>, grid, dim3(256), 0, s, a);
+    return check_launch("narrow_dgrad_tile");
+  }
   const int64_t npix = (int64_t)d->n * d->h * d->w;
   const int ppb = 256 >> a.lg;
   const size_t lds = (size_t)d->kh * d->kw * d->cin_p * sizeof(float4);
@@ -308,12 +552,20 @@ int narrow_wgrad(const of_conv_desc* d, const float* x, int ldx, const float* dy
   OF_CHECK_ARG((int64_t)d->n * d->h * d->w * ldx < (1LL << 29) &&
                    (int64_t)d->n * d->ho * d->wo * lddy < (1LL << 29),
                "narrow conv wgrad: tensors too large");
-  hipLaunchKernelGGL(narrow_wgrad_kernel, dim3(d->kh * d->kw, a.nslice), dim3(256), 0, s, a);
+  if (narrow_tiled(d) && ldx % 4 == 0) {
+    if (d->cout <= 2)
+      hipLaunchKernelGGL(narrow_wgrad_tile<2>, dim3(a.nslice), dim3(256), 0, s, a, tiles_x(d),
+                         tiles_y(d));
+    else
+      hipLaunchKernelGGL(narrow_wgrad_tile<4>, dim3(a.nslice), dim3(256), 0, s, a, tiles_x(d),
+                         tiles_y(d));
+  } else {
+    hipLaunchKernelGGL(narrow_wgrad_kernel, dim3(d->kh * d->kw, a.nslice), dim3(256), 0, s, a);
+  }
   int st = check_launch("narrow_wgrad");
   if (st) return st;
-  const int total = d->kh * d->kw * d->cin * d->cout + d->cout;
-  hipLaunchKernelGGL(narrow_wgrad_final_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
-                     s, a);
+  hipLaunchKernelGGL(narrow_wgrad_final_kernel,
+                     dim3(d->kh * d->kw, (unsigned)cdiv(d->cin_p * 4 + 4, 64)), dim3(256), 0, s, a);
   return check_launch("narrow_wgrad_final");
 }
 

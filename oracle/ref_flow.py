@@ -98,7 +98,7 @@ def _conv2d_same_exact(x, w, b, stride=1):
     pl, pr = same_pads(x.shape[2], kw, stride)
     xn = x.permute(0, 3, 1, 2)
     xn = F.pad(xn, (pl, pr, pt, pb))
-    y = F.conv2d(xn, w.permute(3, 2, 0, 1), b, stride=stride)
+    y = F.conv2d(xn, w.permute(3, 2, 0, 1).contiguous(), b, stride=stride)
     return y.permute(0, 2, 3, 1)
 
 

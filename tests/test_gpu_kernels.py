@@ -21,6 +21,9 @@ CONV_CASES = [
     (2, 16, 24, 115, 128, 3, 1, "leaky", False, False),     # decoder c0 (cin padded)
     (1, 12, 16, 32, 2, 3, 1, "none", False, False),         # flow conv (cout 2): narrow path
     (2, 33, 70, 32, 2, 3, 1, "none", False, False),         # narrow, ragged, many slices
+    (3, 40, 100, 32, 4, 3, 1, "leaky", False, False),       # narrow tiled, cout 4, ragged
+    (1, 9, 33, 32, 1, 3, 1, "relu", False, False),          # narrow tiled, cout 1
+    (2, 17, 65, 32, 3, 3, 1, "none", False, False),         # narrow tiled, cout 3
     (1, 10, 20, 64, 3, 3, 1, "relu", False, False),         # narrow, 16 lanes per pixel
     (2, 8, 8, 3, 2, 3, 1, "leaky", False, False),           # narrow, 1 lane per pixel
     (1, 9, 9, 12, 2, 3, 1, "leaky", False, False),          # cin_p 12: GEMM fallback
