@@ -215,13 +215,19 @@ def main():
     flow_abs = [[round(float(f.abs().mean()), 4), round(float(f.abs().max()), 3)] for f in flows]
 
     # ---- dominant-kernel roofline (instrumented extra steps, outside the timed region) ----
+    # The weight-gradient kernels normally run on a side stream, concurrently with the input
+    # gradients; per-launch hipEvent durations would then include the other stream's share
+    # of the GPU.  The instrumented steps therefore run every conv on one stream, so each
+    # launch's duration is its own.
     lib = _lib.lib()
     ops.TIMING_TAGS = []
+    ops.SIDE_STREAM_WGRAD = False
     lib.of_timing_enable(1)
     for i in range(args.timing_steps):
         trainer.train_step(batch, 10_000 + i)
     torch.cuda.synchronize()
     lib.of_timing_enable(0)
+    ops.SIDE_STREAM_WGRAD = bool(args.side_stream)
     tags, ops.TIMING_TAGS = ops.TIMING_TAGS, None
     cap = 4096
     kinds = (C.c_int * cap)()
@@ -261,14 +267,15 @@ def main():
                 "avg_launch_ms": round(tm / cnt, 4), "gflop_per_launch": round(tf / cnt / 1e9, 3),
                 "all_conv_gemm_tflops": round(allconv, 2),
                 "per_kernel": {kind_name(k):
-                               {"launches": v[2], "ms": round(v[1], 3),
+                               {"launches_per_step": v[2] // max(args.timing_steps, 1),
+                                "ms_per_step": round(v[1] / max(args.timing_steps, 1), 3),
                                 "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
                                for k, v in sorted(per.items())}}
 
     # ---- CPU baseline + EPE vs the oracle (rank 0 only) ----------------------------------
     cpu = None
     parity = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:     # N=1 only (contract)
         pair = batch[:1].cpu().numpy()
         cps, threads, flows_ref, loss_ref = cpu_baseline(pair, vals, args.cpu_steps,
                                                          args.precision, args.levels)

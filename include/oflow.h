@@ -171,6 +171,16 @@ int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
                   const float* z, const float* gamma, const float* mean, const float* var,
                   float eps, float* dz, float* dres, float* dgamma, float* dbeta, float* dbias,
                   int accumulate, void* workspace, void* stream);
+/* The stem's backward in one pass (model.py:12-17: conv1 -> layer1_bn -> ReLU -> out0 and
+ * MaxPool2D): dy(out0) = max-pool backward of dyp (first maximum of each 2x2 window of y,
+ * strict >) + g (out0's gradient from its other consumer; NULL = none); then the
+ * of_bn_act_bwd math with act = ReLU (y = out0 = the max-pool input, z = pre-BN conv output).
+ * n, h, w, c: out0's shape (h, w even); dyp: (n, h/2, w/2, c). */
+size_t of_maxpool_bn_act_bwd_workspace(int n, int h, int w, int c);
+int of_maxpool_bn_act_bwd(int n, int h, int w, int c, const float* dyp, const float* g,
+                          const float* y, const float* z, const float* gamma, const float* mean,
+                          const float* var, float eps, float* dz, float* dgamma, float* dbeta,
+                          float* dbias, int accumulate, void* workspace, void* stream);
 
 /* Max-pool 2x2/2 'valid' (layers.MaxPool2D(), model.py:17) and its gradient (to the first
  * maximum in row-major window order). x: [n][h][w][c] dense. */

@@ -67,6 +67,8 @@ PROTOTYPES = {
     "of_colsum": (I, [P, I64, I, I, P, I, P, P]),
     "of_bn_act_bwd_workspace": (SZ, [I64, I]),
     "of_bn_act_bwd": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, P, I, P, P]),
+    "of_maxpool_bn_act_bwd_workspace": (SZ, [I, I, I, I]),
+    "of_maxpool_bn_act_bwd": (I, [I, I, I, I, P, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     "of_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
     "of_maxpool2_bwd": (I, [P, P, I, I, I, I, P, P]),
     "of_corr_fwd_workspace": (SZ, [I, I, I, I, I]),

@@ -176,6 +176,84 @@ __global__ __launch_bounds__(256) void bn_act_bwd_partial(
   }
 }
 
+
+// Stem backward in one pass (reset18_encoder's conv1 -> layer1_bn -> ReLU -> {out0, max-pool},
+// model.py:12-17): the max-pool gradient (first maximum of each 2x2 window, strict >, as
+// maxpool2_bwd_kernel) plus g, the gradient of out0 from its other consumer, then the
+// BN(inference)+ReLU backward and its channel sums -- one read of y, z, g and the pooled dy,
+// one write of dz, instead of max-pool backward + add + bn_act_bwd (three passes over the
+// largest activation of the encoder).  Pixels are 2x2 windows: npix = n*(h/2)*(w/2).
+__global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
+    int64_t npix, int h, int w, int c, const float* __restrict__ dyp,
+    const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ z,
+    const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ var, float eps, float* __restrict__ dz, int qw, int rows,
+    int64_t ppb, float* __restrict__ part) {
+  __shared__ float4 red[256];
+  const int q = threadIdx.x % qw, r = threadIdx.x / qw;
+  const int ch = (blockIdx.y * qw + q) * 4;
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int64_t p1 = min(npix, p0 + ppb);
+  float4 sb = make_float4(0.f, 0.f, 0.f, 0.f), sg = sb;
+  const bool live = ch < c;
+  const int ho = h / 2, wo = w / 2;
+  if (live) {
+    const float4 gm = *reinterpret_cast<const float4*>(gamma + ch);
+    const float4 mu = *reinterpret_cast<const float4*>(mean + ch);
+    const float4 vr = *reinterpret_cast<const float4*>(var + ch);
+    const float4 is = make_float4(rsqrtf(vr.x + eps), rsqrtf(vr.y + eps), rsqrtf(vr.z + eps),
+                                  rsqrtf(vr.w + eps));
+    const float4 sc = make_float4(gm.x * is.x, gm.y * is.y, gm.z * is.z, gm.w * is.w);
+    for (int64_t p = p0 + r; p < p1; p += rows) {
+      const int ox = (int)(p % wo);
+      const int64_t t2 = p / wo;
+      const int oy = (int)(t2 % ho);
+      const int64_t b = t2 / ho;
+      const int64_t o0 = ((b * h + 2 * oy) * (int64_t)w + 2 * ox) * c + ch;
+      const int64_t offs[4] = {o0, o0 + c, o0 + (int64_t)w * c, o0 + (int64_t)w * c + c};
+      float4 yv[4], zv[4], gv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        yv[k] = *reinterpret_cast<const float4*>(y + offs[k]);
+        zv[k] = *reinterpret_cast<const float4*>(z + offs[k]);
+        gv[k] = g ? *reinterpret_cast<const float4*>(g + offs[k]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const float4 d = *reinterpret_cast<const float4*>(dyp + p * c + ch);
+      // first maximum per channel
+      int bx = 0, by = 0, bz = 0, bw = 0;
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        if (yv[k].x > yv[bx].x) bx = k;
+        if (yv[k].y > yv[by].y) by = k;
+        if (yv[k].z > yv[bz].z) bz = k;
+        if (yv[k].w > yv[bw].w) bw = k;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float4 t;
+        t.x = yv[k].x > 0.f ? gv[k].x + (k == bx ? d.x : 0.f) : 0.f;
+        t.y = yv[k].y > 0.f ? gv[k].y + (k == by ? d.y : 0.f) : 0.f;
+        t.z = yv[k].z > 0.f ? gv[k].z + (k == bz ? d.z : 0.f) : 0.f;
+        t.w = yv[k].w > 0.f ? gv[k].w + (k == bw ? d.w : 0.f) : 0.f;
+        *reinterpret_cast<float4*>(dz + offs[k]) =
+            make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
+        add4(sb, t);
+        sg.x += t.x * (zv[k].x - mu.x) * is.x;
+        sg.y += t.y * (zv[k].y - mu.y) * is.y;
+        sg.z += t.z * (zv[k].z - mu.z) * is.z;
+        sg.w += t.w * (zv[k].w - mu.w) * is.w;
+      }
+    }
+  }
+  sb = rows_reduce(sb, q, r, qw, rows, red);
+  __syncthreads();
+  sg = rows_reduce(sg, q, r, qw, rows, red);
+  if (r == 0 && live) {
+    *reinterpret_cast<float4*>(part + ((int64_t)blockIdx.x * 2 + 0) * c + ch) = sb;
+    *reinterpret_cast<float4*>(part + ((int64_t)blockIdx.x * 2 + 1) * c + ch) = sg;
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_act_bwd_final(const float* __restrict__ part,
                                                         int nblk, int c,
                                                         const float* __restrict__ gamma,
@@ -409,6 +487,36 @@ int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
   int st = check_launch("bn_act_bwd_partial");
   if (st) return st;
   hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c, 16)), dim3(256), 0, s, part, g.nblk, c,
+                     gamma, var, eps, dgamma, dbeta, dbias, accumulate);
+  return check_launch("bn_act_bwd_final");
+}
+
+
+size_t of_maxpool_bn_act_bwd_workspace(int n, int h, int w, int c) {
+  return of_bn_act_bwd_workspace((int64_t)n * (h / 2) * (w / 2), c);
+}
+
+int of_maxpool_bn_act_bwd(int n, int h, int w, int c, const float* dyp, const float* g,
+                          const float* y, const float* z, const float* gamma, const float* mean,
+                          const float* var, float eps, float* dz, float* dgamma, float* dbeta,
+                          float* dbias, int accumulate, void* workspace, void* stream) {
+  OF_CHECK_ARG(dyp && y && z && gamma && mean && var && dz && workspace,
+               "maxpool_bn_act_bwd: args");
+  OF_CHECK_ARG(n > 0 && h % 2 == 0 && w % 2 == 0 && h > 0 && w > 0 && c % 4 == 0,
+               "maxpool_bn_act_bwd: even h, w and c % 4 == 0");
+  OF_CHECK_ARG((((uintptr_t)dyp | (uintptr_t)g | (uintptr_t)y | (uintptr_t)z | (uintptr_t)dz |
+                 (uintptr_t)gamma | (uintptr_t)mean | (uintptr_t)var) & 15) == 0,
+               "maxpool_bn_act_bwd: 16-byte alignment");
+  hipStream_t s = as_stream(stream);
+  const int64_t npix = (int64_t)n * (h / 2) * (w / 2);
+  const RedGeo geo = red_geo(npix, c);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(maxpool_bn_act_bwd_partial, dim3(geo.nblk, cdiv(c / 4, geo.qw)), dim3(256),
+                     0, s, npix, h, w, c, dyp, g, y, z, gamma, mean, var, eps, dz, geo.qw,
+                     geo.rows, geo.ppb, part);
+  int st = check_launch("maxpool_bn_act_bwd_partial");
+  if (st) return st;
+  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c, 16)), dim3(256), 0, s, part, geo.nblk, c,
                      gamma, var, eps, dgamma, dbeta, dbias, accumulate);
   return check_launch("bn_act_bwd_final");
 }

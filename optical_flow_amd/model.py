@@ -162,6 +162,8 @@ class Encoder:
 
     def forward4(self, x4):
         """x4: (N, H, W, 4) images with a zero 4th channel -> 4 feature maps."""
+        if not _PER_LAYER_BLOCKS:
+            return ops.encoder_forward(x4, self.conv1, self.blocks)
         x = self.conv1(x4)
         outs = [x]
         x = ops.maxpool2(x)

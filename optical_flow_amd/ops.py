@@ -305,22 +305,28 @@ def _conv_forward(layer: "ConvLayer", x, residual=None):
     return y, z
 
 
-def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx_out=None):
+def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx_out=None,
+                   dz_given=None):
     """Backward of _conv_forward: BN/activation backward (with the residual gradient), weight
     and bias gradients, input gradient.  needs = (x, kernel, bias, gamma, beta, residual).
     add: a gradient summed into dx by the input-gradient kernel's epilogue (dx_out may be
-    that same buffer).  Returns (dx, d_kernel, d_bias, d_gamma, d_beta, d_residual) with None
-    for gradients written straight into the gradient arena."""
+    that same buffer).  dz_given: the pre-activation gradient already computed, with the BN
+    and bias gradients, by a fused kernel (the stem, of_maxpool_bn_act_bwd).  Returns (dx,
+    d_kernel, d_bias, d_gamma, d_beta, d_residual) with None for gradients written straight
+    into the gradient arena."""
     n, h, w, cx = x.shape
     d = layer.desc(n, h, w)
     _, wd = layer.packed(d)
-    dy = dy.contiguous()
+    dy = dy.contiguous() if dy is not None else None
     s = _stream()
     need_x, need_k, need_b, need_g, need_be, need_res = needs
     ret_k = ret_b = ret_g = ret_be = dres = dx = None
     npix = n * d.ho * d.wo
     # ---- pre-activation gradient dz -----------------------------------------------------
-    if layer.bn is not None:
+    if dz_given is not None:
+        dz = dz_given
+        bias_done = True
+    elif layer.bn is not None:
         gamma, beta, mean, var = layer.bn
         dz = torch.empty_like(dy)
         dres = torch.empty_like(dy) if (has_res and need_res) else None
@@ -356,7 +362,7 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
         side = SIDE_STREAM_WGRAD and tk[1] == 1 and (tbias[0] is None or tbias[1] == 1)
         with torch.cuda.stream(side_stream(x, dzp)) if side else contextlib.nullcontext():
             ss = _stream()
-            ws = torch.empty(wsb // 4 + 1, device=dy.device)
+            ws = torch.empty(wsb // 4 + 1, device=dz.device)
             if tbias[0] is not None and tbias[1] != tk[1]:
                 # mixed arena / fresh targets: compute the bias into a temp, then place it
                 tmpb = torch.empty_like(layer.bias)
@@ -378,7 +384,7 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
                 *(layer.bn[:2] if layer.bn is not None else ()))
     # ---- input gradient -----------------------------------------------------------------
     if need_x:
-        dx = dx_out if dx_out is not None else torch.empty((n, h, w, cx), device=dy.device)
+        dx = dx_out if dx_out is not None else torch.empty((n, h, w, cx), device=dz.device)
         _tag(layer, 1)
         if add is not None:
             add = add.contiguous()
@@ -439,25 +445,122 @@ class _ResBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, ya, za, y, zb, yp, zp = ctx.saved_tensors
-        a, b, p = ctx.block
-        need = ctx.needs_input_grad
-        need_x = need[0]
-        nb = lambda k: tuple(need[1 + 4 * k:5 + 4 * k])     # kernel, bias, gamma, beta of layer k
-        dya, *gb = _conv_backward(b, ya, y, zb, dy, True, (True, *nb(1), True))
-        dres = gb[-1]
-        gb = gb[:-1]
-        if p is not None:
-            dxp, *gp = _conv_backward(p, x, yp, zp, dres, False, (need_x, *nb(2), False))
-            gp = gp[:-1]
-            add, dx_out = dxp, dxp
-        else:
-            gp = []
-            add, dx_out = dres, None
-        dx, *ga = _conv_backward(a, x, ya, za, dya, False, (need_x, *nb(0), False),
-                                 add=add if need_x else None, dx_out=dx_out)
-        ga = ga[:-1]
-        return (dx, *ga, *gb, *gp, None)
+        dx, grads = _res_block_backward(ctx.block, ctx.saved_tensors, dy, ctx.needs_input_grad)
+        return (dx, *grads, None)
+
+
+def _res_block_backward(block, saved, dy, need, extra=None):
+    """Backward of one residual block.  need: needs_input_grad of (x, then kernel, bias,
+    gamma, beta per layer a, b, p).  extra: a further gradient of the block input x (its
+    other consumer) summed by the shortcut's input-gradient epilogue -- no separate add.
+    Returns (dx, [param grads of a, b, p])."""
+    x, ya, za, y, zb, yp, zp = saved
+    a, b, p = block
+    need_x = need[0]
+    nb = lambda k: tuple(need[1 + 4 * k:5 + 4 * k])     # kernel, bias, gamma, beta of layer k
+    dya, *gb = _conv_backward(b, ya, y, zb, dy, True, (True, *nb(1), True))
+    dres = gb[-1]
+    gb = gb[:-1]
+    if p is not None:
+        dxp, *gp = _conv_backward(p, x, yp, zp, dres, False, (need_x, *nb(2), False),
+                                  add=extra if need_x else None)
+        gp = gp[:-1]
+        add, dx_out = dxp, dxp
+    else:
+        gp = []
+        if extra is not None and need_x:
+            call("of_add_inplace", _ptr(dres), _ptr(extra.contiguous()), dres.numel(), _stream())
+        add, dx_out = dres, None
+    dx, *ga = _conv_backward(a, x, ya, za, dya, False, (need_x, *nb(0), False),
+                             add=add if need_x else None, dx_out=dx_out)
+    ga = ga[:-1]
+    return dx, list(ga) + list(gb) + list(gp)
+
+
+class _EncoderFn(torch.autograd.Function):
+    """reset18_encoder (model.py:10-26) forward and backward as ONE autograd node: conv1 +
+    BN + ReLU -> out0 -> max-pool -> residual blocks -> out1..out3 (out4 with levels=5).
+    Each encoder output feeds the decoder and (out0..out2) the next stage, so under plain
+    autograd every such junction costs a full-size add of the two gradients; here the
+    decoder's gradient of out_k is summed by the next stage's shortcut input-gradient
+    epilogue (_res_block_backward extra=), and out0's by the fused stem kernel
+    (of_maxpool_bn_act_bwd: max-pool backward + add + BN/ReLU backward in one pass)."""
+
+    @staticmethod
+    def forward(ctx, x4, *args):
+        conv1, blocks = args[-1]
+        y0, z0 = _conv_forward(conv1, x4.contiguous())
+        n, h, w, c = y0.shape
+        xp = torch.empty((n, h // 2, w // 2, c), device=y0.device)
+        call("of_maxpool2_fwd", _ptr(y0), n, h, w, c, _ptr(xp), _stream())
+        x = xp
+        saved = [x4, y0, z0]
+        outs = [y0]
+        for i, (a, b, p) in enumerate(blocks):
+            ya, za = _conv_forward(a, x)
+            yp = zp = None
+            sc = x
+            if p is not None:
+                yp, zp = _conv_forward(p, x)
+                sc = yp
+            y, zb = _conv_forward(b, ya, residual=sc)
+            saved += [x, ya, za, y, zb, yp, zp]
+            x = y
+            if i % 2 == 1:
+                outs.append(y)
+        ctx.conv1, ctx.blocks = conv1, blocks
+        ctx.save_for_backward(*saved)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        saved = ctx.saved_tensors
+        x4, y0, z0 = saved[:3]
+        conv1, blocks = ctx.conv1, ctx.blocks
+        need = ctx.needs_input_grad          # x4, then per layer kernel/bias/gamma/beta
+        nbk = len(blocks)
+        gouts = [g.contiguous() if g is not None else None for g in gouts]
+        dy = gouts[-1] if gouts[-1] is not None else torch.zeros_like(saved[3 + 7 * (nbk - 1) + 3])
+        grads = []
+        off = 1 + 4                          # after x4 and conv1's 4 parameters
+        pos = []
+        for a, b, p in blocks:
+            pos.append(off)
+            off += 4 * (3 if p is not None else 2)
+        for i in range(nbk - 1, -1, -1):
+            blk = saved[3 + 7 * i:3 + 7 * (i + 1)]
+            extra = gouts[i // 2] if (i % 2 == 0 and i > 0) else None
+            nd = (True,) + tuple(need[pos[i]:pos[i] + 4 * (3 if blocks[i][2] is not None else 2)])
+            dy, g = _res_block_backward(blocks[i], blk, dy, nd, extra=extra)
+            grads = list(g) + grads
+        # stem: max-pool backward + out0's decoder gradient + BN/ReLU backward, one pass
+        n, h, w, c = y0.shape
+        gamma, beta, mean, var = conv1.bn
+        nk, nbias, ng, nbe = need[1:5]
+        tg = grad_target(gamma) if ng else (None, 0, None)
+        tb = grad_target(beta) if nbe else (None, 0, None)
+        tbias = grad_target(conv1.bias) if nbias else (None, 0, None)
+        acc = tg[1] if ng else (tb[1] if nbe else tbias[1])
+        assert all(t[0] is None or t[1] == acc for t in (tg, tb, tbias))
+        dz0 = torch.empty_like(y0)
+        ws = torch.empty(_lib.lib().of_maxpool_bn_act_bwd_workspace(n, h, w, c) // 4 + 1,
+                         device=y0.device)
+        call("of_maxpool_bn_act_bwd", n, h, w, c, _ptr(dy.contiguous()), _ptr(gouts[0]), _ptr(y0),
+             _ptr(z0), _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, _ptr(dz0), _ptr(tg[0]),
+             _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
+        _, gk, _, _, _, _ = _conv_backward(conv1, x4, y0, z0, None, False,
+                                           (False, nk, nbias, ng, nbe, False), dz_given=dz0)
+        stem = [gk, tbias[2], tg[2], tb[2]]
+        return (None, *stem, *grads, None)
+
+
+def encoder_forward(x4, conv1: ConvLayer, blocks):
+    """All encoder outputs [out0, out1, ...] of x4 (N, H, W, 4) through _EncoderFn."""
+    params = [conv1.kernel, conv1.bias, conv1.bn[0], conv1.bn[1]]
+    for a, b, p in blocks:
+        for L in (a, b) + ((p,) if p is not None else ()):
+            params += [L.kernel, L.bias, L.bn[0], L.bn[1]]
+    return list(_EncoderFn.apply(x4, *params, (conv1, blocks)))
 
 
 def res_block(x, a: ConvLayer, b: ConvLayer, p: Optional[ConvLayer] = None):
@@ -643,6 +746,7 @@ class _CorrConcat(torch.autograd.Function):
         used = c + nk + (2 if flow_up is not None else 0)
         assert used <= cp
         x = torch.empty((n, h, w, cp), device=f1.device)
+        ctx.dst = (grad_dst(f1), grad_dst(f2w))
         fu = flow_up.contiguous() if flow_up is not None else None
         ws, wp, wb = _workspace(_lib.lib().of_corr_fwd_workspace(n, h, w, c, max_disp), f1.device)
         call("of_corr_concat_fwd", _ptr(f1), _ptr(f2w), _ptr(fu), n, h, w, c, max_disp, _ptr(x),
@@ -657,8 +761,8 @@ class _CorrConcat(torch.autograd.Function):
         max_disp, cp, nk, has_flow = ctx.meta
         n, h, w, c = f1.shape
         dx = dx.contiguous()
-        df1 = torch.empty_like(f1)
-        df2 = torch.empty_like(f2w) if ctx.needs_input_grad[1] else None
+        df1 = new_grad(ctx.dst[0], f1)
+        df2 = new_grad(ctx.dst[1], f2w) if ctx.needs_input_grad[1] else None
         dflow = None
         if has_flow and ctx.needs_input_grad[2]:
             dflow = torch.empty((n, h, w, 2), device=dx.device)
@@ -682,6 +786,7 @@ class _Warp(torch.autograd.Function):
         n, h, w, c = inp.shape
         assert flow.shape == (n, h, w, 2), "flow must be (B, h, w, 2) like features"
         out = torch.empty_like(inp)
+        ctx.dst = grad_dst(inp)
         call("of_bilinear_fwd" if absolute else "of_warp_fwd", _ptr(inp), n, h, w, c,
              _ptr(flow), _ptr(out), _stream())
         ctx.save_for_backward(inp, flow)
@@ -696,7 +801,7 @@ class _Warp(torch.autograd.Function):
         s = _stream()
         dinp = None
         if ctx.needs_input_grad[0]:
-            dinp = torch.empty_like(inp)
+            dinp = new_grad(ctx.dst, inp)
             call("of_fill", _ptr(dinp), 0.0, dinp.numel(), s)
         dflow = torch.empty_like(flow)
         call("of_bilinear_bwd" if ctx.absolute else "of_warp_bwd", _ptr(dout), _ptr(inp), n, h,
@@ -753,20 +858,63 @@ def split_pair(batch_imgs):
     return out
 
 
+class GradSlab:
+    """The (2B, ...) gradient buffer of a Siamese activation, allocated on first use.  The
+    backward of a consumer of one half writes that half's gradient straight into it
+    (``grad_dst``), so _Halves.backward returns the slab without copying.  A half is handed
+    out once; a second consumer of the same half gets a fresh tensor (autograd then sums as
+    usual and _Halves falls back to copying)."""
+
+    def __init__(self, shape, device):
+        self.shape, self.device = tuple(shape), device
+        self.full = None
+        self.given = [False, False]
+
+    def half(self, k):
+        n = self.shape[0] // 2
+        if self.given[k]:
+            return torch.empty((n,) + self.shape[1:], device=self.device)
+        if self.full is None:
+            self.full = torch.empty(self.shape, device=self.device)
+        self.given[k] = True
+        return self.full.narrow(0, k * n, n)
+
+
+def grad_dst(t):
+    """Forward-time capture: where the gradient of input ``t`` should be written."""
+    return getattr(t, "_of_grad_slab", None)
+
+
+def new_grad(dst, like):
+    """Backward-time buffer for an input gradient captured by grad_dst()."""
+    if dst is not None:
+        return dst[0].half(dst[1])
+    return torch.empty_like(like)
+
+
 class _Halves(torch.autograd.Function):
-    """Split a (2B, ...) Siamese activation into its two (B, ...) halves; the backward writes
-    both halves' gradients into one buffer (no zero-fill + add of slice backward)."""
+    """Split a (2B, ...) Siamese activation into its two (B, ...) halves; the backward returns
+    the GradSlab both halves' gradients were written into (no copies when the consumers used
+    it), else writes them into one buffer."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, slab):
         n = x.shape[0] // 2
         ctx.shape = x.shape
+        ctx.slab = slab
         return x.narrow(0, 0, n), x.narrow(0, n, n)
 
     @staticmethod
     def backward(ctx, g1, g2):
         shape = ctx.shape
+        slab = ctx.slab
         n = shape[0] // 2
+        if slab.full is not None and g1 is not None and g2 is not None:
+            base = slab.full.data_ptr()
+            half_bytes = slab.full.numel() // 2 * slab.full.element_size()
+            if (g1.data_ptr() == base and g2.data_ptr() == base + half_bytes and
+                    g1.is_contiguous() and g2.is_contiguous()):
+                return slab.full, None
         dev = (g1 if g1 is not None else g2).device
         out = torch.empty(shape, device=dev)
         half = out.numel() // 2
@@ -778,11 +926,15 @@ class _Halves(torch.autograd.Function):
             else:
                 g = g.contiguous()
                 call("of_copy_strided", _ptr(g), 1, dst, 1, half, 1, s)
-        return out
+        return out, None
 
 
 def halves(x):
-    return _Halves.apply(x)
+    slab = GradSlab(x.shape, x.device)
+    f1, f2 = _Halves.apply(x, slab)
+    f1._of_grad_slab = (slab, 0)
+    f2._of_grad_slab = (slab, 1)
+    return f1, f2
 
 
 # ================================================================ photometric loss =====

@@ -355,3 +355,38 @@ def test_conv_split_k_matches_unsplit(stride):
     (R.conv2d_same(xo, f64(wt), None, stride) * f64(g)).sum().backward()
     ref = torch.where(f64(x) > 0, xo.grad, 0.3 * xo.grad)
     assert rel_inf(dx1, ref) < REL_TOL and rel_inf(dx2, ref) < REL_TOL
+
+
+@pytest.mark.parametrize("n,h,w,c,with_g", [(2, 8, 12, 64, True), (1, 6, 10, 16, False)])
+def test_maxpool_bn_act_bwd_fused(n, h, w, c, with_g):
+    """The stem's fused backward (max-pool backward + out0's second gradient + BN/ReLU
+    backward) against torch autograd of relu(bn(z)) -> {out0, maxpool} in float64."""
+    import ctypes as C
+    from optical_flow_amd._lib import call, lib
+    torch.manual_seed(0)
+    z = torch.randn(n, h, w, c, dtype=torch.float64)
+    gamma = 1 + 0.2 * torch.rand(c, dtype=torch.float64)
+    beta = 0.1 * torch.randn(c, dtype=torch.float64)
+    mean = 0.1 * torch.randn(c, dtype=torch.float64)
+    var = 1 + 0.2 * torch.rand(c, dtype=torch.float64)
+    dyp = torch.randn(n, h // 2, w // 2, c, dtype=torch.float64)
+    g = torch.randn(n, h, w, c, dtype=torch.float64) if with_g else None
+    zr = z.clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    y = torch.relu((zr - mean) * (gr / torch.sqrt(var + 1e-3)) + br)
+    pooled = torch.nn.functional.max_pool2d(y.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    loss = (pooled * dyp).sum() + ((y * g).sum() if with_g else 0)
+    loss.backward()
+    yv = y.detach()
+    dv = lambda t: t.float().cuda().contiguous()
+    outs = [torch.empty(n, h, w, c, device="cuda")] + [torch.zeros(c, device="cuda") for _ in range(3)]
+    ws = torch.empty(lib().of_maxpool_bn_act_bwd_workspace(n, h, w, c) // 4 + 1, device="cuda")
+    P = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
+    args = [dv(dyp), dv(g) if with_g else None, dv(yv), dv(z), dv(gamma), dv(mean), dv(var)]
+    call("of_maxpool_bn_act_bwd", n, h, w, c, *[P(t) for t in args], 1e-3, P(outs[0]), P(outs[1]),
+         P(outs[2]), P(outs[3]), 0, P(ws), None)
+    torch.cuda.synchronize()
+    dz, dg, db, dbias = [o.double().cpu() for o in outs]
+    exp_dbias = zr.grad.sum(dim=(0, 1, 2))
+    for got, exp in [(dz, zr.grad), (dg, gr.grad), (db, br.grad), (dbias, exp_dbias)]:
+        assert ((got - exp).abs().max() / exp.abs().max()).item() < 1e-5

@@ -33,12 +33,13 @@ def main():
         print("| `%s` | %s | %.2f | %.1f | %.4f |" % (
             r["Name"][:90], r["Calls"], float(r["TotalDurationNs"]) / 1e6,
             100 * float(r["TotalDurationNs"]) / tot, float(r["AverageNs"]) / 1e6))
-    print("\nPer-kernel hipEvent table from the bench (ms per step):\n")
+    print("\nPer-kernel hipEvent table from the bench (instrumented steps, all convs on one "
+          "stream):\n")
     print("| instance | launches/step | ms/step | TFLOP/s |")
     print("|---|---|---|---|")
     for k, v in rf.get("per_kernel", {}).items():
-        print("| %s | %d | %.3f | %.1f |" % (k, v["launches"] // max(1, b["steps"] // b["steps"]),
-                                            v["ms"], v["tflops"]))
+        print("| %s | %d | %.3f | %.1f |" % (k, v["launches_per_step"], v["ms_per_step"],
+                                            v["tflops"]))
 
 
 if __name__ == "__main__":
