@@ -8,9 +8,10 @@ synthetic batch resident in HBM.  Launch: ``python bench.py`` (N=1) or
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
 
 Prints ONE JSON line (rank 0) with the contract fields plus:
-  roofline      -- dominant kernel (the fp32 MFMA implicit-GEMM conv) measured with hipEvents
-                   around every conv launch of extra instrumented steps on the launch stream:
-                   achieved = algorithmic FLOPs / launch duration, vs the fp32 MFMA peak.
+  roofline      -- dominant kernel (the conv instance with the largest total time) measured
+                   with a hipEvent pair around every conv launch of the timed steps, on the
+                   stream it is launched on: achieved = algorithmic FLOPs / launch duration,
+                   vs the MFMA peak of the dtype.
   cpu_baseline  -- the CPU oracle (reference semantics restated in torch-CPU fp32) timed on
                    this host on a bounded sample (1 pair at 384x512), rank 0 only.
   parity        -- EPE / loss error between the HIP path and that oracle run on the same
@@ -152,7 +153,12 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
-    ap.add_argument("--timing-steps", type=int, default=2)
+    ap.add_argument("--timing-steps", type=int, default=2,
+                    help="steps whose conv launches carry hipEvent pairs: the last ones of the "
+                         "timed region (or, with --roofline-window extra, extra steps)")
+    ap.add_argument("--roofline-window", choices=["timed", "extra"], default="timed",
+                    help="timed: per-launch hipEvents over the timed steps (default); extra: "
+                         "separate instrumented steps with every conv on one stream")
     ap.add_argument("--levels", type=int, choices=[4, 5], default=4,
                     help="5: the reference's commented-out 5th pyramid level (model.py:24-25)")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
@@ -191,17 +197,29 @@ def main():
         loss_hip = float(LossLayer()(batch[:1].contiguous(), [f.cuda() for f in flows_hip]))
 
     # ---- training throughput --------------------------------------------------------------
+    # The roofline timing is taken live in the timed region: over its last --timing-steps
+    # steps every conv launch is bracketed by a hipEvent pair on the stream it is launched on
+    # (of_timing_enable), so the per-kernel durations are those of the measured run.  (Event
+    # pairs on every step cost 2-4 % of the step: host-side records for ~110 launches.)
+    lib = _lib.lib()
     for i in range(args.warmup):
         trainer.train_step(batch, i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    live = args.roofline_window == "timed"
+    timed_from = max(0, args.steps - args.timing_steps)      # the last timing_steps steps
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if live and i == timed_from:
+            ops.TIMING_TAGS = []
+            lib.of_timing_enable(1)
         loss, flows = trainer.train_step(batch, args.warmup + i)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if live:
+        lib.of_timing_enable(0)
     if world > 1:
         dist.barrier()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
@@ -214,22 +232,20 @@ def main():
     # the warp backward's atomics depend on where the flows send samples (clipped borders)
     flow_abs = [[round(float(f.abs().mean()), 4), round(float(f.abs().max()), 3)] for f in flows]
 
-    # ---- dominant-kernel roofline (instrumented extra steps, outside the timed region) ----
-    # The weight-gradient kernels normally run on a side stream, concurrently with the input
-    # gradients; per-launch hipEvent durations would then include the other stream's share
-    # of the GPU.  The instrumented steps therefore run every conv on one stream, so each
-    # launch's duration is its own.
-    lib = _lib.lib()
-    ops.TIMING_TAGS = []
-    ops.SIDE_STREAM_WGRAD = False
-    lib.of_timing_enable(1)
-    for i in range(args.timing_steps):
-        trainer.train_step(batch, 10_000 + i)
-    torch.cuda.synchronize()
-    lib.of_timing_enable(0)
-    ops.SIDE_STREAM_WGRAD = bool(args.side_stream)
+    # ---- dominant-kernel roofline ------------------------------------------------------------
+    nsteps = args.steps - timed_from
+    if not live:   # --roofline-window extra: separate instrumented steps, convs on one stream
+        nsteps = args.timing_steps
+        ops.TIMING_TAGS = []
+        ops.SIDE_STREAM_WGRAD = False
+        lib.of_timing_enable(1)
+        for i in range(args.timing_steps):
+            trainer.train_step(batch, 10_000 + i)
+        torch.cuda.synchronize()
+        lib.of_timing_enable(0)
+        ops.SIDE_STREAM_WGRAD = bool(args.side_stream)
     tags, ops.TIMING_TAGS = ops.TIMING_TAGS, None
-    cap = 4096
+    cap = 16384
     kinds = (C.c_int * cap)()
     flops = (C.c_double * cap)()
     ms = (C.c_float * cap)()
@@ -245,7 +261,7 @@ def main():
                         "ms": ms[i]} for i in range(n)], f)
     dom = max(per, key=lambda k: per[k][1]) if per else None
     roof = None
-    conv_ms_step = sum(v[1] for v in per.values()) / max(args.timing_steps, 1)
+    conv_ms_step = sum(v[1] for v in per.values()) / max(nsteps, 1)
     if dom is not None:
         tf, tm, cnt = per[dom]
         achieved = tf / (tm * 1e-3) / 1e12
@@ -263,12 +279,14 @@ def main():
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "launches_per_step": cnt // max(args.timing_steps, 1),
+                "launches_per_step": cnt // max(nsteps, 1),
+                "window": ("timed region, %d steps" % nsteps) if live else
+                          ("%d extra steps, convs on one stream" % nsteps),
                 "avg_launch_ms": round(tm / cnt, 4), "gflop_per_launch": round(tf / cnt / 1e9, 3),
                 "all_conv_gemm_tflops": round(allconv, 2),
                 "per_kernel": {kind_name(k):
-                               {"launches_per_step": v[2] // max(args.timing_steps, 1),
-                                "ms_per_step": round(v[1] / max(args.timing_steps, 1), 3),
+                               {"launches_per_step": v[2] // max(nsteps, 1),
+                                "ms_per_step": round(v[1] / max(nsteps, 1), 3),
                                 "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
                                for k, v in sorted(per.items())}}
 

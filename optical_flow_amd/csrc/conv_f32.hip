@@ -953,15 +953,17 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
     store_b(0);
   }
   __syncthreads();
+  // The next chunk's halo is fetched at the first step of the current chunk and stored after
+  // its last step (KS steps of latency cover); B one step ahead into the other buffer.  Only
+  // the halo store needs the pre-store barrier: the B buffer written at step q was last read
+  // at step q-1, which every wave finished before step q-1's closing barrier.
   for (int q = 0; q < steps; ++q) {
     const int r = q % KS, buf = q & 1;
     const bool more = q + 1 < steps;
     const int nq = q + 1;
     const int nc = c_begin + nq / KS, nr = nq % KS;
-    if (more) {
-      load_b(nc, nr);
-      if (nr == 0) load_halo(nc);
-    }
+    if (more) load_b(nc, nr);
+    if (r == 0 && q + KS < steps) load_halo(c_begin + q / KS + 1);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int dh = MODE == MODE_FWD ? r * HW + s : -(r * HW + s);
@@ -982,7 +984,7 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
       }
     }
-    __syncthreads();
+    if (more && nr == 0) __syncthreads();           // all reads of this chunk's halo done
     if (more) {
       store_b(buf ^ 1);
       if (nr == 0) store_halo();

@@ -6,6 +6,7 @@ Tensors are NHWC float32 on the GPU.  Each Function cites the reference op it re
 from __future__ import annotations
 
 import contextlib
+import os
 import ctypes as C
 from typing import Optional
 
@@ -93,6 +94,10 @@ def _grad_ready(*params):
 # end of the autograd backward (engine callback), so .backward() returning still means every
 # gradient kernel is ordered before whatever the caller enqueues next.
 SIDE_STREAM_WGRAD = True
+# Only layers with at most this many output pixels put their wgrad on the side stream: the
+# overlap pays where grids underfill the chip (coarse flow levels, encoder stages 3-4); a
+# large layer's dgrad already fills it, and sharing the CUs would only stretch both kernels.
+SIDE_STREAM_MAX_PIX = int(os.environ.get("OFLOW_SIDE_MAX_PIX", "65536"))
 _SIDE = {}
 _side_armed = False
 
@@ -359,7 +364,8 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
         tk = grad_target(layer.kernel)
         tbias = grad_target(layer.bias) if (need_b and not bias_done) else (None, 0, None)
         went, wsb = layer.wgrad_entry(d)
-        side = SIDE_STREAM_WGRAD and tk[1] == 1 and (tbias[0] is None or tbias[1] == 1)
+        side = (SIDE_STREAM_WGRAD and tk[1] == 1 and (tbias[0] is None or tbias[1] == 1) and
+                d.n * d.ho * d.wo <= SIDE_STREAM_MAX_PIX)
         with torch.cuda.stream(side_stream(x, dzp)) if side else contextlib.nullcontext():
             ss = _stream()
             ws = torch.empty(wsb // 4 + 1, device=dz.device)
@@ -631,7 +637,7 @@ class _ConvStackFn(torch.autograd.Function):
             if tk[1] != tb[1]:
                 raise RuntimeError("kernel and bias gradients must both use the arena or not")
             went, wsb = layer.wgrad_entry(d)
-            side = SIDE_STREAM_WGRAD and tk[1] == 1
+            side = SIDE_STREAM_WGRAD and tk[1] == 1 and d.n * d.ho * d.wo <= SIDE_STREAM_MAX_PIX
             with torch.cuda.stream(side_stream(x, g)) if side else contextlib.nullcontext():
                 ws = torch.empty(wsb // 4 + 1, device=x.device)
                 _tag(layer, 2)

@@ -1,5 +1,6 @@
 """Per-kernel parity: every HIP kernel through the C ABI vs the CPU oracle (float64) on the
 same seeded inputs.  Tolerance: 1e-3 relative (REL_TOL), per BASELINE.json's north star."""
+import zlib
 import pytest
 import torch
 
@@ -47,7 +48,25 @@ def test_conv_fwd_bwd(case):
     ops = _ops()
     from optical_flow_amd._lib import ACT_LEAKY, ACT_NONE, ACT_RELU
     n, h, w, cin, cout, k, s, act, use_bn, use_res = case
-    seed = hash(case) % 1000
+    seed = zlib.crc32(repr(case).encode()) % 1000   # (hash() of str is salted per process)
+    if act != "none":
+        # Reseed until no pre-activation sits within 1e-4 of the ReLU/LeakyReLU kink, where a
+        # 1-ulp fp32 difference would flip the derivative (a data property, not a kernel bug).
+        for _ in range(20):
+            xx = rng_tensor((n, h, w, cin), seed)
+            ww = rng_tensor((k, k, cin, cout), seed + 1, scale=(2.0 / (k * k * cin)) ** 0.5)
+            pre = R.conv2d_same(f64(xx), f64(ww), f64(rng_tensor((cout,), seed + 2, scale=0.1)), s)
+            if use_bn:
+                pre = R.batchnorm_inference(pre, {
+                    "bn/gamma": f64(rng_tensor((cout,), seed + 3, lo=0.5, hi=1.5)),
+                    "bn/beta": f64(rng_tensor((cout,), seed + 4, scale=0.1)),
+                    "bn/moving_mean": f64(rng_tensor((cout,), seed + 5, scale=0.1)),
+                    "bn/moving_variance": f64(rng_tensor((cout,), seed + 6, lo=0.5, hi=1.5))}, "bn")
+            if use_res:
+                pre = pre + f64(rng_tensor(tuple(pre.shape), seed + 7))
+            if pre.abs().min().item() > 1e-4:
+                break
+            seed += 1000
     x = rng_tensor((n, h, w, cin), seed)
     wt = rng_tensor((k, k, cin, cout), seed + 1, scale=(2.0 / (k * k * cin)) ** 0.5)
     b = rng_tensor((cout,), seed + 2, scale=0.1)
@@ -111,7 +130,7 @@ def test_conv_bf16(case):
     ops = _ops()
     from optical_flow_amd._lib import ACT_LEAKY, ACT_NONE, ACT_RELU
     n, h, w, cin, cout, k, s, act, use_bn, use_res = case
-    seed = hash(case) % 1000 + 17
+    seed = zlib.crc32(repr(case).encode()) % 1000 + 17   # stable across processes
     x = rng_tensor((n, h, w, cin), seed)
     wt = rng_tensor((k, k, cin, cout), seed + 1, scale=(2.0 / (k * k * cin)) ** 0.5)
     b = rng_tensor((cout,), seed + 2, scale=0.1)

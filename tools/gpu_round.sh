@@ -2,7 +2,7 @@
 # Round-end evidence in one GPU call: smoke, GPU tests, the default bench (fp32 config 2,
 # with the CPU baseline), its rocprofv3 kernel-trace summary, FETCH_SIZE / WRITE_SIZE PMC
 # passes, conv and flow micro-benchmarks, and the bf16 (config 3) bench with its summary.
-cd "$GRAFT_REPO_ROOT"
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/round}
 mkdir -p "$OUT"
@@ -29,4 +29,7 @@ run 600 python bench.py --precision bf16 --batch 32 --cpu-steps 0 > "$OUT/bench_
 grep '^{' "$OUT/bench_bf16.log" | head -c 300; echo
 run 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bf16" -o bench -- \
   python bench.py --precision bf16 --batch 32 --no-cpu-baseline > "$OUT/bench_bf16_prof.log" 2>&1 || { echo rocprof bf16 failed; exit 1; }
+run 300 python tools/data_bench.py --batch 8 --out "$OUT/data_bench.json" > "$OUT/data_bench.log" 2>&1 || { echo data bench failed; exit 1; }
+run 600 python bench.py --precision bf16 --height 768 --width 1024 --batch 8 --no-cpu-baseline > "$OUT/bench_cfg5.log" 2>&1 || { echo cfg5 bench failed; exit 1; }
+grep '^{' "$OUT/bench_cfg5.log" | head -c 300; echo
 echo done
