@@ -1979,7 +1979,12 @@ GemmArgs fwd_args(const of_conv_desc* d, const Geo& g, bool bf16 = false) {
   return a;
 }
 
-GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g, bool bf16 = false) {
+// skip_empty: the output already holds the added gradient (in-place accumulation, dx == add),
+// so the stride-2 phase groups that no tap reaches (3 of 4 for a 1x1 stride-2 projection)
+// launch no tiles at all instead of rewriting dx = add.  Splits stay as planned for the
+// full grid, so the slab fits of_conv2d_dgrad_workspace().
+GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g, bool bf16 = false,
+                    bool skip_empty = false) {
   GemmArgs a = base_args(d);
   a.kc = g.cout_p;
   a.N = g.cin_p;
@@ -2023,6 +2028,16 @@ GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g, bool bf16 = false) {
     single_group(a, d, a.M, kmax);
   }
   plan_splits(a, kmax, bf16 ? BKH : BK);
+  if (skip_empty && a.phase) {
+    int tiles = 0;
+    for (int c = 0; c < 4; ++c) {
+      Group& G = a.grp[c];
+      if (G.ntaps == 0) G.m_tiles = 0;
+      G.tiles_begin = tiles;
+      tiles += G.m_tiles;
+    }
+    a.tiles_total = tiles * a.n_tiles;
+  }
   return a;
 }
 
@@ -2448,7 +2463,9 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
     return st;
   }
   const bool tile = bf16 && tile_ok(d);
-  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD) : dgrad_args(d, g, bf16);
+  const bool in_place = add && add == dx && ld_add == lddx;
+  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD) : dgrad_args(d, g, bf16, in_place);
+  if (a.tiles_total == 0) return OF_OK;                 // every output already final
   attach_slab(a, workspace, ws_bytes, tile ? 1 : bf16 ? BKH : BK);
   a.A = dy;
   a.lda = lddy;

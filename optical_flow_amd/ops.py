@@ -469,7 +469,8 @@ def _res_block_backward(block, saved, dy, need, extra=None):
     gb = gb[:-1]
     if p is not None:
         dxp, *gp = _conv_backward(p, x, yp, zp, dres, False, (need_x, *nb(2), False),
-                                  add=extra if need_x else None)
+                                  add=extra if need_x else None,
+                                  dx_out=extra if need_x else None)   # in place: see below
         gp = gp[:-1]
         add, dx_out = dxp, dxp
     else:

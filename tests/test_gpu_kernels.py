@@ -409,3 +409,28 @@ def test_maxpool_bn_act_bwd_fused(n, h, w, c, with_g):
     exp_dbias = zr.grad.sum(dim=(0, 1, 2))
     for got, exp in [(dz, zr.grad), (dg, gr.grad), (db, br.grad), (dbias, exp_dbias)]:
         assert ((got - exp).abs().max() / exp.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("k,s", [(1, 2), (3, 2), (3, 1)])
+def test_dgrad_add_in_place(k, s):
+    """of_conv2d_dgrad_add with dx == add (in-place accumulation; 1x1 stride 2 then launches
+    only the phase group a tap reaches) equals the out-of-place result."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd._lib import ACT_NONE, call
+    n, h, w, cin, cout = 2, 16, 20, 64, 128
+    wt = dev(rng_tensor((k, k, cin, cout), 7, scale=0.1))
+    layer = ops.ConvLayer(wt, dev(rng_tensor((cout,), 8)), stride=s, act=ACT_NONE, cin_p=cin)
+    d = layer.desc(n, h, w)
+    _, wd = layer.packed(d)
+    dy = dev(rng_tensor((n, d.ho, d.wo, cout), 9))
+    add = dev(rng_tensor((n, h, w, cin), 10))
+    entry, wsz = layer.dgrad_add_entry(d)
+    P = lambda t: C.c_void_p(t.data_ptr())
+    ws = torch.empty(wsz // 4 + 1, device="cuda")
+    out = torch.empty_like(add)
+    call(entry, C.byref(d), P(dy), cout, P(wd), P(add), cin, P(out), cin, P(ws), wsz, None)
+    inplace = add.clone()
+    call(entry, C.byref(d), P(dy), cout, P(wd), P(inplace), cin, P(inplace), cin, P(ws), wsz, None)
+    torch.cuda.synchronize()
+    assert torch.equal(inplace, out)
