@@ -826,12 +826,22 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
 // fwd:   out(oy, ox) += in(oy + r - pt, ox + s - pl) . W[r][s]
 // dgrad: out(iy, ix) += dy(iy + pt - r, ix + pl - s) . W[r][s]^T
 // GEMM K = channel chunks: a.K = chunks, a.k_per_split = chunks per K slice.
-constexpr int TT_H = 8, TT_W = 16;
+constexpr int TT_H = 8, TT_W = 16;   // wgrad halo tiles
+// fwd / dgrad halo tiles (conv_tile_bf16): 4 rows x 32 px.  A wave's 32 A-fragment rows are
+// then 32 consecutive halo pixels of one row: with the 80-byte pixel pitch their ds_read_b128
+// 16-byte slots (5 p mod 16) are distinct in every 16-lane bank group.  An 8 x 16 tile puts
+// lanes 16-31 on the next halo row (18 px later) and collides in 2 of 16 slots per group
+// (SQ_LDS_BANK_CONFLICT was 40 % of the LDS cycles).
+#ifndef OF_TF_H
+#define OF_TF_H 4
+#define OF_TF_W 32
+#endif
+constexpr int TF_H = OF_TF_H, TF_W = OF_TF_W;
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE>
 __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
-  constexpr int BM = TT_H * TT_W, KS = 3;
-  constexpr int HH = TT_H + KS - 1, HW = TT_W + KS - 1, HP = HH * HW;
+  constexpr int BM = TF_H * TF_W, KS = 3;
+  constexpr int HH = TF_H + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
   static_assert(WAVES_M * WAVES_N == 4 && TM >= 1 && TN >= 1, "tile");
@@ -851,10 +861,10 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
   const int n0 = tile_n * BN;
   const int OH = MODE == MODE_FWD ? a.ho : a.h, OW = MODE == MODE_FWD ? a.wo : a.w;
   const int SH = MODE == MODE_FWD ? a.h : a.ho, SW = MODE == MODE_FWD ? a.w : a.wo;
-  const int tiles_x = (OW + TT_W - 1) / TT_W, tiles_y = (OH + TT_H - 1) / TT_H;
+  const int tiles_x = (OW + TF_W - 1) / TF_W, tiles_y = (OH + TF_H - 1) / TF_H;
   const int b = tile_m / (tiles_x * tiles_y);
   const int trem = tile_m - b * tiles_x * tiles_y;
-  const int oy0 = (trem / tiles_x) * TT_H, ox0 = (trem % tiles_x) * TT_W;
+  const int oy0 = (trem / tiles_x) * TF_H, ox0 = (trem % tiles_x) * TF_W;
   const int hy0 = MODE == MODE_FWD ? oy0 - a.pt : oy0 + a.pt - (KS - 1);
   const int hx0 = MODE == MODE_FWD ? ox0 - a.pl : ox0 + a.pl - (KS - 1);
   const int c_begin = split * a.k_per_split;
@@ -942,7 +952,7 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wm0 + 32 * i + lrow;
-    const int ty = m / TT_W, tx = m % TT_W;
+    const int ty = m / TF_W, tx = m % TF_W;
     a_hp[i] = MODE == MODE_FWD ? ty * HW + tx : (ty + KS - 1) * HW + tx + KS - 1;
   }
 
@@ -1006,14 +1016,14 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
-        const int oy = oy0 + m / TT_W, ox = ox0 + m % TT_W;
+        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
         aux[rr] = a.splits == 1 && oy < OH && ox < OW
                       ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : EpAux{0.f, 0.f};
       }
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
-        const int oy = oy0 + m / TT_W, ox = ox0 + m % TT_W;
+        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
         if (oy >= OH || ox >= OW) continue;
         const int64_t row = img + (int64_t)oy * OW + ox;
         if (a.splits > 1)
@@ -2093,8 +2103,8 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode) {
   a.nb = fwd ? d->cout : g.nd;
   a.ldb = fwd ? g.kf16 : (int)g.kd16;
   const int OH = fwd ? d->ho : d->h, OW = fwd ? d->wo : d->w;
-  const int m_tiles = d->n * (int)cdiv(OH, TT_H) * (int)cdiv(OW, TT_W);
-  a.bm = TT_H * TT_W;
+  const int m_tiles = d->n * (int)cdiv(OH, TF_H) * (int)cdiv(OW, TF_W);
+  a.bm = TF_H * TF_W;
   a.ngroups = 1;
   Group& G = a.grp[0];
   G = Group{};
