@@ -1284,6 +1284,13 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
   __shared__ uint4 Ds[2][COB * 16];
   __shared__ float csum[NG][COB];
 
+  // LDS swizzles (conflict-free for both the transposing ds_write_b128 stores, 8 lanes =
+  // 8 channel quads / co quads, and the MFMA fragment ds_read_b128 reads, 16-lane groups;
+  // checked exhaustively offline): x row of channel ci -> xrow(ci), its two 16-byte
+  // pixel octets swapped when bit 4 of ci is set; dy row co: octet o -> o ^ dsw(co).
+  auto xrow = [](int ci) { return ci ^ ((ci >> 2) & 2); };
+  auto xoct = [](int ci) { return (ci >> 4) & 1; };
+  auto dsw = [](int co) { return ((co & 15) ^ (((co >> 2) & 7) << 1)) & 15; };
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1360,13 +1367,12 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
                                        make_float4(v[4].z, v[5].z, v[6].z, v[7].z));
           const uint4 r3 = pack_bf16x8(make_float4(v[0].w, v[1].w, v[2].w, v[3].w),
                                        make_float4(v[4].w, v[5].w, v[6].w, v[7].w));
-          const int ci = 4 * xcq;                     // ci & 8 is the same for the quad
-          const int oct = half ^ ((ci >> 3) & 1);
-          uint4* row = &Xs[buf][((s * HH + hy) * CIB + ci) * 2 + oct];
-          row[0] = r0;
-          row[2] = r1;
-          row[4] = r2;
-          row[6] = r3;
+          const int ci = 4 * xcq;
+          uint4* blk = &Xs[buf][(s * HH + hy) * CIB * 2];
+          blk[xrow(ci) * 2 + (half ^ xoct(ci))] = r0;
+          blk[xrow(ci + 1) * 2 + (half ^ xoct(ci + 1))] = r1;
+          blk[xrow(ci + 2) * 2 + (half ^ xoct(ci + 2))] = r2;
+          blk[xrow(ci + 3) * 2 + (half ^ xoct(ci + 3))] = r3;
         }
       }
     }
@@ -1383,10 +1389,10 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
       const uint4 r3 = pack_bf16x8(make_float4(v[0].w, v[1].w, v[2].w, v[3].w),
                                    make_float4(v[4].w, v[5].w, v[6].w, v[7].w));
       const int co = 4 * dcq;
-      Ds[buf][(co + 0) * 16 + (o ^ ((co + 0) & 15))] = r0;
-      Ds[buf][(co + 1) * 16 + (o ^ ((co + 1) & 15))] = r1;
-      Ds[buf][(co + 2) * 16 + (o ^ ((co + 2) & 15))] = r2;
-      Ds[buf][(co + 3) * 16 + (o ^ ((co + 3) & 15))] = r3;
+      Ds[buf][(co + 0) * 16 + (o ^ dsw(co + 0))] = r0;
+      Ds[buf][(co + 1) * 16 + (o ^ dsw(co + 1))] = r1;
+      Ds[buf][(co + 2) * 16 + (o ^ dsw(co + 2))] = r2;
+      Ds[buf][(co + 3) * 16 + (o ^ dsw(co + 3))] = r3;
       if (do_colsum) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) add4(colacc, v[e]);
@@ -1402,8 +1408,9 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
   const int wci0 = (wave / WAVES_CO) * 32;
   const int wco0 = (wave % WAVES_CO) * 32;
   const int lrow = lane & 31, lk = lane >> 5;
-  const int a_base = (wci0 + lrow) * 2 + (lk ^ ((lrow >> 3) & 1));
+  const int a_base = xrow(wci0 + lrow) * 2 + (lk ^ xoct(wci0 + lrow));
   const int b_base = (wco0 + lrow) * 16;
+  const int b_sw = dsw(wco0 + lrow);
 
   if (steps > 0) {
     load(t_begin);
@@ -1416,7 +1423,7 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
     if (more) load(t_begin + i + 1);
 #pragma unroll
     for (int kk = 0; kk < TT_H; ++kk) {
-      const bf16x8 bv = __builtin_bit_cast(bf16x8, Ds[buf][b_base + ((2 * kk + lk) ^ (lrow & 15))]);
+      const bf16x8 bv = __builtin_bit_cast(bf16x8, Ds[buf][b_base + ((2 * kk + lk) ^ b_sw)]);
 #pragma unroll
       for (int r = 0; r < KS; ++r)
 #pragma unroll
