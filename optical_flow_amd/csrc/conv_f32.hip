@@ -1660,6 +1660,90 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a) {
   }
 }
 
+// Split-K epilogue for a few slices over many rows (the common case: 2-6 slices of a layer
+// whose tile grid half-fills the chip).  One (slab row, 4 columns) item per thread in a
+// grid-stride loop; the slices are summed in order with four loads in flight, then the fused
+// epilogue runs on all four columns.  VEC: every row-major operand takes 16-byte accesses
+// (host-checked alignment and leading dimensions).  The 8-lane kernel above is kept for many
+// slices over few rows, where one thread per item would serialise the slice loads.
+__device__ __forceinline__ float4 ld4(const float* p) {
+  return *reinterpret_cast<const float4*>(p);
+}
+
+template <int MODE, bool VEC>
+__global__ __launch_bounds__(256) void splitk_epilogue_flat(GemmArgs a) {
+  const int nq = (a.N + 3) / 4;
+  const int64_t items = (int64_t)(a.tiles_total / a.n_tiles) * a.bm * nq;
+  const int64_t ss = a.split_stride;
+  for (int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; item < items;
+       item += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(item % nq);
+    const int64_t srow = item / nq;
+    const int tm = (int)(srow / a.bm);
+    int gi = 0;
+    for (int g = 1; g < a.ngroups; ++g)
+      if (tm >= a.grp[g].tiles_begin) gi = g;
+    const Group& G = a.grp[gi];
+    const int m = (int)(srow - (int64_t)G.tiles_begin * a.bm);
+    if (m >= G.M) continue;
+    const float* src = a.slab + srow * a.slab_ld + 4 * q;
+    float4 acc = ld4(src);
+    int z = 1;
+    for (; z + 4 <= a.splits; z += 4) {
+      const float4 p0 = ld4(src + z * ss), p1 = ld4(src + (z + 1) * ss);
+      const float4 p2 = ld4(src + (z + 2) * ss), p3 = ld4(src + (z + 3) * ss);
+      add4(acc, p0);
+      add4(acc, p1);
+      add4(acc, p2);
+      add4(acc, p3);
+    }
+    for (; z < a.splits; ++z) add4(acc, ld4(src + z * ss));
+    const int64_t row = out_row(a, G, m);
+    float v[4] = {acc.x, acc.y, acc.z, acc.w};
+    const int n0 = 4 * q;
+    if (VEC) {
+      float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), r4 = s4;
+      if (MODE == MODE_FWD && a.res) s4 = ld4(a.res + row * a.ldr + n0);
+      if (MODE == MODE_DGRAD) {
+        s4 = a.act_src ? ld4(a.act_src + row * a.ld_act + n0) : make_float4(1.f, 1.f, 1.f, 1.f);
+        if (a.res) r4 = ld4(a.res + row * a.ldr + n0);
+      }
+      const float s[4] = {s4.x, s4.y, s4.z, s4.w}, r[4] = {r4.x, r4.y, r4.z, r4.w};
+      float zv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float bias, scale, shift;
+        column_params<MODE>(a, n0 + e, bias, scale, shift);
+        if (MODE == MODE_FWD) {
+          v[e] += bias;
+          zv[e] = v[e];
+          if (a.bn_g) v[e] = v[e] * scale + shift;
+          v[e] = act_fwd(v[e] + s[e], a.act, a.alpha);
+        } else {
+          v[e] *= s[e] > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
+          v[e] += r[e];
+        }
+      }
+      if (MODE == MODE_FWD && a.z)
+        *reinterpret_cast<float4*>(a.z + row * a.ldz + n0) = make_float4(zv[0], zv[1], zv[2], zv[3]);
+      *reinterpret_cast<float4*>(a.C + row * a.ldc + n0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      EpAux aux[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        aux[e] = n0 + e < a.N ? epilogue_aux<MODE>(a, row, n0 + e) : EpAux{0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + e;
+        if (n >= a.N) break;
+        float bias, scale, shift;
+        column_params<MODE>(a, n, bias, scale, shift);
+        epilogue_store<MODE>(a, row, n, v[e], bias, scale, shift, aux[e]);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- weight packing --
 __global__ void pack_fwd_kernel(const float* __restrict__ w, int taps, int cin, int cout,
                                 int cin_p, int kf, int nf, float* __restrict__ out) {
@@ -2058,6 +2142,27 @@ GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g, bool bf16 = false,
   return a;
 }
 
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// fwd/dgrad split-K epilogue: the flat kernel unless many slices meet few rows.
+template <int MODE>
+int launch_splitk_epilogue(const GemmArgs& a, hipStream_t s) {
+  const int64_t items = slab_rows(a) * cdiv(a.N, 4);
+  if (a.splits > 8 && items < 65536) {
+    hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0,
+                       s, a);
+    return check_launch("conv_splitk_epilogue");
+  }
+  bool vec = a.N % 4 == 0 && a.ldc % 4 == 0 && al16(a.C);
+  if (a.res) vec = vec && a.ldr % 4 == 0 && al16(a.res);
+  if (MODE == MODE_FWD && a.z) vec = vec && a.ldz % 4 == 0 && al16(a.z);
+  if (MODE == MODE_DGRAD && a.act_src) vec = vec && a.ld_act % 4 == 0 && al16(a.act_src);
+  const dim3 grid((unsigned)std::min<int64_t>(cdiv(items, 256), 8 * kCUs));
+  if (vec) hipLaunchKernelGGL((splitk_epilogue_flat<MODE, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((splitk_epilogue_flat<MODE, false>), grid, dim3(256), 0, s, a);
+  return check_launch("conv_splitk_epilogue");
+}
+
 // Timing kinds: mode * 8 + tile config (0: 128x128, 1: 128x96, 2: 256x64, 3: 256x32) -- one
 // per conv_gemm_f32 template instance.
 template <int MODE>
@@ -2073,10 +2178,7 @@ int launch_gemm(const GemmArgs& a, hipStream_t s, double flops) {
   if (timing_on()) timing_end(s, MODE * 8 + cfg, flops);
   int st = check_launch("conv_gemm_f32");
   if (st || MODE == MODE_WGRAD || a.splits == 1) return st;
-  const int64_t items = slab_rows(a) * cdiv(a.N, 4);
-  hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
-                     a);
-  return check_launch("conv_splitk_epilogue");
+  return launch_splitk_epilogue<MODE>(a, s);
 }
 
 // bf16 instances: timing kinds 64 + mode * 8 + tile config.
@@ -2093,10 +2195,7 @@ int launch_gemm_bf16(const GemmArgs& a, hipStream_t s, double flops) {
   if (timing_on()) timing_end(s, 64 + MODE * 8 + cfg, flops);
   int st = check_launch("conv_gemm_bf16");
   if (st || a.splits == 1) return st;
-  const int64_t items = slab_rows(a) * cdiv(a.N, 4);
-  hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
-                     a);
-  return check_launch("conv_splitk_epilogue");
+  return launch_splitk_epilogue<MODE>(a, s);
 }
 
 // bf16 3x3 stride-1 fwd / dgrad: halo-tiled kernel (conv_tile_bf16).
@@ -2148,10 +2247,7 @@ int launch_tile_bf16(const GemmArgs& a, hipStream_t s, double flops) {
   if (timing_on()) timing_end(s, 64 + 32 + MODE * 8 + cfg, flops);
   int st = check_launch("conv_tile_bf16");
   if (st || a.splits == 1) return st;
-  const int64_t items = slab_rows(a) * cdiv(a.N, 4);
-  hipLaunchKernelGGL(splitk_epilogue_kernel<MODE>, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
-                     a);
-  return check_launch("conv_splitk_epilogue");
+  return launch_splitk_epilogue<MODE>(a, s);
 }
 
 struct WgradPlan {
