@@ -48,26 +48,41 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md; no spar
 def kind_parts(kind):
     """timing kind -> (mode, tile config, family): f32 GEMMs mode*8+cfg (narrow VALU cfg 7),
     f32 halo-tiled wgrad 32 + mode*8 + cfg,
-    bf16 implicit GEMMs 64 + mode*8 + cfg, bf16 halo-tiled 3x3 96 + mode*8 + cfg
+    bf16 implicit GEMMs 64 + mode*8 + cfg, bf16 halo-tiled 3x3 96 + mode*8 + cfg,
+    fp32 on the split-bf16 halo-tiled 3x3 kernels 128 + mode*8 + cfg
     (optical_flow_amd/csrc/conv_f32.hip)."""
-    fam = ("tile_bf16" if kind >= 96 else "bf16" if kind >= 64 else
+    fam = ("tile_x3" if kind >= 128 else "tile_bf16" if kind >= 96 else "bf16" if kind >= 64 else
            "tile_f32" if kind >= 32 else "f32")
     return (kind % 32) // 8, kind % 8, fam
 
 
 TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1"}
+X3_BN = {0: "128, 2, 4", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1"}   # conv_tile_x3 waves
 
 
 WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>
 
 
+def conv_math(precision):
+    """How the convs compute (the dtype field names the arithmetic type, fp32 or bf16)."""
+    from optical_flow_amd import ops
+    if precision == "bf16":
+        return "bf16 MFMA operands, fp32 accumulation (flow convs cout<=4: fp32 VALU)"
+    if ops.F32_SPLIT:
+        return ("fp32: 3x3 stride-1 fwd/dgrad on bf16 MFMA with an exact 3-term operand split "
+                "(6 products, fp32 accumulation; error vs fp64 at fp32-MFMA level, "
+                "test_conv_x3_accuracy); other convs and all wgrad on fp32 MFMA")
+    return "fp32 MFMA (flow convs cout<=4: fp32 VALU)"
+
+
 def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
-    sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32"}[fam]
+    sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
+           "tile_x3": "_tile_x3"}[fam]
     if fam in ("tile_bf16", "tile_f32") and mode == 2:
         return "wgrad%s<%s>" % (sfx, WGT_WAVES[cfg])
-    return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (TILE_BN if fam == "tile_bf16"
-                                                 else TILE_TEMPLATE)[cfg])
+    return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (TILE_BN if fam == "tile_bf16" else
+                                                 X3_BN if fam == "tile_x3" else TILE_TEMPLATE)[cfg])
 
 
 def kernel_symbol(kind):
@@ -77,8 +92,9 @@ def kernel_symbol(kind):
         return NARROW_SYMBOLS[mode]
     if fam in ("tile_bf16", "tile_f32") and mode == 2:
         return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (fam, WGT_WAVES[cfg])
-    if fam == "tile_bf16":
-        return "void oflow::conv_tile_bf16<%s, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode)
+    if fam in ("tile_bf16", "tile_x3"):
+        return "void oflow::conv_%s<%s, %d>(oflow::GemmArgs)" % (
+            fam, (TILE_BN if fam == "tile_bf16" else X3_BN)[cfg], mode)
     if fam == "bf16" and mode == 2:
         return "void oflow::conv_wgrad_bf16<%s>(oflow::GemmArgs)" % TILE_TEMPLATE[cfg]
     return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_TEMPLATE[cfg], mode)
@@ -274,8 +290,10 @@ def main():
             if pmc.get("kernel") == sym and pmc.get("config") == [H, W, B]:
                 traffic = pmc.get("hbm_bytes_per_launch")
         allconv = sum(v[0] for v in per.values()) / (sum(v[1] for v in per.values()) * 1e-3) / 1e12
-        peak = (FP32_MFMA_PEAK_TFLOPS if kind_parts(dom)[2] in ("f32", "tile_f32")
-                else BF16_MFMA_PEAK_TFLOPS)
+        fam = kind_parts(dom)[2]
+        # the split kernel spends six bf16 MFMAs per fp32 product: its ceiling is 1/6 of bf16
+        peak = (FP32_MFMA_PEAK_TFLOPS if fam in ("f32", "tile_f32") else
+                round(BF16_MFMA_PEAK_TFLOPS / 6, 1) if fam == "tile_x3" else BF16_MFMA_PEAK_TFLOPS)
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -331,6 +349,7 @@ def main():
                        "height": H, "width": W, "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": "dp%d" % world,
                        "params": sum(p.numel() for p in net.trainable_weights),
+                       "conv_math": conv_math(args.precision),
                        **({"levels": args.levels} if args.levels != 4 else {})},
             "algorithmic_gflop_per_pair": round(gfp, 2),
             "model_tflops": round(gfp * value / 1e3, 2),

@@ -151,6 +151,30 @@ int of_conv2d_dgrad_bf16(const of_conv_desc* d, const float* dy, int lddy, const
                          const float* act_src, int ld_act, int act, float alpha, float* dx,
                          int lddx, void* workspace, size_t ws_bytes, void* stream);
 
+/* fp32 3x3 stride-1 fwd / dgrad on bf16 MFMA by an exact three-term operand split
+ * (x = hi + mid + lo, 8 significand bits each; six of the nine bf16 products, each exact,
+ * accumulated in fp32; the dropped terms are below 2^-23 |a||b|).  Same arguments and
+ * epilogues as the bf16 variants; the weights are the three split planes of the bf16 images
+ * (3 * of_conv_w{fwd,bwd}16_elems bf16 elements: hi, mid, lo), packed by
+ * of_conv_pack_weights_x3 or of_conv_pack_table_ex with flag 2.  Replaces the same
+ * Conv2D / Conv2DBackpropInput as of_conv2d_fwd / of_conv2d_dgrad (model.py:104-114, the
+ * resnet blocks' 3x3 convs); OF_EINVAL for any other kernel shape or stride. */
+int of_conv_pack_weights_x3(const of_conv_desc* d, const float* w_hwio, void* w3_fwd,
+                            void* w3_bwd, void* stream);
+size_t of_conv2d_fwd_x3_workspace(const of_conv_desc* d);
+size_t of_conv2d_dgrad_x3_workspace(const of_conv_desc* d);
+int of_conv2d_fwd_x3(const of_conv_desc* d, const float* x, int ldx, const void* w3_fwd,
+                     const float* bias, const float* bn_gamma, const float* bn_beta,
+                     const float* bn_mean, const float* bn_var, float bn_eps,
+                     const float* residual, int ldr, int act, float alpha, float* z, int ldz,
+                     float* y, int ldy, void* workspace, size_t ws_bytes, void* stream);
+int of_conv2d_dgrad_x3(const of_conv_desc* d, const float* dy, int lddy, const void* w3_bwd,
+                       const float* act_src, int ld_act, int act, float alpha, float* dx,
+                       int lddx, void* workspace, size_t ws_bytes, void* stream);
+int of_conv2d_dgrad_add_x3(const of_conv_desc* d, const float* dy, int lddy,
+                           const void* w3_bwd, const float* add, int ld_add, float* dx,
+                           int lddx, void* workspace, size_t ws_bytes, void* stream);
+
 /* Activation backward: dz = dy * act'(y) over n elements (y = forward output). */
 int of_act_bwd(const float* dy, const float* y, int act, float alpha, float* dz, int64_t n,
                void* stream);

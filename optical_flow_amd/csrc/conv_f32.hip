@@ -63,6 +63,7 @@ struct GemmArgs {
   int M, N, K;            // wgrad: M = taps*cin_p, K = output pixels
   const float* A; int lda; int64_t a_bytes;
   const float* B; int ldb; int nb; int64_t b_bytes;
+  int64_t b_plane;        // conv_tile_x3: elements between the hi / mid / lo weight planes
   float* C; int ldc;      // final output (epilogue)
   const float* bias;
   const float* bn_g; const float* bn_b; const float* bn_m; const float* bn_v; float bn_eps;
@@ -1035,6 +1036,242 @@ __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
   }
 }
 
+// ---- fp32 on bf16 MFMA by a three-term split, 3x3 stride 1 -------------------------------
+// Every fp32 operand is cut exactly into three bf16 terms, x = hi + mid + lo (8 + 8 + 8
+// significand bits: hi = x with the low 16 bits cleared, mid = the same of x - hi,
+// lo = x - hi - mid), and a.b is accumulated as the six products whose magnitude can reach
+// 2^-16 |a||b|: hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi.  bf16 x bf16 products are
+// exact, the MFMA accumulates in fp32, and the dropped terms (mid.lo, lo.mid, lo.lo) are
+// below 2^-23 |a||b| together: the error per product is that of one fp32 rounding.  Six
+// v_mfma_f32_32x32x16_bf16 do the work of 8 v_mfma_f32_32x32x2_f32 at 16/6 of their peak.
+// Structure as conv_tile_bf16 (4 x 32 output tiles, LDS halo, 9 taps per chunk) with three
+// halo planes and B staged one tap per step (3 planes x BN rows x 32 channels) to fit LDS;
+// the packed weights are three bf16 planes a.b_plane elements apart.
+__device__ __forceinline__ void split3x4(const float4& v, uint2& h, uint2& m, uint2& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t hb[4], mb[4], lb[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hb[e] = __float_as_uint(x[e]) & 0xffff0000u;
+    const float r = x[e] - __uint_as_float(hb[e]);
+    mb[e] = __float_as_uint(r) & 0xffff0000u;
+    lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));   // <= 8 significant bits: exact
+  }
+  h = make_uint2((hb[0] >> 16) | hb[1], (hb[2] >> 16) | hb[3]);
+  m = make_uint2((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3]);
+  l = make_uint2((lb[0] >> 16) | (lb[1] & 0xffff0000u), (lb[2] >> 16) | (lb[3] & 0xffff0000u));
+}
+
+template <int BN, int WAVES_M, int WAVES_N, int MODE>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_tile_x3(GemmArgs a) {
+  constexpr int BM = TF_H * TF_W, KS = 3, NP = 3;
+  constexpr int HH = TF_H + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int NT = 64 * WAVES_M * WAVES_N;                   // 4-8 waves
+  static_assert(NT % 64 == 0 && NT <= 512 && WM % 32 == 0 && WN % 32 == 0 && TM >= 1 && TN >= 1,
+                "tile");
+  constexpr int HQ = HP * 8, HS = (HQ + NT - 1) / NT;          // halo quads (32 ch)
+  constexpr int BOCT = NP * BN * 4, BSL = (BOCT + NT - 1) / NT; // B octets per tap
+  __shared__ uint4 Ah[NP][HP * SROW16];
+  __shared__ uint4 Bs[2][NP * BN * SROW16];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_n = tile % a.n_tiles;
+  const int tile_m = tile / a.n_tiles;
+  const int n0 = tile_n * BN;
+  const int OH = MODE == MODE_FWD ? a.ho : a.h, OW = MODE == MODE_FWD ? a.wo : a.w;
+  const int SH = MODE == MODE_FWD ? a.h : a.ho, SW = MODE == MODE_FWD ? a.w : a.wo;
+  const int tiles_x = (OW + TF_W - 1) / TF_W, tiles_y = (OH + TF_H - 1) / TF_H;
+  const int b = tile_m / (tiles_x * tiles_y);
+  const int trem = tile_m - b * tiles_x * tiles_y;
+  const int oy0 = (trem / tiles_x) * TF_H, ox0 = (trem % tiles_x) * TF_W;
+  const int hy0 = MODE == MODE_FWD ? oy0 - a.pt : oy0 + a.pt - (KS - 1);
+  const int hx0 = MODE == MODE_FWD ? ox0 - a.pl : ox0 + a.pl - (KS - 1);
+  const int c_begin = split * a.k_per_split;
+  const int c_end = min(a.K, c_begin + a.k_per_split);
+  const int steps = c_end > c_begin ? (c_end - c_begin) * KS * KS : 0;
+
+  const rsrc_t ra_src = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rb_src = make_rsrc(a.B, a.b_bytes);
+
+  int h_off[HS];
+  unsigned h_ok = 0;
+  const int hcq = tid & 7;
+#pragma unroll
+  for (int j = 0; j < HS; ++j) {
+    const int q = tid + NT * j;
+    const int hp = q >> 3;
+    const int sy = hy0 + hp / HW, sx = hx0 + hp % HW;
+    const bool ok = q < HQ && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+    h_off[j] = ok ? (((b * SH + sy) * SW + sx) * a.lda + 4 * hcq) * 4 : 0;
+    h_ok |= (ok ? 1u : 0u) << j;
+  }
+  float4 hv[HS];
+  auto load_halo = [&](int c) {
+    const bool cok = 32 * c + 4 * hcq < a.kc;
+#pragma unroll
+    for (int j = 0; j < HS; ++j)
+      hv[j] = bload4(ra_src, cok && ((h_ok >> j) & 1) ? (uint32_t)(h_off[j] + 128 * c) : kOOB);
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int j = 0; j < HS; ++j) {
+      const int q = tid + NT * j;
+      if (q < HQ) {
+        uint2 h, m, l;
+        split3x4(hv[j], h, m, l);
+        const int off = (q >> 3) * (SROW16 * 16) + 8 * (q & 7);
+        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(Ah[0]) + off) = h;
+        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(Ah[1]) + off) = m;
+        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(Ah[2]) + off) = l;
+      }
+    }
+  };
+  // ---- B slots: (plane, weight row, octet) of one tap; the (tap, chunk) part of the offset
+  // is uniform and rides in the buffer load's scalar offset.
+  uint32_t b_off[BSL];
+#pragma unroll
+  for (int j = 0; j < BSL; ++j) {
+    const int o = tid + NT * j;
+    const int p = o / (BN * 4), rem = o - p * (BN * 4);
+    const int n = n0 + (rem >> 2), oct = rem & 3;
+    const bool ok = o < BOCT && n < a.nb;
+    b_off[j] = ok ? (uint32_t)(((int64_t)p * a.b_plane + (int64_t)n * a.ldb + 8 * oct) * 2) : kOOB;
+  }
+  uint4 rb[BSL];
+  auto load_b = [&](int c, int t) {
+    const int so = (t * a.kc + 32 * c) * 2;
+#pragma unroll
+    for (int j = 0; j < BSL; ++j)
+      rb[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rb_src, b_off[j], so, 0));
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < BSL; ++j) {
+      const int o = tid + NT * j;
+      if (o < BOCT) {
+        const int p = o / (BN * 4), rem = o - p * (BN * 4);
+        Bs[buf][(p * BN + (rem >> 2)) * SROW16 + (rem & 3)] = rb[j];
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int wm0 = (wave / WAVES_N) * WM;
+  const int wn0 = (wave % WAVES_N) * WN;
+  const int lrow = lane & 31, lk = lane >> 5;
+  int a_hp[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wm0 + 32 * i + lrow;
+    const int ty = m / TF_W, tx = m % TF_W;
+    a_hp[i] = MODE == MODE_FWD ? ty * HW + tx : (ty + KS - 1) * HW + tx + KS - 1;
+  }
+
+  if (steps > 0) {
+    load_halo(c_begin);
+    load_b(c_begin, 0);
+    store_halo();
+    store_b(0);
+  }
+  __syncthreads();
+  // Chunk loop with the 9 taps unrolled (fragment offsets are immediates).  Step (chunk, tap)
+  // reads B buffer (chunk + tap) & 1 (9 steps per chunk) and fetches the next step's B; the
+  // next chunk's halo is fetched at tap 0 and stored after tap 8.
+  for (int c = c_begin; c < c_end; ++c) {
+    const int cc = c - c_begin;
+    const bool more_c = c + 1 < c_end;
+    if (more_c) load_halo(c + 1);
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t) {
+      const int buf = (cc + t) & 1;
+      const bool more = t + 1 < KS * KS || more_c;
+      if (more) load_b(t + 1 < KS * KS ? c : c + 1, t + 1 < KS * KS ? t + 1 : 0);
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this step's MFMAs
+      const int r = t / KS, s = t % KS;
+      const int dh = MODE == MODE_FWD ? r * HW + s : -(r * HW + s);
+      bf16x8 av[2][NP][TM], bv[2][NP][TN];
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            av[st][p][i] = __builtin_bit_cast(bf16x8, Ah[p][(a_hp[i] + dh) * SROW16 + 2 * st + lk]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            bv[st][p][j] = __builtin_bit_cast(
+                bf16x8, Bs[buf][(p * BN + wn0 + 32 * j + lrow) * SROW16 + 2 * st + lk]);
+        }
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x16 x = acc[i][j];
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][2][i], bv[st][0][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][2][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][1][i], bv[st][1][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][1][i], bv[st][0][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][1][j], x, 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][0][j], x, 0, 0, 0);
+          }
+      __builtin_amdgcn_sched_barrier(0);   // the stores wait for the prefetch: after the MFMAs
+      if (t + 1 == KS * KS && more_c) __syncthreads();   // all reads of this chunk's halo done
+      if (more) {
+        store_b(buf ^ 1);
+        if (t + 1 == KS * KS && more_c) store_halo();
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue (as conv_tile_bf16)
+  const int64_t img = (int64_t)b * OH * OW;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn0 + 32 * j + lrow;
+    if (n >= a.N) continue;
+    float bias = 0.f, scale = 1.f, shift = 0.f;
+    if (a.splits == 1) column_params<MODE>(a, n, bias, scale, shift);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      EpAux aux[16];
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
+        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
+        aux[rr] = a.splits == 1 && oy < OH && ox < OW
+                      ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : EpAux{0.f, 0.f};
+      }
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
+        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
+        if (oy >= OH || ox >= OW) continue;
+        const int64_t row = img + (int64_t)oy * OW + ox;
+        if (a.splits > 1)
+          a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n] = acc[i][j][rr];
+        else
+          epilogue_store<MODE>(a, row, n, acc[i][j][rr], bias, scale, shift, aux[rr]);
+      }
+    }
+  }
+}
+
 // Weight gradient on bf16 MFMA: C[m=(tap,ci)][n=co] = sum_{k=output pixel} x[pix(k,tap)][ci] *
 // dy[k][co], both operands rounded to bf16 while staged, fp32 accumulation into the split-K
 // slabs (reduced by wgrad_reduce_kernel, as the f32 path).  The MFMA operands need 8
@@ -1796,7 +2033,8 @@ struct PackEntry {
   float* wf;               // f32 packing; bf16 packing: __bf16 buffers
   float* wd;
   int taps, kw, cin, cout, cin_p, cout_p, kf, nf, nd;
-  int bf16;                // 1: transposed bf16 images [n][k] (conv_gemm_bf16)
+  int bf16;                // 1: transposed bf16 images [n][k] (conv_gemm_bf16); 2: the
+                           // three split planes of those images (conv_tile_x3)
   int kf16;
   int64_t kd16;
   int64_t work_begin;      // cumulative elements (fwd then bwd) before this entry
@@ -1809,6 +2047,23 @@ struct PackTableHeader {
   int64_t total;
 };
 
+// bf16 image element k (mode 1: RNE), or its three split terms in planes `plane` apart (mode 2,
+// conv_tile_x3).
+__device__ __forceinline__ void put16(int mode, float* base, int64_t k, int64_t plane, float v) {
+  __bf16* o = reinterpret_cast<__bf16*>(base);
+  if (mode == 1) {
+    o[k] = (__bf16)v;
+    return;
+  }
+  const uint32_t hb = __float_as_uint(v) & 0xffff0000u;
+  const float r = v - __uint_as_float(hb);
+  const uint32_t mb = __float_as_uint(r) & 0xffff0000u;
+  const uint32_t lb = __float_as_uint(r - __uint_as_float(mb));
+  o[k] = __builtin_bit_cast(__bf16, (uint16_t)(hb >> 16));
+  o[k + plane] = __builtin_bit_cast(__bf16, (uint16_t)(mb >> 16));
+  o[k + 2 * plane] = __builtin_bit_cast(__bf16, (uint16_t)(lb >> 16));
+}
+
 // One packed element of entry E (f32: fwd rows [k][n] then bwd rows; bf16: transposed).
 __device__ void pack_elem(const PackEntry& E, int64_t k) {
   if (E.bf16) {
@@ -1819,7 +2074,7 @@ __device__ void pack_elem(const PackEntry& E, int64_t k) {
       float v = 0.f;
       if (tap < E.taps && ci < E.cin && n < E.cout)
         v = E.w[((int64_t)tap * E.cin + ci) * E.cout + n];
-      reinterpret_cast<__bf16*>(E.wf)[k] = (__bf16)v;
+      put16(E.bf16, E.wf, k, (int64_t)E.cout_p * E.kf16, v);
     } else {                                // W16_d[ci][group k block: t*cout_p + co]
       k -= nfwd16;
       const int ci = (int)(k / E.kd16);
@@ -1836,7 +2091,7 @@ __device__ void pack_elem(const PackEntry& E, int64_t k) {
         const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
         v = E.w[((int64_t)(r * E.kw + ss) * E.cin + ci) * E.cout + co];
       }
-      reinterpret_cast<__bf16*>(E.wd)[k] = (__bf16)v;
+      put16(E.bf16, E.wd, k, E.kd16 * E.nd, v);
     }
     return;
   }
@@ -2201,7 +2456,7 @@ int launch_gemm_bf16(const GemmArgs& a, hipStream_t s, double flops) {
 // bf16 3x3 stride-1 fwd / dgrad: halo-tiled kernel (conv_tile_bf16).
 bool tile_ok(const of_conv_desc* d) { return d->kh == 3 && d->kw == 3 && d->stride == 1; }
 
-GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode) {
+GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false) {
   GemmArgs a = base_args(d);
   const bool fwd = mode == MODE_FWD;
   a.kc = fwd ? g.cin_p : g.cout_p;
@@ -2225,8 +2480,8 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode) {
   G.K = a.K;
   a.splits = 1;
   a.k_per_split = a.K;
-  if (a.tiles_total < 2 * kCUs) {
-    int sp = std::max(1, (4 * kCUs) / a.tiles_total);
+  if (a.tiles_total < (x3 ? kCUs : 2 * kCUs)) {
+    int sp = std::max(1, ((x3 ? 2 : 4) * kCUs) / a.tiles_total);
     sp = std::min(sp, std::max(1, a.K / 2));       // >= 2 chunks (6 tap rows) per slice
     a.k_per_split = (int)cdiv(a.K, sp);
     a.splits = (int)cdiv(a.K, a.k_per_split);
@@ -2254,6 +2509,23 @@ struct WgradPlan {
   int splits, k_per_split, M, ldc;
   int64_t split_stride;
 };
+
+// fp32 3x3 stride-1 fwd / dgrad on the split-bf16 kernel: timing kinds 128 + mode * 8 + cfg.
+template <int MODE>
+int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
+  const int bn = pick_bn(a.N);
+  dim3 grid(a.tiles_total * a.splits), block(256);
+  const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
+  if (timing_on()) timing_begin(s);
+  if (cfg == 0) hipLaunchKernelGGL((conv_tile_x3<128, 2, 4, MODE>), grid, dim3(512), 0, s, a);
+  else if (cfg == 1) hipLaunchKernelGGL((conv_tile_x3<96, 2, 3, MODE>), grid, dim3(384), 0, s, a);
+  else if (cfg == 2) hipLaunchKernelGGL((conv_tile_x3<64, 4, 2, MODE>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((conv_tile_x3<32, 4, 1, MODE>), grid, block, 0, s, a);
+  if (timing_on()) timing_end(s, 128 + MODE * 8 + cfg, flops);
+  int st = check_launch("conv_tile_x3");
+  if (st || a.splits == 1) return st;
+  return launch_splitk_epilogue<MODE>(a, s);
+}
 
 // bf16 3x3 stride-1 wgrad on conv_wgrad_tile_bf16: block channel tiles (CIB x COB).
 // bf16: every 3x3 stride-1 layer.  fp32 (MFMA-bound either way): where the implicit GEMM
@@ -2417,7 +2689,7 @@ int of_conv_pack_table_ex(int nconv, const of_conv_desc* descs, const float* con
     int st = validate(&descs[i]);
     if (st) return st;
     OF_CHECK_ARG(w_hwio[i] && w_fwd[i] && w_bwd[i], "pack table: NULL weight pointer");
-    const int b16 = bf16 ? (bf16[i] != 0) : 0;
+    const int b16 = bf16 ? (bf16[i] == 2 ? 2 : bf16[i] != 0) : 0;   // 2: x3 planes
     e[i] = pack_entry(&descs[i], w_hwio[i], w_fwd[i], w_bwd[i], b16);
     e[i].work_begin = work;
     work += pack_work(&descs[i], b16);
@@ -2475,7 +2747,8 @@ int of_conv_path(const of_conv_desc* d) {
   return narrow_ok(d) ? 1 : 0;
 }
 
-static int conv_fwd_impl(bool bf16, const of_conv_desc* d, const float* x, int ldx,
+// prec: 0 fp32 MFMA, 1 bf16, 2 fp32 on the split-bf16 tile kernel (3x3 stride 1 only).
+static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ldx,
                          const void* w_fwd, const float* bias, const float* bn_gamma,
                          const float* bn_beta, const float* bn_mean, const float* bn_var,
                          float bn_eps, const float* residual, int ldr, int act, float alpha,
@@ -2483,6 +2756,8 @@ static int conv_fwd_impl(bool bf16, const of_conv_desc* d, const float* x, int l
                          void* stream) {
   int st = validate(d);
   if (st) return st;
+  const bool bf16 = prec == 1, x3 = prec == 2;
+  OF_CHECK_ARG(!x3 || tile_ok(d), "conv fwd x3: 3x3 stride-1 convolutions only");
   OF_CHECK_ARG(x && w_fwd && y, "conv fwd: NULL pointer");
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv fwd: ldx");
   OF_CHECK_ARG(ldy >= d->cout, "conv fwd: ldy");
@@ -2491,7 +2766,7 @@ static int conv_fwd_impl(bool bf16, const of_conv_desc* d, const float* x, int l
   OF_CHECK_ARG(!z || ldz >= d->cout, "conv fwd: ldz");
   OF_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_fwd & 15) == 0,
                "conv fwd: x / w must be 16-byte aligned");
-  if (!bf16 && narrow_ok(d) && !bn_gamma && !residual && !z) {   // 2-channel layers: VALU
+  if (!prec && narrow_ok(d) && !bn_gamma && !residual && !z) {   // 2-channel layers: VALU
     hipStream_t s = as_stream(stream);
     if (timing_on()) timing_begin(s);
     st = narrow_fwd(d, x, ldx, static_cast<const float*>(w_fwd), bias, act, alpha, y, ldy, s);
@@ -2499,14 +2774,15 @@ static int conv_fwd_impl(bool bf16, const of_conv_desc* d, const float* x, int l
     return st;
   }
   Geo g = geo(d);
-  const bool tile = bf16 && tile_ok(d);
-  GemmArgs a = tile ? tile_args(d, g, MODE_FWD) : fwd_args(d, g, bf16);
+  const bool tile = (bf16 || x3) && tile_ok(d);
+  GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3) : fwd_args(d, g, bf16);
   attach_slab(a, workspace, ws_bytes, tile ? 1 : bf16 ? BKH : BK);
   a.A = x;
   a.lda = ldx;
   a.a_bytes = (int64_t)d->n * d->h * d->w * ldx * 4;
   a.B = static_cast<const float*>(w_fwd);
-  a.b_bytes = bf16 ? (int64_t)g.cout_p * g.kf16 * 2 : (int64_t)g.kf * g.nf * 4;
+  a.b_plane = (int64_t)g.cout_p * g.kf16;
+  a.b_bytes = x3 ? 3 * a.b_plane * 2 : bf16 ? a.b_plane * 2 : (int64_t)g.kf * g.nf * 4;
   OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX,
                "conv fwd: tensors must be < 2 GiB (32-bit buffer offsets)");
   a.C = y;
@@ -2525,7 +2801,8 @@ static int conv_fwd_impl(bool bf16, const of_conv_desc* d, const float* x, int l
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
-  st = tile   ? launch_tile_bf16<MODE_FWD>(a, s, flops)
+  st = x3     ? launch_tile_x3<MODE_FWD>(a, s, flops)
+       : tile ? launch_tile_bf16<MODE_FWD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops)
               : launch_gemm<MODE_FWD>(a, s, flops);
   return st;
@@ -2536,7 +2813,7 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
                   const float* bn_mean, const float* bn_var, float bn_eps,
                   const float* residual, int ldr, int act, float alpha, float* z, int ldz,
                   float* y, int ldy, void* workspace, size_t ws_bytes, void* stream) {
-  return conv_fwd_impl(false, d, x, ldx, w_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
+  return conv_fwd_impl(0, d, x, ldx, w_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
                        bn_eps, residual, ldr, act, alpha, z, ldz, y, ldy, workspace, ws_bytes,
                        stream);
 }
@@ -2546,18 +2823,20 @@ int of_conv2d_fwd_bf16(const of_conv_desc* d, const float* x, int ldx, const voi
                        const float* bn_mean, const float* bn_var, float bn_eps,
                        const float* residual, int ldr, int act, float alpha, float* z, int ldz,
                        float* y, int ldy, void* workspace, size_t ws_bytes, void* stream) {
-  return conv_fwd_impl(true, d, x, ldx, w16_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
+  return conv_fwd_impl(1, d, x, ldx, w16_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
                        bn_eps, residual, ldr, act, alpha, z, ldz, y, ldy, workspace, ws_bytes,
                        stream);
 }
 
-static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, int lddy,
+static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int lddy,
                            const void* w_bwd, const float* act_src, int ld_act, int act,
                            float alpha, const float* add, int ld_add, float* dx, int lddx,
                            void* workspace, size_t ws_bytes, void* stream) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
+  const bool bf16 = prec == 1, x3 = prec == 2;
+  OF_CHECK_ARG(!x3 || tile_ok(d), "conv dgrad x3: 3x3 stride-1 convolutions only");
   OF_CHECK_ARG(dy && w_bwd && dx, "conv dgrad: NULL pointer");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv dgrad: lddy (>= round_up(cout,4))");
   OF_CHECK_ARG(lddx >= d->cin_p, "conv dgrad: lddx");
@@ -2566,7 +2845,7 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
   OF_CHECK_ARG(((uintptr_t)dy & 15) == 0 && ((uintptr_t)w_bwd & 15) == 0,
                "conv dgrad: dy / w must be 16-byte aligned");
   OF_CHECK_ARG(d->stride == 1 || d->stride == 2, "conv dgrad: stride must be 1 or 2");
-  if (!bf16 && narrow_ok(d)) {
+  if (!prec && narrow_ok(d)) {
     OF_CHECK_ARG(!add, "conv dgrad: the Cout <= 4 kernels take no added gradient");
     hipStream_t s = as_stream(stream);
     if (timing_on()) timing_begin(s);
@@ -2575,16 +2854,17 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
     if (timing_on()) timing_end(s, MODE_DGRAD * 8 + KIND_NARROW, conv_flops(d));
     return st;
   }
-  const bool tile = bf16 && tile_ok(d);
+  const bool tile = (bf16 || x3) && tile_ok(d);
   const bool in_place = add && add == dx && ld_add == lddx;
-  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD) : dgrad_args(d, g, bf16, in_place);
+  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3) : dgrad_args(d, g, bf16, in_place);
   if (a.tiles_total == 0) return OF_OK;                 // every output already final
   attach_slab(a, workspace, ws_bytes, tile ? 1 : bf16 ? BKH : BK);
   a.A = dy;
   a.lda = lddy;
   a.a_bytes = (int64_t)d->n * d->ho * d->wo * lddy * 4;
   a.B = static_cast<const float*>(w_bwd);
-  a.b_bytes = bf16 ? g.kd16 * g.nd * 2 : g.kd * g.nd * 4;
+  a.b_plane = g.kd16 * g.nd;
+  a.b_bytes = x3 ? 3 * a.b_plane * 2 : bf16 ? a.b_plane * 2 : g.kd * g.nd * 4;
   OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX,
                "conv dgrad: tensors must be < 2 GiB (32-bit buffer offsets)");
   a.C = dx;
@@ -2597,7 +2877,8 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
   a.ldr = ld_add;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
-  st = tile   ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
+  st = x3     ? launch_tile_x3<MODE_DGRAD>(a, s, flops)
+       : tile ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops)
               : launch_gemm<MODE_DGRAD>(a, s, flops);
   return st;
@@ -2606,28 +2887,74 @@ static int conv_dgrad_impl(bool bf16, const of_conv_desc* d, const float* dy, in
 int of_conv2d_dgrad(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
                     const float* act_src, int ld_act, int act, float alpha, float* dx,
                     int lddx, void* workspace, size_t ws_bytes, void* stream) {
-  return conv_dgrad_impl(false, d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, nullptr, 0,
+  return conv_dgrad_impl(0, d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, nullptr, 0,
                          dx, lddx, workspace, ws_bytes, stream);
 }
 
 int of_conv2d_dgrad_add(const of_conv_desc* d, const float* dy, int lddy, const float* w_bwd,
                         const float* add, int ld_add, float* dx, int lddx, void* workspace,
                         size_t ws_bytes, void* stream) {
-  return conv_dgrad_impl(false, d, dy, lddy, w_bwd, nullptr, 0, OF_ACT_NONE, 0.f, add, ld_add,
+  return conv_dgrad_impl(0, d, dy, lddy, w_bwd, nullptr, 0, OF_ACT_NONE, 0.f, add, ld_add,
                          dx, lddx, workspace, ws_bytes, stream);
 }
 
 int of_conv2d_dgrad_bf16(const of_conv_desc* d, const float* dy, int lddy, const void* w16_bwd,
                          const float* act_src, int ld_act, int act, float alpha, float* dx,
                          int lddx, void* workspace, size_t ws_bytes, void* stream) {
-  return conv_dgrad_impl(true, d, dy, lddy, w16_bwd, act_src, ld_act, act, alpha, nullptr, 0,
+  return conv_dgrad_impl(1, d, dy, lddy, w16_bwd, act_src, ld_act, act, alpha, nullptr, 0,
                          dx, lddx, workspace, ws_bytes, stream);
 }
 
 int of_conv2d_dgrad_add_bf16(const of_conv_desc* d, const float* dy, int lddy,
                              const void* w16_bwd, const float* add, int ld_add, float* dx,
                              int lddx, void* workspace, size_t ws_bytes, void* stream) {
-  return conv_dgrad_impl(true, d, dy, lddy, w16_bwd, nullptr, 0, OF_ACT_NONE, 0.f, add, ld_add,
+  return conv_dgrad_impl(1, d, dy, lddy, w16_bwd, nullptr, 0, OF_ACT_NONE, 0.f, add, ld_add,
+                         dx, lddx, workspace, ws_bytes, stream);
+}
+
+int of_conv_pack_weights_x3(const of_conv_desc* d, const float* w_hwio, void* w3_fwd,
+                            void* w3_bwd, void* stream) {
+  int st = validate(d);
+  if (st) return st;
+  OF_CHECK_ARG(w_hwio && w3_fwd && w3_bwd, "pack x3: NULL pointer");
+  const int64_t total = pack_work(d, 1);
+  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+  hipLaunchKernelGGL(pack_one_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+                     pack_entry(d, w_hwio, w3_fwd, w3_bwd, 2), total);
+  return check_launch("pack_x3");
+}
+
+size_t of_conv2d_fwd_x3_workspace(const of_conv_desc* d) {
+  if (validate(d) != OF_OK || !tile_ok(d)) return 0;
+  return fd_workspace(tile_args(d, geo(d), MODE_FWD, true));
+}
+
+size_t of_conv2d_dgrad_x3_workspace(const of_conv_desc* d) {
+  if (validate(d) != OF_OK || !tile_ok(d)) return 0;
+  return fd_workspace(tile_args(d, geo(d), MODE_DGRAD, true));
+}
+
+int of_conv2d_fwd_x3(const of_conv_desc* d, const float* x, int ldx, const void* w3_fwd,
+                     const float* bias, const float* bn_gamma, const float* bn_beta,
+                     const float* bn_mean, const float* bn_var, float bn_eps,
+                     const float* residual, int ldr, int act, float alpha, float* z, int ldz,
+                     float* y, int ldy, void* workspace, size_t ws_bytes, void* stream) {
+  return conv_fwd_impl(2, d, x, ldx, w3_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
+                       bn_eps, residual, ldr, act, alpha, z, ldz, y, ldy, workspace, ws_bytes,
+                       stream);
+}
+
+int of_conv2d_dgrad_x3(const of_conv_desc* d, const float* dy, int lddy, const void* w3_bwd,
+                       const float* act_src, int ld_act, int act, float alpha, float* dx,
+                       int lddx, void* workspace, size_t ws_bytes, void* stream) {
+  return conv_dgrad_impl(2, d, dy, lddy, w3_bwd, act_src, ld_act, act, alpha, nullptr, 0,
+                         dx, lddx, workspace, ws_bytes, stream);
+}
+
+int of_conv2d_dgrad_add_x3(const of_conv_desc* d, const float* dy, int lddy,
+                           const void* w3_bwd, const float* add, int ld_add, float* dx,
+                           int lddx, void* workspace, size_t ws_bytes, void* stream) {
+  return conv_dgrad_impl(2, d, dy, lddy, w3_bwd, nullptr, 0, OF_ACT_NONE, 0.f, add, ld_add,
                          dx, lddx, workspace, ws_bytes, stream);
 }
 

@@ -140,13 +140,19 @@ def grad_target(param: torch.Tensor):
 
 
 # ====================================================================== convolution ====
+# fp32 3x3 stride-1 fwd / dgrad on the split-bf16 halo-tile kernels (of_conv2d_*_x3: exact
+# three-term operand split, per-product error of one fp32 rounding; tools/x3_accuracy.py and
+# tests/test_gpu_kernels.py::test_conv_x3_accuracy measure it against fp64).
+# OFLOW_F32_SPLIT=0 keeps every fp32 layer on the fp32 MFMA kernels.
+F32_SPLIT = os.environ.get("OFLOW_F32_SPLIT", "1") == "1"
+
 class ConvLayer:
     """One ``layers.Conv2D(filters, k, strides, padding='same')`` (model.py:12,104-114) with an
     optional inference BatchNorm (model.py:14) and activation, holding references to its
     parameters (HWIO kernel, bias, BN vectors) and its per-step packed weights."""
 
     def __init__(self, kernel, bias, stride=1, act=ACT_NONE, alpha=LEAKY_ALPHA, bn=None,
-                 cin_p=None, version_of=None, name="", precision="fp32"):
+                 cin_p=None, version_of=None, name="", precision="fp32", f32_split=None):
         self.kernel, self.bias = kernel, bias
         kh, kw, cin, cout = kernel.shape
         self.kh, self.kw, self.cin, self.cout = kh, kw, cin, cout
@@ -161,6 +167,8 @@ class ConvLayer:
         self._wf = self._wd = None
         self._descs = {}
         self._bf16 = None
+        self._mode = None
+        self.f32_split = F32_SPLIT if f32_split is None else bool(f32_split)
 
     def desc(self, n, h, w) -> ConvDesc:
         key = (n, h, w)
@@ -181,13 +189,26 @@ class ConvLayer:
                           _lib.lib().of_conv_path(C.byref(d)) == 0)
         return self._bf16
 
+    def mode(self, d: ConvDesc = None) -> int:
+        """Kernel family of fwd/dgrad: 0 fp32 MFMA, 1 bf16 MFMA, 2 fp32 on the split-bf16
+        halo-tile kernels (fp32 precision, 3x3 stride-1 GEMM-path layers, F32_SPLIT on)."""
+        if self._mode is None:
+            self._mode = (1 if self.bf16(d) else
+                          2 if (self.f32_split and self.precision == "fp32" and self.kh == 3 and
+                                self.kw == 3 and self.stride == 1 and
+                                _lib.lib().of_conv_path(C.byref(d or self.desc(1, 16, 16))) == 0)
+                          else 0)
+        return self._mode
+
     def alloc_packed(self, d: ConvDesc):
         lib = _lib.lib()
         dev = self.kernel.device
-        if self.bf16(d):
-            self._wf = torch.empty(lib.of_conv_wfwd16_elems(C.byref(d)), device=dev,
+        m = self.mode(d)
+        if m:
+            planes = 3 if m == 2 else 1
+            self._wf = torch.empty(planes * lib.of_conv_wfwd16_elems(C.byref(d)), device=dev,
                                    dtype=torch.bfloat16)
-            self._wd = torch.empty(lib.of_conv_wbwd16_elems(C.byref(d)), device=dev,
+            self._wd = torch.empty(planes * lib.of_conv_wbwd16_elems(C.byref(d)), device=dev,
                                    dtype=torch.bfloat16)
         else:
             self._wf = torch.empty(lib.of_conv_wfwd_elems(C.byref(d)), device=dev)
@@ -198,7 +219,8 @@ class ConvLayer:
         if self._wf is None:
             self.alloc_packed(d)
         if key != self._pack_key or self.version_of is None:
-            call("of_conv_pack_weights_bf16" if self.bf16(d) else "of_conv_pack_weights",
+            call(("of_conv_pack_weights", "of_conv_pack_weights_bf16",
+                  "of_conv_pack_weights_x3")[self.mode(d)],
                  C.byref(d), _ptr(self.kernel), _ptr(self._wf), _ptr(self._wd), _stream())
             self._pack_key = key
         return self._wf, self._wd
@@ -208,6 +230,8 @@ class ConvLayer:
         lib = _lib.lib()
         if self.bf16(d):
             return "of_conv2d_fwd_bf16", lib.of_conv2d_fwd_bf16_workspace(C.byref(d))
+        if self.mode(d) == 2:
+            return "of_conv2d_fwd_x3", lib.of_conv2d_fwd_x3_workspace(C.byref(d))
         return "of_conv2d_fwd", lib.of_conv2d_fwd_workspace(C.byref(d))
 
     def wgrad_entry(self, d):
@@ -221,12 +245,16 @@ class ConvLayer:
         lib = _lib.lib()
         if self.bf16(d):
             return "of_conv2d_dgrad_add_bf16", lib.of_conv2d_dgrad_bf16_workspace(C.byref(d))
+        if self.mode(d) == 2:
+            return "of_conv2d_dgrad_add_x3", lib.of_conv2d_dgrad_x3_workspace(C.byref(d))
         return "of_conv2d_dgrad_add", lib.of_conv2d_dgrad_workspace(C.byref(d))
 
     def dgrad_entry(self, d):
         lib = _lib.lib()
         if self.bf16(d):
             return "of_conv2d_dgrad_bf16", lib.of_conv2d_dgrad_bf16_workspace(C.byref(d))
+        if self.mode(d) == 2:
+            return "of_conv2d_dgrad_x3", lib.of_conv2d_dgrad_x3_workspace(C.byref(d))
         return "of_conv2d_dgrad", lib.of_conv2d_dgrad_workspace(C.byref(d))
 
     def __call__(self, x, residual=None):
@@ -250,7 +278,7 @@ class ConvPacker:
             d = L.desc(1, 16, 16)
             descs[i] = d
             L.alloc_packed(d)
-            flags[i] = 1 if L.bf16(d) else 0
+            flags[i] = L.mode(d)
             wp[i], fp[i], bp[i] = L.kernel.data_ptr(), L._wf.data_ptr(), L._wd.data_ptr()
         nbytes = lib.of_conv_pack_table_bytes(n)
         host = (C.c_char * nbytes)()

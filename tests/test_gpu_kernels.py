@@ -43,8 +43,11 @@ CONV_CASES = [
 ]
 
 
+@pytest.mark.parametrize("split", [True, False], ids=["x3", "f32"])
 @pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: "x".join(map(str, c[:7])) + c[7])
-def test_conv_fwd_bwd(case):
+def test_conv_fwd_bwd(case, split):
+    """split: 3x3 stride-1 fwd/dgrad on the split-bf16 kernels (the fp32 default) or on the
+    fp32 MFMA implicit GEMM; other shapes take the same kernels either way."""
     ops = _ops()
     from optical_flow_amd._lib import ACT_LEAKY, ACT_NONE, ACT_RELU
     n, h, w, cin, cout, k, s, act, use_bn, use_res = case
@@ -95,7 +98,10 @@ def test_conv_fwd_bwd(case):
     wd, bd, gd, bed = [dev(t).requires_grad_(True) for t in (wt, b, g, be)]
     layer = ops.ConvLayer(wd, bd, stride=s,
                           act={"relu": ACT_RELU, "leaky": ACT_LEAKY, "none": ACT_NONE}[act],
-                          bn=(gd, bed, dev(mu), dev(var)) if use_bn else None, cin_p=cin_p)
+                          bn=(gd, bed, dev(mu), dev(var)) if use_bn else None, cin_p=cin_p,
+                          f32_split=split)
+    if split and k == 3 and s == 1 and cout > 4:
+        assert layer.mode(layer.desc(n, h, w)) == 2
     xd.requires_grad_(True)
     resd = dev(res).requires_grad_(True) if use_res else None
     yd = layer(xd, residual=resd)
@@ -169,6 +175,46 @@ def test_conv_bf16(case):
         assert xd.grad[..., cin:].abs().max().item() == 0.0, "padded channels must get 0 grad"
     assert rel_l2(wd.grad, wo_.grad) < REL_TOL, "wgrad"
     assert rel_l2(bd.grad, bo.grad) < REL_TOL, "bias grad"
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 48, 64, 128, 128), (2, 37, 45, 20, 24),
+                                             (1, 96, 128, 64, 96), (2, 24, 32, 256, 256)])
+def test_conv_x3_accuracy(n, h, w, cin, cout):
+    """The split-bf16 fp32 kernels are as accurate as the fp32 MFMA kernels: error against
+    an fp64 reference (max and rms, relative to the reference) within 3x of theirs and at
+    the level of one fp32 rounding per product (tools/x3_accuracy.py prints the numbers)."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd._lib import ACT_NONE, call
+    x = rng_tensor((n, h, w, cin), 11)
+    wt = rng_tensor((3, 3, cin, cout), 12, scale=(2.0 / (9 * cin)) ** 0.5)
+    dy = rng_tensor((n, h, w, cout), 13)
+    yref = R.conv2d_same(f64(x), f64(wt), None, 1)
+    dxref = torch.nn.grad.conv2d_input((n, cin, h, w), f64(wt).permute(3, 2, 0, 1),
+                                       f64(dy).permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    errs = {}
+    for split in (False, True):
+        layer = ops.ConvLayer(dev(wt), dev(torch.zeros(cout)), stride=1, act=ACT_NONE, cin_p=cin,
+                              f32_split=split)
+        d = layer.desc(n, h, w)
+        assert layer.mode(d) == (2 if split else 0)
+        wf, wd = layer.packed(d)
+        fent, fws = layer.fwd_entry(d)
+        dent, dws = layer.dgrad_entry(d)
+        ws = torch.empty(max(fws, dws) // 4 + 4, device="cuda")
+        P, st = ops._ptr, ops._stream()
+        xd, dyd = dev(x), dev(dy)
+        y = torch.empty(n, h, w, cout, device="cuda")
+        dx = torch.empty(n, h, w, cin, device="cuda")
+        call(fent, C.byref(d), P(xd), cin, P(wf), P(layer.bias), None, None, None, None, 1e-3,
+             None, 0, ACT_NONE, 0.0, None, 0, P(y), cout, P(ws), fws, st)
+        call(dent, C.byref(d), P(dyd), cout, P(wd), None, 0, ACT_NONE, 0.0, P(dx), cin, P(ws),
+             dws, st)
+        torch.cuda.synchronize()
+        errs[split] = [rel_inf(y, yref), rel_l2(y, yref), rel_inf(dx, dxref), rel_l2(dx, dxref)]
+    for e3, e32 in zip(errs[True], errs[False]):
+        assert e3 < 3 * e32 + 1e-7, (errs[True], errs[False])
+        assert e3 < 5e-6, errs[True]
 
 
 # ----------------------------------------------------------------------- cost volume ----
@@ -345,7 +391,7 @@ def test_conv_split_k_matches_unsplit(stride):
     x = dev(rng_tensor((n, h, w, cin), 71))
     wt = dev(rng_tensor((k, k, cin, cout), 72, scale=0.05))
     b = dev(rng_tensor((cout,), 73, scale=0.1))
-    layer = ops.ConvLayer(wt, b, stride=stride, act=ACT_LEAKY)
+    layer = ops.ConvLayer(wt, b, stride=stride, act=ACT_LEAKY, f32_split=False)
     d = layer.desc(n, h, w)
     wf, wd = layer.packed(d)
     lib = _lib.lib()
