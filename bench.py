@@ -58,6 +58,7 @@ def kind_parts(kind):
 
 TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1"}
 X3_BN = {0: "128, 2, 4", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1"}   # conv_tile_x3 waves
+X3_WGT = {0: "1, 4, 3", 1: "1, 3, 3", 2: "2, 2, 3"}   # conv_wgrad_tile_x3<WAVES_CI, CO, R>
 
 
 WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>
@@ -79,8 +80,8 @@ def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
            "tile_x3": "_tile_x3"}[fam]
-    if fam in ("tile_bf16", "tile_f32") and mode == 2:
-        return "wgrad%s<%s>" % (sfx, WGT_WAVES[cfg])
+    if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
+        return "wgrad%s<%s>" % (sfx, X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
     return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (TILE_BN if fam == "tile_bf16" else
                                                  X3_BN if fam == "tile_x3" else TILE_TEMPLATE)[cfg])
 
@@ -90,8 +91,9 @@ def kernel_symbol(kind):
     mode, cfg, fam = kind_parts(kind)
     if cfg == 7:
         return NARROW_SYMBOLS[mode]
-    if fam in ("tile_bf16", "tile_f32") and mode == 2:
-        return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (fam, WGT_WAVES[cfg])
+    if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
+        return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (
+            fam, X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
     if fam in ("tile_bf16", "tile_x3"):
         return "void oflow::conv_%s<%s, %d>(oflow::GemmArgs)" % (
             fam, (TILE_BN if fam == "tile_bf16" else X3_BN)[cfg], mode)

@@ -68,6 +68,8 @@ PROTOTYPES = {
     "of_conv2d_fwd_x3": (I, [PD, P, I, P, P, P, P, P, P, F, P, I, I, F, P, I, P, I, P, SZ, P]),
     "of_conv2d_dgrad_x3": (I, [PD, P, I, P, P, I, I, F, P, I, P, SZ, P]),
     "of_conv2d_dgrad_add_x3": (I, [PD, P, I, P, P, I, P, I, P, SZ, P]),
+    "of_conv2d_wgrad_x3_workspace": (SZ, [PD]),
+    "of_conv2d_wgrad_x3": (I, [PD, P, I, P, I, P, P, I, P, SZ, P]),
     "of_act_bwd": (I, [P, P, I, F, P, I64, P]),
     "of_colsum_workspace": (SZ, [I64, I]),
     "of_colsum": (I, [P, I64, I, I, P, I, P, P]),

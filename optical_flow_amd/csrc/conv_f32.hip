@@ -1704,6 +1704,204 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
   }
 }
 
+// ---- fp32 weight gradient on bf16 MFMA by the three-term split, 3x3 stride 1 ------------
+// dW[r][s][ci][co] = sum_p x(p + (r, s) - pad)[ci] . dy(p)[co] with both operands split
+// exactly into hi + mid + lo bf16 terms and the six products of conv_tile_x3.  A workgroup
+// (12 waves) owns CIB = 32 input x COB = 128 output channels for all 9 taps (wave = 32 ci x
+// 32 co x the 3 taps of one kernel row: 48 accumulator registers, so three waves fit per
+// SIMD) and walks 4 x 16 output-pixel tiles of its K slice.  The x halo
+// (6 rows x 18 px) is staged once per tile as three split planes x three copies shifted by
+// s = 0, 1, 2 pixels (aligned 16-byte A fragments, the swizzles of conv_wgrad_tile_bf16);
+// it is single-buffered (55 KB) and register-staged one tile ahead.  dy never enters LDS:
+// a lane loads its B fragment (8 pixels of one channel, coalesced across the 32 channels of
+// a pixel) straight from L2 one k-step ahead and splits it in registers (the three kernel-row
+// waves of a channel block read the same dy lines).  Output: the split-K slabs of the other wgrad kernels.
+constexpr int TX_H = 4;    // conv_wgrad_tile_x3 pixel tile: 4 rows x 16 px
+
+__device__ __forceinline__ void split3x8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
+  uint2 h0, m0, l0, h1, m1, l1;
+  split3x4(make_float4(v[0], v[1], v[2], v[3]), h0, m0, l0);
+  split3x4(make_float4(v[4], v[5], v[6], v[7]), h1, m1, l1);
+  h = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+  m = __builtin_bit_cast(bf16x8, make_uint4(m0.x, m0.y, m1.x, m1.y));
+  l = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+}
+
+template <int WAVES_CI, int WAVES_CO, int WAVES_R>
+__global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wgrad_tile_x3(GemmArgs a) {
+  constexpr int NT = 64 * WAVES_CI * WAVES_CO * WAVES_R;
+  static_assert(WAVES_R == 3, "one kernel row per wave group");
+  constexpr int CIB = 32 * WAVES_CI, COB = 32 * WAVES_CO, KS = 3, HH = TX_H + KS - 1, NP = 3;
+  constexpr int XQ = HH * KS * 2 * (CIB / 4), XS = (XQ + NT - 1) / NT;   // (hy, s, half, ci quad)
+  constexpr int PL = KS * HH * CIB * 2;                              // uint4 per plane
+  __shared__ uint4 Xs[NP * PL];
+
+  auto xrow = [](int ci) { return ci ^ ((ci >> 2) & 2); };
+  auto xoct = [](int ci) { return (ci >> 4) & 1; };
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_co = tile % a.n_tiles;
+  const int tile_ci = tile / a.n_tiles;
+  const int ci0 = tile_ci * CIB, co0 = tile_co * COB;
+  const int t_begin = split * a.k_per_split;
+  const int t_end = min(a.K, t_begin + a.k_per_split);
+  const int steps = max(0, t_end - t_begin);
+  const int tiles_x = (a.wo + TT_W - 1) / TT_W, tiles_y = (a.ho + TX_H - 1) / TX_H;
+  const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
+  const int wr = wave / (WAVES_CI * WAVES_CO);            // this wave's kernel row
+  const int wci0 = ((wave / WAVES_CO) % WAVES_CI) * 32;
+  const int wco0 = (wave % WAVES_CO) * 32;
+  const int lrow = lane & 31, lk = lane >> 5;
+  const bool do_colsum = a.colsum && tile_ci == 0 && wci0 == 0 && wr == 0;
+
+  // ---- x halo slots (channel quad fastest: coalesced 16-B lanes of one pixel)
+  const int xcq = tid % (CIB / 4);
+  const bool xc_ok = ci0 + 4 * xcq < a.kc;
+  // slot q: channel quad (fastest: coalesced), pixel octet half, shift s, halo row hy; it
+  // loads the 8 pixels its shifted copy needs and writes 4 channel rows x 3 planes
+  float4 xv[XS][8];
+  auto load_x = [&](int t) {
+    const int b = t / (tiles_x * tiles_y);
+    const int trem = t - b * tiles_x * tiles_y;
+    const int oy0 = (trem / tiles_x) * TX_H, ox0 = (trem % tiles_x) * TT_W;
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int q = tid + NT * j;
+      const int r2 = q / (CIB / 4);
+      const int half = r2 & 1, s = (r2 >> 1) % KS, hy = (r2 >> 1) / KS;
+      const int iy = oy0 - a.pt + hy;
+      const bool rok = q < XQ && xc_ok && (unsigned)iy < (unsigned)a.h;
+      const int ix0 = ox0 - a.pl + 8 * half + s;
+      const int base = ((b * a.h + iy) * a.w + ix0) * a.lda + ci0 + 4 * xcq;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = rok && (unsigned)(ix0 + e) < (unsigned)a.w;
+        xv[j][e] = bload4(rx, ok ? (uint32_t)((base + e * a.lda) * 4) : kOOB);
+      }
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int q = tid + NT * j;
+      if (q < XQ) {
+        const int r2 = q / (CIB / 4);
+        const int half = r2 & 1, s = (r2 >> 1) % KS, hy = (r2 >> 1) / KS;
+        const int ci = 4 * xcq;
+        uint4* blk = &Xs[(s * HH + hy) * CIB * 2];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float v8[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v8[e] = (&xv[j][e].x)[c];
+          bf16x8 h, m, l;
+          split3x8(v8, h, m, l);
+          const int idx = xrow(ci + c) * 2 + (half ^ xoct(ci + c));
+          blk[idx] = __builtin_bit_cast(uint4, h);
+          blk[PL + idx] = __builtin_bit_cast(uint4, m);
+          blk[2 * PL + idx] = __builtin_bit_cast(uint4, l);
+        }
+      }
+    }
+  };
+  // ---- dy fragment of this lane: output channel co, pixels 8 lk .. 8 lk + 7 of tile row kk
+  const int co = co0 + wco0 + lrow;
+  const bool co_ok = co < a.nb;
+  auto load_dy = [&](float (&dv)[8], int t, int kk) {
+    const int b = t / (tiles_x * tiles_y);
+    const int trem = t - b * tiles_x * tiles_y;
+    const int oy = (trem / tiles_x) * TX_H + kk, ox = (trem % tiles_x) * TT_W + 8 * lk;
+    const bool rok = co_ok && oy < a.ho;
+    const int base = ((b * a.ho + oy) * a.wo + ox) * a.ldb + co;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool ok = rok && ox + e < a.wo;
+      dv[e] = bload1(rd, ok ? (uint32_t)((base + e * a.ldb) * 4) : kOOB);
+    }
+  };
+
+  f32x16 acc[KS];                       // taps (wr, s), s = 0..2
+#pragma unroll
+  for (int t = 0; t < KS; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const int a_base = xrow(wci0 + lrow) * 2 + (lk ^ xoct(wci0 + lrow));
+  float colacc = 0.f;
+  float dcur[8], dnext[8];
+
+  if (steps > 0) {
+    load_x(t_begin);
+    load_dy(dcur, t_begin, 0);
+    store_x();
+  }
+  __syncthreads();
+  for (int i = 0; i < steps; ++i) {
+    const int t = t_begin + i;
+    const bool more = i + 1 < steps;
+    if (more) load_x(t + 1);
+#pragma unroll
+    for (int kk = 0; kk < TX_H; ++kk) {
+      if (kk + 1 < TX_H) load_dy(dnext, t, kk + 1);
+      else if (more) load_dy(dnext, t + 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 bh, bm, bl;
+      split3x8(dcur, bh, bm, bl);
+      if (do_colsum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) colacc += dcur[e];
+      }
+      // A fragments one tap ahead of the MFMAs (bounded register footprint)
+      bf16x8 fa[2][NP];
+      auto load_a = [&](bf16x8 (&f)[NP], int s) {
+        const int xa = (s * HH + kk + wr) * CIB * 2 + a_base;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) f[p] = __builtin_bit_cast(bf16x8, Xs[p * PL + xa]);
+      };
+      load_a(fa[0], 0);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+          if (s + 1 < KS) load_a(fa[(s + 1) & 1], s + 1);
+          __builtin_amdgcn_sched_barrier(0);
+          const bf16x8 ah = fa[s & 1][0], am = fa[s & 1][1], al = fa[s & 1][2];
+          f32x16 x = acc[s];
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, x, 0, 0, 0);
+          acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, x, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dcur[e] = dnext[e];
+    }
+    __syncthreads();              // every wave is done with this tile's halo
+    if (more) store_x();
+    __syncthreads();
+  }
+
+  // ---- raw partial sums into this K slice's slab (+ bias column sums in row M)
+  float* S = a.slab + (int64_t)split * a.split_stride;
+  if (do_colsum) {
+    const float v = colacc + __shfl_xor(colacc, 32);
+    if (lk == 0 && co < a.N) S[(int64_t)a.M * a.slab_ld + co] = v;
+  }
+  if (co < a.N) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = ci0 + wci0 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (ci < a.kc) S[((int64_t)(wr * KS + s) * a.kc + ci) * a.slab_ld + co] = acc[s][r];
+      }
+  }
+}
+
 // ---- fp32 weight gradient, 3x3 stride 1: all 9 taps from one staged halo ----------------
 // dW[r][s][ci][co] = sum_p x(p + (r, s) - pad)[ci] . dy(p)[co] on v_mfma_f32_32x32x2_f32, the
 // fp32 counterpart of conv_wgrad_tile_bf16: a workgroup owns CIB x COB channels for all 9
@@ -2543,12 +2741,37 @@ void wgt_blocks(const of_conv_desc* d, int& cib, int& cob) {
   cob = wgt_cfg(d) == 0 ? 128 : 64;
 }
 
-WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false) {
+// fp32 wgrad on conv_wgrad_tile_x3, 3x3 stride 1, by Cout: channel blocks (CIB x COB)
+// 32 x 128 (cfg 0, Cout % 128 == 0), 32 x 96 (cfg 1, Cout 96), 64 x 64 (cfg 2, Cout 64);
+// other layers keep the fp32 wgrad kernels.
+int wgx3_cfg(const of_conv_desc* d) {
+  if (!tile_ok(d)) return -1;
+  return d->cout % 128 == 0 ? 0 : d->cout == 96 ? 1 : d->cout == 64 ? 2 : -1;
+}
+bool wgx3_ok(const of_conv_desc* d) { return wgx3_cfg(d) >= 0; }
+void wgx3_blocks(const of_conv_desc* d, int& cib, int& cob) {
+  const int c = wgx3_cfg(d);
+  cib = c == 2 ? 64 : 32;
+  cob = c == 0 ? 128 : c == 1 ? 96 : 64;
+}
+
+WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) {
   Geo g = geo(d);
   WgradPlan p;
   p.M = g.taps * g.cin_p;
   p.ldc = g.cout_p;
   p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
+  if (x3 && wgx3_ok(d)) {
+    // K = 4 x 16 pixel tiles; one workgroup per CU, equal slices
+    int cib, cob;
+    wgx3_blocks(d, cib, cob);
+    const int chan_tiles = (int)(cdiv(g.cin_p, cib) * cdiv(d->cout, cob));
+    const int T = d->n * (int)cdiv(d->ho, TX_H) * (int)cdiv(d->wo, TT_W);
+    int splits = std::max(1, std::min(T, kCUs / chan_tiles));
+    p.k_per_split = (int)cdiv(T, splits);
+    p.splits = (int)cdiv(T, p.k_per_split);
+    return p;
+  }
   if (wgt_ok(d, bf16)) {
     // K = 8 x 16 pixel tiles; one workgroup per CU (LDS-bound occupancy), equal slices
     int cib, cob;
@@ -2972,12 +3195,21 @@ size_t of_conv2d_wgrad_bf16_workspace(const of_conv_desc* d) {
   return (size_t)p.splits * p.split_stride * sizeof(float);
 }
 
-static int conv_wgrad_impl(bool bf16, const of_conv_desc* d, const float* x, int ldx,
+size_t of_conv2d_wgrad_x3_workspace(const of_conv_desc* d) {
+  if (validate(d) != OF_OK) return 0;
+  if (narrow_ok(d)) return narrow_wgrad_ws(d);
+  WgradPlan p = wgrad_plan(d, false, true);
+  return (size_t)p.splits * p.split_stride * sizeof(float);
+}
+
+// prec: 0 fp32 MFMA, 1 bf16, 2 fp32 with conv_wgrad_tile_x3 where wgx3_ok (else as 0).
+static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int ldx,
                            const float* dy, int lddy, float* dw, float* db, int accumulate,
                            void* workspace, size_t ws_bytes, void* stream) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
+  const bool bf16 = prec == 1, x3 = prec == 2 && wgx3_ok(d);
   OF_CHECK_ARG(x && dy && dw && workspace, "conv wgrad: NULL pointer");
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv wgrad: lddy");
@@ -2989,7 +3221,7 @@ static int conv_wgrad_impl(bool bf16, const of_conv_desc* d, const float* x, int
     if (timing_on()) timing_end(s, MODE_WGRAD * 8 + KIND_NARROW, conv_flops(d));
     return st;
   }
-  WgradPlan p = wgrad_plan(d, bf16);
+  WgradPlan p = wgrad_plan(d, bf16, x3);
   OF_CHECK_ARG(ws_bytes >= (size_t)p.splits * p.split_stride * sizeof(float),
                "conv wgrad: workspace too small");
   GemmArgs a = base_args(d);
@@ -3015,7 +3247,21 @@ static int conv_wgrad_impl(bool bf16, const of_conv_desc* d, const float* x, int
   a.colsum = db != nullptr;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
-  if (wgt_ok(d, bf16)) {
+  if (x3) {
+    a.K = d->n * (int)cdiv(d->ho, TX_H) * (int)cdiv(d->wo, TT_W);
+    int cib, cob;
+    wgx3_blocks(d, cib, cob);
+    const int cfg = wgx3_cfg(d);
+    a.n_tiles = (int)cdiv(d->cout, cob);
+    a.tiles_total = (int)cdiv(g.cin_p, cib) * a.n_tiles;
+    dim3 grid(a.tiles_total * a.splits);
+    if (timing_on()) timing_begin(s);
+    if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 4, 3>), grid, dim3(768), 0, s, a);
+    else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 3, 3>), grid, dim3(576), 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 2, 3>), grid, dim3(768), 0, s, a);
+    if (timing_on()) timing_end(s, 128 + MODE_WGRAD * 8 + cfg, flops);
+    st = check_launch("conv_wgrad_tile_x3");
+  } else if (wgt_ok(d, bf16)) {
     int cib, cob;
     wgt_blocks(d, cib, cob);
     a.K = d->n * (int)cdiv(d->ho, TT_H) * (int)cdiv(d->wo, TT_W);
@@ -3058,14 +3304,21 @@ static int conv_wgrad_impl(bool bf16, const of_conv_desc* d, const float* x, int
 int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float* dy, int lddy,
                     float* dw, float* db, int accumulate, void* workspace, size_t ws_bytes,
                     void* stream) {
-  return conv_wgrad_impl(false, d, x, ldx, dy, lddy, dw, db, accumulate, workspace, ws_bytes,
+  return conv_wgrad_impl(0, d, x, ldx, dy, lddy, dw, db, accumulate, workspace, ws_bytes,
                          stream);
 }
 
 int of_conv2d_wgrad_bf16(const of_conv_desc* d, const float* x, int ldx, const float* dy,
                          int lddy, float* dw, float* db, int accumulate, void* workspace,
                          size_t ws_bytes, void* stream) {
-  return conv_wgrad_impl(true, d, x, ldx, dy, lddy, dw, db, accumulate, workspace, ws_bytes,
+  return conv_wgrad_impl(1, d, x, ldx, dy, lddy, dw, db, accumulate, workspace, ws_bytes,
+                         stream);
+}
+
+int of_conv2d_wgrad_x3(const of_conv_desc* d, const float* x, int ldx, const float* dy,
+                       int lddy, float* dw, float* db, int accumulate, void* workspace,
+                       size_t ws_bytes, void* stream) {
+  return conv_wgrad_impl(2, d, x, ldx, dy, lddy, dw, db, accumulate, workspace, ws_bytes,
                          stream);
 }
 

@@ -238,6 +238,8 @@ class ConvLayer:
         lib = _lib.lib()
         if self.bf16(d):
             return "of_conv2d_wgrad_bf16", lib.of_conv2d_wgrad_bf16_workspace(C.byref(d))
+        if self.mode(d) == 2:
+            return "of_conv2d_wgrad_x3", lib.of_conv2d_wgrad_x3_workspace(C.byref(d))
         return "of_conv2d_wgrad", lib.of_conv2d_wgrad_workspace(C.byref(d))
 
     def dgrad_add_entry(self, d):
