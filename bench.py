@@ -57,7 +57,9 @@ def kind_parts(kind):
 
 
 TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1"}
-X3_BN = {0: "128, 2, 4", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1"}   # conv_tile_x3 waves
+X3_BN = {0: "128, 4, 2", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1",   # conv_tile_x3 waves
+         4: "128, 2, 4"}
+X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4}                                     # and tile rows
 X3_WGT = {0: "1, 4, 3", 1: "1, 3, 3", 2: "2, 2, 3"}   # conv_wgrad_tile_x3<WAVES_CI, CO, R>
 
 
@@ -95,8 +97,10 @@ def kernel_symbol(kind):
         return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (
             fam, X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
     if fam in ("tile_bf16", "tile_x3"):
-        return "void oflow::conv_%s<%s, %d>(oflow::GemmArgs)" % (
-            fam, (TILE_BN if fam == "tile_bf16" else X3_BN)[cfg], mode)
+        if fam == "tile_x3":
+            return "void oflow::conv_tile_x3<%s, %d, %d>(oflow::GemmArgs)" % (X3_BN[cfg], mode,
+                                                                            X3_TH[cfg])
+        return "void oflow::conv_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_BN[cfg], mode)
     if fam == "bf16" and mode == 2:
         return "void oflow::conv_wgrad_bf16<%s>(oflow::GemmArgs)" % TILE_TEMPLATE[cfg]
     return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_TEMPLATE[cfg], mode)

@@ -838,6 +838,10 @@ constexpr int TT_H = 8, TT_W = 16;   // wgrad halo tiles
 #define OF_TF_W 32
 #endif
 constexpr int TF_H = OF_TF_H, TF_W = OF_TF_W;
+#ifndef OF_X3_TH0
+#define OF_X3_TH0 8
+#endif
+constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows x 32 px
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE>
 __global__ __launch_bounds__(256, 2) void conv_tile_bf16(GemmArgs a) {
@@ -1062,10 +1066,10 @@ __device__ __forceinline__ void split3x4(const float4& v, uint2& h, uint2& m, ui
   l = make_uint2((lb[0] >> 16) | (lb[1] & 0xffff0000u), (lb[2] >> 16) | (lb[3] & 0xffff0000u));
 }
 
-template <int BN, int WAVES_M, int WAVES_N, int MODE>
+template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_tile_x3(GemmArgs a) {
-  constexpr int BM = TF_H * TF_W, KS = 3, NP = 3;
-  constexpr int HH = TF_H + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
+  constexpr int BM = TH * TF_W, KS = 3, NP = 3;
+  constexpr int HH = TH + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int NT = 64 * WAVES_M * WAVES_N;                   // 4-8 waves
@@ -1087,10 +1091,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_tile_x3(GemmAr
   const int n0 = tile_n * BN;
   const int OH = MODE == MODE_FWD ? a.ho : a.h, OW = MODE == MODE_FWD ? a.wo : a.w;
   const int SH = MODE == MODE_FWD ? a.h : a.ho, SW = MODE == MODE_FWD ? a.w : a.wo;
-  const int tiles_x = (OW + TF_W - 1) / TF_W, tiles_y = (OH + TF_H - 1) / TF_H;
+  const int tiles_x = (OW + TF_W - 1) / TF_W, tiles_y = (OH + TH - 1) / TH;
   const int b = tile_m / (tiles_x * tiles_y);
   const int trem = tile_m - b * tiles_x * tiles_y;
-  const int oy0 = (trem / tiles_x) * TF_H, ox0 = (trem % tiles_x) * TF_W;
+  const int oy0 = (trem / tiles_x) * TH, ox0 = (trem % tiles_x) * TF_W;
   const int hy0 = MODE == MODE_FWD ? oy0 - a.pt : oy0 + a.pt - (KS - 1);
   const int hx0 = MODE == MODE_FWD ? ox0 - a.pl : ox0 + a.pl - (KS - 1);
   const int c_begin = split * a.k_per_split;
@@ -2654,6 +2658,12 @@ int launch_gemm_bf16(const GemmArgs& a, hipStream_t s, double flops) {
 // bf16 3x3 stride-1 fwd / dgrad: halo-tiled kernel (conv_tile_bf16).
 bool tile_ok(const of_conv_desc* d) { return d->kh == 3 && d->kw == 3 && d->stride == 1; }
 
+// conv_tile_x3 with BN = 128 takes X3_TH0 x 32 output tiles (twice the MFMAs per staged B
+// tap) when that still leaves >= 4 workgroups per CU, else 4 x 32.
+bool x3_tall(int n, int oh, int ow, int N) {
+  return pick_bn(N) == 128 && (int64_t)n * cdiv(oh, X3_TH0) * cdiv(ow, TF_W) >= 4 * kCUs;
+}
+
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false) {
   GemmArgs a = base_args(d);
   const bool fwd = mode == MODE_FWD;
@@ -2662,8 +2672,9 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   a.nb = fwd ? d->cout : g.nd;
   a.ldb = fwd ? g.kf16 : (int)g.kd16;
   const int OH = fwd ? d->ho : d->h, OW = fwd ? d->wo : d->w;
-  const int m_tiles = d->n * (int)cdiv(OH, TF_H) * (int)cdiv(OW, TF_W);
-  a.bm = TF_H * TF_W;
+  const int th = x3 && x3_tall(d->n, OH, OW, a.N) ? X3_TH0 : TF_H;
+  const int m_tiles = d->n * (int)cdiv(OH, th) * (int)cdiv(OW, TF_W);
+  a.bm = th * TF_W;
   a.ngroups = 1;
   Group& G = a.grp[0];
   G = Group{};
@@ -2713,12 +2724,13 @@ template <int MODE>
 int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
   const int bn = pick_bn(a.N);
   dim3 grid(a.tiles_total * a.splits), block(256);
-  const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
+  const int cfg = bn == 128 ? (a.bm == X3_TH0 * TF_W ? 0 : 4) : bn == 96 ? 1 : bn == 64 ? 2 : 3;
   if (timing_on()) timing_begin(s);
-  if (cfg == 0) hipLaunchKernelGGL((conv_tile_x3<128, 2, 4, MODE>), grid, dim3(512), 0, s, a);
-  else if (cfg == 1) hipLaunchKernelGGL((conv_tile_x3<96, 2, 3, MODE>), grid, dim3(384), 0, s, a);
-  else if (cfg == 2) hipLaunchKernelGGL((conv_tile_x3<64, 4, 2, MODE>), grid, dim3(512), 0, s, a);
-  else hipLaunchKernelGGL((conv_tile_x3<32, 4, 1, MODE>), grid, block, 0, s, a);
+  if (cfg == 0) hipLaunchKernelGGL((conv_tile_x3<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);
+  else if (cfg == 4) hipLaunchKernelGGL((conv_tile_x3<128, 2, 4, MODE, 4>), grid, dim3(512), 0, s, a);
+  else if (cfg == 1) hipLaunchKernelGGL((conv_tile_x3<96, 2, 3, MODE, 4>), grid, dim3(384), 0, s, a);
+  else if (cfg == 2) hipLaunchKernelGGL((conv_tile_x3<64, 4, 2, MODE, 4>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((conv_tile_x3<32, 4, 1, MODE, 4>), grid, block, 0, s, a);
   if (timing_on()) timing_end(s, 128 + MODE * 8 + cfg, flops);
   int st = check_launch("conv_tile_x3");
   if (st || a.splits == 1) return st;
