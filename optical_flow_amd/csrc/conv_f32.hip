@@ -1072,8 +1072,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_tile_x3(GemmAr
   constexpr int HH = TH + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int NT = 64 * WAVES_M * WAVES_N;                   // 4-8 waves
-  static_assert(NT % 64 == 0 && NT <= 512 && WM % 32 == 0 && WN % 32 == 0 && TM >= 1 && TN >= 1,
+  constexpr int NT = 64 * WAVES_M * WAVES_N;                   // 4-12 waves
+  static_assert(NT % 64 == 0 && NT <= 1024 && WM % 32 == 0 && WN % 32 == 0 && TM >= 1 && TN >= 1,
                 "tile");
   constexpr int HQ = HP * 8, HS = (HQ + NT - 1) / NT;          // halo quads (32 ch)
   constexpr int BOCT = NP * BN * 4, BSL = (BOCT + NT - 1) / NT; // B octets per tap
@@ -2658,10 +2658,11 @@ int launch_gemm_bf16(const GemmArgs& a, hipStream_t s, double flops) {
 // bf16 3x3 stride-1 fwd / dgrad: halo-tiled kernel (conv_tile_bf16).
 bool tile_ok(const of_conv_desc* d) { return d->kh == 3 && d->kw == 3 && d->stride == 1; }
 
-// conv_tile_x3 with BN = 128 takes X3_TH0 x 32 output tiles (twice the MFMAs per staged B
-// tap) when that still leaves >= 4 workgroups per CU, else 4 x 32.
+// conv_tile_x3 with BN = 128 or 96 takes X3_TH0 x 32 output tiles (twice the MFMAs per staged
+// B tap) when that still leaves >= 4 workgroups per CU, else 4 x 32.
 bool x3_tall(int n, int oh, int ow, int N) {
-  return pick_bn(N) == 128 && (int64_t)n * cdiv(oh, X3_TH0) * cdiv(ow, TF_W) >= 4 * kCUs;
+  const int bn = pick_bn(N);
+  return (bn == 128 || bn == 96) && (int64_t)n * cdiv(oh, X3_TH0) * cdiv(ow, TF_W) >= 4 * kCUs;
 }
 
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false) {
@@ -2724,10 +2725,12 @@ template <int MODE>
 int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
   const int bn = pick_bn(a.N);
   dim3 grid(a.tiles_total * a.splits), block(256);
-  const int cfg = bn == 128 ? (a.bm == X3_TH0 * TF_W ? 0 : 4) : bn == 96 ? 1 : bn == 64 ? 2 : 3;
+  const bool tall = a.bm == X3_TH0 * TF_W;
+  const int cfg = bn == 128 ? (tall ? 0 : 4) : bn == 96 ? (tall ? 5 : 1) : bn == 64 ? 2 : 3;
   if (timing_on()) timing_begin(s);
   if (cfg == 0) hipLaunchKernelGGL((conv_tile_x3<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);
   else if (cfg == 4) hipLaunchKernelGGL((conv_tile_x3<128, 2, 4, MODE, 4>), grid, dim3(512), 0, s, a);
+  else if (cfg == 5) hipLaunchKernelGGL((conv_tile_x3<96, 4, 3, MODE, X3_TH0>), grid, dim3(768), 0, s, a);
   else if (cfg == 1) hipLaunchKernelGGL((conv_tile_x3<96, 2, 3, MODE, 4>), grid, dim3(384), 0, s, a);
   else if (cfg == 2) hipLaunchKernelGGL((conv_tile_x3<64, 4, 2, MODE, 4>), grid, dim3(512), 0, s, a);
   else hipLaunchKernelGGL((conv_tile_x3<32, 4, 1, MODE, 4>), grid, block, 0, s, a);
