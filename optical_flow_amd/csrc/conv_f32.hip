@@ -1713,14 +1713,16 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
 // exactly into hi + mid + lo bf16 terms and the six products of conv_tile_x3.  A workgroup
 // (12 waves) owns CIB = 32 input x COB = 128 output channels for all 9 taps (wave = 32 ci x
 // 32 co x the 3 taps of one kernel row: 48 accumulator registers, so three waves fit per
-// SIMD) and walks 4 x 16 output-pixel tiles of its K slice.  The x halo
-// (6 rows x 18 px) is staged once per tile as three split planes x three copies shifted by
+// SIMD) and walks XH x 16 output-pixel tiles of its K slice (XH = 8; 4 for the 64 x 64
+// block, whose halo is twice as wide).  The x halo ((XH + 2) rows x 18 px) is staged once
+// per tile as three split planes x three copies shifted by
 // s = 0, 1, 2 pixels (aligned 16-byte A fragments, the swizzles of conv_wgrad_tile_bf16);
-// it is single-buffered (55 KB) and register-staged one tile ahead.  dy never enters LDS:
+// it is single-buffered (92 / 110 KB) and register-staged one tile ahead.  dy never enters LDS:
 // a lane loads its B fragment (8 pixels of one channel, coalesced across the 32 channels of
 // a pixel) straight from L2 one k-step ahead and splits it in registers (the three kernel-row
 // waves of a channel block read the same dy lines).  Output: the split-K slabs of the other wgrad kernels.
-constexpr int TX_H = 4;    // conv_wgrad_tile_x3 pixel tile: 4 rows x 16 px
+// conv_wgrad_tile_x3 pixel tiles: XH rows x 16 px (8 rows where the halo fits LDS)
+int wgx3_rows(int cfg) { return cfg == 2 ? 4 : 8; }
 
 __device__ __forceinline__ void split3x8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
   uint2 h0, m0, l0, h1, m1, l1;
@@ -1731,11 +1733,11 @@ __device__ __forceinline__ void split3x8(const float* v, bf16x8& h, bf16x8& m, b
   l = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
 }
 
-template <int WAVES_CI, int WAVES_CO, int WAVES_R>
+template <int WAVES_CI, int WAVES_CO, int WAVES_R, int XH>
 __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wgrad_tile_x3(GemmArgs a) {
   constexpr int NT = 64 * WAVES_CI * WAVES_CO * WAVES_R;
   static_assert(WAVES_R == 3, "one kernel row per wave group");
-  constexpr int CIB = 32 * WAVES_CI, COB = 32 * WAVES_CO, KS = 3, HH = TX_H + KS - 1, NP = 3;
+  constexpr int CIB = 32 * WAVES_CI, COB = 32 * WAVES_CO, KS = 3, HH = XH + KS - 1, NP = 3;
   constexpr int XQ = HH * KS * 2 * (CIB / 4), XS = (XQ + NT - 1) / NT;   // (hy, s, half, ci quad)
   constexpr int PL = KS * HH * CIB * 2;                              // uint4 per plane
   __shared__ uint4 Xs[NP * PL];
@@ -1754,7 +1756,7 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wg
   const int t_begin = split * a.k_per_split;
   const int t_end = min(a.K, t_begin + a.k_per_split);
   const int steps = max(0, t_end - t_begin);
-  const int tiles_x = (a.wo + TT_W - 1) / TT_W, tiles_y = (a.ho + TX_H - 1) / TX_H;
+  const int tiles_x = (a.wo + TT_W - 1) / TT_W, tiles_y = (a.ho + XH - 1) / XH;
   const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
   const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
   const int wr = wave / (WAVES_CI * WAVES_CO);            // this wave's kernel row
@@ -1772,7 +1774,7 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wg
   auto load_x = [&](int t) {
     const int b = t / (tiles_x * tiles_y);
     const int trem = t - b * tiles_x * tiles_y;
-    const int oy0 = (trem / tiles_x) * TX_H, ox0 = (trem % tiles_x) * TT_W;
+    const int oy0 = (trem / tiles_x) * XH, ox0 = (trem % tiles_x) * TT_W;
 #pragma unroll
     for (int j = 0; j < XS; ++j) {
       const int q = tid + NT * j;
@@ -1819,7 +1821,7 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wg
   auto load_dy = [&](float (&dv)[8], int t, int kk) {
     const int b = t / (tiles_x * tiles_y);
     const int trem = t - b * tiles_x * tiles_y;
-    const int oy = (trem / tiles_x) * TX_H + kk, ox = (trem % tiles_x) * TT_W + 8 * lk;
+    const int oy = (trem / tiles_x) * XH + kk, ox = (trem % tiles_x) * TT_W + 8 * lk;
     const bool rok = co_ok && oy < a.ho;
     const int base = ((b * a.ho + oy) * a.wo + ox) * a.ldb + co;
 #pragma unroll
@@ -1849,8 +1851,8 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wg
     const bool more = i + 1 < steps;
     if (more) load_x(t + 1);
 #pragma unroll
-    for (int kk = 0; kk < TX_H; ++kk) {
-      if (kk + 1 < TX_H) load_dy(dnext, t, kk + 1);
+    for (int kk = 0; kk < XH; ++kk) {
+      if (kk + 1 < XH) load_dy(dnext, t, kk + 1);
       else if (more) load_dy(dnext, t + 1, 0);
       __builtin_amdgcn_sched_barrier(0);
       bf16x8 bh, bm, bl;
@@ -2781,7 +2783,7 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
     int cib, cob;
     wgx3_blocks(d, cib, cob);
     const int chan_tiles = (int)(cdiv(g.cin_p, cib) * cdiv(d->cout, cob));
-    const int T = d->n * (int)cdiv(d->ho, TX_H) * (int)cdiv(d->wo, TT_W);
+    const int T = d->n * (int)cdiv(d->ho, wgx3_rows(wgx3_cfg(d))) * (int)cdiv(d->wo, TT_W);
     int splits = std::max(1, std::min(T, kCUs / chan_tiles));
     p.k_per_split = (int)cdiv(T, splits);
     p.splits = (int)cdiv(T, p.k_per_split);
@@ -3263,7 +3265,7 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
   if (x3) {
-    a.K = d->n * (int)cdiv(d->ho, TX_H) * (int)cdiv(d->wo, TT_W);
+    a.K = d->n * (int)cdiv(d->ho, wgx3_rows(wgx3_cfg(d))) * (int)cdiv(d->wo, TT_W);
     int cib, cob;
     wgx3_blocks(d, cib, cob);
     const int cfg = wgx3_cfg(d);
@@ -3271,9 +3273,9 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     a.tiles_total = (int)cdiv(g.cin_p, cib) * a.n_tiles;
     dim3 grid(a.tiles_total * a.splits);
     if (timing_on()) timing_begin(s);
-    if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 4, 3>), grid, dim3(768), 0, s, a);
-    else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 3, 3>), grid, dim3(576), 0, s, a);
-    else hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 2, 3>), grid, dim3(768), 0, s, a);
+    if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 4, 3, 8>), grid, dim3(768), 0, s, a);
+    else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 3, 3, 8>), grid, dim3(576), 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 2, 3, 4>), grid, dim3(768), 0, s, a);
     if (timing_on()) timing_end(s, 128 + MODE_WGRAD * 8 + cfg, flops);
     st = check_launch("conv_wgrad_tile_x3");
   } else if (wgt_ok(d, bf16)) {
