@@ -293,8 +293,8 @@ def main():
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("kernel") == sym and pmc.get("config") == [H, W, B]:
-                traffic = pmc.get("hbm_bytes_per_launch")
+            if pmc.get("config") == [H, W, B] and sym in pmc.get("kernels", {}):
+                traffic = pmc["kernels"][sym]["hbm_bytes_per_launch"]
         allconv = sum(v[0] for v in per.values()) / (sum(v[1] for v in per.values()) * 1e-3) / 1e12
         fam = kind_parts(dom)[2]
         # the split kernel spends six bf16 MFMAs per fp32 product: its ceiling is 1/6 of bf16

@@ -1,5 +1,5 @@
 """Turn two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of `python bench.py` into HBM bytes
-per launch for every conv_gemm_f32 template instance -> profiles/pmc_traffic.json.
+per launch for every conv kernel template instance -> profiles/pmc_traffic.json.
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts 128-B requests of wide
 coalesced reads as 64 B, i.e. half the bytes of 16-B/lane loads -> doubled here; WRITE_SIZE
@@ -31,7 +31,7 @@ def main():
                    "16-B/lane loads) + WRITE_SIZE*1024; averaged over all launches of the "
                    "bench command (mixed layer shapes)"}
     for k in f:
-        if "conv_gemm_f32" not in k or k not in w:
+        if "oflow::conv_" not in k or k not in w:
             continue
         fb = sum(f[k]) / len(f[k]) * 1024 * 2
         wb = sum(w[k]) / len(w[k]) * 1024
