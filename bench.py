@@ -60,7 +60,7 @@ TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1"}
 X3_BN = {0: "128, 4, 2", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1",   # conv_tile_x3 waves
          4: "128, 2, 4", 5: "96, 4, 3"}
 X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4, 5: 8}                               # and tile rows
-X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4"}   # conv_wgrad_tile_x3<CI, CO, R, rows>
+X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4"}   # conv_wgrad_tile_x3<CI, CO, R, rows>
 
 
 WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>

@@ -1713,8 +1713,8 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
 // exactly into hi + mid + lo bf16 terms and the six products of conv_tile_x3.  A workgroup
 // (12 waves) owns CIB = 32 input x COB = 128 output channels for all 9 taps (wave = 32 ci x
 // 32 co x the 3 taps of one kernel row: 48 accumulator registers, so three waves fit per
-// SIMD) and walks XH x 16 output-pixel tiles of its K slice (XH = 8; 4 for the 64 x 64
-// block, whose halo is twice as wide).  The x halo ((XH + 2) rows x 18 px) is staged once
+// SIMD) and walks XH x 16 output-pixel tiles of its K slice (XH = 8; 4 for the 64-channel
+// input blocks, whose halo is twice as wide).  The x halo ((XH + 2) rows x 18 px) is staged once
 // per tile as three split planes x three copies shifted by
 // s = 0, 1, 2 pixels (aligned 16-byte A fragments, the swizzles of conv_wgrad_tile_bf16);
 // it is single-buffered (92 / 110 KB) and register-staged one tile ahead.  dy never enters LDS:
@@ -1722,7 +1722,7 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
 // a pixel) straight from L2 one k-step ahead and splits it in registers (the three kernel-row
 // waves of a channel block read the same dy lines).  Output: the split-K slabs of the other wgrad kernels.
 // conv_wgrad_tile_x3 pixel tiles: XH rows x 16 px (8 rows where the halo fits LDS)
-int wgx3_rows(int cfg) { return cfg == 2 ? 4 : 8; }
+int wgx3_rows(int cfg) { return cfg >= 2 ? 4 : 8; }
 
 __device__ __forceinline__ void split3x8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
   uint2 h0, m0, l0, h1, m1, l1;
@@ -2759,17 +2759,17 @@ void wgt_blocks(const of_conv_desc* d, int& cib, int& cob) {
 }
 
 // fp32 wgrad on conv_wgrad_tile_x3, 3x3 stride 1, by Cout: channel blocks (CIB x COB)
-// 32 x 128 (cfg 0, Cout % 128 == 0), 32 x 96 (cfg 1, Cout 96), 64 x 64 (cfg 2, Cout 64);
-// other layers keep the fp32 wgrad kernels.
+// 32 x 128 (cfg 0, Cout % 128 == 0), 32 x 96 (cfg 1, Cout 96), 64 x 64 (cfg 2, Cout 64),
+// 64 x 32 (cfg 3, Cout 32); other layers keep the fp32 wgrad kernels.
 int wgx3_cfg(const of_conv_desc* d) {
   if (!tile_ok(d)) return -1;
-  return d->cout % 128 == 0 ? 0 : d->cout == 96 ? 1 : d->cout == 64 ? 2 : -1;
+  return d->cout % 128 == 0 ? 0 : d->cout == 96 ? 1 : d->cout == 64 ? 2 : d->cout == 32 ? 3 : -1;
 }
 bool wgx3_ok(const of_conv_desc* d) { return wgx3_cfg(d) >= 0; }
 void wgx3_blocks(const of_conv_desc* d, int& cib, int& cob) {
   const int c = wgx3_cfg(d);
-  cib = c == 2 ? 64 : 32;
-  cob = c == 0 ? 128 : c == 1 ? 96 : 64;
+  cib = c >= 2 ? 64 : 32;
+  cob = c == 0 ? 128 : c == 1 ? 96 : c == 2 ? 64 : 32;
 }
 
 WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) {
@@ -3275,7 +3275,8 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     if (timing_on()) timing_begin(s);
     if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 4, 3, 8>), grid, dim3(768), 0, s, a);
     else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 3, 3, 8>), grid, dim3(576), 0, s, a);
-    else hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 2, 3, 4>), grid, dim3(768), 0, s, a);
+    else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 2, 3, 4>), grid, dim3(768), 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 1, 3, 4>), grid, dim3(384), 0, s, a);
     if (timing_on()) timing_end(s, 128 + MODE_WGRAD * 8 + cfg, flops);
     st = check_launch("conv_wgrad_tile_x3");
   } else if (wgt_ok(d, bf16)) {
