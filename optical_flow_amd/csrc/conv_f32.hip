@@ -1775,14 +1775,15 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wg
     const int b = t / (tiles_x * tiles_y);
     const int trem = t - b * tiles_x * tiles_y;
     const int oy0 = (trem / tiles_x) * XH, ox0 = (trem % tiles_x) * TT_W;
+    const int iy0 = oy0 - a.pt, ix00 = ox0 - a.pl;
 #pragma unroll
     for (int j = 0; j < XS; ++j) {
       const int q = tid + NT * j;
       const int r2 = q / (CIB / 4);
       const int half = r2 & 1, s = (r2 >> 1) % KS, hy = (r2 >> 1) / KS;
-      const int iy = oy0 - a.pt + hy;
+      const int iy = iy0 + hy;
       const bool rok = q < XQ && xc_ok && (unsigned)iy < (unsigned)a.h;
-      const int ix0 = ox0 - a.pl + 8 * half + s;
+      const int ix0 = ix00 + 8 * half + s;
       const int base = ((b * a.h + iy) * a.w + ix0) * a.lda + ci0 + 4 * xcq;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -1818,10 +1819,23 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wg
   // ---- dy fragment of this lane: output channel co, pixels 8 lk .. 8 lk + 7 of tile row kk
   const int co = co0 + wco0 + lrow;
   const bool co_ok = co < a.nb;
+  // Interior dy rows (all 16 pixels and the whole channel block in range) take fixed per-lane
+  // offsets plus a uniform scalar offset: no per-load address math or bounds tests.
+  const uint32_t dy_lane = (uint32_t)((8 * lk * a.ldb + co) * 4);
+  const bool dy_co_full = co0 + COB <= a.nb;
   auto load_dy = [&](float (&dv)[8], int t, int kk) {
     const int b = t / (tiles_x * tiles_y);
     const int trem = t - b * tiles_x * tiles_y;
-    const int oy = (trem / tiles_x) * XH + kk, ox = (trem % tiles_x) * TT_W + 8 * lk;
+    const int oy = (trem / tiles_x) * XH + kk, ox0 = (trem % tiles_x) * TT_W;
+    if (dy_co_full && oy < a.ho && ox0 + TT_W <= a.wo) {
+      const int so = ((b * a.ho + oy) * a.wo + ox0) * a.ldb * 4;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        dv[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rd, dy_lane + e * a.ldb * 4, so, 0));
+      return;
+    }
+    const int ox = ox0 + 8 * lk;
     const bool rok = co_ok && oy < a.ho;
     const int base = ((b * a.ho + oy) * a.wo + ox) * a.ldb + co;
 #pragma unroll
