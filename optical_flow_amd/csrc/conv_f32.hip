@@ -2706,8 +2706,28 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   G.K = a.K;
   a.splits = 1;
   a.k_per_split = a.K;
-  if (a.tiles_total < (x3 ? kCUs : 2 * kCUs)) {
-    int sp = std::max(1, ((x3 ? 2 : 4) * kCUs) / a.tiles_total);
+  if (x3) {
+    // One workgroup per CU: choose the K split with the least modelled time, in units of one
+    // chunk (9 taps): rounds of 256 workgroups x (chunks per slice + 1 for prologue and
+    // epilogue), plus 0.5 per slice and tile round for the slab write and epilogue pass.
+    // (Measured: enc.l3 384 tiles unsplit, dec1 192 tiles unsplit, enc.l4 96 tiles in 2.)
+    int best = 1;
+    double best_cost = 1e30;
+    for (int sp = 1; sp <= std::min(8, a.K); ++sp) {
+      const int per = (int)cdiv(a.K, sp);
+      if (cdiv(a.K, per) != sp) continue;            // not a distinct slice count
+      const int64_t w = (int64_t)a.tiles_total * sp;
+      const double cost = (double)cdiv(w, kCUs) * (per + 1.0) +
+                          (sp > 1 ? 0.5 * sp * a.tiles_total / (double)kCUs : 0.0);
+      if (cost < best_cost - 1e-9) {
+        best_cost = cost;
+        best = sp;
+      }
+    }
+    a.k_per_split = (int)cdiv(a.K, best);
+    a.splits = (int)cdiv(a.K, a.k_per_split);
+  } else if (a.tiles_total < 2 * kCUs) {
+    int sp = std::max(1, (4 * kCUs) / a.tiles_total);
     sp = std::min(sp, std::max(1, a.K / 2));       // >= 2 chunks (6 tap rows) per slice
     a.k_per_split = (int)cdiv(a.K, sp);
     a.splits = (int)cdiv(a.K, a.k_per_split);
