@@ -56,7 +56,8 @@ def kind_parts(kind):
     return (kind % 32) // 8, kind % 8, fam
 
 
-TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1"}
+TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1", 4: "128, 4, 2"}
+TILE_TH = {0: 4, 1: 4, 2: 4, 3: 4, 4: 8}                # conv_tile_bf16 output tile rows
 X3_BN = {0: "128, 4, 2", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1",   # conv_tile_x3 waves
          4: "128, 2, 4", 5: "96, 4, 3"}
 X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4, 5: 8}                               # and tile rows
@@ -100,7 +101,8 @@ def kernel_symbol(kind):
         if fam == "tile_x3":
             return "void oflow::conv_tile_x3<%s, %d, %d>(oflow::GemmArgs)" % (X3_BN[cfg], mode,
                                                                             X3_TH[cfg])
-        return "void oflow::conv_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_BN[cfg], mode)
+        return "void oflow::conv_tile_bf16<%s, %d, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode,
+                                                                            TILE_TH[cfg])
     if fam == "bf16" and mode == 2:
         return "void oflow::conv_wgrad_bf16<%s>(oflow::GemmArgs)" % TILE_TEMPLATE[cfg]
     return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_TEMPLATE[cfg], mode)
