@@ -295,7 +295,8 @@ def main():
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("config") == [H, W, B] and sym in pmc.get("kernels", {}):
+            same_math = args.precision != "fp32" or pmc.get("f32_split", True) == ops.F32_SPLIT
+            if pmc.get("config") == [H, W, B] and same_math and sym in pmc.get("kernels", {}):
                 traffic = pmc["kernels"][sym]["hbm_bytes_per_launch"]
         allconv = sum(v[0] for v in per.values()) / (sum(v[1] for v in per.values()) * 1e-3) / 1e12
         fam = kind_parts(dom)[2]

@@ -26,7 +26,9 @@ def main():
     fetch_csv, write_csv, H, W, B = sys.argv[1:6]
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
+    # the PMC passes of tools/gpu_round.sh run the default fp32 path (split kernels on)
     out = {"config": [int(H), int(W), int(B)], "kernels": {},
+           "f32_split": os.environ.get("OFLOW_F32_SPLIT", "1") == "1",
            "note": "bytes per launch = 2*FETCH_SIZE*1024 (gfx950 half-count correction for "
                    "16-B/lane loads) + WRITE_SIZE*1024; averaged over all launches of the "
                    "bench command (mixed layer shapes)"}
