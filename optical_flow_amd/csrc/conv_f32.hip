@@ -1062,9 +1062,11 @@ __device__ __forceinline__ void split3x4(const float4& v, uint2& h, uint2& m, ui
     mb[e] = __float_as_uint(r) & 0xffff0000u;
     lb[e] = __float_as_uint(r - __uint_as_float(mb[e]));   // <= 8 significant bits: exact
   }
-  h = make_uint2((hb[0] >> 16) | hb[1], (hb[2] >> 16) | hb[3]);
-  m = make_uint2((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3]);
-  l = make_uint2((lb[0] >> 16) | (lb[1] & 0xffff0000u), (lb[2] >> 16) | (lb[3] & 0xffff0000u));
+  // upper halves of (e0, e1) -> one dword, element 0 low: one v_perm_b32 per pair
+  auto hi2 = [](uint32_t e0, uint32_t e1) { return __builtin_amdgcn_perm(e1, e0, 0x07060302u); };
+  h = make_uint2(hi2(hb[0], hb[1]), hi2(hb[2], hb[3]));
+  m = make_uint2(hi2(mb[0], mb[1]), hi2(mb[2], mb[3]));
+  l = make_uint2(hi2(lb[0], lb[1]), hi2(lb[2], lb[3]));
 }
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH>
