@@ -59,8 +59,9 @@ def kind_parts(kind):
 TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1", 4: "128, 4, 2"}
 TILE_TH = {0: 4, 1: 4, 2: 4, 3: 4, 4: 8}                # conv_tile_bf16 output tile rows
 X3_BN = {0: "128, 4, 2", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1",   # conv_tile_x3 waves
-         4: "128, 2, 4", 5: "96, 4, 3"}
-X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4, 5: 8}                               # and tile rows
+         4: "128, 2, 2", 5: "96, 4, 3", 6: "128, 2, 4"}
+X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4, 5: 8, 6: 4}                         # and tile rows
+X3_NB = {4: 1}                                                             # single-buffered B
 X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4"}   # conv_wgrad_tile_x3<CI, CO, R, rows>
 
 
@@ -99,8 +100,9 @@ def kernel_symbol(kind):
             fam, X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
     if fam in ("tile_bf16", "tile_x3"):
         if fam == "tile_x3":
-            return "void oflow::conv_tile_x3<%s, %d, %d>(oflow::GemmArgs)" % (X3_BN[cfg], mode,
-                                                                            X3_TH[cfg])
+            nb = (", %d" % X3_NB[cfg]) if cfg in X3_NB else ""
+            return "void oflow::conv_tile_x3<%s, %d, %d%s>(oflow::GemmArgs)" % (
+                X3_BN[cfg], mode, X3_TH[cfg], nb)
         return "void oflow::conv_tile_bf16<%s, %d, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode,
                                                                             TILE_TH[cfg])
     if fam == "bf16" and mode == 2:

@@ -1069,8 +1069,10 @@ __device__ __forceinline__ void split3x4(const float4& v, uint2& h, uint2& m, ui
   l = make_uint2(hi2(lb[0], lb[1]), hi2(lb[2], lb[3]));
 }
 
-template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_tile_x3(GemmArgs a) {
+// NB = B buffers: 2 (double-buffered, one barrier per tap) or 1 (80 KB of LDS with TH = 4,
+// so two 4-wave workgroups share a CU; two barriers per tap).
+template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int NB = 2>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_tile_x3(GemmArgs a) {
   constexpr int BM = TH * TF_W, KS = 3, NP = 3;
   constexpr int HH = TH + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -1081,7 +1083,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_tile_x3(GemmAr
   constexpr int HQ = HP * 8, HS = (HQ + NT - 1) / NT;          // halo quads (32 ch)
   constexpr int BOCT = NP * BN * 4, BSL = (BOCT + NT - 1) / NT; // B octets per tap
   __shared__ uint4 Ah[NP][HP * SROW16];
-  __shared__ uint4 Bs[2][NP * BN * SROW16];
+  __shared__ uint4 Bs[NB][NP * BN * SROW16];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1203,7 +1205,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_tile_x3(GemmAr
     if (more_c) load_halo(c + 1);
 #pragma unroll
     for (int t = 0; t < KS * KS; ++t) {
-      const int buf = (cc + t) & 1;
+      const int buf = NB == 2 ? (cc + t) & 1 : 0;
       const bool more = t + 1 < KS * KS || more_c;
       if (more) load_b(t + 1 < KS * KS ? c : c + 1, t + 1 < KS * KS ? t + 1 : 0);
       __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this step's MFMAs
@@ -1237,9 +1239,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_tile_x3(GemmAr
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][0][j], x, 0, 0, 0);
           }
       __builtin_amdgcn_sched_barrier(0);   // the stores wait for the prefetch: after the MFMAs
-      if (t + 1 == KS * KS && more_c) __syncthreads();   // all reads of this chunk's halo done
+      // single B buffer: every wave must be done with it; double: only with the halo
+      if (NB == 1 ? more : (t + 1 == KS * KS && more_c)) __syncthreads();
       if (more) {
-        store_b(buf ^ 1);
+        store_b(NB == 2 ? buf ^ 1 : 0);
         if (t + 1 == KS * KS && more_c) store_halo();
       }
       __syncthreads();
@@ -2684,6 +2687,15 @@ bool x3_tall(int n, int oh, int ow, int N) {
   return (bn == 128 || bn == 96) && (int64_t)n * cdiv(oh, X3_TH0) * cdiv(ow, TF_W) >= 4 * kCUs;
 }
 
+// conv_tile_x3 BN = 128 with 4 x 32 tiles: grids of >= X3_NB1_MIN tiles take the
+// single-buffered 4-wave form (two workgroups per CU: enc.l3 142 -> 150, dec2 dgrad 170 ->
+// 182 TFLOP/s); smaller grids, which split K, keep the 8-wave double-buffered one (the
+// 4-wave form measured dec1 134 -> 108, enc.l4 159 -> 143).
+constexpr int X3_NB1_MIN = 384;
+bool x3_nb1(const GemmArgs& a, bool tall) {
+  return !tall && pick_bn(a.N) == 128 && a.tiles_total >= X3_NB1_MIN;
+}
+
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false) {
   GemmArgs a = base_args(d);
   const bool fwd = mode == MODE_FWD;
@@ -2717,14 +2729,17 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
     // chunk (9 taps): rounds of 256 workgroups x (chunks per slice + 1 for prologue and
     // epilogue), plus 0.5 per slice and tile round for the slab write and epilogue pass.
     // (Measured: enc.l3 384 tiles unsplit, dec1 192 tiles unsplit, enc.l4 96 tiles in 2.)
+    // (The single-buffered BN = 128 4 x 32 configuration, used from X3_NB1_MIN tiles, runs
+    // two workgroups per CU.)
+    const int slots = x3_nb1(a, tall) ? 2 * kCUs : kCUs;
     int best = 1;
     double best_cost = 1e30;
     for (int sp = 1; sp <= std::min(8, a.K); ++sp) {
       const int per = (int)cdiv(a.K, sp);
       if (cdiv(a.K, per) != sp) continue;            // not a distinct slice count
       const int64_t w = (int64_t)a.tiles_total * sp;
-      const double cost = (double)cdiv(w, kCUs) * (per + 1.0) +
-                          (sp > 1 ? 0.5 * sp * a.tiles_total / (double)kCUs : 0.0);
+      const double cost = (double)cdiv(w, slots) * (per + 1.0) +
+                          (sp > 1 ? 0.5 * sp * a.tiles_total / (double)slots : 0.0);
       if (cost < best_cost - 1e-9) {
         best_cost = cost;
         best = sp;
@@ -2770,10 +2785,12 @@ int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
   const int bn = pick_bn(a.N);
   dim3 grid(a.tiles_total * a.splits), block(256);
   const bool tall = a.bm == X3_TH0 * TF_W;
-  const int cfg = bn == 128 ? (tall ? 0 : 4) : bn == 96 ? (tall ? 5 : 1) : bn == 64 ? 2 : 3;
+  const int cfg = bn == 128 ? (tall ? 0 : x3_nb1(a, false) ? 4 : 6)
+                            : bn == 96 ? (tall ? 5 : 1) : bn == 64 ? 2 : 3;
   if (timing_on()) timing_begin(s);
   if (cfg == 0) hipLaunchKernelGGL((conv_tile_x3<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);
-  else if (cfg == 4) hipLaunchKernelGGL((conv_tile_x3<128, 2, 4, MODE, 4>), grid, dim3(512), 0, s, a);
+  else if (cfg == 4) hipLaunchKernelGGL((conv_tile_x3<128, 2, 2, MODE, 4, 1>), grid, block, 0, s, a);
+  else if (cfg == 6) hipLaunchKernelGGL((conv_tile_x3<128, 2, 4, MODE, 4>), grid, dim3(512), 0, s, a);
   else if (cfg == 5) hipLaunchKernelGGL((conv_tile_x3<96, 4, 3, MODE, X3_TH0>), grid, dim3(768), 0, s, a);
   else if (cfg == 1) hipLaunchKernelGGL((conv_tile_x3<96, 2, 3, MODE, 4>), grid, dim3(384), 0, s, a);
   else if (cfg == 2) hipLaunchKernelGGL((conv_tile_x3<64, 4, 2, MODE, 4>), grid, dim3(512), 0, s, a);
