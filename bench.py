@@ -93,7 +93,7 @@ def kind_name(kind):
 def kernel_symbol(kind):
     """rocprofv3 name of the conv kernel instance behind a timing kind."""
     mode, cfg, fam = kind_parts(kind)
-    if cfg == 7:
+    if cfg == 7 and fam == "f32":
         return NARROW_SYMBOLS[mode]
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
         return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (

@@ -217,6 +217,97 @@ def test_conv_x3_accuracy(n, h, w, cin, cout):
         assert e3 < 5e-6, errs[True]
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout,kinds", [
+    (8, 128, 256, 128, 128, {128, 136, 144}),  # 8 x 32 tiles, BN 128 (1024 tiles)
+    (8, 128, 256, 128, 96, {133, 136, 145}),   # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad
+    (8, 64, 128, 128, 128, {132, 140, 144}),   # single-buffered two-per-CU 4 x 32 form
+    (2, 48, 64, 256, 256, {134, 142, 144}),    # 8-wave 4 x 32 form with a K split
+], ids=["tall128", "tall96", "nb1", "split"])
+def test_conv_x3_large_grids(n, h, w, cin, cout, kinds):
+    """The grid-size-selected forms of the split kernels (taller output tiles, the
+    single-buffered two-workgroups-per-CU form, K splits) against the fp32 MFMA kernels on
+    the same inputs, with the fused LeakyReLU / bias (fwd) and activation-derivative (dgrad)
+    epilogues and the weight + bias gradient; both paths are checked against the oracle
+    elsewhere, so agreement within fp32 accumulation-order noise pins these forms."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd._lib import ACT_LEAKY, call
+    x = dev(rng_tensor((n, h, w, cin), 31))
+    wt = dev(rng_tensor((3, 3, cin, cout), 32, scale=(2.0 / (9 * cin)) ** 0.5))
+    b = dev(rng_tensor((cout,), 33, scale=0.1))
+    dy = dev(rng_tensor((n, h, w, cout), 34))
+    act_src = dev(rng_tensor((n, h, w, cin), 35))
+    from optical_flow_amd import _lib
+    lib = _lib.lib()
+    outs = {}
+    lib.of_timing_read(0, None, None, None)          # drop records of earlier launches
+    for split in (True, False):
+        lib.of_timing_enable(1 if split else 0)
+        layer = ops.ConvLayer(wt, b, stride=1, act=ACT_LEAKY, cin_p=cin, f32_split=split)
+        d = layer.desc(n, h, w)
+        assert layer.mode(d) == (2 if split else 0)
+        wf, wd = layer.packed(d)
+        fent, fws = layer.fwd_entry(d)
+        dent, dws = layer.dgrad_entry(d)
+        went, wws = layer.wgrad_entry(d)
+        ws = torch.empty(max(fws, dws, wws) // 4 + 4, device="cuda")
+        P, st = ops._ptr, ops._stream()
+        y = torch.empty(n, h, w, cout, device="cuda")
+        dx = torch.empty(n, h, w, cin, device="cuda")
+        dw = torch.empty_like(wt)
+        db = torch.empty_like(b)
+        call(fent, C.byref(d), P(x), cin, P(wf), P(b), None, None, None, None, 1e-3, None, 0,
+             ACT_LEAKY, 0.3, None, 0, P(y), cout, P(ws), fws, st)
+        call(dent, C.byref(d), P(dy), cout, P(wd), P(act_src), cin, ACT_LEAKY, 0.3, P(dx), cin,
+             P(ws), dws, st)
+        call(went, C.byref(d), P(x), cin, P(dy), cout, P(dw), P(db), 0, P(ws), wws, st)
+        torch.cuda.synchronize()
+        if split:    # the timing kinds name the kernel configurations that ran (bench.py)
+            lib.of_timing_enable(0)
+            cap = 64
+            k_arr, f_arr, m_arr = (C.c_int * cap)(), (C.c_double * cap)(), (C.c_float * cap)()
+            got = {k_arr[i] for i in range(lib.of_timing_read(cap, k_arr, f_arr, m_arr))}
+            assert kinds <= got, (kinds, got)
+        outs[split] = (y, dx, dw, db)
+    for name, a3, a32 in zip(("y", "dx", "dw", "db"), outs[True], outs[False]):
+        assert rel_inf(a3, a32) < 2e-5, name
+        assert rel_l2(a3, a32) < 5e-6, name
+
+
+def test_conv_bf16_tall_fwd():
+    """bf16 forward with 8 x 32 output tiles (grids of >= 1024 tiles, BN 128) against an fp64
+    conv of the bf16-rounded operands (the bf16 kernels round x and w RNE while staging)."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_NONE, call
+    lib = _lib.lib()
+    n, h, w, cin, cout = 8, 128, 256, 128, 128
+    x = rng_tensor((n, h, w, cin), 41)
+    wt = rng_tensor((3, 3, cin, cout), 42, scale=(2.0 / (9 * cin)) ** 0.5)
+    layer = ops.ConvLayer(dev(wt), dev(torch.zeros(cout)), stride=1, act=ACT_NONE, cin_p=cin,
+                          precision="bf16")
+    d = layer.desc(n, h, w)
+    wf, _ = layer.packed(d)
+    fent, fws = layer.fwd_entry(d)
+    ws = torch.empty(fws // 4 + 4, device="cuda")
+    y = torch.empty(n, h, w, cout, device="cuda")
+    lib.of_timing_read(0, None, None, None)
+    lib.of_timing_enable(1)
+    call(fent, C.byref(d), ops._ptr(dev(x)), cin, ops._ptr(wf), ops._ptr(layer.bias), None, None,
+         None, None, 1e-3, None, 0, ACT_NONE, 0.0, None, 0, ops._ptr(y), cout, ops._ptr(ws), fws,
+         ops._stream())
+    torch.cuda.synchronize()
+    lib.of_timing_enable(0)
+    k_arr = (C.c_int * 8)()
+    got = {k_arr[i] for i in range(lib.of_timing_read(8, k_arr, None, None))}
+    assert 100 in got, got                      # conv_tile_bf16<128, 4, 2, 0, 8>
+    xb = x.to(torch.bfloat16).double()
+    wb = wt.to(torch.bfloat16).double()
+    yref = R.conv2d_same(xb, wb, None, 1)
+    assert rel_inf(y, yref) < 1e-5 and rel_l2(y, yref) < 1e-6
+
+
 # ----------------------------------------------------------------------- cost volume ----
 @pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6), (1, 19, 70, 32)])
 def test_cost_volume(shape):
