@@ -175,7 +175,7 @@ int of_conv2d_dgrad_add_x3(const of_conv_desc* d, const float* dy, int lddy,
                            const void* w3_bwd, const float* add, int ld_add, float* dx,
                            int lddx, void* workspace, size_t ws_bytes, void* stream);
 /* Weight gradient with the same split (Conv2DBackpropFilter of those layers): 3x3 stride-1
- * layers with Cout % 128 == 0 run conv_wgrad_tile_x3, every other layer exactly as
+ * layers with Cout in {32, 64, 96} or Cout % 128 == 0 run conv_wgrad_tile_x3, every other layer as
  * of_conv2d_wgrad; arguments and workspace rules as of_conv2d_wgrad. */
 size_t of_conv2d_wgrad_x3_workspace(const of_conv_desc* d);
 int of_conv2d_wgrad_x3(const of_conv_desc* d, const float* x, int ldx, const float* dy,
