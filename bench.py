@@ -74,9 +74,10 @@ def conv_math(precision):
     if precision == "bf16":
         return "bf16 MFMA operands, fp32 accumulation (flow convs cout<=4: fp32 VALU)"
     if ops.F32_SPLIT:
-        return ("fp32: 3x3 stride-1 fwd/dgrad on bf16 MFMA with an exact 3-term operand split "
-                "(6 products, fp32 accumulation; error vs fp64 at fp32-MFMA level, "
-                "test_conv_x3_accuracy); other convs and all wgrad on fp32 MFMA")
+        return ("fp32: 3x3 stride-1 fwd/dgrad (and wgrad for Cout in {32, 64, 96, 128k}) on "
+                "bf16 MFMA with an exact 3-term operand split (6 products, fp32 accumulation; "
+                "error vs fp64 at fp32-MFMA level, test_conv_x3_accuracy); other convs on fp32 "
+                "MFMA, the Cout<=4 flow convs on fp32 VALU")
     return "fp32 MFMA (flow convs cout<=4: fp32 VALU)"
 
 
