@@ -87,8 +87,10 @@ def kind_name(kind):
            "tile_x3": "_tile_x3"}[fam]
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
         return "wgrad%s<%s>" % (sfx, X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
-    return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (TILE_BN if fam == "tile_bf16" else
-                                                 X3_BN if fam == "tile_x3" else TILE_TEMPLATE)[cfg])
+    if fam == "tile_x3":
+        return "%s%s<%s, %d>" % (MODE_NAMES[mode], sfx, X3_BN[cfg], X3_TH[cfg])
+    return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (TILE_BN if fam == "tile_bf16"
+                                                 else TILE_TEMPLATE)[cfg])
 
 
 def kernel_symbol(kind):

@@ -222,7 +222,8 @@ def test_conv_x3_accuracy(n, h, w, cin, cout):
     (8, 128, 256, 128, 96, {133, 136, 145}),   # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad
     (8, 64, 128, 128, 128, {132, 140, 144}),   # single-buffered two-per-CU 4 x 32 form
     (2, 48, 64, 256, 256, {134, 142, 144}),    # 8-wave 4 x 32 form with a K split
-], ids=["tall128", "tall96", "nb1", "split"])
+    (8, 128, 256, 64, 64, {130, 138, 146}),    # BN 64 keeps 4 x 32 tiles on large grids
+], ids=["tall128", "tall96", "nb1", "split", "bn64"])
 def test_conv_x3_large_grids(n, h, w, cin, cout, kinds):
     """The grid-size-selected forms of the split kernels (taller output tiles, the
     single-buffered two-workgroups-per-CU form, K splits) against the fp32 MFMA kernels on
