@@ -103,9 +103,9 @@ def kernel_symbol(kind):
             fam, X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
     if fam in ("tile_bf16", "tile_x3"):
         if fam == "tile_x3":
-            nb = (", %d" % X3_NB[cfg]) if cfg in X3_NB else ""
-            return "void oflow::conv_tile_x3<%s, %d, %d%s>(oflow::GemmArgs)" % (
-                X3_BN[cfg], mode, X3_TH[cfg], nb)
+            # the demangled name prints the defaulted NB too (conv_tile_x3<..., TH, NB>)
+            return "void oflow::conv_tile_x3<%s, %d, %d, %d>(oflow::GemmArgs)" % (
+                X3_BN[cfg], mode, X3_TH[cfg], X3_NB.get(cfg, 2))
         return "void oflow::conv_tile_bf16<%s, %d, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode,
                                                                             TILE_TH[cfg])
     if fam == "bf16" and mode == 2:

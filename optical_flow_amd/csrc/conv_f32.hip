@@ -34,6 +34,7 @@
 namespace oflow {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 constexpr int BK = 16;
@@ -842,6 +843,16 @@ constexpr int TF_H = OF_TF_H, TF_W = OF_TF_W;
 #define OF_X3_TH0 8
 #endif
 constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows x 32 px
+// Timing ablations of conv_tile_x3 (tools/ab_build.sh -DX3_ABL=mask; wrong results by
+// design, never in the shipped build): 1 no barriers in the tap loop, 2 no B restaging,
+// 4 no halo restaging, 8 one MFMA per fragment pair instead of six.
+#ifndef X3_ABL
+#define X3_ABL 0
+#endif
+// conv_tile_x3 MFMA shape: 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16)
+#ifndef X3_MF
+#define X3_MF 16
+#endif
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH = OF_TF_H>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES_N)) void conv_tile_bf16(GemmArgs a) {
@@ -1171,16 +1182,35 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
     }
   };
 
+  // X3_MF == 16: v_mfma_f32_16x16x32_bf16 on 16 x 16 sub-tiles (one MFMA spans the 32
+  // channels of a chunk); 32: v_mfma_f32_32x32x16_bf16 on 32 x 32 tiles, two k-halves.
+  constexpr bool M16 = X3_MF == 16;
+  constexpr int SM = WM / 16, SN = WN / 16;
   f32x16 acc[TM][TN];
+  f32x4 acc4[SM][SN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+#pragma unroll
+    for (int j = 0; j < SN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc4[i][j][r] = 0.f;
   const int wm0 = (wave / WAVES_N) * WM;
   const int wn0 = (wave % WAVES_N) * WN;
   const int lrow = lane & 31, lk = lane >> 5;
+  const int l16 = lane & 15, lq = lane >> 4;
+  int a_hp16[SM];
+#pragma unroll
+  for (int i = 0; i < SM; ++i) {
+    const int m = wm0 + 16 * i + l16;
+    const int ty = m / TF_W, tx = m % TF_W;
+    a_hp16[i] = MODE == MODE_FWD ? ty * HW + tx : (ty + KS - 1) * HW + tx + KS - 1;
+  }
   int a_hp[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -1202,15 +1232,40 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
   for (int c = c_begin; c < c_end; ++c) {
     const int cc = c - c_begin;
     const bool more_c = c + 1 < c_end;
-    if (more_c) load_halo(c + 1);
+    if (more_c && !(X3_ABL & 4)) load_halo(c + 1);
 #pragma unroll
     for (int t = 0; t < KS * KS; ++t) {
       const int buf = NB == 2 ? (cc + t) & 1 : 0;
       const bool more = t + 1 < KS * KS || more_c;
-      if (more) load_b(t + 1 < KS * KS ? c : c + 1, t + 1 < KS * KS ? t + 1 : 0);
+      if (more && !(X3_ABL & 2)) load_b(t + 1 < KS * KS ? c : c + 1, t + 1 < KS * KS ? t + 1 : 0);
       __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this step's MFMAs
       const int r = t / KS, s = t % KS;
       const int dh = MODE == MODE_FWD ? r * HW + s : -(r * HW + s);
+      if constexpr (M16) {
+        bf16x8 av[NP][SM], bv[NP][SN];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+          for (int i = 0; i < SM; ++i)
+            av[p][i] = __builtin_bit_cast(bf16x8, Ah[p][(a_hp16[i] + dh) * SROW16 + lq]);
+#pragma unroll
+          for (int j = 0; j < SN; ++j)
+            bv[p][j] = __builtin_bit_cast(
+                bf16x8, Bs[buf][(p * BN + wn0 + 16 * j + l16) * SROW16 + lq]);
+        }
+#pragma unroll
+        for (int i = 0; i < SM; ++i)
+#pragma unroll
+          for (int j = 0; j < SN; ++j) {
+            f32x4 x = acc4[i][j];
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+          }
+      } else {
       bf16x8 av[2][NP][TM], bv[2][NP][TN];
 #pragma unroll
       for (int st = 0; st < 2; ++st)
@@ -1231,6 +1286,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             f32x16 x = acc[i][j];
+            if (X3_ABL & 8) {      // ablation: one product (the MFMA count of a bf16 conv)
+              asm volatile("" ::"v"(av[st][1][i]), "v"(av[st][2][i]), "v"(bv[st][1][j]),
+                           "v"(bv[st][2][j]));
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][0][j], x, 0, 0, 0);
+              continue;
+            }
             x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][2][i], bv[st][0][j], x, 0, 0, 0);
             x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][2][j], x, 0, 0, 0);
             x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][1][i], bv[st][1][j], x, 0, 0, 0);
@@ -1238,19 +1299,51 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
             x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][1][j], x, 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][0][j], x, 0, 0, 0);
           }
+      }
       __builtin_amdgcn_sched_barrier(0);   // the stores wait for the prefetch: after the MFMAs
       // single B buffer: every wave must be done with it; double: only with the halo
-      if (NB == 1 ? more : (t + 1 == KS * KS && more_c)) __syncthreads();
+      if (!(X3_ABL & 1) && (NB == 1 ? more : (t + 1 == KS * KS && more_c))) __syncthreads();
       if (more) {
-        store_b(NB == 2 ? buf ^ 1 : 0);
-        if (t + 1 == KS * KS && more_c) store_halo();
+        if (!(X3_ABL & 2)) store_b(NB == 2 ? buf ^ 1 : 0);
+        if (t + 1 == KS * KS && more_c && !(X3_ABL & 4)) store_halo();
       }
-      __syncthreads();
+      if (!(X3_ABL & 1)) __syncthreads();
     }
   }
 
   // ---- epilogue (as conv_tile_bf16)
   const int64_t img = (int64_t)b * OH * OW;
+  if constexpr (M16) {
+    // 16 x 16 C layout: column = lane & 15, rows 4 (lane >> 4) + r
+#pragma unroll
+    for (int j = 0; j < SN; ++j) {
+      const int n = n0 + wn0 + 16 * j + l16;
+      if (n >= a.N) continue;
+      float bias = 0.f, scale = 1.f, shift = 0.f;
+      if (a.splits == 1) column_params<MODE>(a, n, bias, scale, shift);
+      EpAux aux[SM * 4];
+#pragma unroll
+      for (int q = 0; q < SM * 4; ++q) {
+        const int m = wm0 + 16 * (q >> 2) + 4 * lq + (q & 3);
+        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
+        aux[q] = a.splits == 1 && oy < OH && ox < OW
+                     ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : EpAux{0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < SM * 4; ++q) {
+        const int m = wm0 + 16 * (q >> 2) + 4 * lq + (q & 3);
+        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
+        if (oy >= OH || ox >= OW) continue;
+        const int64_t row = img + (int64_t)oy * OW + ox;
+        const float v = acc4[q >> 2][j][q & 3];
+        if (a.splits > 1)
+          a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n] = v;
+        else
+          epilogue_store<MODE>(a, row, n, v, bias, scale, shift, aux[q]);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn0 + 32 * j + lrow;
@@ -2687,13 +2780,18 @@ bool x3_tall(int n, int oh, int ow, int N) {
   return (bn == 128 || bn == 96) && (int64_t)n * cdiv(oh, X3_TH0) * cdiv(ow, TF_W) >= 4 * kCUs;
 }
 
-// conv_tile_x3 BN = 128 with 4 x 32 tiles: grids of >= X3_NB1_MIN tiles take the
-// single-buffered 4-wave form (two workgroups per CU: enc.l3 142 -> 150, dec2 dgrad 170 ->
-// 182 TFLOP/s); smaller grids, which split K, keep the 8-wave double-buffered one (the
-// 4-wave form measured dec1 134 -> 108, enc.l4 159 -> 143).
+// conv_tile_x3 BN = 128 with 4 x 32 tiles: unsplit grids of >= X3_NB1_MIN tiles take the
+// single-buffered 4-wave form (two workgroups per CU: enc.l3 142 -> 154, dec2 dgrad 170 ->
+// 185 TFLOP/s); split grids keep the 8-wave double-buffered one (the 4-wave
+// form measured dec1 134 -> 108, enc.l4 159 -> 143).  x3_nb1_candidate() only sizes the
+// K-split cost model (two slots per CU); the launch takes the 4-wave form when the final
+// plan is also unsplit (x3_nb1).
 constexpr int X3_NB1_MIN = 384;
-bool x3_nb1(const GemmArgs& a, bool tall) {
+bool x3_nb1_candidate(const GemmArgs& a, bool tall) {
   return !tall && pick_bn(a.N) == 128 && a.tiles_total >= X3_NB1_MIN;
+}
+bool x3_nb1(const GemmArgs& a) {
+  return a.bm != X3_TH0 * TF_W && a.splits == 1 && x3_nb1_candidate(a, false);
 }
 
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false) {
@@ -2731,7 +2829,7 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
     // (Measured: enc.l3 384 tiles unsplit, dec1 192 tiles unsplit, enc.l4 96 tiles in 2.)
     // (The single-buffered BN = 128 4 x 32 configuration, used from X3_NB1_MIN tiles, runs
     // two workgroups per CU.)
-    const int slots = x3_nb1(a, tall) ? 2 * kCUs : kCUs;
+    const int slots = x3_nb1_candidate(a, tall) ? 2 * kCUs : kCUs;
     int best = 1;
     double best_cost = 1e30;
     for (int sp = 1; sp <= std::min(8, a.K); ++sp) {
@@ -2785,7 +2883,7 @@ int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
   const int bn = pick_bn(a.N);
   dim3 grid(a.tiles_total * a.splits), block(256);
   const bool tall = a.bm == X3_TH0 * TF_W;
-  const int cfg = bn == 128 ? (tall ? 0 : x3_nb1(a, false) ? 4 : 6)
+  const int cfg = bn == 128 ? (tall ? 0 : x3_nb1(a) ? 4 : 6)
                             : bn == 96 ? (tall ? 5 : 1) : bn == 64 ? 2 : 3;
   if (timing_on()) timing_begin(s);
   if (cfg == 0) hipLaunchKernelGGL((conv_tile_x3<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);

@@ -217,14 +217,14 @@ def test_conv_x3_accuracy(n, h, w, cin, cout):
         assert e3 < 5e-6, errs[True]
 
 
-@pytest.mark.parametrize("n,h,w,cin,cout,kinds", [
-    (8, 128, 256, 128, 128, {128, 136, 144}),  # 8 x 32 tiles, BN 128 (1024 tiles)
-    (8, 128, 256, 128, 96, {133, 136, 145}),   # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad
-    (8, 64, 128, 128, 128, {132, 140, 144}),   # single-buffered two-per-CU 4 x 32 form
-    (2, 48, 64, 256, 256, {134, 142, 144}),    # 8-wave 4 x 32 form with a K split
-    (8, 128, 256, 64, 64, {130, 138, 146}),    # BN 64 keeps 4 x 32 tiles on large grids
+@pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
+    ("tall128", 8, 128, 256, 128, 128, {128, 136, 144}),  # 8 x 32 tiles, BN 128 (1024 tiles)
+    ("tall96", 8, 128, 256, 128, 96, {133, 136, 145}),    # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad
+    ("nb1", 8, 64, 128, 128, 128, {132, 140, 144}),       # single-buffered two-per-CU 4 x 32 form
+    ("split", 2, 48, 64, 256, 256, {134, 142, 144}),      # 8-wave 4 x 32 form with a K split
+    ("bn64", 8, 128, 256, 64, 64, {130, 138, 146}),       # BN 64 keeps 4 x 32 tiles on large grids
 ], ids=["tall128", "tall96", "nb1", "split", "bn64"])
-def test_conv_x3_large_grids(n, h, w, cin, cout, kinds):
+def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
     """The grid-size-selected forms of the split kernels (taller output tiles, the
     single-buffered two-workgroups-per-CU form, K splits) against the fp32 MFMA kernels on
     the same inputs, with the fused LeakyReLU / bias (fwd) and activation-derivative (dgrad)
@@ -251,6 +251,13 @@ def test_conv_x3_large_grids(n, h, w, cin, cout, kinds):
         fent, fws = layer.fwd_entry(d)
         dent, dws = layer.dgrad_entry(d)
         went, wws = layer.wgrad_entry(d)
+        if split:
+            # the fwd / dgrad workspace holds the K-split slabs: nonzero exactly when the plan
+            # splits K, so this pins the split / unsplit forms each case is meant to cover
+            if case == "split":
+                assert fws > 0 and dws > 0, (fws, dws)
+            else:
+                assert fws == 0 and dws == 0, (fws, dws)
         ws = torch.empty(max(fws, dws, wws) // 4 + 4, device="cuda")
         P, st = ops._ptr, ops._stream()
         y = torch.empty(n, h, w, cout, device="cuda")

@@ -72,3 +72,22 @@ def test_five_level_spec():
     names = {p.name for p in P.flow_net_spec(levels=5)}
     assert "flow_module_4/conv5/kernel" in names and "ResNet18/res5_1/conv_b/kernel" in names
     assert "flow_module_4/conv0/kernel" not in {p.name for p in P.flow_net_spec()}
+
+
+def test_bench_kernel_symbols_match_pmc_keys():
+    """bench.py names each split-kernel timing kind by its demangled rocprofv3 symbol (the
+    defaulted NB template argument included); every x3 instance that the committed PMC pass
+    saw must be reachable from a kind, or roofline.traffic silently comes out null."""
+    import json
+    import os
+    import bench
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    keys = set(json.load(open(os.path.join(root, "profiles", "pmc_traffic.json")))["kernels"])
+    names = set()
+    for mode in (0, 1):
+        for cfg in bench.X3_BN:
+            names.add(bench.kernel_symbol(128 + mode * 8 + cfg))
+    for cfg in bench.X3_WGT:
+        names.add(bench.kernel_symbol(128 + 16 + cfg))
+    x3_keys = {k for k in keys if "_x3<" in k}
+    assert x3_keys and x3_keys <= names, sorted(x3_keys - names)

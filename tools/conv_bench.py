@@ -113,7 +113,7 @@ def main():
             _lib.lib().of_set_tuning(int(k), int(v))
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     for sh in shapes:
-        if args.only and args.only not in sh[0]:
+        if args.only and not any(o in sh[0] for o in args.only.split(",")):
             continue
         flops, out = bench_one(*sh, args.reps, "bf16" if args.bf16 else "fp32")
         line = "%-10s %7.2f GF " % (sh[0], flops / 1e9)
