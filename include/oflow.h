@@ -303,7 +303,8 @@ int of_fill(float* y, float v, int64_t n, void* stream);
  * kinds (0 fwd, 1 dgrad, 2 wgrad), flops and elapsed ms (synchronises the events). */
 int of_timing_enable(int on);
 /* Kernel-variant switches for A/B measurements: key 1 = fwd/dgrad split-K target workgroups
- * per CU (1-16, default 4), key 2 = minimum 16-deep K chunks per split slice (2-64, default 12). */
+ * per CU (1-16, default 4), key 2 = minimum 16-deep K chunks per split slice (2-64, default 12),
+ * key 3 = the tile kernels' 16-byte (float4-column) epilogue (1, default) or per-element (0). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -81,6 +81,8 @@ struct GemmArgs {
   int colsum;             // wgrad: column sums of B (bias grad) into slab row M
   int bm;                 // M tile of the launched configuration
   int ngroups;
+  int vec_ep;             // tile kernels: 4-column epilogue (N, every ld a multiple of 4,
+                          // every row pointer 16-byte aligned)
   Group grp[MAX_GROUPS];
 };
 
@@ -147,6 +149,67 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int64_t row, i
     v += aux.r;
   }
   a.C[row * a.ldc + n] = v;
+}
+
+template <int MODE>
+__device__ __forceinline__ void column_params(const GemmArgs& a, int n, float& bias,
+                                              float& scale, float& shift);
+
+// The fused epilogue of epilogue_store for four consecutive columns n .. n + 3 of one row,
+// with 16-byte loads and stores (a.vec_ep: N and every leading dimension a multiple of 4,
+// 16-byte aligned bases).  splits > 1 writes the raw sums to this K slice's slab row.
+template <int MODE>
+__device__ __forceinline__ void epilogue_store4(const GemmArgs& a, int split, int64_t row, int n,
+                                                float4 v4) {
+  if (a.splits > 1) {
+    *reinterpret_cast<float4*>(&a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n]) = v4;
+    return;
+  }
+  float v[4] = {v4.x, v4.y, v4.z, v4.w};
+  if (MODE == MODE_FWD) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float bias, scale, shift;
+      column_params<MODE>(a, n + e, bias, scale, shift);
+      v[e] += bias;
+      (void)scale;
+      (void)shift;
+    }
+    if (a.z) *reinterpret_cast<float4*>(&a.z[row * a.ldz + n]) = make_float4(v[0], v[1], v[2], v[3]);
+    if (a.bn_g) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float bias, scale, shift;
+        column_params<MODE>(a, n + e, bias, scale, shift);
+        v[e] = v[e] * scale + shift;
+      }
+    }
+    if (a.res) {
+      const float4 r = *reinterpret_cast<const float4*>(&a.res[row * a.ldr + n]);
+      v[0] += r.x;
+      v[1] += r.y;
+      v[2] += r.z;
+      v[3] += r.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], a.act, a.alpha);
+  } else if (MODE == MODE_DGRAD) {
+    if (a.act_src) {
+      const float4 s4 = *reinterpret_cast<const float4*>(&a.act_src[row * a.ld_act + n]);
+      const float s[4] = {s4.x, s4.y, s4.z, s4.w};
+      const float neg = a.act == OF_ACT_LEAKY ? a.alpha : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= s[e] > 0.f ? 1.f : neg;
+    }
+    if (a.res) {
+      const float4 r = *reinterpret_cast<const float4*>(&a.res[row * a.ldr + n]);
+      v[0] += r.x;
+      v[1] += r.y;
+      v[2] += r.z;
+      v[3] += r.w;
+    }
+  }
+  *reinterpret_cast<float4*>(&a.C[row * a.ldc + n]) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 template <int MODE>
@@ -1093,8 +1156,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
                 "tile");
   constexpr int HQ = HP * 8, HS = (HQ + NT - 1) / NT;          // halo quads (32 ch)
   constexpr int BOCT = NP * BN * 4, BSL = (BOCT + NT - 1) / NT; // B octets per tap
-  __shared__ uint4 Ah[NP][HP * SROW16];
-  __shared__ uint4 Bs[NB][NP * BN * SROW16];
+  // One LDS array: the halo planes, the B buffers, and after the main loop the epilogue's
+  // per-wave transpose images (WM rows x WN + 4 floats).
+  constexpr int AH_U4 = NP * HP * SROW16, BS_U4 = NB * NP * BN * SROW16;
+  constexpr int EPW = WN + 4;
+  static_assert((NT / 64) * WM * EPW * 4 <= (AH_U4 + BS_U4) * 16, "epilogue image fits LDS");
+  __shared__ uint4 smem[AH_U4 + BS_U4];
+  uint4 (*Ah)[HP * SROW16] = reinterpret_cast<uint4 (*)[HP * SROW16]>(smem);
+  uint4 (*Bs)[NP * BN * SROW16] = reinterpret_cast<uint4 (*)[NP * BN * SROW16]>(smem + AH_U4);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1258,6 +1327,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
 #pragma unroll
           for (int j = 0; j < SN; ++j) {
             f32x4 x = acc4[i][j];
+            if (X3_ABL & 8) {      // ablation: one product (the MFMA count of a bf16 conv)
+              asm volatile("" ::"v"(av[1][i]), "v"(av[2][i]), "v"(bv[1][j]), "v"(bv[2][j]));
+              acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+              continue;
+            }
             x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
             x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
             x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
@@ -1313,6 +1387,44 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
 
   // ---- epilogue (as conv_tile_bf16)
   const int64_t img = (int64_t)b * OH * OW;
+  if constexpr (M16 && (X3_ABL & 16)) {   // ablation: one store per lane instead of 4 SM SN
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j) v += acc4[i][j][0] + acc4[i][j][1] + acc4[i][j][2] + acc4[i][j][3];
+    a.C[(img + (int64_t)oy0 * OW + ox0) * a.ldc + (n0 + wn0 + (lane & 31)) % a.N] = v;
+    return;
+  }
+  if (M16 && a.vec_ep) {
+    // The wave's WM x WN accumulator block goes through a private LDS image (every wave passed
+    // the main loop's last barrier after its last halo / B read) and comes back as rows of
+    // float4: 16-byte loads and stores, WN / 4 lanes per pixel row (the MFMA layout holds 4
+    // rows of one column per lane: 4-byte accesses on 64-byte row segments).
+    float* E = reinterpret_cast<float*>(smem) + wave * WM * EPW;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[(16 * i + 4 * lq + r) * EPW + 16 * j + l16] = acc4[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int LPR = WN / 4, RPI = 64 / LPR;            // lanes per row, rows per pass
+    const int c4 = lane % LPR, rr = lane / LPR;
+    const int n = n0 + wn0 + 4 * c4;
+#pragma unroll
+    for (int q = 0; q < WM / RPI; ++q) {
+      const int m = q * RPI + rr;
+      const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
+      const int mt = wm0 + m;
+      const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
+      if (oy < OH && ox < OW && n < a.N)
+        epilogue_store4<MODE>(a, split, img + (int64_t)oy * OW + ox, n, v);
+    }
+    return;
+  }
   if constexpr (M16) {
     // 16 x 16 C layout: column = lane & 15, rows 4 (lane >> 4) + r
 #pragma unroll
@@ -2716,6 +2828,16 @@ GemmArgs dgrad_args(const of_conv_desc* d, const Geo& g, bool bf16 = false,
 
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// The tile kernels' 4-column epilogue (epilogue_store4) needs whole float4 columns and
+// 16-byte aligned rows in every tensor it touches.
+static int g_vec_ep = 1;   // of_set_tuning key 3 (0: per-element epilogue, for A/B and tests)
+bool vec_ep_ok(const GemmArgs& a) {
+  if (!g_vec_ep || a.N % 4) return false;
+  if (a.splits > 1) return a.slab_ld % 4 == 0 && al16(a.slab);
+  auto ok = [](const float* p, int ld) { return !p || (ld % 4 == 0 && al16(p)); };
+  return ok(a.C, a.ldc) && ok(a.res, a.ldr) && ok(a.z, a.ldz) && ok(a.act_src, a.ld_act);
+}
+
 // fwd/dgrad split-K epilogue: the flat kernel unless many slices meet few rows.
 template <int MODE>
 int launch_splitk_epilogue(const GemmArgs& a, hipStream_t s) {
@@ -3067,6 +3189,7 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
 int of_set_tuning(int key, int value) {
   if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }
   if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
+  if (key == 3 && (value == 0 || value == 1)) { g_vec_ep = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -3198,6 +3321,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   a.alpha = alpha;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
+  a.vec_ep = vec_ep_ok(a);
   st = x3     ? launch_tile_x3<MODE_FWD>(a, s, flops)
        : tile ? launch_tile_bf16<MODE_FWD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops)
@@ -3274,6 +3398,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   a.ldr = ld_add;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
+  a.vec_ep = vec_ep_ok(a);
   st = x3     ? launch_tile_x3<MODE_DGRAD>(a, s, flops)
        : tile ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops)

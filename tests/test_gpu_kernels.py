@@ -282,6 +282,68 @@ def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
         assert rel_l2(a3, a32) < 5e-6, name
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout", [
+    (2, 20, 45, 64, 128),     # ragged right edge (45 px), 4 x 32 tiles
+    (8, 128, 256, 128, 128),  # 8 x 32 tiles, BN 128
+    (2, 48, 64, 256, 256),    # K split: the epilogue writes slab rows
+    (2, 16, 24, 64, 96),      # BN 96
+    (3, 9, 40, 32, 64),       # BN 64, odd rows
+    (2, 8, 40, 32, 32),       # BN 32
+    (1, 6, 10, 256, 44),      # N % 4 == 0 but not a tile multiple
+    (1, 6, 10, 64, 42),       # N % 4 != 0: per-element epilogue either way
+])
+def test_conv_x3_vec_epilogue(n, h, w, cin, cout):
+    """The split kernels' 16-byte epilogue (accumulators transposed through LDS, float4
+    columns) is bitwise identical to the per-element one (of_set_tuning key 3): fwd with bias,
+    BN, the residual, z and ReLU; dgrad with the activation derivative and an added gradient."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_LEAKY, ACT_RELU, call
+    lib = _lib.lib()
+    x = dev(rng_tensor((n, h, w, cin), 41))
+    wt = dev(rng_tensor((3, 3, cin, cout), 42, scale=(2.0 / (9 * cin)) ** 0.5))
+    b = dev(rng_tensor((cout,), 43, scale=0.1))
+    g, be = dev(rng_tensor((cout,), 44, scale=0.5)) + 1.0, dev(rng_tensor((cout,), 45, scale=0.1))
+    mu, var = dev(rng_tensor((cout,), 46, scale=0.1)), dev(rng_tensor((cout,), 47)).abs() + 0.5
+    coutp = (cout + 3) // 4 * 4
+    res = dev(rng_tensor((n, h, w, cout), 48))
+    dy = dev(rng_tensor((n, h, w, coutp), 49))
+    act_src = dev(rng_tensor((n, h, w, cin), 50))
+    add = dev(rng_tensor((n, h, w, cin), 51))
+    layer = ops.ConvLayer(wt, b, stride=1, act=ACT_RELU, cin_p=cin, f32_split=True)
+    d = layer.desc(n, h, w)
+    assert layer.mode(d) == 2
+    wf, wd = layer.packed(d)
+    fent, fws = layer.fwd_entry(d)
+    dws = lib.of_conv2d_dgrad_x3_workspace(C.byref(d))
+    ws = torch.empty(max(fws, dws) // 4 + 4, device="cuda")
+    P, st = ops._ptr, ops._stream()
+    outs = []
+    try:
+        for vec in (1, 0):
+            assert lib.of_set_tuning(3, vec) == 0
+            y = torch.full((n, h, w, cout), 7.0, device="cuda")
+            z = torch.full((n, h, w, cout), 7.0, device="cuda")
+            dx = torch.full((n, h, w, cin), 7.0, device="cuda")
+            dx2 = torch.full((n, h, w, cin), 7.0, device="cuda")
+            call(fent, C.byref(d), P(x), cin, P(wf), P(b), P(g), P(be), P(mu), P(var), 1e-3,
+                 P(res), cout, ACT_RELU, 0.0, P(z), cout, P(y), cout, P(ws), fws, st)
+            call("of_conv2d_dgrad_x3", C.byref(d), P(dy), coutp, P(wd), P(act_src), cin,
+                 ACT_LEAKY, 0.3, P(dx), cin, P(ws), dws, st)
+            call("of_conv2d_dgrad_add_x3", C.byref(d), P(dy), coutp, P(wd), P(add), cin,
+                 P(dx2), cin, P(ws), dws, st)
+            torch.cuda.synchronize()
+            outs.append((y, z, dx, dx2))
+    finally:
+        lib.of_set_tuning(3, 1)
+    for name, a1, a0 in zip(("y", "z", "dx", "dx_add"), *outs):
+        assert torch.equal(a1, a0), (name, (a1 - a0).abs().max().item())
+    yref = torch.relu((R.conv2d_same(f64(x), f64(wt), f64(b), 1) - f64(mu)) / torch.sqrt(f64(var) + 1e-3)
+                      * f64(g) + f64(be) + f64(res))
+    assert rel_inf(outs[0][0], yref) < REL_TOL
+
+
 def test_conv_bf16_tall_fwd():
     """bf16 forward with 8 x 32 output tiles (grids of >= 1024 tiles, BN 128) against an fp64
     conv of the bf16-rounded operands (the bf16 kernels round x and w RNE while staging)."""
