@@ -912,10 +912,6 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #ifndef X3_ABL
 #define X3_ABL 0
 #endif
-// conv_tile_x3 MFMA shape: 32 (v_mfma_f32_32x32x16_bf16) or 16 (v_mfma_f32_16x16x32_bf16)
-#ifndef X3_MF
-#define X3_MF 16
-#endif
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH = OF_TF_H>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES_N)) void conv_tile_bf16(GemmArgs a) {
@@ -1143,27 +1139,39 @@ __device__ __forceinline__ void split3x4(const float4& v, uint2& h, uint2& m, ui
   l = make_uint2(hi2(lb[0], lb[1]), hi2(lb[2], lb[3]));
 }
 
-// NB = B buffers: 2 (double-buffered, one barrier per tap) or 1 (80 KB of LDS with TH = 4,
-// so two 4-wave workgroups share a CU; two barriers per tap).
+// NB = B buffers: 2 (double-buffered, one barrier per tap) or 1 (TH = 4: 64 KB of LDS, so two
+// 4-wave workgroups share a CU; two barriers per tap).
+// LDS images (halo pixels, B rows) are rows of 32 bf16 = four 16-byte octets, unpadded; octet
+// o of row p sits in slot o ^ x3_sw(p).  A v_mfma_f32_16x16x32_bf16 fragment read (lanes
+// l & 15 = 16 consecutive rows from ANY start, lanes l >> 4 = the octet) then touches 16
+// distinct 16-byte bank slots in each ds_read_b128 lane group: rows 4 apart share a slot
+// base, and of the four such rows in a group two read octet q and two octet q ^ 1; the
+// swizzle alternates with bit 2 of the row, so the four land on q, q ^ 2, q ^ 1, q ^ 3.  (The
+// 80-byte padded rows that suit the 32 x 32 layout leave 3 of 16 slots 2-way in every group.)
+__device__ __forceinline__ int x3_sw(int p) { return ((p >> 2) & 1) << 1; }
+
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int NB = 2>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_tile_x3(GemmArgs a) {
   constexpr int BM = TH * TF_W, KS = 3, NP = 3;
   constexpr int HH = TH + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
-  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int SM = WM / 16, SN = WN / 16;                    // 16 x 16 MFMA tiles per wave
   constexpr int NT = 64 * WAVES_M * WAVES_N;                   // 4-12 waves
-  static_assert(NT % 64 == 0 && NT <= 1024 && WM % 32 == 0 && WN % 32 == 0 && TM >= 1 && TN >= 1,
+  static_assert(NT % 64 == 0 && NT <= 1024 && WM % 16 == 0 && WN % 16 == 0 && SM >= 1 && SN >= 1,
                 "tile");
   constexpr int HQ = HP * 8, HS = (HQ + NT - 1) / NT;          // halo quads (32 ch)
   constexpr int BOCT = NP * BN * 4, BSL = (BOCT + NT - 1) / NT; // B octets per tap
   // One LDS array: the halo planes, the B buffers, and after the main loop the epilogue's
-  // per-wave transpose images (WM rows x WN + 4 floats).
-  constexpr int AH_U4 = NP * HP * SROW16, BS_U4 = NB * NP * BN * SROW16;
-  constexpr int EPW = WN + 4;
-  static_assert((NT / 64) * WM * EPW * 4 <= (AH_U4 + BS_U4) * 16, "epilogue image fits LDS");
+  // per-wave transpose images (WM rows x 16 EJ + 4 floats, EJ column blocks per pass).
+  constexpr int AH_U4 = NP * HP * 4, BS_U4 = NB * NP * BN * 4;
+  constexpr int LDS_B = (AH_U4 + BS_U4) * 16;
+  constexpr int EJ = (NT / 64) * WM * (16 * SN + 4) * 4 <= LDS_B ? SN
+                     : (NT / 64) * WM * (8 * SN + 4) * 4 <= LDS_B ? SN / 2 : 1;
+  constexpr int EPW = 16 * EJ + 4;
+  static_assert(SN % EJ == 0 && (NT / 64) * WM * EPW * 4 <= LDS_B, "epilogue image fits LDS");
   __shared__ uint4 smem[AH_U4 + BS_U4];
-  uint4 (*Ah)[HP * SROW16] = reinterpret_cast<uint4 (*)[HP * SROW16]>(smem);
-  uint4 (*Bs)[NP * BN * SROW16] = reinterpret_cast<uint4 (*)[NP * BN * SROW16]>(smem + AH_U4);
+  uint4* Ah = smem;                      // [plane][halo pixel][4 octets]
+  uint4* Bs = smem + AH_U4;              // [buf][plane][BN rows][4 octets]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1184,11 +1192,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
   const int hx0 = MODE == MODE_FWD ? ox0 - a.pl : ox0 + a.pl - (KS - 1);
   const int c_begin = split * a.k_per_split;
   const int c_end = min(a.K, c_begin + a.k_per_split);
-  const int steps = c_end > c_begin ? (c_end - c_begin) * KS * KS : 0;
 
   const rsrc_t ra_src = make_rsrc(a.A, a.a_bytes);
   const rsrc_t rb_src = make_rsrc(a.B, a.b_bytes);
 
+  // ---- halo slots: quad (q & 7) of halo pixel (q >> 3)
   int h_off[HS];
   unsigned h_ok = 0;
   const int hcq = tid & 7;
@@ -1215,23 +1223,28 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
       if (q < HQ) {
         uint2 h, m, l;
         split3x4(hv[j], h, m, l);
-        const int off = (q >> 3) * (SROW16 * 16) + 8 * (q & 7);
-        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(Ah[0]) + off) = h;
-        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(Ah[1]) + off) = m;
-        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(Ah[2]) + off) = l;
+        const int hp = q >> 3;
+        const int off = hp * 64 + ((((q & 7) >> 1) ^ x3_sw(hp)) << 4) + 8 * (q & 1);
+        char* base = reinterpret_cast<char*>(Ah);
+        *reinterpret_cast<uint2*>(base + off) = h;
+        *reinterpret_cast<uint2*>(base + HP * 64 + off) = m;
+        *reinterpret_cast<uint2*>(base + 2 * HP * 64 + off) = l;
       }
     }
   };
   // ---- B slots: (plane, weight row, octet) of one tap; the (tap, chunk) part of the offset
   // is uniform and rides in the buffer load's scalar offset.
   uint32_t b_off[BSL];
+  int b_lds[BSL];
 #pragma unroll
   for (int j = 0; j < BSL; ++j) {
     const int o = tid + NT * j;
     const int p = o / (BN * 4), rem = o - p * (BN * 4);
-    const int n = n0 + (rem >> 2), oct = rem & 3;
+    const int row = rem >> 2, oct = rem & 3;
+    const int n = n0 + row;
     const bool ok = o < BOCT && n < a.nb;
     b_off[j] = ok ? (uint32_t)(((int64_t)p * a.b_plane + (int64_t)n * a.ldb + 8 * oct) * 2) : kOOB;
+    b_lds[j] = o < BOCT ? (p * BN + row) * 4 + (oct ^ x3_sw(row)) : -1;
   }
   uint4 rb[BSL];
   auto load_b = [&](int c, int t) {
@@ -1242,27 +1255,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
   };
   auto store_b = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < BSL; ++j) {
-      const int o = tid + NT * j;
-      if (o < BOCT) {
-        const int p = o / (BN * 4), rem = o - p * (BN * 4);
-        Bs[buf][(p * BN + (rem >> 2)) * SROW16 + (rem & 3)] = rb[j];
-      }
-    }
+    for (int j = 0; j < BSL; ++j)
+      if (BOCT % NT == 0 || b_lds[j] >= 0) Bs[buf * NP * BN * 4 + b_lds[j]] = rb[j];
   };
 
-  // X3_MF == 16: v_mfma_f32_16x16x32_bf16 on 16 x 16 sub-tiles (one MFMA spans the 32
-  // channels of a chunk); 32: v_mfma_f32_32x32x16_bf16 on 32 x 32 tiles, two k-halves.
-  constexpr bool M16 = X3_MF == 16;
-  constexpr int SM = WM / 16, SN = WN / 16;
-  f32x16 acc[TM][TN];
   f32x4 acc4[SM][SN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 #pragma unroll
   for (int i = 0; i < SM; ++i)
 #pragma unroll
@@ -1271,24 +1268,18 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
       for (int r = 0; r < 4; ++r) acc4[i][j][r] = 0.f;
   const int wm0 = (wave / WAVES_N) * WM;
   const int wn0 = (wave % WAVES_N) * WN;
-  const int lrow = lane & 31, lk = lane >> 5;
   const int l16 = lane & 15, lq = lane >> 4;
-  int a_hp16[SM];
+  int a_hp16[SM];        // halo pixel of this lane's A row at tap (0, 0)
 #pragma unroll
   for (int i = 0; i < SM; ++i) {
     const int m = wm0 + 16 * i + l16;
     const int ty = m / TF_W, tx = m % TF_W;
     a_hp16[i] = MODE == MODE_FWD ? ty * HW + tx : (ty + KS - 1) * HW + tx + KS - 1;
   }
-  int a_hp[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = wm0 + 32 * i + lrow;
-    const int ty = m / TF_W, tx = m % TF_W;
-    a_hp[i] = MODE == MODE_FWD ? ty * HW + tx : (ty + KS - 1) * HW + tx + KS - 1;
-  }
+  // B fragment rows wn0 + 16 j + l16: the swizzle depends on l16 only
+  const int b_frag = (wn0 + l16) * 4 + (lq ^ x3_sw(l16));
 
-  if (steps > 0) {
+  if (c_end > c_begin) {
     load_halo(c_begin);
     load_b(c_begin, 0);
     store_halo();
@@ -1310,70 +1301,36 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
       __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this step's MFMAs
       const int r = t / KS, s = t % KS;
       const int dh = MODE == MODE_FWD ? r * HW + s : -(r * HW + s);
-      if constexpr (M16) {
-        bf16x8 av[NP][SM], bv[NP][SN];
+      bf16x8 av[NP][SM], bv[NP][SN];
 #pragma unroll
-        for (int p = 0; p < NP; ++p) {
+      for (int i = 0; i < SM; ++i) {
+        const int px = a_hp16[i] + dh;
+        const int ai = px * 4 + (lq ^ x3_sw(px));
 #pragma unroll
-          for (int i = 0; i < SM; ++i)
-            av[p][i] = __builtin_bit_cast(bf16x8, Ah[p][(a_hp16[i] + dh) * SROW16 + lq]);
-#pragma unroll
-          for (int j = 0; j < SN; ++j)
-            bv[p][j] = __builtin_bit_cast(
-                bf16x8, Bs[buf][(p * BN + wn0 + 16 * j + l16) * SROW16 + lq]);
-        }
-#pragma unroll
-        for (int i = 0; i < SM; ++i)
-#pragma unroll
-          for (int j = 0; j < SN; ++j) {
-            f32x4 x = acc4[i][j];
-            if (X3_ABL & 8) {      // ablation: one product (the MFMA count of a bf16 conv)
-              asm volatile("" ::"v"(av[1][i]), "v"(av[2][i]), "v"(bv[1][j]), "v"(bv[2][j]));
-              acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
-              continue;
-            }
-            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
-          }
-      } else {
-      bf16x8 av[2][NP][TM], bv[2][NP][TN];
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-            av[st][p][i] = __builtin_bit_cast(bf16x8, Ah[p][(a_hp[i] + dh) * SROW16 + 2 * st + lk]);
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            bv[st][p][j] = __builtin_bit_cast(
-                bf16x8, Bs[buf][(p * BN + wn0 + 32 * j + lrow) * SROW16 + 2 * st + lk]);
-        }
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            f32x16 x = acc[i][j];
-            if (X3_ABL & 8) {      // ablation: one product (the MFMA count of a bf16 conv)
-              asm volatile("" ::"v"(av[st][1][i]), "v"(av[st][2][i]), "v"(bv[st][1][j]),
-                           "v"(bv[st][2][j]));
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][0][j], x, 0, 0, 0);
-              continue;
-            }
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][2][i], bv[st][0][j], x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][2][j], x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][1][i], bv[st][1][j], x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][1][i], bv[st][0][j], x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][1][j], x, 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[st][0][i], bv[st][0][j], x, 0, 0, 0);
-          }
+        for (int p = 0; p < NP; ++p) av[p][i] = __builtin_bit_cast(bf16x8, Ah[p * HP * 4 + ai]);
       }
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int j = 0; j < SN; ++j)
+          bv[p][j] = __builtin_bit_cast(bf16x8, Bs[(buf * NP + p) * BN * 4 + 64 * j + b_frag]);
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int j = 0; j < SN; ++j) {
+          f32x4 x = acc4[i][j];
+          if (X3_ABL & 8) {      // ablation: one product (the MFMA count of a bf16 conv)
+            asm volatile("" ::"v"(av[1][i]), "v"(av[2][i]), "v"(bv[1][j]), "v"(bv[2][j]));
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+            continue;
+          }
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+        }
       __builtin_amdgcn_sched_barrier(0);   // the stores wait for the prefetch: after the MFMAs
       // single B buffer: every wave must be done with it; double: only with the halo
       if (!(X3_ABL & 1) && (NB == 1 ? more : (t + 1 == KS * KS && more_c))) __syncthreads();
@@ -1385,9 +1342,9 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
     }
   }
 
-  // ---- epilogue (as conv_tile_bf16)
+  // ---- epilogue (16 x 16 C layout: column = lane & 15, rows 4 (lane >> 4) + r)
   const int64_t img = (int64_t)b * OH * OW;
-  if constexpr (M16 && (X3_ABL & 16)) {   // ablation: one store per lane instead of 4 SM SN
+  if constexpr (X3_ABL & 16) {   // ablation: one store per lane instead of 4 SM SN
     float v = 0.f;
 #pragma unroll
     for (int i = 0; i < SM; ++i)
@@ -1396,93 +1353,67 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
     a.C[(img + (int64_t)oy0 * OW + ox0) * a.ldc + (n0 + wn0 + (lane & 31)) % a.N] = v;
     return;
   }
-  if (M16 && a.vec_ep) {
-    // The wave's WM x WN accumulator block goes through a private LDS image (every wave passed
-    // the main loop's last barrier after its last halo / B read) and comes back as rows of
-    // float4: 16-byte loads and stores, WN / 4 lanes per pixel row (the MFMA layout holds 4
-    // rows of one column per lane: 4-byte accesses on 64-byte row segments).
+  if (a.vec_ep) {
+    // The wave's accumulator block goes through a private LDS image, EJ column blocks per
+    // pass (every wave passed the main loop's last barrier after its last halo / B read), and
+    // comes back as rows of float4: 16-byte loads and stores, 4 EJ lanes per pixel row (the
+    // MFMA layout holds 4 rows of one column per lane: 4-byte accesses on 64-byte segments).
     float* E = reinterpret_cast<float*>(smem) + wave * WM * EPW;
-#pragma unroll
-    for (int i = 0; i < SM; ++i)
-#pragma unroll
-      for (int j = 0; j < SN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) E[(16 * i + 4 * lq + r) * EPW + 16 * j + l16] = acc4[i][j][r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    constexpr int LPR = WN / 4, RPI = 64 / LPR;            // lanes per row, rows per pass
+    constexpr int LPR = 4 * EJ, RPI = 64 / LPR;            // lanes per row, rows per pass
     const int c4 = lane % LPR, rr = lane / LPR;
-    const int n = n0 + wn0 + 4 * c4;
 #pragma unroll
-    for (int q = 0; q < WM / RPI; ++q) {
-      const int m = q * RPI + rr;
-      const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
-      const int mt = wm0 + m;
-      const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
-      if (oy < OH && ox < OW && n < a.N)
-        epilogue_store4<MODE>(a, split, img + (int64_t)oy * OW + ox, n, v);
-    }
-    return;
-  }
-  if constexpr (M16) {
-    // 16 x 16 C layout: column = lane & 15, rows 4 (lane >> 4) + r
+    for (int jp = 0; jp < SN; jp += EJ) {
 #pragma unroll
-    for (int j = 0; j < SN; ++j) {
-      const int n = n0 + wn0 + 16 * j + l16;
-      if (n >= a.N) continue;
-      float bias = 0.f, scale = 1.f, shift = 0.f;
-      if (a.splits == 1) column_params<MODE>(a, n, bias, scale, shift);
-      EpAux aux[SM * 4];
+      for (int i = 0; i < SM; ++i)
 #pragma unroll
-      for (int q = 0; q < SM * 4; ++q) {
-        const int m = wm0 + 16 * (q >> 2) + 4 * lq + (q & 3);
-        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
-        aux[q] = a.splits == 1 && oy < OH && ox < OW
-                     ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : EpAux{0.f, 0.f};
+        for (int j = 0; j < EJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            E[(16 * i + 4 * lq + r) * EPW + 16 * j + l16] = acc4[i][jp + j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int n = n0 + wn0 + 16 * jp + 4 * c4;
+#pragma unroll
+      for (int q = 0; q < WM / RPI; ++q) {
+        const int m = q * RPI + rr;
+        const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
+        const int mt = wm0 + m;
+        const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
+        if (oy < OH && ox < OW && n < a.N)
+          epilogue_store4<MODE>(a, split, img + (int64_t)oy * OW + ox, n, v);
       }
-#pragma unroll
-      for (int q = 0; q < SM * 4; ++q) {
-        const int m = wm0 + 16 * (q >> 2) + 4 * lq + (q & 3);
-        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
-        if (oy >= OH || ox >= OW) continue;
-        const int64_t row = img + (int64_t)oy * OW + ox;
-        const float v = acc4[q >> 2][j][q & 3];
-        if (a.splits > 1)
-          a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n] = v;
-        else
-          epilogue_store<MODE>(a, row, n, v, bias, scale, shift, aux[q]);
-      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     return;
   }
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn0 + 32 * j + lrow;
+  for (int j = 0; j < SN; ++j) {
+    const int n = n0 + wn0 + 16 * j + l16;
     if (n >= a.N) continue;
     float bias = 0.f, scale = 1.f, shift = 0.f;
     if (a.splits == 1) column_params<MODE>(a, n, bias, scale, shift);
+    EpAux aux[SM * 4];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      EpAux aux[16];
+    for (int q = 0; q < SM * 4; ++q) {
+      const int m = wm0 + 16 * (q >> 2) + 4 * lq + (q & 3);
+      const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
+      aux[q] = a.splits == 1 && oy < OH && ox < OW
+                   ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : EpAux{0.f, 0.f};
+    }
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
-        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
-        aux[rr] = a.splits == 1 && oy < OH && ox < OW
-                      ? epilogue_aux<MODE>(a, img + (int64_t)oy * OW + ox, n) : EpAux{0.f, 0.f};
-      }
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int m = wm0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * lk;
-        const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
-        if (oy >= OH || ox >= OW) continue;
-        const int64_t row = img + (int64_t)oy * OW + ox;
-        if (a.splits > 1)
-          a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n] = acc[i][j][rr];
-        else
-          epilogue_store<MODE>(a, row, n, acc[i][j][rr], bias, scale, shift, aux[rr]);
-      }
+    for (int q = 0; q < SM * 4; ++q) {
+      const int m = wm0 + 16 * (q >> 2) + 4 * lq + (q & 3);
+      const int oy = oy0 + m / TF_W, ox = ox0 + m % TF_W;
+      if (oy >= OH || ox >= OW) continue;
+      const int64_t row = img + (int64_t)oy * OW + ox;
+      const float v = acc4[q >> 2][j][q & 3];
+      if (a.splits > 1)
+        a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n] = v;
+      else
+        epilogue_store<MODE>(a, row, n, v, bias, scale, shift, aux[q]);
     }
   }
 }
