@@ -212,6 +212,30 @@ __device__ __forceinline__ void epilogue_store4(const GemmArgs& a, int split, in
   *reinterpret_cast<float4*>(&a.C[row * a.ldc + n]) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// One wave's 32 x 32 accumulator block in the v_mfma_f32_32x32x* layout (column lane & 31,
+// rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) through a private 4 KB LDS image E, back as
+// float4 rows: f(row 0..31, column quad 0..7, value) for the 4 rows x 1 quad each lane owns.
+// Unpadded 32-float rows: the ds_write_b32 of a lane group cover one row (32 banks) and the
+// ds_read_b128 groups (rows 4 apart sharing a slot base) hit 16 distinct slots.
+template <typename F>
+__device__ __forceinline__ void transpose32(float* E, const f32x16& acc, int lane, F&& f) {
+  const int lrow = lane & 31, lk = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) E[((r & 3) + 8 * (r >> 2) + 4 * lk) * 32 + lrow] = acc[r];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int c4 = lane & 7, rr = lane >> 3;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = 8 * q + rr;
+    f(row, c4, *reinterpret_cast<const float4*>(&E[row * 32 + 4 * c4]));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // reads done before the next block
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int MODE>
 __device__ __forceinline__ void column_params(const GemmArgs& a, int n, float& bias,
                                               float& scale, float& shift) {
@@ -241,8 +265,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   constexpr int B_SLOTS = (B_QUADS + 255) / 256;
   static_assert(A_SLOTS >= 1, "BM >= 64");
 
-  __shared__ float As[2][BK * SA];
-  __shared__ float Bs[2][BK * SB];
+  // One LDS array: both operand buffers, and after the main loop the epilogue's 4 KB
+  // per-wave transpose images.
+  static_assert(2 * BK * (SA + SB) >= 4 * 1024, "epilogue images fit LDS");
+  __shared__ float smem[2 * BK * (SA + SB)];
+  float (*As)[BK * SA] = reinterpret_cast<float (*)[BK * SA]>(smem);
+  float (*Bs)[BK * SB] = reinterpret_cast<float (*)[BK * SB]>(smem + 2 * BK * SA);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -549,6 +577,28 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   }
 
   // ---------------- epilogue ---------------------------------------------------------------
+  if (a.vec_ep) {
+    // 16-byte rows through LDS (transpose32; the loop's last barrier freed the operand
+    // buffers): slab rows, or the fused epilogue on output rows
+    float* E = smem + wave * 1024;
+    float* S = a.slab + (int64_t)split * a.split_stride;
+    const int row_base = (MODE == MODE_WGRAD) ? 0 : G.tiles_begin * BM;
+    const bool slab = MODE == MODE_WGRAD || a.splits > 1;
+    if (do_colsum && tid < BN && n0 + tid < a.N) S[(int64_t)M * a.slab_ld + n0 + tid] = colacc;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        transpose32(E, acc[i][j], lane, [&](int row, int c4, float4 v) {
+          const int m = m0 + wm0 + 32 * i + row, n = n0 + wn0 + 32 * j + 4 * c4;
+          if (m >= M || n >= a.N) return;
+          if (slab)
+            *reinterpret_cast<float4*>(&S[(int64_t)(row_base + m) * a.slab_ld + n]) = v;
+          else
+            epilogue_store4<MODE>(a, 0, out_row(a, G, m), n, v);
+        });
+    return;
+  }
   if (MODE == MODE_WGRAD || a.splits > 1) {
     // raw partial sums into this K slice's slab; rows of group g start at tiles_begin*BM
     float* S = a.slab + (int64_t)split * a.split_stride;
@@ -634,8 +684,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
   constexpr int B_SLOTS = (B_OCTS + 255) / 256;
   static_assert(A_SLOTS >= 1, "BM >= 64");
 
-  __shared__ uint4 As[2][BM * SROW16];
-  __shared__ uint4 Bs[2][BN * SROW16];
+  // One LDS array: both operand buffers, then the epilogue's 4 KB per-wave transpose images.
+  static_assert(2 * (BM + BN) * SROW16 * 16 >= 4 * 4096, "epilogue images fit LDS");
+  __shared__ uint4 smem[2 * (BM + BN) * SROW16];
+  uint4 (*As)[BM * SROW16] = reinterpret_cast<uint4 (*)[BM * SROW16]>(smem);
+  uint4 (*Bs)[BN * SROW16] = reinterpret_cast<uint4 (*)[BN * SROW16]>(smem + 2 * BM * SROW16);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -837,6 +890,24 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
   }
 
   // ---------------- epilogue (as conv_gemm_f32) ----------------------------------------------
+  if (a.vec_ep) {
+    float* E = reinterpret_cast<float*>(smem) + wave * 1024;
+    float* S = a.slab + (int64_t)split * a.split_stride;
+    const int row_base = G.tiles_begin * BM;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        transpose32(E, acc[i][j], lane, [&](int row, int c4, float4 v) {
+          const int m = m0 + wm0 + 32 * i + row, n = n0 + wn0 + 32 * j + 4 * c4;
+          if (m >= M || n >= a.N) return;
+          if (a.splits > 1)
+            *reinterpret_cast<float4*>(&S[(int64_t)(row_base + m) * a.slab_ld + n]) = v;
+          else
+            epilogue_store4<MODE>(a, 0, out_row(a, G, m), n, v);
+        });
+    return;
+  }
   if (a.splits > 1) {
     float* S = a.slab + (int64_t)split * a.split_stride;
     const int row_base = G.tiles_begin * BM;
@@ -923,8 +994,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES
   static_assert((NT == 256 || NT == 512) && TM >= 1 && TN >= 1, "tile");
   constexpr int HQ = HP * 8, HS = (HQ + NT - 1) / NT;        // halo quads (32 ch)
   constexpr int BOCT = KS * BN * 4, BSL = (BOCT + NT - 1) / NT; // B octets per kernel row
-  __shared__ uint4 Ah[HP * SROW16];
-  __shared__ uint4 Bs[2][KS * BN * SROW16];
+  // One LDS array: the halo, the B buffers, then the epilogue's 4 KB per-wave images.
+  static_assert((HP + 2 * KS * BN) * SROW16 * 16 >= (NT / 64) * 4096, "epilogue images fit LDS");
+  __shared__ uint4 smem[(HP + 2 * KS * BN) * SROW16];
+  uint4* Ah = smem;
+  uint4 (*Bs)[KS * BN * SROW16] = reinterpret_cast<uint4 (*)[KS * BN * SROW16]>(smem + HP * SROW16);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1080,6 +1154,20 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES
 
   // ---- epilogue
   const int64_t img = (int64_t)b * OH * OW;
+  if (a.vec_ep) {   // 16-byte rows through LDS (the loop's last barrier freed the images)
+    float* E = reinterpret_cast<float*>(smem) + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        transpose32(E, acc[i][j], lane, [&](int row, int c4, float4 v) {
+          const int mt = wm0 + 32 * i + row, n = n0 + wn0 + 32 * j + 4 * c4;
+          const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
+          if (oy < OH && ox < OW && n < a.N)
+            epilogue_store4<MODE>(a, split, img + (int64_t)oy * OW + ox, n, v);
+        });
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn0 + 32 * j + lrow;
@@ -1162,12 +1250,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
   constexpr int HQ = HP * 8, HS = (HQ + NT - 1) / NT;          // halo quads (32 ch)
   constexpr int BOCT = NP * BN * 4, BSL = (BOCT + NT - 1) / NT; // B octets per tap
   // One LDS array: the halo planes, the B buffers, and after the main loop the epilogue's
-  // per-wave transpose images (WM rows x 16 EJ + 4 floats, EJ column blocks per pass).
+  // per-wave transpose images (WM rows x 16 EJ floats, EJ column blocks per pass; unpadded:
+  // rows 4 apart share a bank-slot base, and the float4 reads of a ds_read_b128 lane group
+  // (4 EJ lanes per row) cover 16 distinct slots; the 2-way ds_write_b32 conflict is free).
   constexpr int AH_U4 = NP * HP * 4, BS_U4 = NB * NP * BN * 4;
   constexpr int LDS_B = (AH_U4 + BS_U4) * 16;
-  constexpr int EJ = (NT / 64) * WM * (16 * SN + 4) * 4 <= LDS_B ? SN
-                     : (NT / 64) * WM * (8 * SN + 4) * 4 <= LDS_B ? SN / 2 : 1;
-  constexpr int EPW = 16 * EJ + 4;
+  constexpr int EJ = (NT / 64) * WM * 16 * SN * 4 <= LDS_B ? SN
+                     : (NT / 64) * WM * 8 * SN * 4 <= LDS_B ? SN / 2 : 1;
+  constexpr int EPW = 16 * EJ;
   static_assert(SN % EJ == 0 && (NT / 64) * WM * EPW * 4 <= LDS_B, "epilogue image fits LDS");
   __shared__ uint4 smem[AH_U4 + BS_U4];
   uint4* Ah = smem;                      // [plane][halo pixel][4 octets]
@@ -2764,7 +2854,8 @@ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static int g_vec_ep = 1;   // of_set_tuning key 3 (0: per-element epilogue, for A/B and tests)
 bool vec_ep_ok(const GemmArgs& a) {
   if (!g_vec_ep || a.N % 4) return false;
-  if (a.splits > 1) return a.slab_ld % 4 == 0 && al16(a.slab);
+  if (a.slab && !(a.slab_ld % 4 == 0 && a.split_stride % 4 == 0 && al16(a.slab))) return false;
+  if (a.splits > 1) return a.slab != nullptr;
   auto ok = [](const float* p, int ld) { return !p || (ld % 4 == 0 && al16(p)); };
   return ok(a.C, a.ldc) && ok(a.res, a.ldr) && ok(a.z, a.ldz) && ok(a.act_src, a.ld_act);
 }
@@ -3475,6 +3566,7 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   a.k_per_split = p.k_per_split;
   a.split_stride = p.split_stride;
   a.colsum = db != nullptr;
+  a.vec_ep = vec_ep_ok(a);
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
   if (x3) {

@@ -344,6 +344,77 @@ def test_conv_x3_vec_epilogue(n, h, w, cin, cout):
     assert rel_inf(outs[0][0], yref) < REL_TOL
 
 
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("n,h,w,cin,cout,k,s", [
+    (2, 32, 48, 4, 64, 7, 2),      # stem: 256 x 64 tiles, split-K slabs
+    (2, 16, 24, 64, 128, 3, 2),    # stride-2 block conv: dgrad phase groups
+    (2, 16, 24, 64, 128, 1, 2),    # 1x1 projection: in-place dgrad add skips 3 phase groups
+    (2, 12, 20, 128, 96, 3, 1),    # f32: 128 x 96 tiles; bf16: halo tiles
+    (1, 6, 10, 64, 36, 3, 1),      # 256 x 64 tiles, N not a tile multiple
+    (2, 20, 45, 128, 128, 3, 1),   # bf16 halo tiles, ragged right edge
+])
+def test_conv_gemm_vec_epilogue(n, h, w, cin, cout, k, s, prec):
+    """The fp32 / bf16 implicit-GEMM and bf16 halo-tile kernels' 16-byte epilogue
+    (transpose32) is bitwise identical to the per-element one: fwd (bias, BN, residual, z,
+    ReLU), dgrad (activation derivative; added gradient, in place), wgrad slabs + bias sums."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_LEAKY, ACT_RELU, call
+    lib = _lib.lib()
+    x = dev(rng_tensor((n, h, w, cin), 61))
+    wt = dev(rng_tensor((k, k, cin, cout), 62, scale=(2.0 / (k * k * cin)) ** 0.5))
+    b = dev(rng_tensor((cout,), 63, scale=0.1))
+    g, be = dev(rng_tensor((cout,), 64, scale=0.5)) + 1.0, dev(rng_tensor((cout,), 65, scale=0.1))
+    mu, var = dev(rng_tensor((cout,), 66, scale=0.1)), dev(rng_tensor((cout,), 67)).abs() + 0.5
+    if prec == "bf16":
+        layer = ops.ConvLayer(wt, b, stride=s, act=ACT_RELU, cin_p=cin, precision="bf16")
+    else:
+        layer = ops.ConvLayer(wt, b, stride=s, act=ACT_RELU, cin_p=cin, f32_split=False)
+    d = layer.desc(n, h, w)
+    sfx = "_bf16" if prec == "bf16" else ""
+    assert layer.mode(d) == 0 or prec == "bf16"
+    ho, wo = d.ho, d.wo
+    coutp = (cout + 3) // 4 * 4
+    res = dev(rng_tensor((n, ho, wo, cout), 68))
+    dy = dev(rng_tensor((n, ho, wo, coutp), 69))
+    act_src = dev(rng_tensor((n, h, w, cin), 70))
+    add = dev(rng_tensor((n, h, w, cin), 71))
+    wf, wd = layer.packed(d)
+    fws = getattr(lib, "of_conv2d_fwd%s_workspace" % sfx)(C.byref(d))
+    dws = getattr(lib, "of_conv2d_dgrad%s_workspace" % sfx)(C.byref(d))
+    wws = getattr(lib, "of_conv2d_wgrad%s_workspace" % sfx)(C.byref(d))
+    ws = torch.empty(max(fws, dws, wws) // 4 + 4, device="cuda")
+    P, st = ops._ptr, ops._stream()
+    outs = []
+    try:
+        for vec in (1, 0):
+            assert lib.of_set_tuning(3, vec) == 0
+            y = torch.full((n, ho, wo, cout), 7.0, device="cuda")
+            z = torch.full((n, ho, wo, cout), 7.0, device="cuda")
+            dx = torch.full((n, h, w, cin), 7.0, device="cuda")
+            dx2 = add.clone()
+            dw = torch.full_like(wt, 7.0)
+            db = torch.full_like(b, 7.0)
+            call("of_conv2d_fwd" + sfx, C.byref(d), P(x), cin, P(wf), P(b), P(g), P(be), P(mu),
+                 P(var), 1e-3, P(res), cout, ACT_RELU, 0.0, P(z), cout, P(y), cout, P(ws), fws, st)
+            if k < 7:
+                call("of_conv2d_dgrad" + sfx, C.byref(d), P(dy), coutp, P(wd), P(act_src), cin,
+                     ACT_LEAKY, 0.3, P(dx), cin, P(ws), dws, st)
+                call("of_conv2d_dgrad_add" + sfx, C.byref(d), P(dy), coutp, P(wd), P(dx2), cin,
+                     P(dx2), cin, P(ws), dws, st)
+            call("of_conv2d_wgrad" + sfx, C.byref(d), P(x), cin, P(dy), coutp, P(dw), P(db), 0,
+                 P(ws), wws, st)
+            torch.cuda.synchronize()
+            outs.append((y, z, dx, dx2, dw, db))
+    finally:
+        lib.of_set_tuning(3, 1)
+    for name, a1, a0 in zip(("y", "z", "dx", "dx_add", "dw", "db"), *outs):
+        assert torch.equal(a1, a0), (name, (a1 - a0).abs().max().item())
+    zref = R.conv2d_same(f64(x), f64(wt), f64(b), s)
+    assert rel_inf(outs[0][1], zref) < (2e-2 if prec == "bf16" else REL_TOL)
+
+
 def test_conv_bf16_tall_fwd():
     """bf16 forward with 8 x 32 output tiles (grids of >= 1024 tiles, BN 128) against an fp64
     conv of the bf16-rounded operands (the bf16 kernels round x and w RNE while staging)."""

@@ -29,7 +29,10 @@ SHAPES = [
     ("enc.conv1", 16, 384, 512, 3, 64, 7, 2),
     ("enc.l2", 16, 96, 128, 64, 64, 3, 1),
     ("enc.l3.c0", 16, 96, 128, 64, 128, 3, 2),
+    ("enc.l3.proj", 16, 96, 128, 64, 128, 1, 2),
     ("enc.l3", 16, 48, 64, 128, 128, 3, 1),
+    ("enc.l4.c0", 16, 48, 64, 128, 256, 3, 2),
+    ("enc.l4.proj", 16, 48, 64, 128, 256, 1, 2),
     ("enc.l4", 16, 24, 32, 256, 256, 3, 1),
 ]
 
