@@ -62,7 +62,8 @@ X3_BN = {0: "128, 4, 2", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1",   # conv_t
          4: "128, 2, 2", 5: "96, 4, 3", 6: "128, 2, 4"}
 X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4, 5: 8, 6: 4}                         # and tile rows
 X3_NB = {4: 1}                                                             # single-buffered B
-X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4"}   # conv_wgrad_tile_x3<CI, CO, R, rows>
+X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4",   # conv_wgrad_tile_x3<CI, CO, R, rows>
+          4: "2, 4, 8", 5: "2, 3, 8", 6: "4, 2, 4", 7: "4, 1, 4"}             # conv_wgrad_tile_x3b<CI, CO, rows>
 
 
 WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>
@@ -86,6 +87,8 @@ def kind_name(kind):
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
            "tile_x3": "_tile_x3"}[fam]
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
+        if fam == "tile_x3" and cfg >= 4:
+            sfx = "_tile_x3b"
         return "wgrad%s<%s>" % (sfx, X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
     if fam == "tile_x3":
         return "%s%s<%s, %d>" % (MODE_NAMES[mode], sfx, X3_BN[cfg], X3_TH[cfg])
@@ -100,7 +103,8 @@ def kernel_symbol(kind):
         return NARROW_SYMBOLS[mode]
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
         return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (
-            fam, X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
+            fam + ("b" if fam == "tile_x3" and cfg >= 4 else ""),
+            X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
     if fam in ("tile_bf16", "tile_x3"):
         if fam == "tile_x3":
             # the demangled name prints the defaulted NB too (conv_tile_x3<..., TH, NB>)

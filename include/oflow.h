@@ -304,7 +304,9 @@ int of_fill(float* y, float v, int64_t n, void* stream);
 int of_timing_enable(int on);
 /* Kernel-variant switches for A/B measurements: key 1 = fwd/dgrad split-K target workgroups
  * per CU (1-16, default 4), key 2 = minimum 16-deep K chunks per split slice (2-64, default 12),
- * key 3 = the tile kernels' 16-byte (float4-column) epilogue (1, default) or per-element (0). */
+ * key 3 = the tile kernels' 16-byte (float4-column) epilogue (1, default) or per-element (0),
+ * key 4 = the 9-tap split-bf16 weight gradient for Cout % 128 == 0 (1, default), for every
+ * Cout (2) or never (0: the 3-tap form). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -146,6 +146,11 @@ def load(path: str = LIB_PATH):
             fn.argtypes = args
         if lib.of_abi_version() != 1:
             raise OflowError("liboflow ABI mismatch")
+        # OFLOW_TUNE="key=value,...": of_set_tuning switches for A/B runs (include/oflow.h)
+        for kv in filter(None, os.environ.get("OFLOW_TUNE", "").split(",")):
+            k, v = kv.split("=")
+            if lib.of_set_tuning(int(k), int(v)) != OF_OK:
+                raise OflowError("OFLOW_TUNE: " + lib.of_last_error().decode(errors="replace"))
         _lib = lib
         return lib
 

@@ -2154,6 +2154,263 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wg
   }
 }
 
+// ---- conv_wgrad_tile_x3b: the same weight gradient with all 9 taps per wave ---------------
+// Wave = 16 ci x 32 co x 9 taps on v_mfma_f32_16x16x32_bf16 (18 accumulator tiles, 72
+// registers): one 32-pixel k-step (two tile rows of 16 px) takes one dy fragment per 16-column
+// block (8 pixels of one channel per lane, from L2, split in registers) and feeds it to 9 taps
+// x 6 products, so a loaded and split dy value serves 54 MFMAs (the 3-tap form: 18, and three
+// waves split the same value).  Workgroup = WAVES_CI x WAVES_CO waves over CIB = 16 WAVES_CI
+// input x COB = 32 WAVES_CO output channels; the x halo ((XH + 2) rows x 18 px) is staged once
+// per XH x 16 tile as three split planes x three pixel-shifted copies, single-buffered and
+// register-staged one tile ahead.  LDS row block (plane, s, hy): 8-channel groups of
+// 256 bytes, (ci, octet) in slot (2 (ci & 7) + octet) ^ 2 ((ci >> 3) & 3): the 16x16x32
+// A-fragment reads (16 consecutive channels x 2 octets x 2 rows) and the staging stores (8
+// lanes = 8 channel quads) are both conflict-free.  Output: the split-K slabs (+ bias row).
+__device__ __forceinline__ int wgx3b_slot(int ci, int oct) {
+  return (ci >> 3) * 16 + ((2 * (ci & 7) + oct) ^ (((ci >> 3) & 3) << 1));
+}
+
+template <int WAVES_CI, int WAVES_CO, int XH>
+__global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x3b(GemmArgs a) {
+  constexpr int NT = 64 * WAVES_CI * WAVES_CO;
+  constexpr int CIB = 16 * WAVES_CI, COB = 32 * WAVES_CO, KS = 3, HH = XH + KS - 1, NP = 3;
+  static_assert(XH % 2 == 0 && CIB % 32 == 0, "k-steps of 2 tile rows; 8-channel slot groups");
+  constexpr int XQ = HH * KS * 2 * (CIB / 4), XS = (XQ + NT - 1) / NT;   // (hy, s, half, ci quad)
+  constexpr int RB = CIB * 2;                      // uint4 per (plane, s, hy) row block
+  constexpr int PL = KS * HH * RB;                 // uint4 per plane
+  static_assert(NT / 64 * 16 * 32 * 4 <= NP * PL * 16, "epilogue images fit LDS");
+  __shared__ uint4 Xs[NP * PL];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_co = tile % a.n_tiles;
+  const int tile_ci = tile / a.n_tiles;
+  const int ci0 = tile_ci * CIB, co0 = tile_co * COB;
+  const int t_begin = split * a.k_per_split;
+  const int t_end = min(a.K, t_begin + a.k_per_split);
+  const int steps = max(0, t_end - t_begin);
+  const int tiles_x = (a.wo + TT_W - 1) / TT_W, tiles_y = (a.ho + XH - 1) / XH;
+  const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
+  const int wci0 = (wave / WAVES_CO) * 16;
+  const int wco0 = (wave % WAVES_CO) * 32;
+  const int l16 = lane & 15, lq = lane >> 4;
+
+  // ---- x halo slots (channel quad fastest: coalesced 16-byte lanes of one pixel)
+  const int xcq = tid % (CIB / 4);
+  const bool xc_ok = ci0 + 4 * xcq < a.kc;
+  float4 xv[XS][8];
+  auto load_x = [&](int t) {
+    const int b = t / (tiles_x * tiles_y);
+    const int trem = t - b * tiles_x * tiles_y;
+    const int oy0 = (trem / tiles_x) * XH, ox0 = (trem % tiles_x) * TT_W;
+    const int iy0 = oy0 - a.pt, ix00 = ox0 - a.pl;
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int q = tid + NT * j;
+      const int r2 = q / (CIB / 4);
+      const int half = r2 & 1, s = (r2 >> 1) % KS, hy = (r2 >> 1) / KS;
+      const int iy = iy0 + hy;
+      const bool rok = q < XQ && xc_ok && (unsigned)iy < (unsigned)a.h;
+      const int ix0 = ix00 + 8 * half + s;
+      const int base = ((b * a.h + iy) * a.w + ix0) * a.lda + ci0 + 4 * xcq;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = rok && (unsigned)(ix0 + e) < (unsigned)a.w;
+        xv[j][e] = bload4(rx, ok ? (uint32_t)((base + e * a.lda) * 4) : kOOB);
+      }
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int j = 0; j < XS; ++j) {
+      const int q = tid + NT * j;
+      if (XQ % NT == 0 || q < XQ) {
+        const int r2 = q / (CIB / 4);
+        const int half = r2 & 1, s = (r2 >> 1) % KS, hy = (r2 >> 1) / KS;
+        uint4* blk = &Xs[(s * HH + hy) * RB];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float v8[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v8[e] = (&xv[j][e].x)[c];
+          bf16x8 h, m, l;
+          split3x8(v8, h, m, l);
+          const int idx = wgx3b_slot(4 * xcq + c, half);
+          blk[idx] = __builtin_bit_cast(uint4, h);
+          blk[PL + idx] = __builtin_bit_cast(uint4, m);
+          blk[2 * PL + idx] = __builtin_bit_cast(uint4, l);
+        }
+      }
+    }
+  };
+  // ---- dy fragments: column blocks j = 0, 1 (co = co0 + wco0 + 16 j + l16), pixels
+  // 8 (lq & 1) .. + 7 of tile row 2 kk + (lq >> 1)
+  int co[2];
+  bool co_ok[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    co[j] = co0 + wco0 + 16 * j + l16;
+    co_ok[j] = co[j] < a.nb;
+  }
+  const int prow = lq >> 1, pcol = 8 * (lq & 1);
+  // Interior dy rows (the whole 16-pixel row and channel block in range) take fixed per-lane
+  // offsets plus a uniform scalar offset: no per-load address math or bounds tests.
+  const bool dy_co_full = co0 + COB <= a.nb;
+  const uint32_t dy_lane = (uint32_t)(((prow * a.wo + pcol) * a.ldb + co0 + wco0 + l16) * 4);
+  auto load_dy = [&](float (&dv)[2][8], int t, int kk) {
+    const int b = t / (tiles_x * tiles_y);
+    const int trem = t - b * tiles_x * tiles_y;
+    const int oyr = (trem / tiles_x) * XH + 2 * kk, ox0 = (trem % tiles_x) * TT_W;
+    if (dy_co_full && oyr + 1 < a.ho && ox0 + TT_W <= a.wo) {
+      const int so = ((b * a.ho + oyr) * a.wo + ox0) * a.ldb * 4;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          dv[j][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                   rd, dy_lane + (e * a.ldb + 16 * j) * 4, so, 0));
+      return;
+    }
+    const int oy = oyr + prow, ox = ox0 + pcol;
+    const bool rok = oy < a.ho;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int base = ((b * a.ho + oy) * a.wo + ox) * a.ldb + co[j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = rok && co_ok[j] && ox + e < a.wo;
+        dv[j][e] = bload1(rd, ok ? (uint32_t)((base + e * a.ldb) * 4) : kOOB);
+      }
+    }
+  };
+
+  f32x4 acc[KS * KS][2];
+#pragma unroll
+  for (int t = 0; t < KS * KS; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t][j][r] = 0.f;
+  // A fragment of tap (r, s) at k-step kk: row block (s, 2 kk + prow + r), this lane's slot
+  const int a_lane = prow * RB + wgx3b_slot(wci0 + l16, lq & 1);
+  const bool do_colsum = a.colsum && tile_ci == 0 && wci0 == 0;
+  float colacc[2] = {0.f, 0.f};
+  float dcur[2][8], dnext[2][8];
+
+  if (steps > 0) {
+    load_x(t_begin);
+    load_dy(dcur, t_begin, 0);
+    store_x();
+  }
+  __syncthreads();
+  for (int i = 0; i < steps; ++i) {
+    const int t = t_begin + i;
+    const bool more = i + 1 < steps;
+    if (more) load_x(t + 1);
+#pragma unroll
+    for (int kk = 0; kk < XH / 2; ++kk) {
+      if (kk + 1 < XH / 2) load_dy(dnext, t, kk + 1);
+      else if (more) load_dy(dnext, t + 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 bh[2], bm[2], bl[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) split3x8(dcur[j], bh[j], bm[j], bl[j]);
+      if (do_colsum) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) colacc[j] += dcur[j][e];
+      }
+      // A fragments one tap ahead of the MFMAs (bounded register footprint)
+      bf16x8 fa[2][NP];
+      auto load_a = [&](bf16x8 (&f)[NP], int tap) {
+        const int r = tap / KS, s = tap % KS;
+        const int xa = (s * HH + 2 * kk + r) * RB + a_lane;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) f[p] = __builtin_bit_cast(bf16x8, Xs[p * PL + xa]);
+      };
+      load_a(fa[0], 0);
+#pragma unroll
+      for (int tap = 0; tap < KS * KS; ++tap) {
+        if (tap + 1 < KS * KS) load_a(fa[(tap + 1) & 1], tap + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 ah = fa[tap & 1][0], am = fa[tap & 1][1], al = fa[tap & 1][2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 x = acc[tap][j];
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm[j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh[j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm[j], x, 0, 0, 0);
+          acc[tap][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], x, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dcur[j][e] = dnext[j][e];
+    }
+    __syncthreads();              // every wave is done with this tile's halo
+    if (more) store_x();
+    __syncthreads();
+  }
+
+  // ---- raw partial sums into this K slice's slab (+ bias column sums in row M)
+  float* S = a.slab + (int64_t)split * a.split_stride;
+  if (do_colsum) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float v = colacc[j] + __shfl_xor(colacc[j], 16);
+      v += __shfl_xor(v, 32);
+      if (lq == 0 && co[j] < a.N) S[(int64_t)a.M * a.slab_ld + co[j]] = v;
+    }
+  }
+  // 16 x 32 blocks per tap through a private 2 KB LDS image (the loop's last barrier freed
+  // the halo), back as float4 rows of 8 column quads: slab rows tap * kc + ci
+  float* E = reinterpret_cast<float*>(Xs) + wave * 512;
+  const int c4 = lane & 7, rr = lane >> 3;
+  const bool vec = a.vec_ep;
+#pragma unroll
+  for (int tap = 0; tap < KS * KS; ++tap) {
+    if (vec) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[(4 * lq + r) * 32 + 16 * j + l16] = acc[tap][j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int row = 8 * q + rr;
+        const int ci = ci0 + wci0 + row, n = co0 + wco0 + 4 * c4;
+        const float4 v = *reinterpret_cast<const float4*>(&E[row * 32 + 4 * c4]);
+        if (ci < a.kc && n < a.N)
+          *reinterpret_cast<float4*>(&S[((int64_t)tap * a.kc + ci) * a.slab_ld + n]) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ci = ci0 + wci0 + 4 * lq + r;
+          if (ci < a.kc && co[j] < a.N)
+            S[((int64_t)tap * a.kc + ci) * a.slab_ld + co[j]] = acc[tap][j][r];
+        }
+    }
+  }
+}
+
 // ---- fp32 weight gradient, 3x3 stride 1: all 9 taps from one staged halo ----------------
 // dW[r][s][ci][co] = sum_p x(p + (r, s) - pad)[ci] . dy(p)[co] on v_mfma_f32_32x32x2_f32, the
 // fp32 counterpart of conv_wgrad_tile_bf16: a workgroup owns CIB x COB channels for all 9
@@ -2852,6 +3109,10 @@ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // The tile kernels' 4-column epilogue (epilogue_store4) needs whole float4 columns and
 // 16-byte aligned rows in every tensor it touches.
 static int g_vec_ep = 1;   // of_set_tuning key 3 (0: per-element epilogue, for A/B and tests)
+// of_set_tuning key 4: conv_wgrad_tile_x3b for Cout % 128 == 0 (1, default), for every
+// x3 weight gradient (2), or never (0: the 3-tap form).  Measured per layer (same box): the
+// 9-tap form +6-11 % on the Cout = 128 layers, even on Cout 96 / 64, -6 % on Cout 32.
+static int g_wgx3b = 1;
 bool vec_ep_ok(const GemmArgs& a) {
   if (!g_vec_ep || a.N % 4) return false;
   if (a.slab && !(a.slab_ld % 4 == 0 && a.split_stride % 4 == 0 && al16(a.slab))) return false;
@@ -3212,6 +3473,7 @@ int of_set_tuning(int key, int value) {
   if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }
   if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
   if (key == 3 && (value == 0 || value == 1)) { g_vec_ep = value; return OF_OK; }
+  if (key == 4 && value >= 0 && value <= 2) { g_wgx3b = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -3578,11 +3840,18 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     a.tiles_total = (int)cdiv(g.cin_p, cib) * a.n_tiles;
     dim3 grid(a.tiles_total * a.splits);
     if (timing_on()) timing_begin(s);
-    if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 4, 3, 8>), grid, dim3(768), 0, s, a);
+    const bool x3b = g_wgx3b == 2 || (g_wgx3b == 1 && cfg == 0);
+    if (x3b) {
+      if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 4, 8>), grid, dim3(512), 0, s, a);
+      else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 3, 8>), grid, dim3(384), 0, s, a);
+      else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_x3b<4, 2, 4>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((conv_wgrad_tile_x3b<4, 1, 4>), grid, dim3(256), 0, s, a);
+    } else if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 4, 3, 8>), grid, dim3(768), 0, s, a);
     else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 3, 3, 8>), grid, dim3(576), 0, s, a);
     else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 2, 3, 4>), grid, dim3(768), 0, s, a);
     else hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 1, 3, 4>), grid, dim3(384), 0, s, a);
-    if (timing_on()) timing_end(s, 128 + MODE_WGRAD * 8 + cfg, flops);
+    // timing kinds 144-147: the 3-tap form, 148-151: conv_wgrad_tile_x3b (bench.py X3_WGT)
+    if (timing_on()) timing_end(s, 128 + MODE_WGRAD * 8 + cfg + (x3b ? 4 : 0), flops);
     st = check_launch("conv_wgrad_tile_x3");
   } else if (wgt_ok(d, bf16)) {
     int cib, cob;

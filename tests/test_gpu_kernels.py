@@ -218,10 +218,11 @@ def test_conv_x3_accuracy(n, h, w, cin, cout):
 
 
 @pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
-    ("tall128", 8, 128, 256, 128, 128, {128, 136, 144}),  # 8 x 32 tiles, BN 128 (1024 tiles)
+    # kinds: 128 + 8 mode + cfg; wgrad 144 + cfg (3-tap form) / 148 + cfg (9-tap x3b form)
+    ("tall128", 8, 128, 256, 128, 128, {128, 136, 148}),  # 8 x 32 tiles, BN 128 (1024 tiles)
     ("tall96", 8, 128, 256, 128, 96, {133, 136, 145}),    # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad
-    ("nb1", 8, 64, 128, 128, 128, {132, 140, 144}),       # single-buffered two-per-CU 4 x 32 form
-    ("split", 2, 48, 64, 256, 256, {134, 142, 144}),      # 8-wave 4 x 32 form with a K split
+    ("nb1", 8, 64, 128, 128, 128, {132, 140, 148}),       # single-buffered two-per-CU 4 x 32 form
+    ("split", 2, 48, 64, 256, 256, {134, 142, 148}),      # 8-wave 4 x 32 form with a K split
     ("bn64", 8, 128, 256, 64, 64, {130, 138, 146}),       # BN 64 keeps 4 x 32 tiles on large grids
 ], ids=["tall128", "tall96", "nb1", "split", "bn64"])
 def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
@@ -342,6 +343,56 @@ def test_conv_x3_vec_epilogue(n, h, w, cin, cout):
     yref = torch.relu((R.conv2d_same(f64(x), f64(wt), f64(b), 1) - f64(mu)) / torch.sqrt(f64(var) + 1e-3)
                       * f64(g) + f64(be) + f64(res))
     assert rel_inf(outs[0][0], yref) < REL_TOL
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout", [
+    (2, 20, 45, 128, 128),   # <2,4,8>: ragged right edge, 2 channel tiles
+    (1, 13, 32, 64, 96),     # <2,3,8>: odd rows (half k-step at the bottom)
+    (2, 24, 32, 64, 64),     # <4,2,4>
+    (1, 9, 40, 64, 32),      # <4,1,4>
+    (2, 8, 16, 256, 256),    # deep split over tiles, 16 channel tiles
+    (1, 6, 10, 44, 128),     # cin 44: partial channel block
+])
+def test_wgrad_x3_forms(n, h, w, cin, cout):
+    """The 9-tap split-bf16 weight gradient (conv_wgrad_tile_x3b: of_set_tuning key 4 = 2
+    runs it for every Cout) against fp64 and against the 3-tap form (key 4 = 0): weights and
+    bias gradient, with the 16-byte slab epilogue and the per-element one."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_NONE, call
+    lib = _lib.lib()
+    x = dev(rng_tensor((n, h, w, cin), 81))
+    wt = dev(rng_tensor((3, 3, cin, cout), 82, scale=(2.0 / (9 * cin)) ** 0.5))
+    b = dev(rng_tensor((cout,), 83, scale=0.1))
+    coutp = (cout + 3) // 4 * 4
+    dy = dev(rng_tensor((n, h, w, coutp), 84))
+    layer = ops.ConvLayer(wt, b, stride=1, act=ACT_NONE, cin_p=cin, f32_split=True)
+    d = layer.desc(n, h, w)
+    wws = lib.of_conv2d_wgrad_x3_workspace(C.byref(d))
+    ws = torch.empty(wws // 4 + 4, device="cuda")
+    P, st = ops._ptr, ops._stream()
+    dwref = torch.nn.grad.conv2d_weight(f64(x).permute(0, 3, 1, 2), (cout, cin, 3, 3),
+                                        f64(dy[..., :cout]).permute(0, 3, 1, 2),
+                                        padding=1).permute(2, 3, 1, 0)
+    dbref = f64(dy[..., :cout]).sum((0, 1, 2))
+    outs = {}
+    try:
+        for form, vec in ((2, 1), (2, 0), (0, 1)):
+            assert lib.of_set_tuning(4, form) == 0 and lib.of_set_tuning(3, vec) == 0
+            dw = torch.full_like(wt, 7.0)
+            db = torch.full_like(b, 7.0)
+            call("of_conv2d_wgrad_x3", C.byref(d), P(x), cin, P(dy), coutp, P(dw), P(db), 0,
+                 P(ws), wws, st)
+            torch.cuda.synchronize()
+            outs[(form, vec)] = (dw, db)
+    finally:
+        lib.of_set_tuning(4, 1)
+        lib.of_set_tuning(3, 1)
+    assert torch.equal(outs[(2, 1)][0], outs[(2, 0)][0]) and torch.equal(outs[(2, 1)][1], outs[(2, 0)][1])
+    for key, (dw, db) in outs.items():
+        assert rel_inf(dw, dwref) < 5e-6, (key, rel_inf(dw, dwref))
+        assert rel_inf(db, dbref) < 5e-6, (key, rel_inf(db, dbref))
 
 
 @pytest.mark.parametrize("prec", ["f32", "bf16"])
