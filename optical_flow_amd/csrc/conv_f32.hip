@@ -2155,12 +2155,13 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wg
 }
 
 // ---- conv_wgrad_tile_x3b: the same weight gradient with all 9 taps per wave ---------------
-// Wave = 16 ci x 32 co x 9 taps on v_mfma_f32_16x16x32_bf16 (18 accumulator tiles, 72
-// registers): one 32-pixel k-step (two tile rows of 16 px) takes one dy fragment per 16-column
-// block (8 pixels of one channel per lane, from L2, split in registers) and feeds it to 9 taps
-// x 6 products, so a loaded and split dy value serves 54 MFMAs (the 3-tap form: 18, and three
-// waves split the same value).  Workgroup = WAVES_CI x WAVES_CO waves over CIB = 16 WAVES_CI
-// input x COB = 32 WAVES_CO output channels; the x halo ((XH + 2) rows x 18 px) is staged once
+// Wave = 16 MI ci x 16 NJ co x 9 taps on v_mfma_f32_16x16x32_bf16 (MI NJ = 2: 18 accumulator
+// tiles, 72 registers): one 32-pixel k-step (two tile rows of 16 px) takes one dy fragment per
+// 16-column block (8 pixels of one channel per lane, from L2, split in registers) and feeds it
+// to 9 taps x MI row blocks x 6 products: with MI = 2 a loaded and split dy value serves 108
+// MFMAs and no other wave loads it (the 3-tap form: 18, three waves splitting the same value).
+// Workgroup = WAVES_CI x WAVES_CO waves over CIB = 16 MI WAVES_CI input x COB = 16 NJ WAVES_CO
+// output channels; the x halo ((XH + 2) rows x 18 px) is staged once
 // per XH x 16 tile as three split planes x three pixel-shifted copies, single-buffered and
 // register-staged one tile ahead.  LDS row block (plane, s, hy): 8-channel groups of
 // 256 bytes, (ci, octet) in slot (2 (ci & 7) + octet) ^ 2 ((ci >> 3) & 3): the 16x16x32
@@ -2170,15 +2171,17 @@ __device__ __forceinline__ int wgx3b_slot(int ci, int oct) {
   return (ci >> 3) * 16 + ((2 * (ci & 7) + oct) ^ (((ci >> 3) & 3) << 1));
 }
 
-template <int WAVES_CI, int WAVES_CO, int XH>
+template <int WAVES_CI, int WAVES_CO, int XH, int MI = 1>
 __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x3b(GemmArgs a) {
+  constexpr int NJ = 2 / MI;
+  static_assert(MI * NJ == 2, "18 accumulator tiles per wave");
   constexpr int NT = 64 * WAVES_CI * WAVES_CO;
-  constexpr int CIB = 16 * WAVES_CI, COB = 32 * WAVES_CO, KS = 3, HH = XH + KS - 1, NP = 3;
+  constexpr int CIB = 16 * MI * WAVES_CI, COB = 16 * NJ * WAVES_CO, KS = 3, HH = XH + KS - 1, NP = 3;
   static_assert(XH % 2 == 0 && CIB % 32 == 0, "k-steps of 2 tile rows; 8-channel slot groups");
   constexpr int XQ = HH * KS * 2 * (CIB / 4), XS = (XQ + NT - 1) / NT;   // (hy, s, half, ci quad)
   constexpr int RB = CIB * 2;                      // uint4 per (plane, s, hy) row block
   constexpr int PL = KS * HH * RB;                 // uint4 per plane
-  static_assert(NT / 64 * 16 * 32 * 4 <= NP * PL * 16, "epilogue images fit LDS");
+  static_assert(NT / 64 * 512 * 4 <= NP * PL * 16, "epilogue images fit LDS");
   __shared__ uint4 Xs[NP * PL];
 
   const int tid = threadIdx.x;
@@ -2196,8 +2199,8 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
   const int tiles_x = (a.wo + TT_W - 1) / TT_W, tiles_y = (a.ho + XH - 1) / XH;
   const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
   const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
-  const int wci0 = (wave / WAVES_CO) * 16;
-  const int wco0 = (wave % WAVES_CO) * 32;
+  const int wci0 = (wave / WAVES_CO) * 16 * MI;
+  const int wco0 = (wave % WAVES_CO) * 16 * NJ;
   const int l16 = lane & 15, lq = lane >> 4;
 
   // ---- x halo slots (channel quad fastest: coalesced 16-byte lanes of one pixel)
@@ -2248,12 +2251,12 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
       }
     }
   };
-  // ---- dy fragments: column blocks j = 0, 1 (co = co0 + wco0 + 16 j + l16), pixels
+  // ---- dy fragments: column blocks j < NJ (co = co0 + wco0 + 16 j + l16), pixels
   // 8 (lq & 1) .. + 7 of tile row 2 kk + (lq >> 1)
-  int co[2];
-  bool co_ok[2];
+  int co[NJ];
+  bool co_ok[NJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     co[j] = co0 + wco0 + 16 * j + l16;
     co_ok[j] = co[j] < a.nb;
   }
@@ -2262,14 +2265,14 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
   // offsets plus a uniform scalar offset: no per-load address math or bounds tests.
   const bool dy_co_full = co0 + COB <= a.nb;
   const uint32_t dy_lane = (uint32_t)(((prow * a.wo + pcol) * a.ldb + co0 + wco0 + l16) * 4);
-  auto load_dy = [&](float (&dv)[2][8], int t, int kk) {
+  auto load_dy = [&](float (&dv)[NJ][8], int t, int kk) {
     const int b = t / (tiles_x * tiles_y);
     const int trem = t - b * tiles_x * tiles_y;
     const int oyr = (trem / tiles_x) * XH + 2 * kk, ox0 = (trem % tiles_x) * TT_W;
     if (dy_co_full && oyr + 1 < a.ho && ox0 + TT_W <= a.wo) {
       const int so = ((b * a.ho + oyr) * a.wo + ox0) * a.ldb * 4;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           dv[j][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
@@ -2279,7 +2282,7 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
     const int oy = oyr + prow, ox = ox0 + pcol;
     const bool rok = oy < a.ho;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int base = ((b * a.ho + oy) * a.wo + ox) * a.ldb + co[j];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -2289,18 +2292,25 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
     }
   };
 
-  f32x4 acc[KS * KS][2];
+  f32x4 acc[KS * KS][MI][NJ];
 #pragma unroll
   for (int t = 0; t < KS * KS; ++t)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[t][j][r] = 0.f;
-  // A fragment of tap (r, s) at k-step kk: row block (s, 2 kk + prow + r), this lane's slot
-  const int a_lane = prow * RB + wgx3b_slot(wci0 + l16, lq & 1);
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][i][j][r] = 0.f;
+  // A fragment of tap (r, s) at k-step kk, row block i: row block (s, 2 kk + prow + r), this
+  // lane's slot for channel wci0 + 16 i + l16
+  int a_lane[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) a_lane[i] = prow * RB + wgx3b_slot(wci0 + 16 * i + l16, lq & 1);
   const bool do_colsum = a.colsum && tile_ci == 0 && wci0 == 0;
-  float colacc[2] = {0.f, 0.f};
-  float dcur[2][8], dnext[2][8];
+  float colacc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) colacc[j] = 0.f;
+  float dcur[NJ][8], dnext[NJ][8];
 
   if (steps > 0) {
     load_x(t_begin);
@@ -2317,43 +2327,49 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
       if (kk + 1 < XH / 2) load_dy(dnext, t, kk + 1);
       else if (more) load_dy(dnext, t + 1, 0);
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 bh[2], bm[2], bl[2];
+      bf16x8 bh[NJ], bm[NJ], bl[NJ];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) split3x8(dcur[j], bh[j], bm[j], bl[j]);
+      for (int j = 0; j < NJ; ++j) split3x8(dcur[j], bh[j], bm[j], bl[j]);
       if (do_colsum) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int e = 0; e < 8; ++e) colacc[j] += dcur[j][e];
       }
       // A fragments one tap ahead of the MFMAs (bounded register footprint)
-      bf16x8 fa[2][NP];
-      auto load_a = [&](bf16x8 (&f)[NP], int tap) {
+      bf16x8 fa[2][MI][NP];
+      auto load_a = [&](bf16x8 (&f)[MI][NP], int tap) {
         const int r = tap / KS, s = tap % KS;
-        const int xa = (s * HH + 2 * kk + r) * RB + a_lane;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) f[p] = __builtin_bit_cast(bf16x8, Xs[p * PL + xa]);
+        for (int i = 0; i < MI; ++i) {
+          const int xa = (s * HH + 2 * kk + r) * RB + a_lane[i];
+#pragma unroll
+          for (int p = 0; p < NP; ++p) f[i][p] = __builtin_bit_cast(bf16x8, Xs[p * PL + xa]);
+        }
       };
       load_a(fa[0], 0);
 #pragma unroll
       for (int tap = 0; tap < KS * KS; ++tap) {
         if (tap + 1 < KS * KS) load_a(fa[(tap + 1) & 1], tap + 1);
         __builtin_amdgcn_sched_barrier(0);
-        const bf16x8 ah = fa[tap & 1][0], am = fa[tap & 1][1], al = fa[tap & 1][2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x4 x = acc[tap][j];
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm[j], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh[j], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm[j], x, 0, 0, 0);
-          acc[tap][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], x, 0, 0, 0);
+        for (int i = 0; i < MI; ++i) {
+          const bf16x8 ah = fa[tap & 1][i][0], am = fa[tap & 1][i][1], al = fa[tap & 1][i][2];
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            f32x4 x = acc[tap][i][j];
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm[j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh[j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm[j], x, 0, 0, 0);
+            acc[tap][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], x, 0, 0, 0);
+          }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) dcur[j][e] = dnext[j][e];
     }
@@ -2366,32 +2382,35 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
   float* S = a.slab + (int64_t)split * a.split_stride;
   if (do_colsum) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       float v = colacc[j] + __shfl_xor(colacc[j], 16);
       v += __shfl_xor(v, 32);
       if (lq == 0 && co[j] < a.N) S[(int64_t)a.M * a.slab_ld + co[j]] = v;
     }
   }
-  // 16 x 32 blocks per tap through a private 2 KB LDS image (the loop's last barrier freed
-  // the halo), back as float4 rows of 8 column quads: slab rows tap * kc + ci
+  // (16 MI) x (16 NJ) blocks per tap through a private 2 KB LDS image (the loop's last barrier
+  // freed the halo), back as float4 rows of 4 NJ column quads: slab rows tap * kc + ci
+  constexpr int EW = 16 * NJ, LPR = 4 * NJ, RPI = 64 / LPR;
   float* E = reinterpret_cast<float*>(Xs) + wave * 512;
-  const int c4 = lane & 7, rr = lane >> 3;
+  const int c4 = lane % LPR, rr = lane / LPR;
   const bool vec = a.vec_ep;
 #pragma unroll
   for (int tap = 0; tap < KS * KS; ++tap) {
     if (vec) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) E[(4 * lq + r) * 32 + 16 * j + l16] = acc[tap][j][r];
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) E[(16 * i + 4 * lq + r) * EW + 16 * j + l16] = acc[tap][i][j][r];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int row = 8 * q + rr;
+      for (int q = 0; q < 16 * MI / RPI; ++q) {
+        const int row = RPI * q + rr;
         const int ci = ci0 + wci0 + row, n = co0 + wco0 + 4 * c4;
-        const float4 v = *reinterpret_cast<const float4*>(&E[row * 32 + 4 * c4]);
+        const float4 v = *reinterpret_cast<const float4*>(&E[row * EW + 4 * c4]);
         if (ci < a.kc && n < a.N)
           *reinterpret_cast<float4*>(&S[((int64_t)tap * a.kc + ci) * a.slab_ld + n]) = v;
       }
@@ -2400,13 +2419,15 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     } else {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int ci = ci0 + wci0 + 4 * lq + r;
-          if (ci < a.kc && co[j] < a.N)
-            S[((int64_t)tap * a.kc + ci) * a.slab_ld + co[j]] = acc[tap][j][r];
-        }
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ci = ci0 + wci0 + 16 * i + 4 * lq + r;
+            if (ci < a.kc && co[j] < a.N)
+              S[((int64_t)tap * a.kc + ci) * a.slab_ld + co[j]] = acc[tap][i][j][r];
+          }
     }
   }
 }
@@ -3113,6 +3134,10 @@ static int g_vec_ep = 1;   // of_set_tuning key 3 (0: per-element epilogue, for 
 // x3 weight gradient (2), or never (0: the 3-tap form).  Measured per layer (same box): the
 // 9-tap form +6-11 % on the Cout = 128 layers, even on Cout 96 / 64, -6 % on Cout 32.
 static int g_wgx3b = 1;
+// of_set_tuning key 5: conv_wgrad_tile_x3b wave shape, 16 MI ci x 32 / MI co (MI = 1 or 2).
+// MI = 2 halves the dy loads and splits per MFMA and measured the same (dec3.c1 0.516 vs
+// 0.517 ms): the split VALU is not what bounds the kernel.
+static int g_wgx3b_mi = 1;
 bool vec_ep_ok(const GemmArgs& a) {
   if (!g_vec_ep || a.N % 4) return false;
   if (a.slab && !(a.slab_ld % 4 == 0 && a.split_stride % 4 == 0 && al16(a.slab))) return false;
@@ -3474,6 +3499,7 @@ int of_set_tuning(int key, int value) {
   if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
   if (key == 3 && (value == 0 || value == 1)) { g_vec_ep = value; return OF_OK; }
   if (key == 4 && value >= 0 && value <= 2) { g_wgx3b = value; return OF_OK; }
+  if (key == 5 && (value == 1 || value == 2)) { g_wgx3b_mi = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -3842,7 +3868,12 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     if (timing_on()) timing_begin(s);
     const bool x3b = g_wgx3b == 2 || (g_wgx3b == 1 && cfg == 0);
     if (x3b) {
-      if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 4, 8>), grid, dim3(512), 0, s, a);
+      if (g_wgx3b_mi == 2) {   // waves of 32 ci x 16 co
+        if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3b<1, 8, 8, 2>), grid, dim3(512), 0, s, a);
+        else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3b<1, 6, 8, 2>), grid, dim3(384), 0, s, a);
+        else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 4, 4, 2>), grid, dim3(512), 0, s, a);
+        else hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 2, 4, 2>), grid, dim3(256), 0, s, a);
+      } else if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 4, 8>), grid, dim3(512), 0, s, a);
       else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 3, 8>), grid, dim3(384), 0, s, a);
       else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_x3b<4, 2, 4>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((conv_wgrad_tile_x3b<4, 1, 4>), grid, dim3(256), 0, s, a);
