@@ -983,6 +983,12 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #ifndef X3_ABL
 #define X3_ABL 0
 #endif
+// conv_tile_x3 B staging by LDS DMA (buffer_load ... lds) in the double-buffered forms
+// (measured against register staging, same box: dec3.c0 fwd / dgrad -5 / -4 %, dec3.c3 fwd
+// -6 %, enc.l4 -7 %; -DX3_BDMA=0 builds the register-staged form)
+#ifndef X3_BDMA
+#define X3_BDMA 1
+#endif
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH = OF_TF_H>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES_N)) void conv_tile_bf16(GemmArgs a) {
@@ -1238,6 +1244,13 @@ __device__ __forceinline__ void split3x4(const float4& v, uint2& h, uint2& m, ui
 // 80-byte padded rows that suit the 32 x 32 layout leave 3 of 16 slots 2-way in every group.)
 __device__ __forceinline__ int x3_sw(int p) { return ((p >> 2) & 1) << 1; }
 
+// One LDS-DMA wave-instruction (buffer_load_dwordx4 ... lds): lane L's 16 bytes at byte
+// offset voff + soff of r land at dst + 16 L (dst wave-uniform); out-of-range lanes write 0.
+__device__ __forceinline__ void dma16_to_lds(rsrc_t r, uint4* dst, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16,
+                                           voff, soff, 0, 0);
+}
+
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int NB = 2>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_tile_x3(GemmArgs a) {
   constexpr int BM = TH * TF_W, KS = 3, NP = 3;
@@ -1348,6 +1361,30 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
     for (int j = 0; j < BSL; ++j)
       if (BOCT % NT == 0 || b_lds[j] >= 0) Bs[buf * NP * BN * 4 + b_lds[j]] = rb[j];
   };
+  // X3_BDMA (double-buffered forms): B goes global -> LDS by buffer_load ... lds, no VGPR
+  // staging and no ds_write: one wave-instruction fills 16 rows x 64 bytes (lane-linear), so
+  // lane L loads octet (L & 3) ^ x3_sw(L >> 2) of its row to keep the swizzled image.
+  constexpr bool BDMA = X3_BDMA && NB == 2;
+  constexpr int NW = NT / 64, BDI = NP * BN / 16, BDW = (BDI + NW - 1) / NW;
+  uint32_t bd_off[BDW];
+  int bd_lds[BDW];
+#pragma unroll
+  for (int k = 0; k < BDW; ++k) {
+    const int g = wave + NW * k;
+    const int p = g / (BN / 16), rbk = g % (BN / 16);
+    const int n = rbk * 16 + (lane >> 2), o = (lane & 3) ^ x3_sw(lane >> 2);
+    bd_off[k] = g < BDI && n0 + n < a.nb
+                    ? (uint32_t)(((int64_t)p * a.b_plane + (int64_t)(n0 + n) * a.ldb + 8 * o) * 2)
+                    : kOOB;
+    bd_lds[k] = g < BDI ? (p * BN + rbk * 16) * 4 : -1;
+  }
+  auto dma_b = [&](int c, int t, int buf) {
+    const int so = (t * a.kc + 32 * c) * 2;
+#pragma unroll
+    for (int k = 0; k < BDW; ++k)
+      if (BDI % NW == 0 || bd_lds[k] >= 0)
+        dma16_to_lds(rb_src, Bs + buf * NP * BN * 4 + bd_lds[k], bd_off[k], so);
+  };
 
   f32x4 acc4[SM][SN];
 #pragma unroll
@@ -1371,10 +1408,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
 
   if (c_end > c_begin) {
     load_halo(c_begin);
-    load_b(c_begin, 0);
+    if constexpr (BDMA) dma_b(c_begin, 0, 0);
+    else load_b(c_begin, 0);
     store_halo();
-    store_b(0);
+    if constexpr (!BDMA) store_b(0);
   }
+  if constexpr (BDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // Chunk loop with the 9 taps unrolled (fragment offsets are immediates).  Step (chunk, tap)
   // reads B buffer (chunk + tap) & 1 (9 steps per chunk) and fetches the next step's B; the
@@ -1387,7 +1426,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
     for (int t = 0; t < KS * KS; ++t) {
       const int buf = NB == 2 ? (cc + t) & 1 : 0;
       const bool more = t + 1 < KS * KS || more_c;
-      if (more && !(X3_ABL & 2)) load_b(t + 1 < KS * KS ? c : c + 1, t + 1 < KS * KS ? t + 1 : 0);
+      if (more && !(X3_ABL & 2)) {
+        if constexpr (BDMA) dma_b(t + 1 < KS * KS ? c : c + 1, t + 1 < KS * KS ? t + 1 : 0, buf ^ 1);
+        else load_b(t + 1 < KS * KS ? c : c + 1, t + 1 < KS * KS ? t + 1 : 0);
+      }
       __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this step's MFMAs
       const int r = t / KS, s = t % KS;
       const int dh = MODE == MODE_FWD ? r * HW + s : -(r * HW + s);
@@ -1425,9 +1467,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
       // single B buffer: every wave must be done with it; double: only with the halo
       if (!(X3_ABL & 1) && (NB == 1 ? more : (t + 1 == KS * KS && more_c))) __syncthreads();
       if (more) {
-        if (!(X3_ABL & 2)) store_b(NB == 2 ? buf ^ 1 : 0);
+        if (!(X3_ABL & 2) && !BDMA) store_b(NB == 2 ? buf ^ 1 : 0);
         if (t + 1 == KS * KS && more_c && !(X3_ABL & 4)) store_halo();
       }
+      if constexpr (BDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own B DMA landed
       if (!(X3_ABL & 1)) __syncthreads();
     }
   }
