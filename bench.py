@@ -49,9 +49,10 @@ def kind_parts(kind):
     """timing kind -> (mode, tile config, family): f32 GEMMs mode*8+cfg (narrow VALU cfg 7),
     f32 halo-tiled wgrad 32 + mode*8 + cfg,
     bf16 implicit GEMMs 64 + mode*8 + cfg, bf16 halo-tiled 3x3 96 + mode*8 + cfg,
-    fp32 on the split-bf16 halo-tiled 3x3 kernels 128 + mode*8 + cfg
-    (optical_flow_amd/csrc/conv_f32.hip)."""
-    fam = ("tile_x3" if kind >= 128 else "tile_bf16" if kind >= 96 else "bf16" if kind >= 64 else
+    fp32 on the split-bf16 halo-tiled 3x3 kernels 128 + mode*8 + cfg, on the split-bf16
+    implicit GEMM (other shapes) 160 + mode*8 + cfg (optical_flow_amd/csrc/conv_f32.hip)."""
+    fam = ("gemm_x3" if kind >= 160 else "tile_x3" if kind >= 128 else "tile_bf16" if kind >= 96 else
+           "bf16" if kind >= 64 else
            "tile_f32" if kind >= 32 else "f32")
     return (kind % 32) // 8, kind % 8, fam
 
@@ -62,6 +63,8 @@ X3_BN = {0: "128, 4, 2", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1",   # conv_t
          4: "128, 2, 2", 5: "96, 4, 3", 6: "128, 2, 4"}
 X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4, 5: 8, 6: 4}                         # and tile rows
 X3_NB = {4: 1}                                                             # single-buffered B
+GX3 = {0: "128, 128, 4, 2", 1: "256, 64, 8, 1"}   # conv_gemm_x3<BM, BN, WAVES_M, WAVES_N>
+GX3_WG = {0: "128, 128, 4, 2", 1: "128, 64, 4, 2"}  # conv_wgrad_x3<BM, BN, WAVES_M, WAVES_N>
 X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4",   # conv_wgrad_tile_x3<CI, CO, R, rows>
           4: "2, 4, 8", 5: "2, 3, 8", 6: "4, 2, 4", 7: "4, 1, 4"}             # conv_wgrad_tile_x3b<CI, CO, rows>
 
@@ -75,9 +78,10 @@ def conv_math(precision):
     if precision == "bf16":
         return "bf16 MFMA operands, fp32 accumulation (flow convs cout<=4: fp32 VALU)"
     if ops.F32_SPLIT:
-        return ("fp32: 3x3 stride-1 fwd/dgrad (and wgrad for Cout in {32, 64, 96, 128k}) on "
-                "bf16 MFMA with an exact 3-term operand split (6 products, fp32 accumulation; "
-                "error vs fp64 at fp32-MFMA level, test_conv_x3_accuracy); other convs on fp32 "
+        return ("fp32: every conv with >= 16 input channels (3x3 stride-1 halo tiles; stride-2 "
+                "and 1x1 implicit GEMMs) fwd/dgrad/wgrad on bf16 MFMA with an exact 3-term "
+                "operand split (6 products, fp32 accumulation; error vs fp64 at fp32-MFMA level, "
+                "test_conv_x3_accuracy / test_conv_gemm_x3_accuracy); the 3-channel stem on fp32 "
                 "MFMA, the Cout<=4 flow convs on fp32 VALU")
     return "fp32 MFMA (flow convs cout<=4: fp32 VALU)"
 
@@ -85,7 +89,9 @@ def conv_math(precision):
 def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
-           "tile_x3": "_tile_x3"}[fam]
+           "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3"}[fam]
+    if fam == "gemm_x3":
+        return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (GX3_WG if mode == 2 else GX3)[cfg])
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
         if fam == "tile_x3" and cfg >= 4:
             sfx = "_tile_x3b"
@@ -101,6 +107,10 @@ def kernel_symbol(kind):
     mode, cfg, fam = kind_parts(kind)
     if cfg == 7 and fam == "f32":
         return NARROW_SYMBOLS[mode]
+    if fam == "gemm_x3":
+        if mode == 2:
+            return "void oflow::conv_wgrad_x3<%s>(oflow::GemmArgs)" % GX3_WG[cfg]
+        return "void oflow::conv_gemm_x3<%s, %d>(oflow::GemmArgs)" % (GX3[cfg], mode)
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
         return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (
             fam + ("b" if fam == "tile_x3" and cfg >= 4 else ""),
@@ -311,7 +321,8 @@ def main():
         fam = kind_parts(dom)[2]
         # the split kernel spends six bf16 MFMAs per fp32 product: its ceiling is 1/6 of bf16
         peak = (FP32_MFMA_PEAK_TFLOPS if fam in ("f32", "tile_f32") else
-                round(BF16_MFMA_PEAK_TFLOPS / 6, 1) if fam == "tile_x3" else BF16_MFMA_PEAK_TFLOPS)
+                round(BF16_MFMA_PEAK_TFLOPS / 6, 1) if fam in ("tile_x3", "gemm_x3")
+                else BF16_MFMA_PEAK_TFLOPS)
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,

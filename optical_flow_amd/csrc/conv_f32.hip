@@ -989,6 +989,9 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #ifndef X3_BDMA
 #define X3_BDMA 1
 #endif
+#ifndef X3_PRIO
+#define X3_PRIO 0
+#endif
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH = OF_TF_H>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES_N)) void conv_tile_bf16(GemmArgs a) {
@@ -1415,6 +1418,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
   }
   if constexpr (BDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (X3_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // the later-dispatched half
   // Chunk loop with the 9 taps unrolled (fragment offsets are immediates).  Step (chunk, tap)
   // reads B buffer (chunk + tap) & 1 (9 steps per chunk) and fetches the next step's B; the
   // next chunk's halo is fetched at tap 0 and stored after tap 8.
@@ -1548,6 +1552,288 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
       else
         epilogue_store<MODE>(a, row, n, v, bias, scale, shift, aux[q]);
     }
+  }
+}
+
+// ---- fp32 on bf16 MFMA by the three-term split: implicit-GEMM fwd / dgrad ------------------
+// The shapes the halo tiles do not cover (the 7x7 stride-2 stem, the 3x3 stride-2 block
+// convs and the 1x1 stride-2 projections, with the stride-2 input gradient as phase groups):
+// conv_gemm_bf16's geometry (tap walkers, phase groups, K in 32-deep chunks of the packed
+// [n][k] images, split-K slabs) with the operands cut into the hi / mid / lo planes of
+// conv_tile_x3 and six v_mfma_f32_16x16x32_bf16 per fragment pair.  A (activations) is
+// register-staged and split while it is stored; B (the x3 weight planes) comes in by LDS DMA;
+// both LDS images are double-buffered rows of four octets in the x3_sw swizzle (one barrier
+// per chunk).  Waves own WM x WN blocks of 16 x 16 tiles.  Wave w stages octet w & 3 of every
+// chunk (two channel quads with their own tap walks) for row group w >> 2.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_gemm_x3(GemmArgs a) {
+  static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "x3 GEMM: fwd / dgrad");
+  constexpr int NT = 64 * WAVES_M * WAVES_N, NW = NT / 64, NP = 3;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, SM = WM / 16, SN = WN / 16;
+  static_assert(NW % 4 == 0 && SM >= 1 && SN >= 1 && WM % 16 == 0 && WN % 16 == 0, "tile");
+  constexpr int RG = NW / 4;                     // row groups (4 waves each: one per octet)
+  constexpr int A_SL = BM / (64 * RG);           // A rows per lane
+  static_assert(A_SL >= 1 && BM % (64 * RG) == 0, "BM");
+  constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
+  constexpr int BDI = NP * BN / 16, BDW = (BDI + NW - 1) / NW;   // B DMA wave-instructions
+  static_assert(NW * WM * WN * 4 <= 2 * (A_U4 + B_U4) * 16, "epilogue images fit LDS");
+  __shared__ uint4 smem[2 * (A_U4 + B_U4)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_n = tile % a.n_tiles;
+  const int tile_mg = tile / a.n_tiles;
+  int gi = 0;
+#pragma unroll
+  for (int g = 1; g < MAX_GROUPS; ++g)
+    if (g < a.ngroups && tile_mg >= a.grp[g].tiles_begin) gi = g;
+  const Group& G = a.grp[gi];
+  const int tile_m = tile_mg - G.tiles_begin;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int M = G.M;
+  const int k_begin = split * a.k_per_split;
+  const int k_end = min(G.K, k_begin + a.k_per_split);
+  const int nchunks = k_end > k_begin ? (k_end - k_begin + BKH - 1) / BKH : 0;
+  const rsrc_t ra_src = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rb_src = make_rsrc(a.B, a.b_bytes);
+
+  // ---------------- A rows (conv_gemm_bf16's geometry) --------------------------------------
+  const int oct = wave & 3, rgrp = wave >> 2;
+  const int src_h = (MODE == MODE_DGRAD) ? a.ho : a.h;
+  const int src_w = (MODE == MODE_DGRAD) ? a.wo : a.w;
+  int a_off[A_SL];
+  uint64_t a_msk[A_SL];
+#pragma unroll
+  for (int i = 0; i < A_SL; ++i) {
+    const int m = m0 + 64 * (rgrp + RG * i) + lane;
+    const bool okm = m < M;
+    const int mm = okm ? m : 0;
+    int b, yb, xb;
+    if (MODE == MODE_FWD) {
+      const int hw = a.ho * a.wo;
+      b = mm / hw;
+      const int rem = mm - b * hw;
+      const int oy = rem / a.wo, ox = rem - oy * a.wo;
+      yb = oy * a.stride - a.pt;
+      xb = ox * a.stride - a.pl;
+    } else if (a.phase) {
+      const int hw = G.hc * G.wc;
+      b = mm / hw;
+      const int rem = mm - b * hw;
+      const int u = rem / G.wc, v = rem - u * G.wc;
+      yb = (2 * u + G.ry + a.pt - G.r0) >> 1;
+      xb = (2 * v + G.rx + a.pl - G.s0) >> 1;
+    } else {
+      const int hw = a.h * a.w;
+      b = mm / hw;
+      const int rem = mm - b * hw;
+      const int iy = rem / a.w, ix = rem - iy * a.w;
+      yb = iy + a.pt;
+      xb = ix + a.pl;
+    }
+    a_off[i] = (int)(((int64_t)(b * src_h + yb) * src_w + xb) * a.lda * 4);
+    uint64_t msk = 0;
+    if (okm) {
+      uint64_t colmask = 0;
+      for (int ts = 0; ts < G.ns; ++ts) {
+        const int sx = (MODE == MODE_FWD) ? xb + ts : xb - ts;
+        if ((unsigned)sx < (unsigned)src_w) colmask |= (uint64_t)1 << ts;
+      }
+      int t = 0;
+      for (int tr = 0; t < G.ntaps; ++tr, t += G.ns) {
+        const int sy = (MODE == MODE_FWD) ? yb + tr : yb - tr;
+        if ((unsigned)sy < (unsigned)src_h) msk |= colmask << t;
+      }
+      if (G.ntaps < 64) msk &= ((uint64_t)1 << G.ntaps) - 1;
+    }
+    a_msk[i] = msk;
+  }
+  // two wave-uniform tap walkers: channel quads 2 oct and 2 oct + 1 of the chunk
+  int ks_t[2], ks_tr[2], ks_ts[2], ks_ci[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k0 = k_begin + oct * 8 + 4 * h;
+    ks_t[h] = k0 / a.kc;
+    ks_ci[h] = k0 - ks_t[h] * a.kc;
+    ks_tr[h] = ks_t[h] / G.ns;
+    ks_ts[h] = ks_t[h] - ks_tr[h] * G.ns;
+  }
+  const int sgn = MODE == MODE_FWD ? 1 : -1;
+  const int tap_step = sgn * src_w * a.lda * 4;
+  float4 ra[A_SL][2];
+  auto load_a = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool tap_ok = ks_t[h] < G.ntaps;
+      const int koff = ks_tr[h] * tap_step + sgn * ks_ts[h] * a.lda * 4 + ks_ci[h] * 4;
+#pragma unroll
+      for (int i = 0; i < A_SL; ++i) {
+        const bool ok = tap_ok && ((a_msk[i] >> ks_t[h]) & 1);
+        ra[i][h] = bload4(ra_src, ok ? (uint32_t)(a_off[i] + koff) : kOOB);
+      }
+    }
+  };
+  auto advance_a = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      ks_ci[h] += BKH;
+      while (ks_ci[h] >= a.kc) {
+        ks_ci[h] -= a.kc;
+        ++ks_t[h];
+        if (++ks_ts[h] >= G.ns) {
+          ks_ts[h] = 0;
+          ++ks_tr[h];
+        }
+      }
+    }
+  };
+  auto store_a = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_SL; ++i) {
+      uint2 h0, m0v, l0, h1, m1, l1;
+      split3x4(ra[i][0], h0, m0v, l0);
+      split3x4(ra[i][1], h1, m1, l1);
+      const int row = 64 * (rgrp + RG * i) + lane;
+      uint4* img = smem + buf * A_U4 + row * 4 + (oct ^ x3_sw(row));
+      img[0] = make_uint4(h0.x, h0.y, h1.x, h1.y);
+      img[BM * 4] = make_uint4(m0v.x, m0v.y, m1.x, m1.y);
+      img[2 * BM * 4] = make_uint4(l0.x, l0.y, l1.x, l1.y);
+    }
+  };
+  // ---------------- B (x3 weight planes [plane][n][k]) by LDS DMA ----------------------------
+  uint32_t bd_off[BDW];
+  int bd_lds[BDW];
+#pragma unroll
+  for (int k = 0; k < BDW; ++k) {
+    const int g = wave + NW * k;
+    const int p = g / (BN / 16), rbk = g % (BN / 16);
+    const int n = rbk * 16 + (lane >> 2), o = (lane & 3) ^ x3_sw(lane >> 2);
+    bd_off[k] = g < BDI && n0 + n < a.nb
+                    ? (uint32_t)(((int64_t)p * a.b_plane + (int64_t)(n0 + n) * a.ldb + G.b_off +
+                                  8 * o) * 2)
+                    : kOOB;
+    bd_lds[k] = g < BDI ? (p * BN + rbk * 16) * 4 : -1;
+  }
+  auto dma_b = [&](int buf, int bk) {
+#pragma unroll
+    for (int k = 0; k < BDW; ++k)
+      if (BDI % NW == 0 || bd_lds[k] >= 0)
+        dma16_to_lds(rb_src, smem + 2 * A_U4 + buf * B_U4 + bd_lds[k], bd_off[k], bk * 2);
+  };
+
+  // ---------------- main loop --------------------------------------------------------------
+  f32x4 acc[SM][SN];
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+#pragma unroll
+    for (int j = 0; j < SN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+  const int wm0 = (wave / WAVES_N) * WM;
+  const int wn0 = (wave % WAVES_N) * WN;
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int frag = l16 * 4 + (lq ^ x3_sw(l16));   // rows 16-aligned + l16: swizzle of l16
+  int b_k = k_begin;
+  if (nchunks > 0) {
+    load_a();
+    dma_b(0, b_k);
+    store_a(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      advance_a();
+      b_k += BKH;
+      load_a();
+      dma_b(buf ^ 1, b_k);
+    }
+    const uint4* As = smem + buf * A_U4;
+    const uint4* Bs = smem + 2 * A_U4 + buf * B_U4;
+    bf16x8 av[NP][SM], bv[NP][SN];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+        av[p][i] = __builtin_bit_cast(bf16x8, As[p * BM * 4 + (wm0 + 16 * i) * 4 + frag]);
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+        bv[p][j] = __builtin_bit_cast(bf16x8, Bs[p * BN * 4 + (wn0 + 16 * j) * 4 + frag]);
+    }
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        f32x4 x = acc[i][j];
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+      }
+    if (more) store_a(buf ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own B DMA landed
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------------------------------------------------------
+  const int row_base = G.tiles_begin * BM;
+  float* S = a.slab + (int64_t)split * a.split_stride;
+  if (a.vec_ep) {
+    // the wave's WM x WN block through a private LDS image, back as float4 rows
+    float* E = reinterpret_cast<float*>(smem) + wave * WM * WN;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[(16 * i + 4 * lq + r) * WN + 16 * j + l16] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int LPR = WN / 4, RPI = 64 / LPR;
+    const int c4 = lane % LPR, rr = lane / LPR;
+    const int n = n0 + wn0 + 4 * c4;
+#pragma unroll
+    for (int q = 0; q < WM / RPI; ++q) {
+      const int ml = q * RPI + rr;
+      const int m = m0 + wm0 + ml;
+      const float4 v = *reinterpret_cast<const float4*>(&E[ml * WN + 4 * c4]);
+      if (m >= M || n >= a.N) continue;
+      if (a.splits > 1)
+        *reinterpret_cast<float4*>(&S[(int64_t)(row_base + m) * a.slab_ld + n]) = v;
+      else
+        epilogue_store4<MODE>(a, 0, out_row(a, G, m), n, v);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < SN; ++j) {
+    const int n = n0 + wn0 + 16 * j + l16;
+    if (n >= a.N) continue;
+    float bias = 0.f, scale = 1.f, shift = 0.f;
+    if (a.splits == 1) column_params<MODE>(a, n, bias, scale, shift);
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm0 + 16 * i + 4 * lq + r;
+        if (m >= M) continue;
+        if (a.splits > 1) {
+          S[(int64_t)(row_base + m) * a.slab_ld + n] = acc[i][j][r];
+        } else {
+          const int64_t row = out_row(a, G, m);
+          epilogue_store<MODE>(a, row, n, acc[i][j][r], bias, scale, shift,
+                               epilogue_aux<MODE>(a, row, n));
+        }
+      }
   }
 }
 
@@ -2475,6 +2761,263 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
   }
 }
 
+// ---- fp32 weight gradient on the split-bf16 MFMA: implicit GEMM (other shapes) ------------
+// C[m = (tap, ci)][n = co] = sum over output pixels k of x(pix(k, tap))[ci] . dy(k)[co] for
+// the stem, the stride-2 block convs and the projections: conv_wgrad_bf16's staging (slots of
+// 4 channels x 8 pixels, coalesced across the channel quads of a pixel, written transposed as
+// [channel row][pixel octet] images) with every value cut into the hi / mid / lo bf16 planes
+// and six v_mfma_f32_16x16x32_bf16 per fragment pair.  LDS rows are four octets; octet o of
+// row r sits in slot o ^ [0, 2, 3, 1][(r >> 2) & 3], which keeps the 16x16x32 fragment reads
+// conflict-free and the staging stores (8 lanes = rows 4 apart) at 2-way.  Double-buffered,
+// one barrier per 32-pixel chunk; split-K slabs + the bias column sums, as the other wgrads.
+__device__ __forceinline__ int wx3_sw(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_wgrad_x3(GemmArgs a) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N, NW = NT / 64, NP = 3;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, SM = WM / 16, SN = WN / 16;
+  static_assert(SM >= 1 && SN >= 1 && WM % 16 == 0 && WN % 16 == 0, "tile");
+  constexpr int NSLOT = BM + BN, SPT = (NSLOT + NT - 1) / NT;
+  constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
+  static_assert(NW * WM * WN * 4 <= 2 * (A_U4 + B_U4) * 16 && 4 * BN * 4 <= A_U4 * 16,
+                "epilogue / column-sum images fit LDS");
+  __shared__ uint4 smem[2 * (A_U4 + B_U4)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_n = tile % a.n_tiles;
+  const int tile_m = tile / a.n_tiles;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int M = a.M;
+  const int k_begin = split * a.k_per_split;
+  const int k_end = min(a.K, k_begin + a.k_per_split);
+  const int nchunks = k_end > k_begin ? (k_end - k_begin + BKH - 1) / BKH : 0;
+  const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
+  const bool do_colsum = a.colsum && tile_m == 0;
+
+  // ---- per-slot fixed state (slot = channel quad x pixel octet of the 32-pixel chunk)
+  bool s_isa[SPT], s_ok[SPT];
+  int s_row[SPT], s_oc[SPT], s_col[SPT], s_r[SPT], s_s[SPT];
+  int s_b[SPT], s_oy[SPT], s_ox[SPT];
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int sl = tid + NT * j;
+    const bool live = sl < NSLOT;
+    const bool isa = sl < BM;
+    const int q = isa ? sl : sl - BM;
+    const int nq = isa ? BM / 4 : BN / 4;
+    const int rq = q % nq, oc = q / nq;
+    s_isa[j] = isa;
+    s_row[j] = 4 * rq;
+    s_oc[j] = live ? oc : -1;
+    if (isa) {
+      const int m = m0 + 4 * rq;
+      s_ok[j] = live && m < M;
+      const int mm = m < M ? m : 0;
+      const int tap = mm / a.kc;
+      s_col[j] = mm - tap * a.kc;
+      s_r[j] = tap / a.kw;
+      s_s[j] = tap - s_r[j] * a.kw;
+    } else {
+      const int n = n0 + 4 * rq;
+      s_ok[j] = live && n < a.nb;
+      s_col[j] = n;
+      s_r[j] = s_s[j] = 0;
+    }
+    const int k = k_begin + 8 * oc;
+    const int hw = a.ho * a.wo;
+    const int kk = k < a.K ? k : 0;
+    s_b[j] = kk / hw;
+    const int rem = kk - s_b[j] * hw;
+    s_oy[j] = rem / a.wo;
+    s_ox[j] = rem - s_oy[j] * a.wo;
+  }
+  float4 stg[SPT][8];
+  float4 colacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int kc0 = k_begin;
+  auto load = [&]() {
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      int b = s_b[j], oy = s_oy[j], ox = s_ox[j];
+      const int kbase = kc0 + 8 * s_oc[j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool okk = s_ok[j] && s_oc[j] >= 0 && kbase + e < k_end;
+        uint32_t off = kOOB;
+        if (s_isa[j]) {
+          const int sy = oy * a.stride - a.pt + s_r[j], sx = ox * a.stride - a.pl + s_s[j];
+          if (okk && (unsigned)sy < (unsigned)a.h && (unsigned)sx < (unsigned)a.w)
+            off = (uint32_t)((((b * a.h + sy) * a.w + sx) * a.lda + s_col[j]) * 4);
+          stg[j][e] = bload4(rx, off);
+        } else {
+          if (okk) off = (uint32_t)(((kbase + e) * a.ldb + s_col[j]) * 4);
+          stg[j][e] = bload4(rd, off);
+        }
+        if (++ox >= a.wo) {
+          ox = 0;
+          if (++oy >= a.ho) {
+            oy = 0;
+            ++b;
+          }
+        }
+      }
+    }
+  };
+  auto advance = [&]() {
+    kc0 += BKH;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      s_ox[j] += BKH;
+      while (s_ox[j] >= a.wo) {
+        s_ox[j] -= a.wo;
+        if (++s_oy[j] >= a.ho) {
+          s_oy[j] = 0;
+          ++s_b[j];
+        }
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      if (s_oc[j] < 0) continue;
+      const int rows = s_isa[j] ? BM : BN;
+      uint4* img = smem + (s_isa[j] ? buf * A_U4 : 2 * A_U4 + buf * B_U4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float v8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v8[e] = (&stg[j][e].x)[c];
+        bf16x8 h, m, l;
+        split3x8(v8, h, m, l);
+        const int row = s_row[j] + c;
+        const int idx = row * 4 + (s_oc[j] ^ wx3_sw(row));
+        img[idx] = __builtin_bit_cast(uint4, h);
+        img[rows * 4 + idx] = __builtin_bit_cast(uint4, m);
+        img[2 * rows * 4 + idx] = __builtin_bit_cast(uint4, l);
+      }
+      if (!s_isa[j] && do_colsum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) add4(colacc, stg[j][e]);
+      }
+    }
+  };
+
+  f32x4 acc[SM][SN];
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+#pragma unroll
+    for (int j = 0; j < SN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+  const int wm0 = (wave / WAVES_N) * WM;
+  const int wn0 = (wave % WAVES_N) * WN;
+  const int l16 = lane & 15, lq = lane >> 4;
+  const int frag = l16 * 4 + (lq ^ wx3_sw(l16));   // rows 16-aligned + l16
+
+  if (nchunks > 0) {
+    load();
+    store(0);
+  }
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      advance();
+      load();
+    }
+    const uint4* As = smem + buf * A_U4;
+    const uint4* Bs = smem + 2 * A_U4 + buf * B_U4;
+    bf16x8 av[NP][SM], bv[NP][SN];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+        av[p][i] = __builtin_bit_cast(bf16x8, As[p * BM * 4 + (wm0 + 16 * i) * 4 + frag]);
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+        bv[p][j] = __builtin_bit_cast(bf16x8, Bs[p * BN * 4 + (wn0 + 16 * j) * 4 + frag]);
+    }
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        f32x4 x = acc[i][j];
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+      }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- raw partial sums into this K slice's slab (+ bias column sums in row M)
+  float* S = a.slab + (int64_t)split * a.split_stride;
+  if (do_colsum) {
+    // B-slot threads hold 4 columns x their pixel octet: 4 octets per column quad, summed in a
+    // fixed order (the loop's last barrier freed the images)
+    float* csum = reinterpret_cast<float*>(smem);      // [4 octets][BN]
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      if (!s_isa[j] && s_oc[j] >= 0) {
+        const int cq = s_row[j];
+        csum[s_oc[j] * BN + cq] = colacc.x;
+        csum[s_oc[j] * BN + cq + 1] = colacc.y;
+        csum[s_oc[j] * BN + cq + 2] = colacc.z;
+        csum[s_oc[j] * BN + cq + 3] = colacc.w;
+      }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N)
+      S[(int64_t)M * a.slab_ld + n0 + tid] =
+          csum[tid] + csum[BN + tid] + csum[2 * BN + tid] + csum[3 * BN + tid];
+    __syncthreads();
+  }
+  if (a.vec_ep) {
+    float* E = reinterpret_cast<float*>(smem) + wave * WM * WN;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[(16 * i + 4 * lq + r) * WN + 16 * j + l16] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int LPR = WN / 4, RPI = 64 / LPR;
+    const int c4 = lane % LPR, rr = lane / LPR;
+    const int n = n0 + wn0 + 4 * c4;
+#pragma unroll
+    for (int q = 0; q < WM / RPI; ++q) {
+      const int ml = q * RPI + rr, m = m0 + wm0 + ml;
+      const float4 v = *reinterpret_cast<const float4*>(&E[ml * WN + 4 * c4]);
+      if (m < M && n < a.N) *reinterpret_cast<float4*>(&S[(int64_t)m * a.slab_ld + n]) = v;
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < SN; ++j) {
+    const int n = n0 + wn0 + 16 * j + l16;
+    if (n >= a.N) continue;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm0 + 16 * i + 4 * lq + r;
+        if (m < M) S[(int64_t)m * a.slab_ld + n] = acc[i][j][r];
+      }
+  }
+}
+
 // ---- fp32 weight gradient, 3x3 stride 1: all 9 taps from one staged halo ----------------
 // dW[r][s][ci][co] = sum_p x(p + (r, s) - pad)[ci] . dy(p)[co] on v_mfma_f32_32x32x2_f32, the
 // fp32 counterpart of conv_wgrad_tile_bf16: a workgroup owns CIB x COB channels for all 9
@@ -3181,6 +3724,9 @@ static int g_wgx3b = 1;
 // MI = 2 halves the dy loads and splits per MFMA and measured the same (dec3.c1 0.516 vs
 // 0.517 ms): the split VALU is not what bounds the kernel.
 static int g_wgx3b_mi = 1;
+// of_set_tuning key 6: the other shapes' fp32 weight gradient on the split-bf16 implicit GEMM
+// (conv_wgrad_x3, 1) or on the fp32 MFMA GEMM (0).
+static int g_wgx3_gemm = 1;
 bool vec_ep_ok(const GemmArgs& a) {
   if (!g_vec_ep || a.N % 4) return false;
   if (a.slab && !(a.slab_ld % 4 == 0 && a.split_stride % 4 == 0 && al16(a.slab))) return false;
@@ -3372,6 +3918,59 @@ int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
   return launch_splitk_epilogue<MODE>(a, s);
 }
 
+// fp32 implicit GEMM on the split-bf16 kernel (conv_gemm_x3, every non-3x3-stride-1 shape):
+// BN 128 (8 waves of 32 x 64) for N > 64, else 256 x 64 tiles; one workgroup per CU, so K
+// splits come from the cost model of tile_args (rounds of 256 workgroups x (chunks per slice
+// + 1) + half a chunk per slice and tile round for the slab pass).  Timing kinds 160 + 8 mode
+// + (0: 128 x 128, 1: 256 x 64).
+void gemm_x3_plan(GemmArgs& a) {
+  const int bm = a.N > 64 ? 128 : 256, bn = a.N > 64 ? 128 : 64;
+  int tiles = 0, tiles_all = 0, kmax = 0;
+  for (int g = 0; g < a.ngroups; ++g) {
+    Group& G = a.grp[g];
+    if (G.m_tiles) G.m_tiles = (int)cdiv(G.M, bm);   // (phase groups skipped in place stay 0)
+    G.tiles_begin = tiles;
+    tiles += G.m_tiles;
+    tiles_all += (int)cdiv(G.M, bm);
+    kmax = std::max(kmax, G.K);
+  }
+  a.bm = bm;
+  a.n_tiles = (int)cdiv(a.N, bn);
+  a.tiles_total = tiles * a.n_tiles;
+  // the split is planned on the full grid, so of_conv2d_dgrad_x3_workspace() covers the
+  // in-place form (fewer tiles, fewer slab rows) too
+  const int64_t plan_tiles = (int64_t)tiles_all * a.n_tiles;
+  const int chunks = (int)cdiv(kmax, BKH);
+  int best = 1;
+  double best_cost = 1e30;
+  for (int sp = 1; sp <= std::min(8, chunks); ++sp) {
+    const int per = (int)cdiv(chunks, sp);
+    if (cdiv(chunks, per) != sp) continue;
+    const int64_t w = plan_tiles * sp;
+    const double cost = (double)cdiv(w, kCUs) * (per + 1.0) +
+                        (sp > 1 ? 0.5 * sp * plan_tiles / (double)kCUs : 0.0);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = sp;
+    }
+  }
+  a.k_per_split = (int)cdiv(chunks, best) * BKH;
+  a.splits = (int)cdiv(kmax, a.k_per_split);
+}
+
+template <int MODE>
+int launch_gemm_x3(const GemmArgs& a, hipStream_t s, double flops) {
+  const int cfg = a.N > 64 ? 0 : 1;
+  dim3 grid(a.tiles_total * a.splits), block(512);
+  if (timing_on()) timing_begin(s);
+  if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3<128, 128, 4, 2, MODE>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((conv_gemm_x3<256, 64, 8, 1, MODE>), grid, block, 0, s, a);
+  if (timing_on()) timing_end(s, 160 + MODE * 8 + cfg, flops);
+  int st = check_launch("conv_gemm_x3");
+  if (st || a.splits == 1) return st;
+  return launch_splitk_epilogue<MODE>(a, s);
+}
+
 // bf16 3x3 stride-1 wgrad on conv_wgrad_tile_bf16: block channel tiles (CIB x COB).
 // bf16: every 3x3 stride-1 layer.  fp32 (MFMA-bound either way): where the implicit GEMM
 // loses to its N = 64 tiles or to many small split-K slabs (measured, tools/conv_bench.py):
@@ -3417,6 +4016,17 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
     int splits = std::max(1, std::min(T, kCUs / chan_tiles));
     p.k_per_split = (int)cdiv(T, splits);
     p.splits = (int)cdiv(T, p.k_per_split);
+    return p;
+  }
+  if (x3 && !narrow_ok(d)) {
+    // conv_wgrad_x3: 128 x (128 | 64) tiles, one workgroup per CU; K = output pixels in
+    // 32-pixel chunks, split to fill the CUs with at least 8 chunks per slice
+    const int K = d->n * d->ho * d->wo;
+    const int tiles = (int)(cdiv(p.M, 128) * cdiv(d->cout, d->cout > 64 ? 128 : 64));
+    int splits = std::max(1, kCUs / tiles);
+    splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * BKH)));
+    p.k_per_split = (int)round_up(cdiv(K, splits), BKH);
+    p.splits = (int)cdiv(K, p.k_per_split);
     return p;
   }
   if (wgt_ok(d, bf16)) {
@@ -3543,6 +4153,7 @@ int of_set_tuning(int key, int value) {
   if (key == 3 && (value == 0 || value == 1)) { g_vec_ep = value; return OF_OK; }
   if (key == 4 && value >= 0 && value <= 2) { g_wgx3b = value; return OF_OK; }
   if (key == 5 && (value == 1 || value == 2)) { g_wgx3b_mi = value; return OF_OK; }
+  if (key == 6 && (value == 0 || value == 1)) { g_wgx3_gemm = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -3630,7 +4241,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   int st = validate(d);
   if (st) return st;
   const bool bf16 = prec == 1, x3 = prec == 2;
-  OF_CHECK_ARG(!x3 || tile_ok(d), "conv fwd x3: 3x3 stride-1 convolutions only");
+  OF_CHECK_ARG(!x3 || !narrow_ok(d), "conv fwd x3: the Cout <= 4 layers take the fp32 kernels");
   OF_CHECK_ARG(x && w_fwd && y, "conv fwd: NULL pointer");
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv fwd: ldx");
   OF_CHECK_ARG(ldy >= d->cout, "conv fwd: ldy");
@@ -3648,8 +4259,9 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   }
   Geo g = geo(d);
   const bool tile = (bf16 || x3) && tile_ok(d);
-  GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3) : fwd_args(d, g, bf16);
-  attach_slab(a, workspace, ws_bytes, tile ? 1 : bf16 ? BKH : BK);
+  GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3) : fwd_args(d, g, bf16 || x3);
+  if (x3 && !tile) gemm_x3_plan(a);
+  attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
   a.A = x;
   a.lda = ldx;
   a.a_bytes = (int64_t)d->n * d->h * d->w * ldx * 4;
@@ -3675,7 +4287,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   a.vec_ep = vec_ep_ok(a);
-  st = x3     ? launch_tile_x3<MODE_FWD>(a, s, flops)
+  st = x3     ? (tile ? launch_tile_x3<MODE_FWD>(a, s, flops) : launch_gemm_x3<MODE_FWD>(a, s, flops))
        : tile ? launch_tile_bf16<MODE_FWD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops)
               : launch_gemm<MODE_FWD>(a, s, flops);
@@ -3710,7 +4322,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   if (st) return st;
   Geo g = geo(d);
   const bool bf16 = prec == 1, x3 = prec == 2;
-  OF_CHECK_ARG(!x3 || tile_ok(d), "conv dgrad x3: 3x3 stride-1 convolutions only");
+  OF_CHECK_ARG(!x3 || !narrow_ok(d), "conv dgrad x3: the Cout <= 4 layers take the fp32 kernels");
   OF_CHECK_ARG(dy && w_bwd && dx, "conv dgrad: NULL pointer");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv dgrad: lddy (>= round_up(cout,4))");
   OF_CHECK_ARG(lddx >= d->cin_p, "conv dgrad: lddx");
@@ -3730,9 +4342,10 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   }
   const bool tile = (bf16 || x3) && tile_ok(d);
   const bool in_place = add && add == dx && ld_add == lddx;
-  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3) : dgrad_args(d, g, bf16, in_place);
+  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3) : dgrad_args(d, g, bf16 || x3, in_place);
+  if (x3 && !tile) gemm_x3_plan(a);
   if (a.tiles_total == 0) return OF_OK;                 // every output already final
-  attach_slab(a, workspace, ws_bytes, tile ? 1 : bf16 ? BKH : BK);
+  attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
   a.A = dy;
   a.lda = lddy;
   a.a_bytes = (int64_t)d->n * d->ho * d->wo * lddy * 4;
@@ -3752,7 +4365,8 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   a.vec_ep = vec_ep_ok(a);
-  st = x3     ? launch_tile_x3<MODE_DGRAD>(a, s, flops)
+  st = x3     ? (tile ? launch_tile_x3<MODE_DGRAD>(a, s, flops)
+                     : launch_gemm_x3<MODE_DGRAD>(a, s, flops))
        : tile ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops)
               : launch_gemm<MODE_DGRAD>(a, s, flops);
@@ -3800,13 +4414,19 @@ int of_conv_pack_weights_x3(const of_conv_desc* d, const float* w_hwio, void* w3
 }
 
 size_t of_conv2d_fwd_x3_workspace(const of_conv_desc* d) {
-  if (validate(d) != OF_OK || !tile_ok(d)) return 0;
-  return fd_workspace(tile_args(d, geo(d), MODE_FWD, true));
+  if (validate(d) != OF_OK || narrow_ok(d)) return 0;
+  if (tile_ok(d)) return fd_workspace(tile_args(d, geo(d), MODE_FWD, true));
+  GemmArgs a = fwd_args(d, geo(d), true);
+  gemm_x3_plan(a);
+  return fd_workspace(a);
 }
 
 size_t of_conv2d_dgrad_x3_workspace(const of_conv_desc* d) {
-  if (validate(d) != OF_OK || !tile_ok(d)) return 0;
-  return fd_workspace(tile_args(d, geo(d), MODE_DGRAD, true));
+  if (validate(d) != OF_OK || narrow_ok(d)) return 0;
+  if (tile_ok(d)) return fd_workspace(tile_args(d, geo(d), MODE_DGRAD, true));
+  GemmArgs a = dgrad_args(d, geo(d), true);
+  gemm_x3_plan(a);
+  return fd_workspace(a);
 }
 
 int of_conv2d_fwd_x3(const of_conv_desc* d, const float* x, int ldx, const void* w3_fwd,
@@ -3850,7 +4470,7 @@ size_t of_conv2d_wgrad_bf16_workspace(const of_conv_desc* d) {
 size_t of_conv2d_wgrad_x3_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
   if (narrow_ok(d)) return narrow_wgrad_ws(d);
-  WgradPlan p = wgrad_plan(d, false, true);
+  WgradPlan p = wgrad_plan(d, false, wgx3_ok(d) || g_wgx3_gemm);
   return (size_t)p.splits * p.split_stride * sizeof(float);
 }
 
@@ -3862,6 +4482,7 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   if (st) return st;
   Geo g = geo(d);
   const bool bf16 = prec == 1, x3 = prec == 2 && wgx3_ok(d);
+  const bool x3g = prec == 2 && !x3 && g_wgx3_gemm;   // conv_wgrad_x3 (other shapes)
   OF_CHECK_ARG(x && dy && dw && workspace, "conv wgrad: NULL pointer");
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv wgrad: lddy");
@@ -3873,7 +4494,7 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     if (timing_on()) timing_end(s, MODE_WGRAD * 8 + KIND_NARROW, conv_flops(d));
     return st;
   }
-  WgradPlan p = wgrad_plan(d, bf16, x3);
+  WgradPlan p = wgrad_plan(d, bf16, x3 || x3g);
   OF_CHECK_ARG(ws_bytes >= (size_t)p.splits * p.split_stride * sizeof(float),
                "conv wgrad: workspace too small");
   GemmArgs a = base_args(d);
@@ -3927,6 +4548,16 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     // timing kinds 144-147: the 3-tap form, 148-151: conv_wgrad_tile_x3b (bench.py X3_WGT)
     if (timing_on()) timing_end(s, 128 + MODE_WGRAD * 8 + cfg + (x3b ? 4 : 0), flops);
     st = check_launch("conv_wgrad_tile_x3");
+  } else if (x3g) {
+    const int bn = d->cout > 64 ? 128 : 64;
+    a.n_tiles = (int)cdiv(d->cout, bn);
+    a.tiles_total = (int)cdiv(a.M, 128) * a.n_tiles;
+    dim3 grid(a.tiles_total * a.splits), block(512);
+    if (timing_on()) timing_begin(s);
+    if (bn == 128) hipLaunchKernelGGL((conv_wgrad_x3<128, 128, 4, 2>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_x3<128, 64, 4, 2>), grid, block, 0, s, a);
+    if (timing_on()) timing_end(s, 160 + MODE_WGRAD * 8 + (bn == 128 ? 0 : 1), flops);
+    st = check_launch("conv_wgrad_x3");
   } else if (wgt_ok(d, bf16)) {
     int cib, cob;
     wgt_blocks(d, cib, cob);

@@ -145,6 +145,13 @@ def grad_target(param: torch.Tensor):
 # tests/test_gpu_kernels.py::test_conv_x3_accuracy measure it against fp64).
 # OFLOW_F32_SPLIT=0 keeps every fp32 layer on the fp32 MFMA kernels.
 F32_SPLIT = os.environ.get("OFLOW_F32_SPLIT", "1") == "1"
+# With F32_SPLIT, the other GEMM-path fp32 layers with >= 16 input channels (the stride-2
+# block convs and the 1x1 projections) take the split-bf16 implicit GEMMs (conv_gemm_x3,
+# conv_wgrad_x3) too: 10-25 % faster per pass than the fp32 MFMA GEMM.  The stem (3 input
+# channels, K = 49 taps x 4) measured 9 % / 37 % slower there (fwd / wgrad) and stays fp32.
+# OFLOW_X3_GEMM=0 keeps them all on the fp32 MFMA kernels.
+X3_GEMM = os.environ.get("OFLOW_X3_GEMM", "1") == "1"
+X3_GEMM_MIN_CIN = 16
 
 class ConvLayer:
     """One ``layers.Conv2D(filters, k, strides, padding='same')`` (model.py:12,104-114) with an
@@ -191,11 +198,13 @@ class ConvLayer:
 
     def mode(self, d: ConvDesc = None) -> int:
         """Kernel family of fwd/dgrad: 0 fp32 MFMA, 1 bf16 MFMA, 2 fp32 on the split-bf16
-        halo-tile kernels (fp32 precision, 3x3 stride-1 GEMM-path layers, F32_SPLIT on)."""
+        kernels (fp32 precision, GEMM-path layers, F32_SPLIT on: the halo tiles for 3x3
+        stride 1, the implicit GEMM conv_gemm_x3 for the other shapes when X3_GEMM)."""
         if self._mode is None:
+            tile = self.kh == 3 and self.kw == 3 and self.stride == 1
             self._mode = (1 if self.bf16(d) else
-                          2 if (self.f32_split and self.precision == "fp32" and self.kh == 3 and
-                                self.kw == 3 and self.stride == 1 and
+                          2 if (self.f32_split and self.precision == "fp32" and
+                                (tile or (X3_GEMM and self.cin_p >= X3_GEMM_MIN_CIN)) and
                                 _lib.lib().of_conv_path(C.byref(d or self.desc(1, 16, 16))) == 0)
                           else 0)
         return self._mode

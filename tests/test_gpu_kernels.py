@@ -217,6 +217,62 @@ def test_conv_x3_accuracy(n, h, w, cin, cout):
         assert e3 < 5e-6, errs[True]
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout,k,s", [(4, 64, 96, 4, 64, 7, 2),   # stem (cin 3 -> 4)
+                                               (4, 48, 64, 64, 128, 3, 2),   # res3_0 conv_a
+                                               (4, 24, 32, 128, 256, 3, 2),  # res4_0 conv_a
+                                               (4, 48, 64, 64, 128, 1, 2)])  # projection
+def test_conv_gemm_x3_accuracy(n, h, w, cin, cout, k, s, monkeypatch):
+    """The split-bf16 implicit GEMMs (conv_gemm_x3 fwd / dgrad with phase groups,
+    conv_wgrad_x3: stem, stride-2 and 1x1 layers) are as accurate as the fp32 MFMA kernels:
+    against fp64, within 3x of the fp32 MFMA kernel's error and at the level of one fp32
+    rounding per product."""
+    import ctypes as C
+    ops = _ops()
+    monkeypatch.setattr(ops, "X3_GEMM_MIN_CIN", 0)   # the stem shape too (the model keeps it fp32)
+    from optical_flow_amd._lib import ACT_NONE, call
+    x = rng_tensor((n, h, w, cin), 91)
+    wt = rng_tensor((k, k, cin, cout), 92, scale=(2.0 / (k * k * cin)) ** 0.5)
+    errs = {}
+    for split in (False, True):
+        layer = ops.ConvLayer(dev(wt), dev(torch.zeros(cout)), stride=s, act=ACT_NONE, cin_p=cin,
+                              f32_split=split)
+        d = layer.desc(n, h, w)
+        assert layer.mode(d) == (2 if split else 0)
+        dy = rng_tensor((n, d.ho, d.wo, cout), 93)
+        pad = (d.pad_top, d.pad_left)
+        yref = R.conv2d_same(f64(x), f64(wt), None, s)
+        wf, wd = layer.packed(d)
+        fent, fws = layer.fwd_entry(d)
+        dent, dws = layer.dgrad_entry(d)
+        ws = torch.empty(max(fws, dws) // 4 + 4, device="cuda")
+        P, st = ops._ptr, ops._stream()
+        xd, dyd = dev(x), dev(dy)
+        y = torch.empty(n, d.ho, d.wo, cout, device="cuda")
+        dx = torch.empty(n, h, w, cin, device="cuda")
+        call(fent, C.byref(d), P(xd), cin, P(wf), P(layer.bias), None, None, None, None, 1e-3,
+             None, 0, ACT_NONE, 0.0, None, 0, P(y), cout, P(ws), fws, st)
+        e = [rel_inf(y, yref), rel_l2(y, yref)]
+        went, wws = layer.wgrad_entry(d)
+        wsw = torch.empty(wws // 4 + 4, device="cuda")
+        dw = torch.empty(k, k, cin, cout, device="cuda")
+        call(went, C.byref(d), P(xd), cin, P(dyd), cout, P(dw), None, 0, P(wsw), wws, st)
+        wo = f64(wt).requires_grad_(True)
+        (R.conv2d_same(f64(x), wo, None, s) * f64(dy)).sum().backward()
+        e += [rel_inf(dw, wo.grad), rel_l2(dw, wo.grad)]
+        if k < 7:
+            call(dent, C.byref(d), P(dyd), cout, P(wd), None, 0, ACT_NONE, 0.0, P(dx), cin, P(ws),
+                 dws, st)
+            xo = f64(x).requires_grad_(True)
+            (R.conv2d_same(xo, f64(wt), None, s) * f64(dy)).sum().backward()
+            e += [rel_inf(dx, xo.grad), rel_l2(dx, xo.grad)]
+        torch.cuda.synchronize()
+        errs[split] = e
+        assert pad is not None
+    for e3, e32 in zip(errs[True], errs[False]):
+        assert e3 < 3 * e32 + 1e-7, (errs[True], errs[False])
+        assert e3 < 5e-6, errs[True]
+
+
 @pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
     # kinds: 128 + 8 mode + cfg; wgrad 144 + cfg (3-tap form) / 148 + cfg (9-tap x3b form)
     ("tall128", 8, 128, 256, 128, 128, {128, 136, 148}),  # 8 x 32 tiles, BN 128 (1024 tiles)
@@ -395,7 +451,7 @@ def test_wgrad_x3_forms(n, h, w, cin, cout):
         assert rel_inf(db, dbref) < 5e-6, (key, rel_inf(db, dbref))
 
 
-@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("prec", ["f32", "bf16", "x3"])
 @pytest.mark.parametrize("n,h,w,cin,cout,k,s", [
     (2, 32, 48, 4, 64, 7, 2),      # stem: 256 x 64 tiles, split-K slabs
     (2, 16, 24, 64, 128, 3, 2),    # stride-2 block conv: dgrad phase groups
@@ -404,12 +460,13 @@ def test_wgrad_x3_forms(n, h, w, cin, cout):
     (1, 6, 10, 64, 36, 3, 1),      # 256 x 64 tiles, N not a tile multiple
     (2, 20, 45, 128, 128, 3, 1),   # bf16 halo tiles, ragged right edge
 ])
-def test_conv_gemm_vec_epilogue(n, h, w, cin, cout, k, s, prec):
-    """The fp32 / bf16 implicit-GEMM and bf16 halo-tile kernels' 16-byte epilogue
-    (transpose32) is bitwise identical to the per-element one: fwd (bias, BN, residual, z,
+def test_conv_gemm_vec_epilogue(n, h, w, cin, cout, k, s, prec, monkeypatch):
+    """The fp32 / bf16 / split-bf16 (x3) implicit-GEMM and the halo-tile kernels' 16-byte
+    epilogues are bitwise identical to the per-element one: fwd (bias, BN, residual, z,
     ReLU), dgrad (activation derivative; added gradient, in place), wgrad slabs + bias sums."""
     import ctypes as C
     ops = _ops()
+    monkeypatch.setattr(ops, "X3_GEMM_MIN_CIN", 0)   # the stem shape on conv_gemm_x3 too
     from optical_flow_amd import _lib
     from optical_flow_amd._lib import ACT_LEAKY, ACT_RELU, call
     lib = _lib.lib()
@@ -421,10 +478,10 @@ def test_conv_gemm_vec_epilogue(n, h, w, cin, cout, k, s, prec):
     if prec == "bf16":
         layer = ops.ConvLayer(wt, b, stride=s, act=ACT_RELU, cin_p=cin, precision="bf16")
     else:
-        layer = ops.ConvLayer(wt, b, stride=s, act=ACT_RELU, cin_p=cin, f32_split=False)
+        layer = ops.ConvLayer(wt, b, stride=s, act=ACT_RELU, cin_p=cin, f32_split=prec == "x3")
     d = layer.desc(n, h, w)
-    sfx = "_bf16" if prec == "bf16" else ""
-    assert layer.mode(d) == 0 or prec == "bf16"
+    sfx = {"bf16": "_bf16", "x3": "_x3", "f32": ""}[prec]
+    assert layer.mode(d) == {"f32": 0, "bf16": 1, "x3": 2}[prec]
     ho, wo = d.ho, d.wo
     coutp = (cout + 3) // 4 * 4
     res = dev(rng_tensor((n, ho, wo, cout), 68))
@@ -463,7 +520,13 @@ def test_conv_gemm_vec_epilogue(n, h, w, cin, cout, k, s, prec):
     for name, a1, a0 in zip(("y", "z", "dx", "dx_add", "dw", "db"), *outs):
         assert torch.equal(a1, a0), (name, (a1 - a0).abs().max().item())
     zref = R.conv2d_same(f64(x), f64(wt), f64(b), s)
-    assert rel_inf(outs[0][1], zref) < (2e-2 if prec == "bf16" else REL_TOL)
+    assert rel_inf(outs[0][1], zref) < {"bf16": 2e-2, "f32": REL_TOL, "x3": 5e-6}[prec]
+    if s == 1:
+        dxref = torch.nn.grad.conv2d_input((n, cin, h, w), f64(wt).permute(3, 2, 0, 1),
+                                           f64(dy[..., :cout]).permute(0, 3, 1, 2),
+                                           padding=k // 2)
+        assert rel_inf(outs[0][2], torch.where(f64(act_src) > 0, 1.0, 0.3) *
+                       dxref.permute(0, 2, 3, 1)) < {"bf16": 2e-2, "f32": REL_TOL, "x3": 5e-6}[prec]
 
 
 def test_conv_bf16_tall_fwd():
