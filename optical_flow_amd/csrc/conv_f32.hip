@@ -989,9 +989,7 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #ifndef X3_BDMA
 #define X3_BDMA 1
 #endif
-#ifndef X3_PRIO
-#define X3_PRIO 0
-#endif
+
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH = OF_TF_H>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES_N)) void conv_tile_bf16(GemmArgs a) {
@@ -1418,7 +1416,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
   }
   if constexpr (BDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (X3_PRIO && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // the later-dispatched half
   // Chunk loop with the 9 taps unrolled (fragment offsets are immediates).  Step (chunk, tap)
   // reads B buffer (chunk + tap) & 1 (9 steps per chunk) and fetches the next step's B; the
   // next chunk's halo is fetched at tap 0 and stored after tap 8.
