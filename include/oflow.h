@@ -308,7 +308,9 @@ int of_timing_enable(int on);
  * key 4 = the 9-tap split-bf16 weight gradient for Cout % 128 == 0 (1, default), for every
  * Cout (2) or never (0: the 3-tap form), key 5 = its wave shape, 16 MI input x 32 / MI output
  * channels (MI = 1 default, or 2), key 6 = the other shapes' fp32 weight gradient (stem,
- * stride 2, 1x1) on the split-bf16 implicit GEMM (1, default) or the fp32 MFMA GEMM (0). */
+ * stride 2, 1x1) on the split-bf16 implicit GEMM (1, default) or the fp32 MFMA GEMM (0),
+ * key 7 = the feature-warp backward with its scatter aggregated per tile in LDS (1, default)
+ * or with LDS aggregation of the clipped border corners only (0). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -60,6 +60,8 @@ __device__ __forceinline__ float4 bload_quad(rsrc_t r, bool ok, uint32_t off, in
                      bload1(r, ok && n > 3 ? off + 12 : kOOB));
 }
 
+extern int g_warp_win;   // of_set_tuning key 7 (flow_ops.hip: warp backward form)
+
 }  // namespace oflow
 
 #define OF_CHECK_ARG(cond, msg)                                   \

@@ -4145,6 +4145,7 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
 }
 
 int of_set_tuning(int key, int value) {
+  if (key == 7 && (value == 0 || value == 1)) { g_warp_win = value; return OF_OK; }
   if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }
   if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
   if (key == 3 && (value == 0 || value == 1)) { g_vec_ep = value; return OF_OK; }

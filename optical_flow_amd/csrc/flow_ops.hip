@@ -573,6 +573,209 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
   }
 }
 
+// Backward with the scatter of a tile turned into a gather (grid + flow, c % 64 == 0).
+// Smooth flows send the 4 corners of an 8 x 8 output tile onto a small destination window
+// (about 9 x 9 pixels for sub-pixel flows; a clipped tile onto a strip of the border).  The
+// workgroup (one 64-channel pass) takes the window's bounding box, counting-sorts its 256
+// (pixel, corner) entries by destination (integer LDS atomics for the ranks, a wave scan for
+// the bucket starts), and each wave then sums the weighted dout rows of one destination's
+// entries in registers (lanes = 64 channels, dout rows staged in LDS) and adds the result to
+// global memory once: one 256-B atomic wave-instruction per touched destination, about 1.3 per
+// pixel instead of 4.  (Adding the corners into an LDS window with ds_add_f32 instead measured
+// slower than the 4 global adds: 524 vs 323 us at 192x256x64, float LDS atomics on repeated
+// addresses serialise.)  The flow gradient: lanes work 4 pixels x 16 channel quads (16-byte
+// corner loads, a DPP row reduction over the 16 lanes of a pixel).  A tile whose window
+// exceeds WG_CAP slots adds each corner's row straight to global memory.
+constexpr int WG_T = 8, WG_CAP = 1024, WG_NT = 256;
+int g_warp_win = 1;   // of_set_tuning key 7: warp_bwd_gather (1) or warp_bwd_agg (0)
+
+__device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes of a DPP row
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x122, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xF, 0xF, false));
+  return v;                                              // row_ror 8, 4, 2, 1
+}
+
+__global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict__ dout,
+                                                         const float* __restrict__ inp, int n,
+                                                         int h, int w, int c,
+                                                         const float* __restrict__ flow,
+                                                         float* __restrict__ dinp,
+                                                         float* __restrict__ dflow) {
+  constexpr int NP = WG_T * WG_T;                       // 64 pixels, 256 (pixel, corner) entries
+  __shared__ float dtile[NP * 64];                     // dout rows of this pass
+  __shared__ int2 ent[NP * 4];                         // entries sorted by destination
+  __shared__ int cnt[WG_CAP], st[WG_CAP];              // per destination slot: count, start
+  __shared__ int nzs[NP * 4];                          // touched slots
+  __shared__ int bb[5];                                // min/max row, min/max col, #touched
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_i = (h + WG_T - 1) / WG_T, tiles_j = (w + WG_T - 1) / WG_T;
+  const int passes = c / 64;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int cc = (bid % passes) * 64;
+  const int tile = bid / passes;
+  const int b = tile / (tiles_i * tiles_j);
+  const int rem = tile - b * tiles_i * tiles_j;
+  const int i0 = (rem / tiles_j) * WG_T, j0 = (rem % tiles_j) * WG_T;
+  const int64_t img = (int64_t)b * h * w;
+
+  // corners of pixel (i, j): rows {y0, y1} x columns {x0, x1} (the reference's transposed grid)
+  auto corners = [&](int i, int j, float2 f, int& y0, int& y1, int& x0, int& x1, float& a,
+                     float& bq) {
+    const float x = (float)i + f.x, y = (float)j + f.y;
+    const int xi = (int)fmaxf(fminf(floorf(x), 2147483520.f), -2147483520.f);
+    const int yi = (int)fmaxf(fminf(floorf(y), 2147483520.f), -2147483520.f);
+    x0 = min(max(xi, 0), w - 1), x1 = min(max(xi + 1, 0), w - 1);
+    y0 = min(max(yi, 0), h - 1), y1 = min(max(yi + 1, 0), h - 1);
+    a = (float)x1 - x, bq = (float)y1 - y;
+  };
+  auto tile_pix = [&](int p, bool& ok) {
+    const int i = i0 + p / WG_T, j = j0 + p % WG_T;
+    ok = i < h && j < w;
+    return img + (int64_t)min(i, h - 1) * w + min(j, w - 1);
+  };
+
+  // ---- flow-gradient lanes: pixel group pg of 4, channel quad q; corner loads issued first
+  constexpr int IT = NP / (4 * WG_NT / 64);
+  const int q = lane & 15, pg = lane >> 4;
+  bool okg[IT];
+  int64_t pixg[IT];
+  float ag[IT], bg[IT];
+  float4 pv[IT][4];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int pr = (it * (WG_NT / 64) + wave) * 4 + pg;
+    pixg[it] = tile_pix(pr, okg[it]);
+    const float2 f = okg[it] ? *reinterpret_cast<const float2*>(flow + 2 * pixg[it]) : make_float2(0.f, 0.f);
+    int y0, y1, x0, x1;
+    corners((int)(pixg[it] - img) / w, (int)((pixg[it] - img) % w), f, y0, y1, x0, x1, ag[it], bg[it]);
+    const int ys[4] = {y0, y1, y0, y1}, xs[4] = {x0, x0, x1, x1};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      pv[it][k] = *reinterpret_cast<const float4*>(inp + (img + (int64_t)ys[k] * w + xs[k]) * c + cc + 4 * q);
+  }
+  // ---- dout rows of the tile -> LDS
+#pragma unroll
+  for (int u = tid; u < NP * 16; u += WG_NT) {
+    const int p = u >> 4, qq = u & 15;
+    bool ok;
+    const int64_t px = tile_pix(p, ok);
+    const float4 g = ok ? *reinterpret_cast<const float4*>(dout + px * c + cc + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(&dtile[p * 64 + 4 * qq]) = g;
+  }
+  // ---- this thread's entry: pixel tid >> 2, corner tid & 3
+  const int pe = tid >> 2, ke = tid & 3;
+  bool oke;
+  const int64_t pxe = tile_pix(pe, oke);
+  int ye = 0, xe = 0;
+  float wte = 0.f;
+  {
+    const float2 f = oke ? *reinterpret_cast<const float2*>(flow + 2 * pxe) : make_float2(0.f, 0.f);
+    int y0, y1, x0, x1;
+    float a, bq;
+    corners((int)(pxe - img) / w, (int)((pxe - img) % w), f, y0, y1, x0, x1, a, bq);
+    ye = (ke & 1) ? y1 : y0;
+    xe = (ke & 2) ? x1 : x0;
+    wte = ((ke & 2) ? 1.f - a : a) * ((ke & 1) ? 1.f - bq : bq);
+  }
+  if (dinp) {
+    if (tid == 0) bb[0] = INT32_MAX, bb[1] = -1, bb[2] = INT32_MAX, bb[3] = -1;
+    __syncthreads();
+    int v0 = oke ? ye : INT32_MAX, v1 = oke ? ye : -1, v2 = oke ? xe : INT32_MAX, v3 = oke ? xe : -1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      v0 = min(v0, __shfl_xor(v0, o, 64));
+      v1 = max(v1, __shfl_xor(v1, o, 64));
+      v2 = min(v2, __shfl_xor(v2, o, 64));
+      v3 = max(v3, __shfl_xor(v3, o, 64));
+    }
+    if (lane == 0) {
+      atomicMin(&bb[0], v0);
+      atomicMax(&bb[1], v1);
+      atomicMin(&bb[2], v2);
+      atomicMax(&bb[3], v3);
+    }
+  }
+  __syncthreads();                                     // dtile and the bounding box
+  if (dinp) {
+    const int wy0 = bb[0], wx0 = bb[2], wwx = bb[3] - wx0 + 1;
+    const int wsz = (bb[1] - wy0 + 1) * wwx;
+    if (bb[1] >= 0 && wsz <= WG_CAP) {
+      for (int k = tid; k < wsz; k += WG_NT) cnt[k] = 0;
+      __syncthreads();
+      const int slot = (ye - wy0) * wwx + (xe - wx0);
+      const int rank = oke ? atomicAdd(&cnt[slot], 1) : 0;
+      __syncthreads();
+      if (wave == 0) {                                 // bucket starts + touched-slot list
+        const int per = (wsz + 63) / 64, k0 = min(wsz, lane * per), k1 = min(wsz, k0 + per);
+        int sum = 0, nz = 0;
+        for (int k = k0; k < k1; ++k) sum += cnt[k], nz += cnt[k] > 0;
+        int isum = sum, inz = nz;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int ts = __shfl_up(isum, o, 64), tn = __shfl_up(inz, o, 64);
+          if (lane >= o) isum += ts, inz += tn;
+        }
+        int run = isum - sum, nzp = inz - nz;
+        for (int k = k0; k < k1; ++k) {
+          const int ck = cnt[k];
+          st[k] = run;
+          run += ck;
+          if (ck > 0) nzs[nzp++] = k;
+        }
+        if (lane == 63) bb[4] = inz;
+      }
+      __syncthreads();
+      if (oke) ent[st[slot] + rank] = make_int2(pe, __float_as_int(wte));
+      __syncthreads();
+      const int nnz = bb[4];
+      for (int u = wave; u < nnz; u += WG_NT / 64) {
+        const int k = nzs[u], s0 = st[k], ne = cnt[k];
+        float acc = 0.f;
+        for (int e2 = 0; e2 < ne; ++e2) {
+          const int2 en = ent[s0 + e2];
+          acc += __int_as_float(en.y) * dtile[en.x * 64 + lane];
+        }
+        const int yy = wy0 + k / wwx, xx = wx0 + k % wwx;
+        atomicAdd(dinp + (img + (int64_t)yy * w + xx) * c + cc + lane, acc);
+      }
+    } else {                                           // spread flows: one add per corner
+      ent[tid] = make_int2(oke ? (ye * w + xe) : -1, __float_as_int(wte));
+      __syncthreads();
+      for (int u = wave; u < NP * 4; u += WG_NT / 64) {
+        const int2 en = ent[u];
+        if (en.x < 0) continue;                        // wave-uniform
+        atomicAdd(dinp + (img + en.x) * c + cc + lane,
+                  __int_as_float(en.y) * dtile[(u >> 2) * 64 + lane]);
+      }
+    }
+  }
+  // ---- flow gradient
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int pr = (it * (WG_NT / 64) + wave) * 4 + pg;
+    const float a = ag[it], bq = bg[it];
+    const float4 g = *reinterpret_cast<const float4*>(&dtile[pr * 64 + 4 * q]);
+    const float4* P = pv[it];
+    auto dot = [](float4 u, float4 v) { return u.x * v.x + u.y * v.y + u.z * v.z + u.w * v.w; };
+    auto sub = [](float4 u, float4 v) { return make_float4(u.x - v.x, u.y - v.y, u.z - v.z, u.w - v.w); };
+    float gx = -(bq * dot(g, sub(P[0], P[2])) + (1.f - bq) * dot(g, sub(P[1], P[3])));
+    float gy = -(a * dot(g, sub(P[0], P[1])) + (1.f - a) * dot(g, sub(P[2], P[3])));
+    gx = row16_sum(gx);
+    gy = row16_sum(gy);
+    if (q == 0 && okg[it]) {
+      if (passes == 1) {
+        *reinterpret_cast<float2*>(dflow + 2 * pixg[it]) = make_float2(gx, gy);
+      } else {                                         // dflow zeroed by the launcher
+        atomicAdd(dflow + 2 * pixg[it], gx);
+        atomicAdd(dflow + 2 * pixg[it] + 1, gy);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void warp_bwd_scalar(const float* __restrict__ dout,
                                                        const float* __restrict__ inp, int n,
                                                        int h, int w, int c,
@@ -1016,13 +1219,21 @@ static int warp_bwd_impl(const float* dout, const float* inp, int n, int h, int 
   hipStream_t s = as_stream(stream);
   const int64_t npix = (int64_t)n * h * w;
   if (!absolute && c % 64 == 0 && (int64_t)h * w < INT32_MAX) {
-    const int64_t blocks =
-        (int64_t)n * ((h + WH_T - 1) / WH_T) * ((w + WH_T - 1) / WH_T) * (c / 64);
-    OF_CHECK_ARG(blocks < INT32_MAX, "warp bwd: too many tiles");
     if (c > 64 && hipMemsetAsync(dflow, 0, (size_t)npix * 2 * sizeof(float), s) != hipSuccess)
       return check_launch("warp_bwd: dflow memset");
-    hipLaunchKernelGGL(warp_bwd_agg, dim3((unsigned)blocks), dim3(64 * WH_WAVES), 0, s, dout,
-                       inp, n, h, w, c, flow, dinp, dflow);
+    if (g_warp_win) {
+      const int64_t blocks =
+          (int64_t)n * ((h + WG_T - 1) / WG_T) * ((w + WG_T - 1) / WG_T) * (c / 64);
+      OF_CHECK_ARG(blocks < INT32_MAX, "warp bwd: too many tiles");
+      hipLaunchKernelGGL(warp_bwd_gather, dim3((unsigned)blocks), dim3(WG_NT), 0, s, dout,
+                         inp, n, h, w, c, flow, dinp, dflow);
+    } else {
+      const int64_t blocks =
+          (int64_t)n * ((h + WH_T - 1) / WH_T) * ((w + WH_T - 1) / WH_T) * (c / 64);
+      OF_CHECK_ARG(blocks < INT32_MAX, "warp bwd: too many tiles");
+      hipLaunchKernelGGL(warp_bwd_agg, dim3((unsigned)blocks), dim3(64 * WH_WAVES), 0, s, dout,
+                         inp, n, h, w, c, flow, dinp, dflow);
+    }
   } else if (c >= 16) {
     const int g = grid_for(npix * 64, 256, 16384);
     hipLaunchKernelGGL(warp_bwd_wave, dim3(g), dim3(256), 0, s, dout, inp, n, h, w, c, flow,

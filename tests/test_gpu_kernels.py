@@ -637,6 +637,38 @@ def test_warp(shape, flow_scale):
     assert rel_inf(fd.grad, fo.grad) < REL_TOL
 
 
+@pytest.mark.parametrize("form", [1, 0])
+@pytest.mark.parametrize("shape,flow_scale,offset", [((2, 40, 56, 64), 0.3, 0.0),
+                                                     ((2, 24, 40, 128), 0.8, 0.0),
+                                                     ((1, 33, 45, 64), 0.3, 30.0),
+                                                     ((1, 33, 45, 64), 0.3, -30.0),
+                                                     ((2, 20, 28, 64), 5.0, 0.0)])
+def test_warp_bwd_forms(form, shape, flow_scale, offset):
+    """Feature-warp backward with the tile scatter aggregated in LDS (of_set_tuning key 7 = 1:
+    sub-pixel flows, clipped tiles on a border strip, and spread flows that fall back to direct
+    atomics) and with the border-corner cache only (key 7 = 0), against fp64 autograd."""
+    from optical_flow_amd import _lib
+    ops = _ops()
+    n, h, w, c = shape
+    f2 = rng_tensor(shape, 31)
+    fl = rng_tensor((n, h, w, 2), 32, scale=flow_scale) + offset
+    a, fo = f64(f2).requires_grad_(True), f64(fl).requires_grad_(True)
+    out = R.warp_features(fo, a)
+    g = rng_tensor(tuple(out.shape), 33)
+    (out * f64(g)).sum().backward()
+    lib = _lib.lib()
+    try:
+        assert lib.of_set_tuning(7, form) == 0
+        ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
+        od = ops.warp(ad, fd)
+        (od * dev(g)).sum().backward()
+        torch.cuda.synchronize()
+    finally:
+        lib.of_set_tuning(7, 1)
+    assert rel_inf(ad.grad, a.grad) < REL_TOL
+    assert rel_inf(fd.grad, fo.grad) < REL_TOL
+
+
 def test_bilinear_interpolation_absolute():
     from optical_flow_amd.transformations import bilinear_interpolation
     n, h, w, c = 2, 9, 11, 8

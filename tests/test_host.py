@@ -89,5 +89,10 @@ def test_bench_kernel_symbols_match_pmc_keys():
             names.add(bench.kernel_symbol(128 + mode * 8 + cfg))
     for cfg in bench.X3_WGT:
         names.add(bench.kernel_symbol(128 + 16 + cfg))
+    for mode in (0, 1):
+        for cfg in bench.GX3:
+            names.add(bench.kernel_symbol(160 + mode * 8 + cfg))
+    for cfg in bench.GX3_WG:
+        names.add(bench.kernel_symbol(176 + cfg))
     x3_keys = {k for k in keys if "_x3<" in k or "_x3b<" in k}
     assert x3_keys and x3_keys <= names, sorted(x3_keys - names)
