@@ -3164,6 +3164,22 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_f32(GemmArgs a) {
 // Workgroup = 32 items x 8 split lanes; item = (slab row, 4 columns); the 8 lanes each sum
 // every 8th slice (many independent loads in flight), then a fixed-order LDS reduction.
 constexpr int EP_ITEMS = 32, EP_LANES = 8;
+// sum over z = z0, z0 + EP_LANES, ... < zend of src[z * stride .. + 3], in that order, with
+// four loads in flight (the split-K reductions are latency-bound at one load per step)
+__device__ __forceinline__ float4 strided_sum4(const float* src, int z0, int zend, int64_t stride) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int z = z0;
+  for (; z + 3 * EP_LANES < zend; z += 4 * EP_LANES) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      v[u] = *reinterpret_cast<const float4*>(src + (int64_t)(z + u * EP_LANES) * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) add4(acc, v[u]);
+  }
+  for (; z < zend; z += EP_LANES) add4(acc, *reinterpret_cast<const float4*>(src + (int64_t)z * stride));
+  return acc;
+}
 
 template <int MODE>
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a) {
@@ -3177,9 +3193,7 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(GemmArgs a) {
   const int64_t srow = live ? item / nq : 0;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (live) {
-    const float* src = a.slab + srow * a.slab_ld + 4 * q;
-    for (int z = sl; z < a.splits; z += EP_LANES)
-      add4(acc, *reinterpret_cast<const float4*>(src + (int64_t)z * a.split_stride));
+    acc = strided_sum4(a.slab + srow * a.slab_ld + 4 * q, sl, a.splits, a.split_stride);
   }
   red[sl][it] = acc;
   __syncthreads();
@@ -3480,9 +3494,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (live) {
-    const float* src = ws + m * ldc + 4 * q;
-    for (int z = sl; z < splits; z += EP_LANES)
-      add4(acc, *reinterpret_cast<const float4*>(src + (int64_t)z * split_stride));
+    acc = strided_sum4(ws + m * ldc + 4 * q, sl, splits, split_stride);
   }
   red[sl][it] = acc;
   __syncthreads();

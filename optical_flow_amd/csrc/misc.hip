@@ -254,38 +254,64 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
   }
 }
 
-__global__ __launch_bounds__(256) void bn_act_bwd_final(const float* __restrict__ part,
-                                                        int nblk, int c,
-                                                        const float* __restrict__ gamma,
-                                                        const float* __restrict__ var,
-                                                        float eps, float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta,
-                                                        float* __restrict__ dbias, int accum) {
-  __shared__ float red[2][16][17];
-  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int ch = blockIdx.x * 16 + cl;
-  float sb = 0.f, sg = 0.f;
+// Sum the partial rows of bn_act_bwd_partial / maxpool_bn_act_bwd_partial in a fixed order:
+// workgroup = 16 channel quads x 64 row groups (1024 threads, grid.x = cdiv(c / 4, 16)); each
+// thread sums its rows with 8 float4 loads in flight, then a fixed tree over the 64 groups.
+// (A 16-row-group form with one scalar load in flight per step took 15 us per call: latency.)
+constexpr int BNF_Q = 16, BNF_G = 64;
+__global__ __launch_bounds__(BNF_Q * BNF_G) void bn_act_bwd_final(const float* __restrict__ part,
+                                                                  int nblk, int c,
+                                                                  const float* __restrict__ gamma,
+                                                                  const float* __restrict__ var,
+                                                                  float eps, float* __restrict__ dgamma,
+                                                                  float* __restrict__ dbeta,
+                                                                  float* __restrict__ dbias, int accum) {
+  __shared__ float4 red[2][BNF_G][BNF_Q];
+  const int ql = threadIdx.x % BNF_Q, g = threadIdx.x / BNF_Q;
+  const int ch = (blockIdx.x * BNF_Q + ql) * 4;
+  float4 sb = make_float4(0.f, 0.f, 0.f, 0.f), sg = sb;
   if (ch < c) {
-    for (int b = g; b < nblk; b += 16) {
-      sb += part[((int64_t)b * 2 + 0) * c + ch];
-      sg += part[((int64_t)b * 2 + 1) * c + ch];
+    int b = g;
+    for (; b + 3 * BNF_G < nblk; b += 4 * BNF_G) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[2 * u] = *reinterpret_cast<const float4*>(part + ((int64_t)(b + u * BNF_G) * 2 + 0) * c + ch);
+        v[2 * u + 1] = *reinterpret_cast<const float4*>(part + ((int64_t)(b + u * BNF_G) * 2 + 1) * c + ch);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        add4(sb, v[2 * u]);
+        add4(sg, v[2 * u + 1]);
+      }
+    }
+    for (; b < nblk; b += BNF_G) {
+      add4(sb, *reinterpret_cast<const float4*>(part + ((int64_t)b * 2 + 0) * c + ch));
+      add4(sg, *reinterpret_cast<const float4*>(part + ((int64_t)b * 2 + 1) * c + ch));
     }
   }
-  red[0][g][cl] = sb;
-  red[1][g][cl] = sg;
+  red[0][g][ql] = sb;
+  red[1][g][ql] = sg;
   __syncthreads();
-  if (g == 0 && ch < c) {
-    sb = 0.f;
-    sg = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      sb += red[0][k][cl];
-      sg += red[1][k][cl];
+  for (int s = BNF_G / 2; s > 0; s >>= 1) {
+    if (g < s) {
+      add4(sb, red[0][g + s][ql]);
+      add4(sg, red[1][g + s][ql]);
+      red[0][g][ql] = sb;
+      red[1][g][ql] = sg;
     }
-    const float db = sb * gamma[ch] * rsqrtf(var[ch] + eps);
-    if (dbeta) dbeta[ch] = accum ? dbeta[ch] + sb : sb;
-    if (dgamma) dgamma[ch] = accum ? dgamma[ch] + sg : sg;
-    if (dbias) dbias[ch] = accum ? dbias[ch] + db : db;
+    __syncthreads();
+  }
+  if (g == 0 && ch < c) {
+    const float vb[4] = {sb.x, sb.y, sb.z, sb.w}, vg[4] = {sg.x, sg.y, sg.z, sg.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = ch + e;
+      const float db = vb[e] * gamma[k] * rsqrtf(var[k] + eps);
+      if (dbeta) dbeta[k] = accum ? dbeta[k] + vb[e] : vb[e];
+      if (dgamma) dgamma[k] = accum ? dgamma[k] + vg[e] : vg[e];
+      if (dbias) dbias[k] = accum ? dbias[k] + db : db;
+    }
   }
 }
 
@@ -486,8 +512,8 @@ int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
                      part);
   int st = check_launch("bn_act_bwd_partial");
   if (st) return st;
-  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c, 16)), dim3(256), 0, s, part, g.nblk, c,
-                     gamma, var, eps, dgamma, dbeta, dbias, accumulate);
+  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c / 4, BNF_Q)), dim3(BNF_Q * BNF_G), 0, s, part,
+                     g.nblk, c, gamma, var, eps, dgamma, dbeta, dbias, accumulate);
   return check_launch("bn_act_bwd_final");
 }
 
@@ -516,8 +542,8 @@ int of_maxpool_bn_act_bwd(int n, int h, int w, int c, const float* dyp, const fl
                      geo.rows, geo.ppb, part);
   int st = check_launch("maxpool_bn_act_bwd_partial");
   if (st) return st;
-  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c, 16)), dim3(256), 0, s, part, geo.nblk, c,
-                     gamma, var, eps, dgamma, dbeta, dbias, accumulate);
+  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c / 4, BNF_Q)), dim3(BNF_Q * BNF_G), 0, s, part,
+                     geo.nblk, c, gamma, var, eps, dgamma, dbeta, dbias, accumulate);
   return check_launch("bn_act_bwd_final");
 }
 
