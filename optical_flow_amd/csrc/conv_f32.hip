@@ -3390,83 +3390,100 @@ __device__ __forceinline__ void put16(int mode, float* base, int64_t k, int64_t 
 }
 
 // One packed element of entry E (f32: fwd rows [k][n] then bwd rows; bf16: transposed).
-__device__ void pack_elem(const PackEntry& E, int64_t k) {
+// k < 2^31 (entry-local; the host checks): 32-bit index arithmetic.
+__device__ void pack_elem(const PackEntry& E, int k) {
   if (E.bf16) {
-    const int64_t nfwd16 = (int64_t)E.cout_p * E.kf16;
+    const int nfwd16 = E.cout_p * E.kf16;
     if (k < nfwd16) {                       // W16_f[n][tap*cin_p + ci]
-      const int n = (int)(k / E.kf16), kk = (int)(k - (int64_t)n * E.kf16);
+      const int n = k / E.kf16, kk = k - n * E.kf16;
       const int tap = kk / E.cin_p, ci = kk - tap * E.cin_p;
       float v = 0.f;
       if (tap < E.taps && ci < E.cin && n < E.cout)
-        v = E.w[((int64_t)tap * E.cin + ci) * E.cout + n];
-      put16(E.bf16, E.wf, k, (int64_t)E.cout_p * E.kf16, v);
+        v = E.w[(tap * E.cin + ci) * E.cout + n];
+      put16(E.bf16, E.wf, k, nfwd16, v);
     } else {                                // W16_d[ci][group k block: t*cout_p + co]
       k -= nfwd16;
-      const int ci = (int)(k / E.kd16);
-      const int64_t kc = k - (int64_t)ci * E.kd16;
+      const int kd16 = (int)E.kd16;
+      const int ci = k / kd16;
+      const int kc = k - ci * kd16;
       const PackGroups& pg = E.pg;
       int g = 0;
       for (int q = 1; q < pg.ngroups; ++q)
         if (kc >= pg.row_begin16[q]) g = q;
-      const int kk = (int)(kc - pg.row_begin16[g]);
+      const int kk = kc - (int)pg.row_begin16[g];
       const int t = kk / E.cout_p, co = kk - t * E.cout_p;
       float v = 0.f;
       if (t < pg.ntaps[g] && co < E.cout && ci < E.cin) {
         const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
         const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
-        v = E.w[((int64_t)(r * E.kw + ss) * E.cin + ci) * E.cout + co];
+        v = E.w[((r * E.kw + ss) * E.cin + ci) * E.cout + co];
       }
       put16(E.bf16, E.wd, k, E.kd16 * E.nd, v);
     }
     return;
   }
-  const int64_t nfwd = (int64_t)E.kf * E.nf;
+  const int nfwd = E.kf * E.nf;
   if (k < nfwd) {
-    const int kk = (int)(k / E.nf), nn = (int)(k - (int64_t)kk * E.nf);
+    const int kk = k / E.nf, nn = k - kk * E.nf;
     const int tap = kk / E.cin_p, ci = kk - tap * E.cin_p;
     float v = 0.f;
     if (tap < E.taps && ci < E.cin && nn < E.cout)
-      v = E.w[((int64_t)tap * E.cin + ci) * E.cout + nn];
+      v = E.w[(tap * E.cin + ci) * E.cout + nn];
     E.wf[k] = v;
   } else {
     k -= nfwd;
-    const int64_t row = k / E.nd;
-    const int nn = (int)(k - row * E.nd);
+    const int row = k / E.nd;
+    const int nn = k - row * E.nd;
     const PackGroups& pg = E.pg;
     int g = 0;
     for (int q = 1; q < pg.ngroups; ++q)
       if (row >= pg.row_begin[q]) g = q;
-    const int kk = (int)(row - pg.row_begin[g]);
+    const int kk = row - (int)pg.row_begin[g];
     const int t = kk / E.cout_p, co = kk - t * E.cout_p;
     float v = 0.f;
     if (t < pg.ntaps[g] && co < E.cout && nn < E.cin) {
       const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
       const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
-      v = E.w[((int64_t)(r * E.kw + ss) * E.cin + nn) * E.cout + co];
+      v = E.w[((r * E.kw + ss) * E.cin + nn) * E.cout + co];
     }
     E.wd[k] = v;
   }
 }
 
-__global__ void pack_many_kernel(const char* __restrict__ table) {
+// Workgroup = PACK_PT x 256 consecutive elements (lane-strided: coalesced stores); the entry
+// of its first element is found once and advanced at entry boundaries (no per-element search
+// of the table).  The entry is read in place: a register copy of PackEntry (dynamically
+// indexed group arrays) lands in scratch.
+constexpr int PACK_PT = 8;
+__global__ __launch_bounds__(256) void pack_many_kernel(const char* __restrict__ table) {
   const PackTableHeader* h = reinterpret_cast<const PackTableHeader*>(table);
   const PackEntry* e = reinterpret_cast<const PackEntry*>(table + sizeof(PackTableHeader));
   const int n = h->nconv;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < h->total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (e[mid].work_begin <= idx) lo = mid; else hi = mid - 1;
+  const int64_t total = h->total;
+  const int64_t base = (int64_t)blockIdx.x * 256 * PACK_PT;
+  if (base >= total) return;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (e[mid].work_begin <= base) lo = mid; else hi = mid - 1;
+  }
+  int cur = lo;
+  int64_t next = cur + 1 < n ? e[cur + 1].work_begin : total;
+  for (int u = 0; u < PACK_PT; ++u) {
+    const int64_t idx = base + u * 256 + threadIdx.x;
+    if (idx >= total) break;
+    while (idx >= next) {
+      ++cur;
+      next = cur + 1 < n ? e[cur + 1].work_begin : total;
     }
-    pack_elem(e[lo], idx - e[lo].work_begin);
+    pack_elem(e[cur], (int)(idx - e[cur].work_begin));   // entry fields: cached global loads
   }
 }
 
 __global__ void pack_one_kernel(PackEntry E, int64_t total) {
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x)
-    pack_elem(E, idx);
+    pack_elem(E, (int)idx);
 }
 
 // dw[tap][ci][co] (HWIO) = sum_z slab[z][tap*kc + ci][co]; optional db[co] = sum_z slab[z][M][co].
@@ -4126,6 +4143,7 @@ int of_conv_pack_weights_bf16(const of_conv_desc* d, const float* w_hwio, void* 
   if (st) return st;
   OF_CHECK_ARG(w_hwio && w16_fwd && w16_bwd, "pack bf16: NULL pointer");
   const int64_t total = pack_work(d, 1);
+  OF_CHECK_ARG(total < INT32_MAX, "pack: layer too large");
   const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
   hipLaunchKernelGGL(pack_one_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
                      pack_entry(d, w_hwio, w16_fwd, w16_bwd, 1), total);
@@ -4186,6 +4204,7 @@ int of_conv_pack_table_ex(int nconv, const of_conv_desc* descs, const float* con
     const int b16 = bf16 ? (bf16[i] == 2 ? 2 : bf16[i] != 0) : 0;   // 2: x3 planes
     e[i] = pack_entry(&descs[i], w_hwio[i], w_fwd[i], w_bwd[i], b16);
     e[i].work_begin = work;
+    OF_CHECK_ARG(pack_work(&descs[i], b16) < INT32_MAX, "pack table: layer too large");
     work += pack_work(&descs[i], b16);
   }
   h->nconv = nconv;
@@ -4202,8 +4221,9 @@ int of_conv_pack_table(int nconv, const of_conv_desc* descs, const float* const*
 
 int of_conv_pack_many(const void* dev_table, int64_t total_work, void* stream) {
   OF_CHECK_ARG(dev_table && total_work > 0, "pack many: args");
-  const int blocks = (int)std::min<int64_t>(cdiv(total_work, 256), 8192);
-  hipLaunchKernelGGL(pack_many_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+  const int64_t blocks = cdiv(total_work, 256 * PACK_PT);
+  OF_CHECK_ARG(blocks < INT32_MAX, "pack many: too much work");
+  hipLaunchKernelGGL(pack_many_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
                      static_cast<const char*>(dev_table));
   return check_launch("pack_many");
 }
@@ -4417,6 +4437,7 @@ int of_conv_pack_weights_x3(const of_conv_desc* d, const float* w_hwio, void* w3
   if (st) return st;
   OF_CHECK_ARG(w_hwio && w3_fwd && w3_bwd, "pack x3: NULL pointer");
   const int64_t total = pack_work(d, 1);
+  OF_CHECK_ARG(total < INT32_MAX, "pack: layer too large");
   const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
   hipLaunchKernelGGL(pack_one_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
                      pack_entry(d, w_hwio, w3_fwd, w3_bwd, 2), total);
