@@ -51,6 +51,8 @@ def kind_parts(kind):
     bf16 implicit GEMMs 64 + mode*8 + cfg, bf16 halo-tiled 3x3 96 + mode*8 + cfg,
     fp32 on the split-bf16 halo-tiled 3x3 kernels 128 + mode*8 + cfg, on the split-bf16
     implicit GEMM (other shapes) 160 + mode*8 + cfg (optical_flow_amd/csrc/conv_f32.hip)."""
+    if kind == KIND_STEM_X3:
+        return 0, 0, "stem_x3"
     fam = ("gemm_x3" if kind >= 160 else "tile_x3" if kind >= 128 else "tile_bf16" if kind >= 96 else
            "bf16" if kind >= 64 else
            "tile_f32" if kind >= 32 else "f32")
@@ -81,13 +83,19 @@ def conv_math(precision):
         return ("fp32: every conv with >= 16 input channels (3x3 stride-1 halo tiles; stride-2 "
                 "and 1x1 implicit GEMMs) fwd/dgrad/wgrad on bf16 MFMA with an exact 3-term "
                 "operand split (6 products, fp32 accumulation; error vs fp64 at fp32-MFMA level, "
-                "test_conv_x3_accuracy / test_conv_gemm_x3_accuracy); the 3-channel stem on fp32 "
-                "MFMA, the Cout<=4 flow convs on fp32 VALU")
+                "test_conv_x3_accuracy / test_conv_gemm_x3_accuracy); the 3-channel stem forward on "
+                "its own split-bf16 kernel and its weight gradient on fp32 MFMA, the Cout<=4 flow "
+                "convs on fp32 VALU")
     return "fp32 MFMA (flow convs cout<=4: fp32 VALU)"
+
+
+KIND_STEM_X3 = 184   # conv_stem_x3 (the 7x7 stride-2 stem forward on the split-bf16 MFMA)
 
 
 def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
+    if fam == "stem_x3":
+        return "fwd_stem_x3"
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
            "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3"}[fam]
     if fam == "gemm_x3":
@@ -105,6 +113,8 @@ def kind_name(kind):
 def kernel_symbol(kind):
     """rocprofv3 name of the conv kernel instance behind a timing kind."""
     mode, cfg, fam = kind_parts(kind)
+    if fam == "stem_x3":
+        return "void oflow::conv_stem_x3<32>(oflow::GemmArgs)"   # of_set_tuning key 8 default
     if cfg == 7 and fam == "f32":
         return NARROW_SYMBOLS[mode]
     if fam == "gemm_x3":
@@ -321,7 +331,7 @@ def main():
         fam = kind_parts(dom)[2]
         # the split kernel spends six bf16 MFMAs per fp32 product: its ceiling is 1/6 of bf16
         peak = (FP32_MFMA_PEAK_TFLOPS if fam in ("f32", "tile_f32") else
-                round(BF16_MFMA_PEAK_TFLOPS / 6, 1) if fam in ("tile_x3", "gemm_x3")
+                round(BF16_MFMA_PEAK_TFLOPS / 6, 1) if fam in ("tile_x3", "gemm_x3", "stem_x3")
                 else BF16_MFMA_PEAK_TFLOPS)
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",

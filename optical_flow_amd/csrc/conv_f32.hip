@@ -1552,6 +1552,148 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
   }
 }
 
+// ---- the stem (7x7 stride 2, 3 -> 4 padded input channels, 64 outputs) on the split-bf16
+// MFMA.  conv_gemm_x3's im2col staging gathers 16-byte (one pixel's 4 channels) pieces per tap;
+// here a 32-deep K chunk is one kernel row r: lane octet sp holds taps (r, 2 sp), (r, 2 sp + 1)
+// x 4 channels = two horizontally adjacent input pixels, i.e. one aligned 16-byte read of the
+// bf16 halo image (tap 7 is a zero weight column).  The workgroup stages the whole K (7 rows x
+// 32) of B once, 3 planes x 64 rows with a 464-byte pitch (fragment reads conflict-free), and
+// the tile's input halo ((2 TH + 5) x (2 TW + 6) pixels) once as 3 split planes; then 7 chunks
+// of 6 MFMAs per fragment pair, the epilogue through per-wave LDS images (16-byte stores).
+// CO = 64: 8 waves, 4 x 2 of 64 pixels (2 tile rows) x 32 output channels, 125 KB of LDS;
+// CO = 32: each workgroup takes half the output channels with 4 waves and 80 KB, so two share
+// a CU and one's staging / epilogue overlaps the other's MFMAs.
+constexpr int ST_TH = 8, ST_TW = 32;
+constexpr int ST_HH = 2 * ST_TH + 5, ST_HW = 2 * ST_TW + 6, ST_HWP = 72;
+constexpr int ST_BROW = 232;      // bf16 per B row: 7 x 32 + 8
+
+template <int CO>
+__global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : 2) void conv_stem_x3(GemmArgs a) {
+  constexpr int NP = 3, SM = 4, SN = 2, WM = 64, WN = 32, NW = CO / 8, NT = 64 * NW;
+  constexpr int B_U4 = CO * ST_BROW / 8;              // uint4 per B plane
+  constexpr int H_PIX = ST_HH * ST_HWP;               // halo pixels (8 bytes each) per plane
+  constexpr int SMEM_U4 = NP * B_U4 + NP * H_PIX / 2;
+  static_assert(NW * WM * WN * 4 <= SMEM_U4 * 16, "epilogue images fit");
+  __shared__ uint4 smem[SMEM_U4];
+  char* Bs = reinterpret_cast<char*>(smem);                          // [plane][co][k']
+  char* Hs = reinterpret_cast<char*>(smem + NP * B_U4);              // [plane][hy][hx] 8 B
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int co0 = (wgid0 % (64 / CO)) * CO, wgid = wgid0 / (64 / CO);
+  const int tiles_x = (a.wo + ST_TW - 1) / ST_TW, tiles_y = (a.ho + ST_TH - 1) / ST_TH;
+  const int b = wgid / (tiles_x * tiles_y);
+  const int trem = wgid - b * tiles_x * tiles_y;
+  const int oy0 = (trem / tiles_x) * ST_TH, ox0 = (trem % tiles_x) * ST_TW;
+  const int iy0 = 2 * oy0 - a.pt, ix0 = 2 * ox0 - a.pl;
+
+  // ---- B: entry (plane, co, kernel row r, octet sp) <- taps (r, 2 sp), (r, 2 sp + 1) of the
+  // x3 fwd image W16_f[co][tap * 4 + ci] (8-byte aligned pieces; tap 7 is zero)
+  const rsrc_t rb = make_rsrc(a.B, a.b_bytes);
+  for (int e = tid; e < NP * CO * 28; e += NT) {
+    const int p = e / (CO * 28), rem = e - p * (CO * 28);
+    const int co = rem / 28, rs = rem - co * 28, r = rs >> 2, sp = rs & 3;
+    const uint32_t src =
+        (uint32_t)((p * a.b_plane + (int64_t)(co0 + co) * a.ldb + (r * 7 + 2 * sp) * 4) * 2);
+    const bool ok = co0 + co < a.nb;
+    const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok ? src : kOOB, 0, 0));
+    const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok && sp < 3 ? src + 8 : kOOB, 0, 0));
+    *reinterpret_cast<uint4*>(Bs + ((p * CO + co) * ST_BROW + r * 32 + sp * 8) * 2) =
+        make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+  // ---- halo: input pixel (iy0 + hy, ix0 + hx), 4 channels, split into 3 planes
+  const rsrc_t ra = make_rsrc(a.A, a.a_bytes);
+  for (int q = tid; q < ST_HH * ST_HW; q += NT) {
+    const int hy = q / ST_HW, hx = q - hy * ST_HW;
+    const int iy = iy0 + hy, ix = ix0 + hx;
+    const bool ok = (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    const float4 v = bload4(ra, ok ? (uint32_t)((((int64_t)b * a.h + iy) * a.w + ix) * a.lda * 4) : kOOB);
+    uint2 h, m, l;
+    split3x4(v, h, m, l);
+    const int o = (hy * ST_HWP + hx) * 8;
+    *reinterpret_cast<uint2*>(Hs + o) = h;
+    *reinterpret_cast<uint2*>(Hs + H_PIX * 8 + o) = m;
+    *reinterpret_cast<uint2*>(Hs + 2 * H_PIX * 8 + o) = l;
+  }
+  __syncthreads();
+
+  const int wm = CO == 64 ? wave >> 1 : wave, wn = CO == 64 ? wave & 1 : 0;
+  const int l16 = lane & 15, sp = lane >> 4;
+  f32x4 acc4[SM][SN];
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+#pragma unroll
+    for (int j = 0; j < SN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc4[i][j][r] = 0.f;
+  // A block i: output row 2 wm + (i >> 1), columns 16 (i & 1) + l16 -> halo pixel at kernel row 0
+  int a_off[SM];
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+    a_off[i] = ((2 * (2 * wm + (i >> 1))) * ST_HWP + 2 * (16 * (i & 1) + l16) + 2 * sp) * 8;
+  const int b_off = ((wn * WN + l16) * ST_BROW + sp * 8) * 2;
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    bf16x8 av[NP][SM], bv[NP][SN];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+        av[p][i] = *reinterpret_cast<const bf16x8*>(Hs + p * H_PIX * 8 + a_off[i] + r * ST_HWP * 8);
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+        bv[p][j] = *reinterpret_cast<const bf16x8*>(Bs + p * B_U4 * 16 + b_off + (16 * j * ST_BROW + r * 32) * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        f32x4 x = acc4[i][j];
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
+        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+      }
+  }
+  __syncthreads();                      // B / halo reads done: LDS becomes the epilogue images
+
+  // ---- epilogue: the wave's 64 x 32 block through a private LDS image, float4 rows
+  constexpr int EPW = 32, LPR = 8, RPI = 8;
+  float* E = reinterpret_cast<float*>(smem) + wave * WM * EPW;
+  const int lq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+#pragma unroll
+    for (int j = 0; j < SN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) E[(16 * i + 4 * lq + r) * EPW + 16 * j + l16] = acc4[i][j][r];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int c4 = lane % LPR, rr = lane / LPR;
+  const int n = co0 + wn * WN + 4 * c4;
+  const int64_t img = (int64_t)b * a.ho * a.wo;
+#pragma unroll
+  for (int q = 0; q < WM / RPI; ++q) {
+    const int m = q * RPI + rr;
+    const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
+    const int oy = oy0 + 2 * wm + m / 32, ox = ox0 + m % 32;
+    if (oy < a.ho && ox < a.wo && n < a.N)
+      epilogue_store4<MODE_FWD>(a, 0, img + (int64_t)oy * a.wo + ox, n, v);
+  }
+}
+
+// of_set_tuning key 8: the stem on conv_stem_x3 (1: two 32-channel workgroups per CU,
+// default; 2: one 64-channel workgroup) or on conv_gemm_x3 (0).
+static int g_stem_x3 = 1;
+bool stem_x3_ok(const of_conv_desc* d) {
+  return d->kh == 7 && d->kw == 7 && d->stride == 2 && d->cin_p == 4 && d->cout == 64 &&
+         d->pad_top >= 0 && d->pad_top <= 3 && d->pad_left >= 0 && d->pad_left <= 3;
+}
+
 // ---- fp32 on bf16 MFMA by the three-term split: implicit-GEMM fwd / dgrad ------------------
 // The shapes the halo tiles do not cover (the 7x7 stride-2 stem, the 3x3 stride-2 block
 // convs and the 1x1 stride-2 projections, with the stride-2 input gradient as phase groups):
@@ -4175,6 +4317,7 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
 }
 
 int of_set_tuning(int key, int value) {
+  if (key == 8 && value >= 0 && value <= 2) { g_stem_x3 = value; return OF_OK; }
   if (key == 7 && (value == 0 || value == 1)) { g_warp_win = value; return OF_OK; }
   if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }
   if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
@@ -4230,6 +4373,7 @@ int of_conv_pack_many(const void* dev_table, int64_t total_work, void* stream) {
 
 // Timing kind of the narrow (VALU) path; GEMM kinds are MODE * 8 + tile config (0..3).
 constexpr int KIND_NARROW = 7;
+constexpr int KIND_STEM_X3 = 184;   // conv_stem_x3 (bench.py kind_name)
 
 double conv_flops(const of_conv_desc* d) {
   return 2.0 * d->n * d->ho * d->wo * (double)d->cout * d->kh * d->kw * d->cin;
@@ -4290,8 +4434,21 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   Geo g = geo(d);
   const bool tile = (bf16 || x3) && tile_ok(d);
   GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3) : fwd_args(d, g, bf16 || x3);
-  if (x3 && !tile) gemm_x3_plan(a);
-  attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
+  bool stem = x3 && !tile && g_stem_x3 && stem_x3_ok(d);
+  if (stem) {                            // conv_stem_x3: one workgroup per output tile, no split
+    a.splits = 1;
+    a.k_per_split = a.K;
+    a.slab = nullptr;
+  }
+  a.C = y;   // (vec_ep_ok reads the output fields)
+  a.ldc = ldy;
+  a.res = residual;
+  a.ldr = ldr;
+  a.z = z;
+  a.ldz = ldz;
+  stem = stem && vec_ep_ok(a);
+  if (x3 && !tile && !stem) gemm_x3_plan(a);
+  if (!stem) attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
   a.A = x;
   a.lda = ldx;
   a.a_bytes = (int64_t)d->n * d->h * d->w * ldx * 4;
@@ -4317,6 +4474,17 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   a.vec_ep = vec_ep_ok(a);
+  if (stem) {
+    const int64_t tiles = (int64_t)d->n * cdiv(d->ho, ST_TH) * cdiv(d->wo, ST_TW);
+    OF_CHECK_ARG(tiles < INT32_MAX, "conv stem: too many tiles");
+    if (timing_on()) timing_begin(s);
+    if (g_stem_x3 == 2)
+      hipLaunchKernelGGL(conv_stem_x3<64>, dim3((unsigned)tiles), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL(conv_stem_x3<32>, dim3((unsigned)(2 * tiles)), dim3(256), 0, s, a);
+    if (timing_on()) timing_end(s, KIND_STEM_X3, flops);
+    return check_launch("conv_stem_x3");
+  }
   st = x3     ? (tile ? launch_tile_x3<MODE_FWD>(a, s, flops) : launch_gemm_x3<MODE_FWD>(a, s, flops))
        : tile ? launch_tile_bf16<MODE_FWD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops)

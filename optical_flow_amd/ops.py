@@ -148,10 +148,19 @@ F32_SPLIT = os.environ.get("OFLOW_F32_SPLIT", "1") == "1"
 # With F32_SPLIT, the other GEMM-path fp32 layers with >= 16 input channels (the stride-2
 # block convs and the 1x1 projections) take the split-bf16 implicit GEMMs (conv_gemm_x3,
 # conv_wgrad_x3) too: 10-25 % faster per pass than the fp32 MFMA GEMM.  The stem (3 input
-# channels, K = 49 taps x 4) measured 9 % / 37 % slower there (fwd / wgrad) and stays fp32.
+# channels, K = 49 taps x 4) measured 9 % / 37 % slower there (fwd / wgrad); its forward has a
+# kernel of its own (conv_stem_x3, STEM_X3) and its weight gradient stays on the fp32 GEMM.
 # OFLOW_X3_GEMM=0 keeps them all on the fp32 MFMA kernels.
 X3_GEMM = os.environ.get("OFLOW_X3_GEMM", "1") == "1"
 X3_GEMM_MIN_CIN = 16
+STEM_X3 = os.environ.get("OFLOW_STEM_X3", "1") == "1"
+
+
+def _stem_x3(layer) -> bool:
+    """The shape conv_stem_x3 covers (of its stem_x3_ok): 7x7 stride 2, 4 padded input
+    channels, 64 outputs."""
+    return (STEM_X3 and layer.kh == 7 and layer.kw == 7 and layer.stride == 2 and
+            layer.cin_p == 4 and layer.cout == 64)
 
 class ConvLayer:
     """One ``layers.Conv2D(filters, k, strides, padding='same')`` (model.py:12,104-114) with an
@@ -204,7 +213,8 @@ class ConvLayer:
             tile = self.kh == 3 and self.kw == 3 and self.stride == 1
             self._mode = (1 if self.bf16(d) else
                           2 if (self.f32_split and self.precision == "fp32" and
-                                (tile or (X3_GEMM and self.cin_p >= X3_GEMM_MIN_CIN)) and
+                                (tile or _stem_x3(self) or
+                                 (X3_GEMM and self.cin_p >= X3_GEMM_MIN_CIN)) and
                                 _lib.lib().of_conv_path(C.byref(d or self.desc(1, 16, 16))) == 0)
                           else 0)
         return self._mode
@@ -247,7 +257,7 @@ class ConvLayer:
         lib = _lib.lib()
         if self.bf16(d):
             return "of_conv2d_wgrad_bf16", lib.of_conv2d_wgrad_bf16_workspace(C.byref(d))
-        if self.mode(d) == 2:
+        if self.mode(d) == 2 and not _stem_x3(self):
             return "of_conv2d_wgrad_x3", lib.of_conv2d_wgrad_x3_workspace(C.byref(d))
         return "of_conv2d_wgrad", lib.of_conv2d_wgrad_workspace(C.byref(d))
 

@@ -273,6 +273,63 @@ def test_conv_gemm_x3_accuracy(n, h, w, cin, cout, k, s, monkeypatch):
         assert e3 < 5e-6, errs[True]
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (2, 38, 130)])
+def test_conv_stem_x3(n, h, w):
+    """The stem forward on its own split-bf16 kernel (conv_stem_x3: 7x7 stride 2, 3 -> 4
+    input channels, 64 outputs; bias, BN, ReLU and z in the epilogue; ragged output tiles)
+    against fp64 and against conv_gemm_x3 (of_set_tuning key 8 = 0), as accurate as one fp32
+    rounding per product; the 32- and 64-channel workgroup forms (key 8 = 1, 2) bitwise equal;
+    the timing kind says which kernel ran."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_RELU, call
+    lib = _lib.lib()
+    cin, cout = 4, 64
+    xc = rng_tensor((n, h, w, 3), 61)
+    x = torch.cat([xc, torch.zeros(n, h, w, 1)], -1)
+    wt = rng_tensor((7, 7, 3, cout), 62, scale=(2.0 / 147) ** 0.5)
+    wp = torch.cat([wt, torch.zeros(7, 7, 1, cout)], 2)
+    b = rng_tensor((cout,), 63, scale=0.1)
+    g, be = rng_tensor((cout,), 64, scale=0.5) + 1.0, rng_tensor((cout,), 65, scale=0.1)
+    mu, var = rng_tensor((cout,), 66, scale=0.1), rng_tensor((cout,), 67).abs() + 0.5
+    layer = ops.ConvLayer(dev(wt), dev(b), stride=2, act=ACT_RELU, cin_p=cin, f32_split=True)
+    d = layer.desc(n, h, w)
+    assert layer.mode(d) == 2
+    wf, _ = layer.packed(d)
+    fent, fws = layer.fwd_entry(d)
+    ws = torch.empty(fws // 4 + 4, device="cuda")
+    P, st = ops._ptr, ops._stream()
+    xd, bd, gd, bed, mud, vard = [dev(t) for t in (x, b, g, be, mu, var)]
+    outs, kinds = [], []
+    try:
+        for form in (1, 2, 0):
+            assert lib.of_set_tuning(8, form) == 0
+            y = torch.full((n, d.ho, d.wo, cout), 7.0, device="cuda")
+            z = torch.full((n, d.ho, d.wo, cout), 7.0, device="cuda")
+            lib.of_timing_enable(1)
+            call(fent, C.byref(d), P(xd), cin, P(wf), P(bd), P(gd), P(bed), P(mud), P(vard), 1e-3,
+                 None, 0, ACT_RELU, 0.0, P(z), cout, P(y), cout, P(ws), fws, st)
+            torch.cuda.synchronize()
+            lib.of_timing_enable(0)
+            kk = (C.c_int * 16)()
+            fl = (C.c_double * 16)()
+            ms = (C.c_float * 16)()
+            cnt = lib.of_timing_read(16, kk, fl, ms)
+            kinds.append({kk[i] for i in range(cnt)})
+            outs.append((y, z))
+    finally:
+        lib.of_set_tuning(8, 1)
+        lib.of_timing_enable(0)
+    assert kinds[0] == {184} and kinds[1] == {184} and 184 not in kinds[2], kinds
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    zref = R.conv2d_same(f64(x), f64(wp), f64(b), 2)
+    yref = torch.relu((zref - f64(mu)) / torch.sqrt(f64(var) + 1e-3) * f64(g) + f64(be))
+    for (y, z) in outs:
+        assert rel_inf(z, zref) < 5e-6 and rel_inf(y, yref) < 5e-6, (rel_inf(z, zref), rel_inf(y, yref))
+    assert rel_l2(outs[0][0], yref) < 3 * rel_l2(outs[2][0], yref) + 1e-7
+
+
 @pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
     # kinds: 128 + 8 mode + cfg; wgrad 144 + cfg (3-tap form) / 148 + cfg (9-tap x3b form)
     ("tall128", 8, 128, 256, 128, 128, {128, 136, 148}),  # 8 x 32 tiles, BN 128 (1024 tiles)
@@ -489,6 +546,9 @@ def test_conv_gemm_vec_epilogue(n, h, w, cin, cout, k, s, prec, monkeypatch):
     act_src = dev(rng_tensor((n, h, w, cin), 70))
     add = dev(rng_tensor((n, h, w, cin), 71))
     wf, wd = layer.packed(d)
+    # the stem shape: conv_gemm_x3 in both arms (conv_stem_x3 has the 16-byte epilogue only;
+    # test_conv_stem_x3 covers it), of_set_tuning key 8 restored below
+    assert lib.of_set_tuning(8, 0) == 0
     fws = getattr(lib, "of_conv2d_fwd%s_workspace" % sfx)(C.byref(d))
     dws = getattr(lib, "of_conv2d_dgrad%s_workspace" % sfx)(C.byref(d))
     wws = getattr(lib, "of_conv2d_wgrad%s_workspace" % sfx)(C.byref(d))
@@ -517,6 +577,7 @@ def test_conv_gemm_vec_epilogue(n, h, w, cin, cout, k, s, prec, monkeypatch):
             outs.append((y, z, dx, dx2, dw, db))
     finally:
         lib.of_set_tuning(3, 1)
+        lib.of_set_tuning(8, 1)
     for name, a1, a0 in zip(("y", "z", "dx", "dx_add", "dw", "db"), *outs):
         assert torch.equal(a1, a0), (name, (a1 - a0).abs().max().item())
     zref = R.conv2d_same(f64(x), f64(wt), f64(b), s)
