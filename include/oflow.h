@@ -309,8 +309,11 @@ int of_timing_enable(int on);
  * Cout (2) or never (0: the 3-tap form), key 5 = its wave shape, 16 MI input x 32 / MI output
  * channels (MI = 1 default, or 2), key 6 = the other shapes' fp32 weight gradient (stem,
  * stride 2, 1x1) on the split-bf16 implicit GEMM (1, default) or the fp32 MFMA GEMM (0),
- * key 7 = the feature-warp backward with its scatter aggregated per tile in LDS (1, default)
- * or with LDS aggregation of the clipped border corners only (0). */
+ * key 7 = the feature-warp backward as a per-tile gather (counting sort of the tile's corner
+ * destinations in LDS, one atomic add per touched destination; 1, default) or with LDS
+ * aggregation of the clipped border corners only (0), key 8 = the 7x7 stride-2 stem forward
+ * (of_conv2d_fwd_x3) on its own split kernel with two 32-channel workgroups per CU (1,
+ * default), one 64-channel workgroup (2), or on the generic split implicit GEMM (0). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -94,5 +94,6 @@ def test_bench_kernel_symbols_match_pmc_keys():
             names.add(bench.kernel_symbol(160 + mode * 8 + cfg))
     for cfg in bench.GX3_WG:
         names.add(bench.kernel_symbol(176 + cfg))
+    names.add(bench.kernel_symbol(bench.KIND_STEM_X3))
     x3_keys = {k for k in keys if "_x3<" in k or "_x3b<" in k}
     assert x3_keys and x3_keys <= names, sorted(x3_keys - names)
