@@ -9,7 +9,13 @@ namespace oflow {
 // a wave reads whole contiguous pixel rows), 4 pixels in flight per thread; the workgroup
 // writes one partial row.  Pass 2: every channel's partial rows summed in a fixed order by a
 // 64-channel x 4-row workgroup -> bitwise reproducible, no atomics.
-constexpr int RED_TARGET_BLOCKS = 512;
+#ifndef RED_BLOCKS
+#define RED_BLOCKS 512
+#endif
+#ifndef BNP_UNROLL
+#define BNP_UNROLL 4   // 4 pixel rows of 3 float4 loads in flight per thread (2: -8 % on the step's BN backward)
+#endif
+constexpr int RED_TARGET_BLOCKS = RED_BLOCKS;
 
 struct RedGeo {
   int qw;       // channel quads per row (<= 64)
@@ -146,7 +152,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_partial(
                                   rsqrtf(vr.w + eps));
     const float4 sc = make_float4(gm.x * is.x, gm.y * is.y, gm.z * is.z, gm.w * is.w);
     const bool relu = act == OF_ACT_RELU;
-#pragma unroll 2
+#pragma unroll BNP_UNROLL
     for (int64_t p = p0 + r; p < p1; p += rows) {
       const int64_t o = p * c + ch;
       const float4 g = *reinterpret_cast<const float4*>(dy + o);
