@@ -277,7 +277,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
   // XCD-aware bijective remap: consecutive work ids -> one XCD's L2 (cdna guide T1).
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  // Stride-2 input gradients (phase groups of 4 / 2 / 2 / 1 taps, contiguous in the tile
+  // space) skip the XCD remap: it would hand each XCD the tiles of one or two groups (the
+  // 4-tap group's XCDs then run 1.8x the average), while block order deals every group
+  // evenly over the 8 XCDs and starts the longest tiles first.
+  const int wgid = a.phase ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   // work id = split * tiles_total + tile: all tiles of one K slice are consecutive.
   const int split = wgid / a.tiles_total;
   const int tile = wgid - split * a.tiles_total;
@@ -694,7 +698,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  // Stride-2 input gradients (phase groups of 4 / 2 / 2 / 1 taps, contiguous in the tile
+  // space) skip the XCD remap: it would hand each XCD the tiles of one or two groups (the
+  // 4-tap group's XCDs then run 1.8x the average), while block order deals every group
+  // evenly over the 8 XCDs and starts the longest tiles first.
+  const int wgid = a.phase ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int split = wgid / a.tiles_total;
   const int tile = wgid - split * a.tiles_total;
   const int tile_n = tile % a.n_tiles;
@@ -1721,7 +1729,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_gemm_x3(GemmAr
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  // Stride-2 input gradients (phase groups of 4 / 2 / 2 / 1 taps, contiguous in the tile
+  // space) skip the XCD remap: it would hand each XCD the tiles of one or two groups (the
+  // 4-tap group's XCDs then run 1.8x the average), while block order deals every group
+  // evenly over the 8 XCDs and starts the longest tiles first.
+  const int wgid = a.phase ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int split = wgid / a.tiles_total;
   const int tile = wgid - split * a.tiles_total;
   const int tile_n = tile % a.n_tiles;
