@@ -4331,6 +4331,7 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
 int of_set_tuning(int key, int value) {
   if (key == 8 && value >= 0 && value <= 2) { g_stem_x3 = value; return OF_OK; }
   if (key == 7 && (value == 0 || value == 1)) { g_warp_win = value; return OF_OK; }
+  if (key == 9 && value >= 0 && value <= 3) { g_corr_blk = value; return OF_OK; }
   if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }
   if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
   if (key == 3 && (value == 0 || value == 1)) { g_vec_ep = value; return OF_OK; }

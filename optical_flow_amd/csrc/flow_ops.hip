@@ -180,6 +180,205 @@ __global__ __launch_bounds__(256) void corr_slab_sum_kernel(const float* __restr
   }
 }
 
+// ---- register-blocked forward (of_set_tuning key 9 = 1, the default) ---------------------
+// The form above keeps 2 workgroups of 4 waves per CU, each loading a 60 KB halo and then
+// computing, with nothing in flight while it computes: at 192x256x64 it ran 179 us, 4x the
+// HBM time of its operands.  Here:
+//   * tile 8 x 16 pixels; thread = (4 adjacent pixels of a row, offset row i): 28
+//     accumulators (7 column offsets x 4 pixels) over ALL channels, so no cross-lane sums;
+//     per channel quad 4 f1 + 10 f2 ds_read_b128 feed 56 v_pk_fma_f32 (the form above: 1:1);
+//   * 32-channel slabs; the workgroup is persistent over (tile, slab group) items and the next
+//     slab's f1 tile + f2 halo are loaded into registers while the current slab computes;
+//   * small levels (few tiles, many channels) split the slabs into groups whose partial sums
+//     corr_slab_sum_kernel adds in group order (deterministic).
+// LDS: halo rows of 25 pixels (pitch = 1 mod 4) and f1 rows of 17, both 36 floats a pixel:
+// the ds_read_b128 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} hold tile rows with
+// distinct (row mod 4), which with 4-pixel column steps puts their 16 pixels on 16 distinct
+// 16-byte bank slots.  70 KB: two workgroups per CU.
+// Measured (kernel trace, batch 8, concat form): 192x256x64 168 -> 122 us, 96x128x64 46 -> 38,
+// 48x64x128 46 -> 22 + 12 (slab sum).  Both forms are bound by the HBM stream (f1, f2 with
+// the 14 x 22 / 8 x 16 halo re-reads, the 116-channel concat rows written: ~4.3 TB/s).
+constexpr int CB_Y = 8, CB_X = 16, CB_PIX = CB_Y * CB_X, CB_QX = CB_X / 4, CB_NQ = CB_Y * CB_QX;
+constexpr int CB_SC = 32, CB_PS = CB_SC + 4;                 // slab channels, LDS pixel stride
+constexpr int CB_HY = CB_Y + 6, CB_HX = CB_X + 6, CB_HXP = 25, CB_F1P = CB_X + 1;
+constexpr int CB_NT = CB_NQ * 7;                             // 224 threads
+constexpr int CB_HQ = CB_HY * CB_HX * (CB_SC / 4), CB_HU = (CB_HQ + CB_NT - 1) / CB_NT;
+constexpr int CB_FQ = CB_PIX * (CB_SC / 4), CB_FU = (CB_FQ + CB_NT - 1) / CB_NT;
+constexpr int CB_LDS_HALO = CB_HY * CB_HXP * CB_PS, CB_LDS_F1 = CB_Y * CB_F1P * CB_PS;
+static_assert(CB_PIX * 49 <= CB_LDS_HALO, "epilogue staging reuses the halo region");
+
+struct CorrBlkArgs {
+  CorrFwdArgs a;
+  int slabs;          // ceil(c / 32)
+  int spg, groups;    // slabs per group, groups per tile
+  int tiles_x, tiles_y, items;
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(CB_NT, 2) void corr_fwd_blk(CorrBlkArgs p) {
+  __shared__ float4 lds4[(CB_LDS_HALO + CB_LDS_F1) / 4];
+  float* hal = reinterpret_cast<float*>(lds4);
+  float* f1s = hal + CB_LDS_HALO;
+  const CorrFwdArgs& a = p.a;
+  const int h = a.h, w = a.w, tid = threadIdx.x;
+  const int tiles = p.tiles_x * p.tiles_y;
+  const int64_t npix_all = (int64_t)(p.items / (tiles * p.groups)) * h * w;
+  constexpr bool vec = VEC;
+  // compute role
+  const int oi = tid >> 5, qd = tid & 31;
+  const int cty = qd / CB_QX, ctx = (qd % CB_QX) * 4;
+  const int f1b = (cty * CB_F1P + ctx) * CB_PS, f2b = ((cty + oi) * CB_HXP + ctx) * CB_PS;
+
+  float4 hv[CB_HU], fv[CB_FU];
+  auto decode = [&](int it, int s, int& b, int& y0, int& x0, int& g, int& c_lo) {
+    g = it % p.groups;
+    const int r = it / p.groups, tl = r % tiles;
+    b = r / tiles;
+    y0 = (tl / p.tiles_x) * CB_Y, x0 = (tl % p.tiles_x) * CB_X;
+    c_lo = (g * p.spg + s) * CB_SC;
+  };
+  auto load = [&](int it, int s) {
+    int b, y0, x0, g, c_lo;
+    decode(it, s, b, y0, x0, g, c_lo);
+    const int cs = min(CB_SC, a.c - c_lo);
+    const int64_t img = (int64_t)b * h * w;
+    const rsrc_t r1 = make_rsrc(a.f1 + img * a.ld1, (int64_t)h * w * a.ld1 * 4);
+    const rsrc_t r2 = make_rsrc(a.f2 + img * a.ld2, (int64_t)h * w * a.ld2 * 4);
+#pragma unroll
+    for (int u = 0; u < CB_HU; ++u) {
+      const int q = tid + CB_NT * u;
+      const int hp = q >> 3, cq = q & 7;
+      const int sy = y0 - 3 + hp / CB_HX, sx = x0 - 3 + hp % CB_HX;
+      const bool ok = q < CB_HQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
+      hv[u] = bload_quad(r2, ok, 4 * ((sy * w + sx) * a.ld2 + c_lo + 4 * cq), cs - 4 * cq, vec);
+    }
+#pragma unroll
+    for (int u = 0; u < CB_FU; ++u) {
+      const int q = tid + CB_NT * u;
+      const int pp = q >> 3, cq = q & 7;
+      const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X;
+      const bool ok = q < CB_FQ && sy < h && sx < w;
+      fv[u] = bload_quad(r1, ok, 4 * ((sy * w + sx) * a.ld1 + c_lo + 4 * cq), cs - 4 * cq, vec);
+    }
+  };
+
+  // Persistent walk, XCD-aware: the workgroups of one XCD (blockIdx % 8) walk one contiguous
+  // eighth of the items, so tiles that share halo rows are in flight on the same L2.
+  const int nx = (gridDim.x >= 64 && (gridDim.x & 7) == 0) ? 8 : 1;
+  const int part = blockIdx.x % nx, per = gridDim.x / nx, chunk = (p.items + nx - 1) / nx;
+  auto valid = [&](int l) { return l < chunk && part * chunk + l < p.items; };
+  int lt = blockIdx.x / nx, s = 0;
+  if (!valid(lt)) return;                          // uniform over the workgroup
+  int it = part * chunk + lt;
+  load(it, s);
+  f32x2 acc[28];
+  for (;;) {
+    int b, y0, x0, g, c_lo;
+    decode(it, s, b, y0, x0, g, c_lo);
+    const int64_t img = (int64_t)b * h * w;
+    // install the loaded slab
+#pragma unroll
+    for (int u = 0; u < CB_HU; ++u) {
+      const int q = tid + CB_NT * u;
+      const int hp = q >> 3, cq = q & 7;
+      if (q < CB_HQ)
+        *reinterpret_cast<float4*>(&hal[((hp / CB_HX) * CB_HXP + hp % CB_HX) * CB_PS + 4 * cq]) = hv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < CB_FU; ++u) {
+      const int q = tid + CB_NT * u;
+      const int pp = q >> 3, cq = q & 7;
+      if (q < CB_FQ) {
+        *reinterpret_cast<float4*>(&f1s[((pp / CB_X) * CB_F1P + pp % CB_X) * CB_PS + 4 * cq]) = fv[u];
+        if (a.cat) {                                 // f1 slice of the concat row
+          const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X, ch = c_lo + 4 * cq;
+          const int n = a.c - ch;
+          if (sy < h && sx < w && n > 0) {
+            float* dst = a.cat + (img + sy * w + sx) * a.ldcv + ch;
+            if (vec) {
+              *reinterpret_cast<float4*>(dst) = fv[u];
+            } else {
+              const float t[4] = {fv[u].x, fv[u].y, fv[u].z, fv[u].w};
+#pragma unroll
+              for (int k = 0; k < 4; ++k)
+                if (k < n) dst[k] = t[k];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // next step, prefetched while this slab computes
+    const int nsl = min(p.slabs - g * p.spg, p.spg);
+    int nlt = lt, ns = s + 1;
+    if (ns == nsl) nlt = lt + per, ns = 0;
+    const bool more = valid(nlt);
+    const int nit = part * chunk + nlt;
+    if (more) load(nit, ns);
+    if (s == 0) {
+#pragma unroll
+      for (int k = 0; k < 28; ++k) acc[k] = f32x2{0.f, 0.f};
+    }
+#pragma unroll 2
+    for (int c4 = 0; c4 < CB_SC / 4; ++c4) {
+      float4 fa[4], wv[10];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) fa[m] = *reinterpret_cast<const float4*>(&f1s[f1b + m * CB_PS + 4 * c4]);
+#pragma unroll
+      for (int j = 0; j < 10; ++j) wv[j] = *reinterpret_cast<const float4*>(&hal[f2b + j * CB_PS + 4 * c4]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+          acc[m * 7 + j] = __builtin_elementwise_fma(f32x2{fa[m].x, fa[m].y},
+                                                     f32x2{wv[m + j].x, wv[m + j].y}, acc[m * 7 + j]);
+          acc[m * 7 + j] = __builtin_elementwise_fma(f32x2{fa[m].z, fa[m].w},
+                                                     f32x2{wv[m + j].z, wv[m + j].w}, acc[m * 7 + j]);
+        }
+      }
+    }
+    __syncthreads();                               // halo / f1 tile no longer read
+    if (ns == 0) {                                 // last slab of the item: epilogue
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < 7; ++j)
+          hal[(cty * CB_X + ctx + m) * 49 + oi * 7 + j] = acc[m * 7 + j].x + acc[m * 7 + j].y;
+      __syncthreads();
+      float* out;
+      int64_t ld;
+      if (p.groups == 1) {
+        out = a.cv, ld = a.ldcv;
+      } else {
+        out = a.part + g * npix_all * 49, ld = 49;
+      }
+      for (int q = tid; q < CB_PIX * 49; q += CB_NT) {
+        const int pp = q / 49, k = q - pp * 49;
+        const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X;
+        if (sy < h && sx < w) out[(img + sy * w + sx) * ld + k] = hal[q];
+      }
+      if (a.cat && g == 0) {                       // flow and zero channel padding
+        for (int pp = tid; pp < CB_PIX; pp += CB_NT) {
+          const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X;
+          if (sy >= h || sx >= w) continue;
+          const int64_t pl = img + sy * w + sx;
+          float* row = a.cat + pl * a.ldcv;
+          int ch = a.c + 49;
+          if (a.flow) {
+            row[ch] = a.flow[2 * pl];
+            row[ch + 1] = a.flow[2 * pl + 1];
+            ch += 2;
+          }
+          for (; ch < a.ldcv; ++ch) row[ch] = 0.f;
+        }
+      }
+      __syncthreads();                             // staging read before the next install
+    }
+    if (!more) break;
+    lt = nlt, it = nit, s = ns;
+  }
+}
+
 // Gradient of the cost volume w.r.t. one input (gather form, no atomics):
 //   SIGN=+1 (df1): df[p][c] = init[p][c] + sum_k g[p][k]       * src[p + d_k][c]   (src = f2)
 //   SIGN=-1 (df2): df[q][c] = init[q][c] + sum_k g[q - d_k][k] * src[q - d_k][c]   (src = f1)
@@ -333,6 +532,162 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
           if (k < cs - ch) o[k] = acc[4 * e + k];
       }
     }
+  }
+}
+
+// ---- register-blocked backward (of_set_tuning key 9 bit 1, the default) -------------------
+// Same tile, slab and halo image as corr_fwd_blk; thread = (4 adjacent pixels, one channel
+// quad of the slab), 256 threads.  The tile's 49 x 128 coefficients sit in LDS [k][pixel]
+// (loaded once per tile, lanes over pixels: conflict-free b32 writes, and the b128 reads of
+// 4 pixels' coefficients hit 16 distinct slots); per offset row, 10 src quads + 7 coefficient
+// quads feed 112 FMAs (the form above: 4 per 5 loads).  Slabs are independent outputs, so
+// items are (tile, slab group) without partial sums; the next slab's src halo, the init
+// values and (for a new tile) the coefficients are loaded into registers while the current
+// slab computes.  75 KB of LDS: two workgroups per CU.
+// Measured slower than corr_bwd_kernel (192x256x64, both inputs: 266 vs 255 us; the
+// coefficient rows and the src halo stream at the same ~4.3 TB/s), so it is not the default.
+constexpr int CBB_NT = CB_NQ * (CB_SC / 4);                  // 256 threads
+constexpr int CBB_HU = (CB_HQ + CBB_NT - 1) / CBB_NT;
+constexpr int CBB_GQ = 49 * CB_PIX, CBB_GU = (CBB_GQ + CBB_NT - 1) / CBB_NT;
+
+template <int SIGN, bool VEC>
+__global__ __launch_bounds__(CBB_NT, 2) void corr_bwd_blk(CorrBwdArgs a, int slabs, int spg,
+                                                          int groups, int items) {
+  __shared__ float4 lds4[(CB_LDS_HALO + 49 * CB_PIX) / 4];
+  float* hal = reinterpret_cast<float*>(lds4);
+  float* G = hal + CB_LDS_HALO;
+  const int h = a.h, w = a.w, tid = threadIdx.x;
+  const int tiles = a.tiles_x * a.tiles_y;
+  constexpr bool vec = VEC;
+  const int qd = tid & 31, c4 = tid >> 5;
+  const int cty = qd / CB_QX, ctx = (qd % CB_QX) * 4;
+
+  float4 hv[CBB_HU], iv[4];
+  float gv[CBB_GU];
+  auto decode = [&](int it, int s, int& b, int& y0, int& x0, int& c_lo) {
+    const int g = it % groups, r = it / groups, tl = r % tiles;
+    b = r / tiles;
+    y0 = (tl / a.tiles_x) * CB_Y, x0 = (tl % a.tiles_x) * CB_X;
+    c_lo = (g * spg + s) * CB_SC;
+  };
+  auto load = [&](int it, int s) {
+    int b, y0, x0, c_lo;
+    decode(it, s, b, y0, x0, c_lo);
+    const int cs = min(CB_SC, a.c - c_lo);
+    const int64_t img = (int64_t)b * h * w;
+    const rsrc_t rs = make_rsrc(a.src + img * a.lds, (int64_t)h * w * a.lds * 4);
+#pragma unroll
+    for (int u = 0; u < CBB_HU; ++u) {
+      const int q = tid + CBB_NT * u;
+      const int hp = q >> 3, cq = q & 7;
+      const int sy = y0 - 3 + hp / CB_HX, sx = x0 - 3 + hp % CB_HX;
+      const bool ok = q < CB_HQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
+      hv[u] = bload_quad(rs, ok, 4 * ((sy * w + sx) * a.lds + c_lo + 4 * cq), cs - 4 * cq, vec);
+    }
+    const rsrc_t ri = make_rsrc(a.init ? a.init + img * a.ldinit : nullptr,
+                                a.init ? (int64_t)h * w * a.ldinit * 4 : 0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int sy = y0 + cty, sx = x0 + ctx + m;
+      iv[m] = bload_quad(ri, sy < h && sx < w, 4 * ((sy * w + sx) * a.ldinit + c_lo + 4 * c4),
+                         cs - 4 * c4, vec);
+    }
+    if (s == 0) {                                  // coefficients of a new tile
+      const rsrc_t rg = make_rsrc(a.g + img * a.ldg, (int64_t)h * w * a.ldg * 4);
+#pragma unroll
+      for (int u = 0; u < CBB_GU; ++u) {
+        const int q = tid + CBB_NT * u;
+        const int k = q / CB_PIX, pp = q % CB_PIX;
+        int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X;
+        const bool in = sy < h && sx < w;
+        if (SIGN < 0) sy -= k / 7 - 3, sx -= k % 7 - 3;   // g[p - d_k][k]
+        const bool ok = q < CBB_GQ && in && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
+        gv[u] = bload1(rg, ok ? 4 * ((sy * w + sx) * a.ldg + k) : kOOB);
+      }
+    }
+  };
+
+  // Persistent walk, XCD-aware: the workgroups of one XCD (blockIdx % 8) walk one contiguous
+  // eighth of the items, so tiles that share halo rows are in flight on the same L2.
+  const int nx = (gridDim.x >= 64 && (gridDim.x & 7) == 0) ? 8 : 1;
+  const int part = blockIdx.x % nx, per = gridDim.x / nx, chunk = (items + nx - 1) / nx;
+  auto valid = [&](int l) { return l < chunk && part * chunk + l < items; };
+  int lt = blockIdx.x / nx, s = 0;
+  if (!valid(lt)) return;                          // uniform over the workgroup
+  int it = part * chunk + lt;
+  load(it, s);
+  for (;;) {
+    int b, y0, x0, c_lo;
+    decode(it, s, b, y0, x0, c_lo);
+    const int cs = min(CB_SC, a.c - c_lo);
+    const int64_t img = (int64_t)b * h * w;
+#pragma unroll
+    for (int u = 0; u < CBB_HU; ++u) {
+      const int q = tid + CBB_NT * u;
+      const int hp = q >> 3, cq = q & 7;
+      if (q < CB_HQ)
+        *reinterpret_cast<float4*>(&hal[((hp / CB_HX) * CB_HXP + hp % CB_HX) * CB_PS + 4 * cq]) = hv[u];
+    }
+    if (s == 0) {
+#pragma unroll
+      for (int u = 0; u < CBB_GU; ++u) {
+        const int q = tid + CBB_NT * u;
+        if (q < CBB_GQ) G[q] = gv[u];
+      }
+    }
+    f32x2 acc[8];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      acc[2 * m] = f32x2{iv[m].x, iv[m].y};
+      acc[2 * m + 1] = f32x2{iv[m].z, iv[m].w};
+    }
+    __syncthreads();
+    const int gid = it % groups;
+    const int nsl = min(slabs - gid * spg, spg);
+    int nlt = lt, ns = s + 1;
+    if (ns == nsl) nlt = lt + per, ns = 0;
+    const bool more = valid(nlt);
+    const int nit = part * chunk + nlt;
+    if (more) load(nit, ns);
+#pragma unroll 1
+    for (int i = 0; i < 7; ++i) {
+      const int oy = SIGN > 0 ? i : 6 - i;
+      const float* wb = &hal[((cty + oy) * CB_HXP + ctx) * CB_PS + 4 * c4];
+      float4 wv[10];
+#pragma unroll
+      for (int j = 0; j < 10; ++j) wv[j] = *reinterpret_cast<const float4*>(wb + j * CB_PS);
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        const float4 gq = *reinterpret_cast<const float4*>(&G[(i * 7 + j) * CB_PIX + cty * CB_X + ctx]);
+        const int ox = SIGN > 0 ? j : 6 - j;
+        const float gm[4] = {gq.x, gq.y, gq.z, gq.w};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const float4 v = wv[m + ox];
+          acc[2 * m] = __builtin_elementwise_fma(f32x2{gm[m], gm[m]}, f32x2{v.x, v.y}, acc[2 * m]);
+          acc[2 * m + 1] = __builtin_elementwise_fma(f32x2{gm[m], gm[m]}, f32x2{v.z, v.w}, acc[2 * m + 1]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int sy = y0 + cty, sx = x0 + ctx + m, ch = 4 * c4;
+      if (sy < h && sx < w && ch < cs) {
+        float* o = a.df + (img + sy * w + sx) * a.lddf + c_lo + ch;
+        if (vec) {
+          *reinterpret_cast<float4*>(o) = make_float4(acc[2 * m].x, acc[2 * m].y, acc[2 * m + 1].x,
+                                                      acc[2 * m + 1].y);
+        } else {
+          const float t[4] = {acc[2 * m].x, acc[2 * m].y, acc[2 * m + 1].x, acc[2 * m + 1].y};
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k < cs - ch) o[k] = t[k];
+        }
+      }
+    }
+    __syncthreads();                               // halo / coefficients no longer read
+    if (!more) break;
+    lt = nlt, it = nit, s = ns;
   }
 }
 
@@ -588,6 +943,7 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
 // exceeds WG_CAP slots adds each corner's row straight to global memory.
 constexpr int WG_T = 8, WG_CAP = 1024, WG_NT = 256;
 int g_warp_win = 1;   // of_set_tuning key 7: warp_bwd_gather (1) or warp_bwd_agg (0)
+int g_corr_blk = 1;   // of_set_tuning key 9: bit 0 corr_fwd_blk (else corr_fwd_kernel), bit 1 corr_bwd_blk
 
 __device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes of a DPP row
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
@@ -1057,19 +1413,58 @@ extern "C" {
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// Slab groups of the register-blocked forward: the fewest that give >= 512 (tile, group)
+// items, one per workgroup slot of the persistent grid (96x128x64: one group of 768 tiles
+// ran 38 us + no slab sum against 38 + 12 us with two groups).
+static void corr_blk_plan(int n, int h, int w, int c, CorrBlkArgs& p) {
+  p.slabs = (int)cdiv(c, CB_SC);
+  p.tiles_x = (int)cdiv(w, CB_X), p.tiles_y = (int)cdiv(h, CB_Y);
+  const int64_t tiles = (int64_t)n * p.tiles_x * p.tiles_y;
+  const int want = (int)std::min<int64_t>(p.slabs, std::max<int64_t>(1, cdiv(512, tiles)));
+  p.spg = (int)cdiv(p.slabs, want);
+  p.groups = (int)cdiv(p.slabs, p.spg);
+  p.items = (int)(tiles * p.groups);
+}
+
+// Persistent grid: two workgroups per CU, a multiple of 8 (one partition per XCD) from 64 up.
+static int corr_blk_grid(int items) {
+  const int g = std::min(items, 2 * 256);
+  return g >= 64 ? g & ~7 : g;
+}
+
 static size_t corr_fwd_ws(int n, int h, int w, int c) {
   const int slabs = (int)cdiv(c, CSLAB);
-  return slabs > 1 ? (size_t)slabs * n * h * w * 49 * sizeof(float) : 0;
+  CorrBlkArgs p{};
+  corr_blk_plan(n, h, w, c, p);
+  const int parts = std::max(slabs > 1 ? slabs : 0, p.groups > 1 ? p.groups : 0);
+  return (size_t)parts * n * h * w * 49 * sizeof(float);
 }
 
 static int corr_fwd_launch(CorrFwdArgs a, int n, void* ws, size_t ws_bytes, void* stream) {
   OF_CHECK_ARG((int64_t)a.h * a.w * std::max(std::max(a.ld1, a.ld2), a.ldcv) < (1LL << 29),
                "corr: one image must hold < 2^29 elements (32-bit buffer offsets)");
-  a.slabs = (int)cdiv(a.c, CSLAB);
   const size_t need = corr_fwd_ws(n, a.h, a.w, a.c);
   OF_CHECK_ARG(ws_bytes >= need && (need == 0 || ws), "corr fwd: workspace too small");
   a.part = static_cast<float*>(ws);
   hipStream_t s = as_stream(stream);
+  if (g_corr_blk & 1) {
+    CorrBlkArgs p{};
+    p.a = a;
+    corr_blk_plan(n, a.h, a.w, a.c, p);
+    OF_CHECK_ARG((int64_t)n * p.tiles_x * p.tiles_y * p.groups < INT32_MAX, "corr fwd: too many tiles");
+    const int grid = corr_blk_grid(p.items);
+    if (a.vec)
+      hipLaunchKernelGGL(corr_fwd_blk<true>, dim3(grid), dim3(CB_NT), 0, s, p);
+    else
+      hipLaunchKernelGGL(corr_fwd_blk<false>, dim3(grid), dim3(CB_NT), 0, s, p);
+    int st = check_launch("corr_fwd_blk");
+    if (st || p.groups == 1) return st;
+    const int64_t npix = (int64_t)n * a.h * a.w;
+    hipLaunchKernelGGL(corr_slab_sum_kernel, dim3(grid_for(npix * 49)), dim3(256), 0, s, a.part,
+                       p.groups, npix, 49, a.cv, a.ldcv);
+    return check_launch("corr_slab_sum");
+  }
+  a.slabs = (int)cdiv(a.c, CSLAB);
   a.tiles_x = (int)cdiv(a.w, CT_X), a.tiles_y = (int)cdiv(a.h, CT_Y);
   const dim3 grid((unsigned)((int64_t)a.tiles_x * a.tiles_y * n * a.slabs));
   if (a.vec)
@@ -1088,6 +1483,16 @@ static int corr_bwd_launch(int sign, CorrBwdArgs a, int n, hipStream_t s) {
   OF_CHECK_ARG((int64_t)a.h * a.w * std::max(std::max(a.ldg, a.lds), std::max(a.lddf, a.ldinit)) <
                    (1LL << 29),
                "corr: one image must hold < 2^29 elements (32-bit buffer offsets)");
+  if (g_corr_blk & 2) {
+    CorrBlkArgs p{};
+    corr_blk_plan(n, a.h, a.w, a.c, p);
+    a.tiles_x = p.tiles_x, a.tiles_y = p.tiles_y;
+    const int grid = corr_blk_grid(p.items);
+    auto k = sign > 0 ? (a.vec ? corr_bwd_blk<1, true> : corr_bwd_blk<1, false>)
+                      : (a.vec ? corr_bwd_blk<-1, true> : corr_bwd_blk<-1, false>);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(CBB_NT), 0, s, a, p.slabs, p.spg, p.groups, p.items);
+    return check_launch(sign > 0 ? "corr_bwd_blk_f1" : "corr_bwd_blk_f2");
+  }
   a.slabs = (int)cdiv(a.c, CSLAB);
   a.tiles_x = (int)cdiv(a.w, CT_X), a.tiles_y = (int)cdiv(a.h, CT_Y);
   const dim3 grid((unsigned)((int64_t)a.tiles_x * a.tiles_y * n * a.slabs));

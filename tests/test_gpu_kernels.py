@@ -625,8 +625,32 @@ def test_conv_bf16_tall_fwd():
 
 
 # ----------------------------------------------------------------------- cost volume ----
-@pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6), (1, 19, 70, 32)])
-def test_cost_volume(shape):
+CORR_FORM_DEFAULT = 1      # of_set_tuning key 9: bit 0 corr_fwd_blk, bit 1 corr_bwd_blk
+
+
+class _corr_form:
+    """Select the cost-volume kernel forms (key 9) for a block, restoring the default."""
+
+    def __init__(self, form):
+        self.form = form
+
+    def __enter__(self):
+        from optical_flow_amd import _lib
+        assert _lib.lib().of_set_tuning(9, self.form) == 0
+
+    def __exit__(self, *exc):
+        from optical_flow_amd import _lib
+        _lib.lib().of_set_tuning(9, CORR_FORM_DEFAULT)
+
+
+@pytest.mark.parametrize("form", [1, 3, 0])
+@pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6), (1, 19, 70, 32),
+                                   (3, 40, 56, 64), (1, 17, 35, 100)])
+def test_cost_volume(form, shape):
+    """Cost volume and both input gradients against fp64 autograd, for the register-blocked
+    forms (key 9 = 3: persistent grid, slab groups with partial sums on small grids) and the
+    per-pixel forms (key 9 = 0); ragged tiles, channel counts that are not a slab multiple
+    and not a multiple of 4 (scalar loads)."""
     ops = _ops()
     f1, f2 = rng_tensor(shape, 1), rng_tensor(shape, 2)
     a, b = f64(f1).requires_grad_(True), f64(f2).requires_grad_(True)
@@ -634,9 +658,11 @@ def test_cost_volume(shape):
     g = rng_tensor(tuple(cv.shape), 3)
     (cv * f64(g)).sum().backward()
     ad, bd = dev(f1).requires_grad_(True), dev(f2).requires_grad_(True)
-    cvd = ops.cost_volume(ad, bd, 3)
-    assert rel_inf(cvd, cv) < REL_TOL
-    (cvd * dev(g)).sum().backward()
+    with _corr_form(form):
+        cvd = ops.cost_volume(ad, bd, 3)
+        assert rel_inf(cvd, cv) < REL_TOL
+        (cvd * dev(g)).sum().backward()
+        torch.cuda.synchronize()
     assert rel_inf(ad.grad, a.grad) < REL_TOL
     assert rel_inf(bd.grad, b.grad) < REL_TOL
 
@@ -650,11 +676,13 @@ def test_cost_volume(shape):
                                                   (2, 97, 33, 128, 180, True),
                                                   (1, 96, 20, 6, 60, False),
                                                   (1, 4, 8, 128, 180, True),
-                                                  (1, 2, 4, 256, 308, False)])
-def test_corr_concat(n, h, w, c, cp, has_flow):
-    """The fused concat([f1, cost volume, flow]) kernel and its gradient: 2-D tile kernels
-    (h < 96) and strip sweeps (h >= 96), multi-tile and ragged shapes, 1 and 2 channel
-    slabs, with and without flow, float4 and scalar paths."""
+                                                  (1, 2, 4, 256, 308, False),
+                                                  (8, 48, 64, 128, 180, True)])
+@pytest.mark.parametrize("form", [1, 3, 0])
+def test_corr_concat(form, n, h, w, c, cp, has_flow):
+    """The fused concat([f1, cost volume, flow]) kernel and its gradient, for both kernel
+    forms (key 9): multi-tile and ragged shapes, 1 to 8 channel slabs (and slab groups with
+    partial sums), with and without flow, float4 and scalar paths."""
     ops = _ops()
     f1, f2, fl = rng_tensor((n, h, w, c), 4), rng_tensor((n, h, w, c), 5), rng_tensor((n, h, w, 2), 6)
     a, b, fo = [f64(t).requires_grad_(True) for t in (f1, f2, fl)]
@@ -664,13 +692,15 @@ def test_corr_concat(n, h, w, c, cp, has_flow):
     g = rng_tensor(tuple(xo.shape), 7)
     (xo * f64(g)).sum().backward()
     ad, bd, fd = [dev(t).requires_grad_(True) for t in (f1, f2, fl)]
-    xd = ops.corr_concat(ad, bd, fd if has_flow else None, 3, cp)
-    assert rel_inf(xd[..., :used], xo) < REL_TOL
-    assert xd[..., used:].abs().max().item() == 0
-    gd = torch.zeros((n, h, w, cp), device="cuda")
-    gd[..., :used] = dev(g)
-    gd[..., used:] = 1.0        # gradient on the padding must not leak anywhere
-    (xd * gd).sum().backward()
+    with _corr_form(form):
+        xd = ops.corr_concat(ad, bd, fd if has_flow else None, 3, cp)
+        assert rel_inf(xd[..., :used], xo) < REL_TOL
+        assert xd[..., used:].abs().max().item() == 0
+        gd = torch.zeros((n, h, w, cp), device="cuda")
+        gd[..., :used] = dev(g)
+        gd[..., used:] = 1.0        # gradient on the padding must not leak anywhere
+        (xd * gd).sum().backward()
+        torch.cuda.synchronize()
     pairs = ((ad, a), (bd, b)) + (((fd, fo),) if has_flow else ())
     for d_, o_ in pairs:
         assert rel_inf(d_.grad, o_.grad) < REL_TOL

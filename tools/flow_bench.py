@@ -41,8 +41,12 @@ def main():
                     help="std of the random flows in pixels (at init the net's are ~0.1)")
     ap.add_argument("--flow-offset", type=float, default=0.0,
                     help="constant added to both flow channels (large: clipped samples)")
+    ap.add_argument("--corr-form", type=int, default=None,
+                    help="of_set_tuning key 9 (cost-volume kernel forms; default: the library's)")
     args = ap.parse_args()
     _lib.load()
+    if args.corr_form is not None:
+        assert _lib.lib().of_set_tuning(9, args.corr_form) == 0
     n = args.batch
     P = ops._ptr
     st = ops._stream()
