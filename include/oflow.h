@@ -313,7 +313,9 @@ int of_timing_enable(int on);
  * destinations in LDS, one atomic add per touched destination; 1, default) or with LDS
  * aggregation of the clipped border corners only (0), key 8 = the 7x7 stride-2 stem forward
  * (of_conv2d_fwd_x3) on its own split kernel with two 32-channel workgroups per CU (1,
- * default), one 64-channel workgroup (2), or on the generic split implicit GEMM (0). */
+ * default), one 64-channel workgroup (2), or on the generic split implicit GEMM (0), key 9 =
+ * the cost-volume kernel forms (of_corr_*): bit 0 the register-blocked persistent forward
+ * (default 1), bit 1 the register-blocked backward (default off: measured slower). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -64,7 +64,7 @@ def test_train_steps_trajectory():
     trainer = Trainer(net, KerasAdam(net.store, learning_rate=1e-4))
     bd = dev(torch.from_numpy(batch))
     bo = torch.tensor(batch, dtype=torch.float64)
-    for step in range(5):
+    for step in range(10):                        # SURVEY.md §8 d: a 10-step loss trajectory
         lo, _, _ = R.train_step(bo, p, blocks, opt_o)
         ld, _ = trainer.train_step(bd, step)
         rel = abs(ld.item() - lo.item()) / abs(lo.item())
