@@ -4181,6 +4181,9 @@ void wgx3_blocks(const of_conv_desc* d, int& cib, int& cob) {
   cob = c == 0 ? 128 : c == 1 ? 96 : c == 2 ? 64 : 32;
 }
 
+// of_set_tuning key 10: fp32 / bf16 GEMM weight-gradient split-K target workgroups per CU.
+static int g_wgrad_wgs = 4;
+
 WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) {
   Geo g = geo(d);
   WgradPlan p;
@@ -4223,9 +4226,9 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
   const int bk = bf16 ? BKH : BK;
   const int K = d->n * d->ho * d->wo;
   const int tiles = (int)(cdiv(p.M, pick_bm(d->cout)) * cdiv(d->cout, pick_bn(d->cout)));
-  // Fill up to 4 workgroups per CU without overshooting a multiple of the CU count (an
-  // overshoot leaves a few CUs with one extra long-running workgroup: a tail).
-  int splits = std::max(1, (4 * kCUs) / tiles);
+  // Fill up to g_wgrad_wgs (4) workgroups per CU without overshooting a multiple of the CU
+  // count (an overshoot leaves a few CUs with one extra long-running workgroup: a tail).
+  int splits = std::max(1, (g_wgrad_wgs * kCUs) / tiles);
   splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * bk)));
   p.k_per_split = (int)round_up(cdiv(K, splits), bk);
   p.splits = (int)cdiv(K, p.k_per_split);
@@ -4332,6 +4335,7 @@ int of_set_tuning(int key, int value) {
   if (key == 8 && value >= 0 && value <= 2) { g_stem_x3 = value; return OF_OK; }
   if (key == 7 && (value == 0 || value == 1)) { g_warp_win = value; return OF_OK; }
   if (key == 9 && value >= 0 && value <= 3) { g_corr_blk = value; return OF_OK; }
+  if (key == 10 && value >= 1 && value <= 16) { g_wgrad_wgs = value; return OF_OK; }
   if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }
   if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
   if (key == 3 && (value == 0 || value == 1)) { g_vec_ep = value; return OF_OK; }
