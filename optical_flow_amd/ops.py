@@ -95,9 +95,22 @@ def _grad_ready(*params):
 # gradient kernel is ordered before whatever the caller enqueues next.
 SIDE_STREAM_WGRAD = True
 # Only layers with at most this many output pixels put their wgrad on the side stream: the
-# overlap pays where grids underfill the chip (coarse flow levels, encoder stages 3-4); a
-# large layer's dgrad already fills it, and sharing the CUs would only stretch both kernels.
-SIDE_STREAM_MAX_PIX = int(os.environ.get("OFLOW_SIDE_MAX_PIX", "65536"))
+# overlap pays where grids underfill the chip (coarse flow levels, encoder stages 3-4, the
+# H/8 flow level); a large layer's dgrad already fills it, and sharing the CUs would only
+# stretch both kernels.  Measured A/B (tools/gpu_abenv.sh, one box, 2 rounds): fp32 B=8
+# 65536 -> 131072 (adds the 96x128 level) +1.0 %, every wgrad on the side +0.6 %; bf16 B=32
+# 65536 -> 524288 (the same layers at 4x the batch) +2-4 %, 131072 +0.6 %.  Per precision
+# by default (the bf16 kernels are ~2.5x faster per FLOP, so the same layer underfills the
+# chip at 4x the pixels); OFLOW_SIDE_MAX_PIX overrides both.
+_SIDE_ENV = os.environ.get("OFLOW_SIDE_MAX_PIX")
+SIDE_STREAM_MAX_PIX = int(_SIDE_ENV) if _SIDE_ENV else None
+SIDE_MAX_PIX_DEFAULT = {"fp32": 131072, "bf16": 524288}
+
+
+def _side_max_pix(layer) -> int:
+    if SIDE_STREAM_MAX_PIX is not None:
+        return SIDE_STREAM_MAX_PIX
+    return SIDE_MAX_PIX_DEFAULT[layer.precision]
 _SIDE = {}
 _side_armed = False
 
@@ -414,7 +427,7 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
         tbias = grad_target(layer.bias) if (need_b and not bias_done) else (None, 0, None)
         went, wsb = layer.wgrad_entry(d)
         side = (SIDE_STREAM_WGRAD and tk[1] == 1 and (tbias[0] is None or tbias[1] == 1) and
-                d.n * d.ho * d.wo <= SIDE_STREAM_MAX_PIX)
+                d.n * d.ho * d.wo <= _side_max_pix(layer))
         with torch.cuda.stream(side_stream(x, dzp)) if side else contextlib.nullcontext():
             ss = _stream()
             ws = torch.empty(wsb // 4 + 1, device=dz.device)
@@ -687,7 +700,8 @@ class _ConvStackFn(torch.autograd.Function):
             if tk[1] != tb[1]:
                 raise RuntimeError("kernel and bias gradients must both use the arena or not")
             went, wsb = layer.wgrad_entry(d)
-            side = SIDE_STREAM_WGRAD and tk[1] == 1 and d.n * d.ho * d.wo <= SIDE_STREAM_MAX_PIX
+            side = (SIDE_STREAM_WGRAD and tk[1] == 1 and
+                    d.n * d.ho * d.wo <= _side_max_pix(layer))
             with torch.cuda.stream(side_stream(x, g)) if side else contextlib.nullcontext():
                 ws = torch.empty(wsb // 4 + 1, device=x.device)
                 _tag(layer, 2)
