@@ -118,7 +118,7 @@ _side_armed = False
 def _side_join():
     global _side_armed
     _side_armed = False
-    for dev, s in _SIDE.items():
+    for dev, s in list(_SIDE.items()) + list(_CORR_SIDE.items()):
         torch.cuda.current_stream(dev).wait_stream(s)
 
 
@@ -139,6 +139,41 @@ def side_stream(*tensors):
         _side_armed = True
         torch.autograd.Variable._execution_engine.queue_callback(_side_join)
     return s
+
+
+# The cost volume's gradient w.r.t. features1 (of_corr_concat_bwd's df1) is read only by the
+# encoder's backward, which runs after every flow module's: with CORR_DF1_SIDE it runs on a
+# stream of its own beside the decoder's input-gradient chain (df2 -> warp backward -> the
+# coarser level), and the encoder backward waits for that stream (corr_side_wait).
+# Measured A/B (one box): fp32 B=8 587-589 -> 581-586 pairs/s (the main chain's convs already
+# fill the chip; the memory-bound df1 only slows them), bf16 B=32 1353 -> 1363: off by default.
+CORR_DF1_SIDE = os.environ.get("OFLOW_CORR_DF1_SIDE", "0") == "1"
+_CORR_SIDE = {}
+
+
+def corr_side_stream(*tensors):
+    """The df1 stream of the current device, ordered after the current stream's work so far;
+    ``tensors`` are marked in use by it for the caching allocator."""
+    global _side_armed
+    cur = torch.cuda.current_stream()
+    s = _CORR_SIDE.get(cur.device)
+    if s is None:
+        s = _CORR_SIDE[cur.device] = torch.cuda.Stream(cur.device)
+    s.wait_stream(cur)
+    for t in tensors:
+        if t is not None:
+            t.record_stream(s)
+    if not _side_armed:
+        _side_armed = True
+        torch.autograd.Variable._execution_engine.queue_callback(_side_join)
+    return s
+
+
+def corr_side_wait(device):
+    """Order the current stream after the df1 stream (before anything reads a df1)."""
+    s = _CORR_SIDE.get(torch.device(device))
+    if s is not None:
+        torch.cuda.current_stream(device).wait_stream(s)
 
 
 def grad_target(param: torch.Tensor):
@@ -583,6 +618,7 @@ class _EncoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *gouts):
+        corr_side_wait(gouts[0].device if gouts[0] is not None else ctx.saved_tensors[0].device)
         saved = ctx.saved_tensors
         x4, y0, z0 = saved[:3]
         conv1, blocks = ctx.conv1, ctx.blocks
@@ -836,6 +872,21 @@ class _CorrConcat(torch.autograd.Function):
         dflow = None
         if has_flow and ctx.needs_input_grad[2]:
             dflow = torch.empty((n, h, w, 2), device=dx.device)
+        if CORR_DF1_SIDE and dx.is_cuda and _in_slab(ctx.dst[0], df1):
+            # df1 lands in the encoder output's gradient slab: its only reader is the encoder
+            # backward (corr_side_wait there and in _Halves' copy path); a df1 that autograd
+            # would sum with another consumer's gradient stays on the current stream
+            s = _stream()
+            if df2 is not None:
+                call("of_corr_bwd", C.c_void_p(dx.data_ptr() + 4 * c), cp, _ptr(f1), c,
+                     _ptr(f2w), c, n, h, w, c, max_disp, None, c, 0, _ptr(df2), c, 0, s)
+            if dflow is not None:
+                call("of_copy_strided", C.c_void_p(dx.data_ptr() + 4 * (c + nk)), cp,
+                     _ptr(dflow), 2, n * h * w, 2, s)
+            with torch.cuda.stream(corr_side_stream(dx, f1, f2w, df1)):
+                call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c,
+                     max_disp, _ptr(df1), None, None, _stream())
+            return df1, df2, dflow, None, None
         call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c, max_disp,
              _ptr(df1), _ptr(df2), _ptr(dflow), _stream())
         return df1, df2, dflow, None, None
@@ -955,6 +1006,15 @@ def grad_dst(t):
     return getattr(t, "_of_grad_slab", None)
 
 
+def _in_slab(dst, g) -> bool:
+    """True when ``g`` is the GradSlab half that grad_dst() captured (not a fresh tensor
+    handed to a second consumer of the same half)."""
+    if dst is None or dst[0].full is None:
+        return False
+    slab, k = dst
+    return g.data_ptr() == slab.full.data_ptr() + k * (slab.full.numel() // 2) * 4
+
+
 def new_grad(dst, like):
     """Backward-time buffer for an input gradient captured by grad_dst()."""
     if dst is not None:
@@ -986,6 +1046,7 @@ class _Halves(torch.autograd.Function):
                     g1.is_contiguous() and g2.is_contiguous()):
                 return slab.full, None
         dev = (g1 if g1 is not None else g2).device
+        corr_side_wait(dev)                  # a df1 may still be in flight on its stream
         out = torch.empty(shape, device=dev)
         half = out.numel() // 2
         s = _stream()

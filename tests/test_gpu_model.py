@@ -56,6 +56,28 @@ def test_flow_net_forward_backward(H, W, B):
     print("worst grad rel_l2 %.2e" % worst)
 
 
+def test_corr_df1_side_stream(monkeypatch):
+    """ops.CORR_DF1_SIDE (the cost volume's features1 gradient on a stream of its own, joined
+    by the encoder backward): every gradient equal to the single-stream step up to the
+    feature-warp backward's atomic-order noise (a missing join reads stale or partial df1:
+    O(1) errors), large enough (B=4 at 128x256) that the df1 kernels are still in flight when
+    the decoder's chain reaches the encoder."""
+    from optical_flow_amd import ops
+    from optical_flow_amd.loss import LossLayer
+    net, vals, batch, blocks = _setup(128, 256, 4, seed=5)
+    bd = dev(torch.from_numpy(batch))
+    res = []
+    for side in (False, True):
+        monkeypatch.setattr(ops, "CORR_DF1_SIDE", side)
+        net.store.zero_grad()
+        flows = net(bd)
+        LossLayer()(bd, flows).backward()
+        torch.cuda.synchronize()
+        res.append({k: g.detach().clone() for k, g in net.store.grads().items()})
+    for k in res[0]:
+        assert rel_l2(res[1][k], res[0][k]) < 1e-5, k
+
+
 def test_train_steps_trajectory():
     from optical_flow_amd.train import KerasAdam, Trainer
     net, vals, batch, blocks = _setup(64, 128, 2, seed=3)
