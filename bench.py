@@ -56,6 +56,8 @@ def kind_parts(kind):
     fam = ("gemm_x3" if kind >= 160 else "tile_x3" if kind >= 128 else "tile_bf16" if kind >= 96 else
            "bf16" if kind >= 64 else
            "tile_f32" if kind >= 32 else "f32")
+    if fam == "tile_x3" and kind >= 152:          # conv_wgrad_tile_x3b configs 8+ (cfg 4 of
+        return 2, 8 + kind - 152, fam             # the C dispatch: 32 x 64 channel blocks)
     return (kind % 32) // 8, kind % 8, fam
 
 
@@ -68,7 +70,8 @@ X3_NB = {4: 1}                                                             # sin
 GX3 = {0: "128, 128, 4, 2", 1: "256, 64, 8, 1"}   # conv_gemm_x3<BM, BN, WAVES_M, WAVES_N>
 GX3_WG = {0: "128, 128, 4, 2", 1: "128, 64, 4, 2"}  # conv_wgrad_x3<BM, BN, WAVES_M, WAVES_N>
 X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4",   # conv_wgrad_tile_x3<CI, CO, R, rows>
-          4: "2, 4, 8, 1", 5: "2, 3, 8, 1", 6: "4, 2, 4, 1", 7: "4, 1, 4, 1"}  # conv_wgrad_tile_x3b<CI, CO, rows, MI>
+          4: "2, 4, 8, 1", 5: "2, 3, 8, 1", 6: "4, 2, 4, 1", 7: "4, 1, 4, 1",  # conv_wgrad_tile_x3b<CI, CO, rows, MI>
+          8: "2, 2, 8, 1"}
 
 
 WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>

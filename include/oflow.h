@@ -315,7 +315,10 @@ int of_timing_enable(int on);
  * (of_conv2d_fwd_x3) on its own split kernel with two 32-channel workgroups per CU (1,
  * default), one 64-channel workgroup (2), or on the generic split implicit GEMM (0), key 9 =
  * the cost-volume kernel forms (of_corr_*): bit 0 the register-blocked persistent forward
- * (default 1), bit 1 the register-blocked backward (default off: measured slower). */
+ * (default 1), bit 1 the register-blocked backward (default off: measured slower), key 10 =
+ * the fp32 / bf16 GEMM weight gradients' split-K target workgroups per CU (1-16, default 4),
+ * key 11 = the split weight gradient of Cout-64 layers whose Cin is not a multiple of 64 on
+ * 32 x 64 channel blocks (1, default) or on 64 x 64 blocks (0). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -2434,7 +2434,7 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
 // a pixel) straight from L2 one k-step ahead and splits it in registers (the three kernel-row
 // waves of a channel block read the same dy lines).  Output: the split-K slabs of the other wgrad kernels.
 // conv_wgrad_tile_x3 pixel tiles: XH rows x 16 px (8 rows where the halo fits LDS)
-int wgx3_rows(int cfg) { return cfg >= 2 ? 4 : 8; }
+int wgx3_rows(int cfg) { return cfg == 2 || cfg == 3 ? 4 : 8; }
 
 __device__ __forceinline__ void split3x8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
   uint2 h0, m0, l0, h1, m1, l1;
@@ -3904,6 +3904,9 @@ static int g_wgx3b = 1;
 // MI = 2 halves the dy loads and splits per MFMA and measured the same (dec3.c1 0.516 vs
 // 0.517 ms): the split VALU is not what bounds the kernel.
 static int g_wgx3b_mi = 1;
+// of_set_tuning key 11: the 32 x 64 channel-block weight gradient (cfg 4) for Cout 64 layers
+// whose Cin is not a multiple of 64 (1, default) or the 64 x 64 blocks (0).
+static int g_wgx3_c4 = 1;
 // of_set_tuning key 6: the other shapes' fp32 weight gradient on the split-bf16 implicit GEMM
 // (conv_wgrad_x3, 1) or on the fp32 MFMA GEMM (0).
 static int g_wgx3_gemm = 1;
@@ -4169,16 +4172,19 @@ void wgt_blocks(const of_conv_desc* d, int& cib, int& cob) {
 
 // fp32 wgrad on conv_wgrad_tile_x3, 3x3 stride 1, by Cout: channel blocks (CIB x COB)
 // 32 x 128 (cfg 0, Cout % 128 == 0), 32 x 96 (cfg 1, Cout 96), 64 x 64 (cfg 2, Cout 64),
-// 64 x 32 (cfg 3, Cout 32); other layers keep the fp32 wgrad kernels.
+// 64 x 32 (cfg 3, Cout 32), 32 x 64 (cfg 4: Cout 64 with Cin not a multiple of 64 -- the
+// 96 -> 64 flow-head convs, whose second 64-channel input block was half empty; 9-tap form
+// only); other layers keep the fp32 wgrad kernels.
 int wgx3_cfg(const of_conv_desc* d) {
   if (!tile_ok(d)) return -1;
-  return d->cout % 128 == 0 ? 0 : d->cout == 96 ? 1 : d->cout == 64 ? 2 : d->cout == 32 ? 3 : -1;
+  if (d->cout == 64) return d->cin_p % 64 == 0 || !g_wgx3_c4 ? 2 : 4;
+  return d->cout % 128 == 0 ? 0 : d->cout == 96 ? 1 : d->cout == 32 ? 3 : -1;
 }
 bool wgx3_ok(const of_conv_desc* d) { return wgx3_cfg(d) >= 0; }
 void wgx3_blocks(const of_conv_desc* d, int& cib, int& cob) {
   const int c = wgx3_cfg(d);
-  cib = c >= 2 ? 64 : 32;
-  cob = c == 0 ? 128 : c == 1 ? 96 : c == 2 ? 64 : 32;
+  cib = c == 2 || c == 3 ? 64 : 32;
+  cob = c == 0 ? 128 : c == 1 ? 96 : c == 2 || c == 4 ? 64 : 32;
 }
 
 // of_set_tuning key 10: fp32 / bf16 GEMM weight-gradient split-K target workgroups per CU.
@@ -4336,6 +4342,7 @@ int of_set_tuning(int key, int value) {
   if (key == 7 && (value == 0 || value == 1)) { g_warp_win = value; return OF_OK; }
   if (key == 9 && value >= 0 && value <= 3) { g_corr_blk = value; return OF_OK; }
   if (key == 10 && value >= 1 && value <= 16) { g_wgrad_wgs = value; return OF_OK; }
+  if (key == 11 && (value == 0 || value == 1)) { g_wgx3_c4 = value; return OF_OK; }
   if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }
   if (key == 2 && value >= 2 && value <= 64) { g_split_min_chunks = value; return OF_OK; }
   if (key == 3 && (value == 0 || value == 1)) { g_vec_ep = value; return OF_OK; }
@@ -4746,14 +4753,16 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     a.tiles_total = (int)cdiv(g.cin_p, cib) * a.n_tiles;
     dim3 grid(a.tiles_total * a.splits);
     if (timing_on()) timing_begin(s);
-    const bool x3b = g_wgx3b == 2 || (g_wgx3b == 1 && cfg == 0);
+    const bool x3b = g_wgx3b == 2 || (g_wgx3b == 1 && cfg == 0) || cfg == 4;
     if (x3b) {
       if (g_wgx3b_mi == 2) {   // waves of 32 ci x 16 co
-        if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3b<1, 8, 8, 2>), grid, dim3(512), 0, s, a);
+        if (cfg == 4) hipLaunchKernelGGL((conv_wgrad_tile_x3b<1, 4, 8, 2>), grid, dim3(256), 0, s, a);
+        else if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3b<1, 8, 8, 2>), grid, dim3(512), 0, s, a);
         else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3b<1, 6, 8, 2>), grid, dim3(384), 0, s, a);
         else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 4, 4, 2>), grid, dim3(512), 0, s, a);
         else hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 2, 4, 2>), grid, dim3(256), 0, s, a);
-      } else if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 4, 8>), grid, dim3(512), 0, s, a);
+      } else if (cfg == 4) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 2, 8>), grid, dim3(256), 0, s, a);
+      else if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 4, 8>), grid, dim3(512), 0, s, a);
       else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3b<2, 3, 8>), grid, dim3(384), 0, s, a);
       else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_x3b<4, 2, 4>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((conv_wgrad_tile_x3b<4, 1, 4>), grid, dim3(256), 0, s, a);
@@ -4761,8 +4770,9 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_x3<1, 3, 3, 8>), grid, dim3(576), 0, s, a);
     else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 2, 3, 4>), grid, dim3(768), 0, s, a);
     else hipLaunchKernelGGL((conv_wgrad_tile_x3<2, 1, 3, 4>), grid, dim3(384), 0, s, a);
-    // timing kinds 144-147: the 3-tap form, 148-151: conv_wgrad_tile_x3b (bench.py X3_WGT)
-    if (timing_on()) timing_end(s, 128 + MODE_WGRAD * 8 + cfg + (x3b ? 4 : 0), flops);
+    // timing kinds 144-147: the 3-tap form, 148-151: conv_wgrad_tile_x3b, 152: its cfg 4
+    // (bench.py X3_WGT)
+    if (timing_on()) timing_end(s, cfg == 4 ? 152 : 128 + MODE_WGRAD * 8 + cfg + (x3b ? 4 : 0), flops);
     st = check_launch("conv_wgrad_tile_x3");
   } else if (x3g) {
     const int bn = d->cout > 64 ? 128 : 64;

@@ -508,6 +508,53 @@ def test_wgrad_x3_forms(n, h, w, cin, cout):
         assert rel_inf(db, dbref) < 5e-6, (key, rel_inf(db, dbref))
 
 
+@pytest.mark.parametrize("n,h,w,cin", [(2, 24, 32, 96), (1, 13, 40, 32), (1, 9, 20, 160)])
+def test_wgrad_x3_cout64_32ci_blocks(n, h, w, cin):
+    """Cout 64 with Cin not a multiple of 64 (the 96 -> 64 flow-head convs): the 9-tap split
+    weight gradient on 32 x 64 channel blocks (cfg 4, of_set_tuning key 11 = 1, timing kind
+    152) against fp64 and against the 64 x 64 blocks (key 11 = 0; odd rows, ragged columns)."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_NONE, call
+    lib = _lib.lib()
+    cout = 64
+    x = dev(rng_tensor((n, h, w, cin), 91))
+    wt = dev(rng_tensor((3, 3, cin, cout), 92, scale=(2.0 / (9 * cin)) ** 0.5))
+    b = dev(rng_tensor((cout,), 93, scale=0.1))
+    dy = dev(rng_tensor((n, h, w, cout), 94))
+    layer = ops.ConvLayer(wt, b, stride=1, act=ACT_NONE, cin_p=cin, f32_split=True)
+    d = layer.desc(n, h, w)
+    P, st = ops._ptr, ops._stream()
+    dwref = torch.nn.grad.conv2d_weight(f64(x).permute(0, 3, 1, 2), (cout, cin, 3, 3),
+                                        f64(dy).permute(0, 3, 1, 2), padding=1).permute(2, 3, 1, 0)
+    dbref = f64(dy).sum((0, 1, 2))
+    outs = {}
+    k_arr = (C.c_int * 8)()
+    try:
+        for c4 in (1, 0):
+            assert lib.of_set_tuning(11, c4) == 0
+            wws = lib.of_conv2d_wgrad_x3_workspace(C.byref(d))
+            ws = torch.empty(wws // 4 + 4, device="cuda")
+            dw = torch.full_like(wt, 7.0)
+            db = torch.full_like(b, 7.0)
+            lib.of_timing_read(0, None, None, None)
+            lib.of_timing_enable(1)
+            call("of_conv2d_wgrad_x3", C.byref(d), P(x), cin, P(dy), cout, P(dw), P(db), 0,
+                 P(ws), wws, st)
+            torch.cuda.synchronize()
+            lib.of_timing_enable(0)
+            kinds = {k_arr[i] for i in range(lib.of_timing_read(8, k_arr, None, None))}
+            assert kinds == ({152} if c4 else {146}), (c4, kinds)
+            outs[c4] = (dw, db)
+    finally:
+        lib.of_set_tuning(11, 1)
+        lib.of_timing_enable(0)
+    for key, (dw, db) in outs.items():
+        assert rel_inf(dw, dwref) < 5e-6, (key, rel_inf(dw, dwref))
+        assert rel_inf(db, dbref) < 5e-6, (key, rel_inf(db, dbref))
+
+
 @pytest.mark.parametrize("prec", ["f32", "bf16", "x3"])
 @pytest.mark.parametrize("n,h,w,cin,cout,k,s", [
     (2, 32, 48, 4, 64, 7, 2),      # stem: 256 x 64 tiles, split-K slabs

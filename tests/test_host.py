@@ -88,7 +88,7 @@ def test_bench_kernel_symbols_match_pmc_keys():
         for cfg in bench.X3_BN:
             names.add(bench.kernel_symbol(128 + mode * 8 + cfg))
     for cfg in bench.X3_WGT:
-        names.add(bench.kernel_symbol(128 + 16 + cfg))
+        names.add(bench.kernel_symbol(128 + 16 + cfg if cfg < 8 else 152 + cfg - 8))
     for mode in (0, 1):
         for cfg in bench.GX3:
             names.add(bench.kernel_symbol(160 + mode * 8 + cfg))
