@@ -1486,6 +1486,7 @@ static int corr_bwd_launch(int sign, CorrBwdArgs a, int n, hipStream_t s) {
   if (g_corr_blk & 2) {
     CorrBlkArgs p{};
     corr_blk_plan(n, a.h, a.w, a.c, p);
+    OF_CHECK_ARG((int64_t)n * p.tiles_x * p.tiles_y * p.groups < INT32_MAX, "corr bwd: too many tiles");
     a.tiles_x = p.tiles_x, a.tiles_y = p.tiles_y;
     const int grid = corr_blk_grid(p.items);
     auto k = sign > 0 ? (a.vec ? corr_bwd_blk<1, true> : corr_bwd_blk<1, false>)
