@@ -298,9 +298,11 @@ int of_copy_strided(const float* src, int lds, float* dst, int ldd, int64_t npix
                     void* stream);                                             /* per pixel */
 int of_fill(float* y, float v, int64_t n, void* stream);
 
-/* Per-launch timing of the conv kernels (bench instrumentation): when enabled, every conv
- * launch records a hipEvent pair on its stream; of_timing_read() returns the count and fills
- * kinds (0 fwd, 1 dgrad, 2 wgrad), flops and elapsed ms (synchronises the events). */
+/* Per-launch timing of the conv kernels (bench instrumentation): when enabled (on = 1), every
+ * conv launch records a hipEvent pair on its stream; on = 2 times the next conv launch only
+ * (then timing is off again); of_timing_read() returns the count and fills kinds (the kernel
+ * family / pass / tile configuration code, bench.py kind_parts), flops and elapsed ms
+ * (synchronises the events). */
 int of_timing_enable(int on);
 /* Kernel-variant switches for A/B measurements: key 1 = fwd/dgrad split-K target workgroups
  * per CU (1-16, default 4), key 2 = minimum 16-deep K chunks per split slice (2-64, default 12),

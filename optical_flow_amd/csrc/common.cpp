@@ -30,6 +30,7 @@ struct TimedLaunch {
 
 static std::mutex g_tmu;
 static bool g_timing = false;
+static bool g_timing_oneshot = false;   // of_timing_enable(2): the next conv launch only
 static std::vector<TimedLaunch> g_launches;
 static std::vector<hipEvent_t> g_event_pool;
 static hipEvent_t g_pending_start = nullptr;
@@ -61,6 +62,7 @@ void timing_end(hipStream_t s, int kind, double flops) {
   (void)hipEventRecord(stop, s);
   g_launches.push_back({kind, flops, g_pending_start, stop});
   g_pending_start = nullptr;
+  if (g_timing_oneshot) g_timing = g_timing_oneshot = false;
 }
 
 }  // namespace oflow
@@ -86,7 +88,9 @@ int of_same_pads(int n, int k, int s, int* before, int* after, int* out) {
 
 int of_timing_enable(int on) {
   std::lock_guard<std::mutex> lk(g_tmu);
+  OF_CHECK_ARG(on >= 0 && on <= 2, "timing_enable: 0, 1 or 2");
   g_timing = on != 0;
+  g_timing_oneshot = on == 2;
   return OF_OK;
 }
 

@@ -21,10 +21,18 @@ BN_EPS = 1e-3          # keras BatchNormalization default (model.py:14)
 
 # Bench instrumentation: when TIMING_TAGS is a list, every conv launch appends
 # (layer name, kind) in launch order, matching the hipEvent records of of_timing_read().
+# With TIMING_ONLY a set of (layer name, kind), only those launches are timed (one-shot
+# of_timing_enable(2) per launch) and tagged: the bench times the dominant kernel's launches
+# in the timed region without event pairs around the other ~250 launches of the step.
 TIMING_TAGS = None
+TIMING_ONLY = None
 
 
 def _tag(layer, kind):
+    if TIMING_ONLY is not None:
+        if (layer.name, kind) not in TIMING_ONLY:
+            return
+        _lib.lib().of_timing_enable(2)
     if TIMING_TAGS is not None:
         TIMING_TAGS.append((layer.name, kind))
 
