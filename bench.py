@@ -13,9 +13,10 @@ Prints ONE JSON line (rank 0) with the contract fields plus:
                    stream it is launched on: achieved = algorithmic FLOPs / launch duration,
                    vs the MFMA peak of the dtype.
   cpu_baseline  -- the CPU oracle (reference semantics restated in torch-CPU fp32) timed on
-                   this host on a bounded sample (1 pair at 384x512), rank 0 only.
+                   this host's usable cores on the bench batch (B=8 at 384x512: 1 untimed +
+                   3 timed steps, capped at 60 s), rank 0 only.
   parity        -- EPE / loss error between the HIP path and that oracle run on the same
-                   pair and initial weights.
+                   batch and initial weights.
 """
 from __future__ import annotations
 
@@ -171,17 +172,41 @@ def gflop_per_pair(H, W, max_disp=3, levels=4):
     return (2 * macs + 3 * corr) / 1e9
 
 
-def cpu_baseline(pair_np, vals, steps=2, precision="fp32", levels=4):
-    """Oracle train_step (torch CPU fp32, reference semantics) on one pair; returns
-    (pairs/s, threads, flows_at_init, loss_at_init).  With precision "bf16" the reference
-    outputs come from the oracle with the build's bf16 operand rounding; the timed steps are
-    always the fp32 reference semantics."""
+def host_cores():
+    """(cores this process may use, CPUs the host reports).  On the GPU box os.cpu_count()
+    shows the whole machine while the job gets a share of it (a cgroup CPU quota, and
+    OMP_NUM_THREADS set to that share): the usable count is the smallest of the affinity
+    mask, the quota and OMP_NUM_THREADS."""
+    total = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            usable = min(usable, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        usable = min(usable, int(omp))
+    return usable, total
+
+
+def cpu_baseline(batch_np, vals, steps=3, precision="fp32", levels=4, max_s=60.0):
+    """The oracle's train_step (torch CPU fp32, the reference semantics restated) on the
+    bench's own batch (SURVEY.md §8 d: B=8 at 384x512), all usable host cores: 1 untimed step
+    (which also gives the reference flows / loss at the initial weights for the parity
+    probe), then ``steps`` timed steps, stopping early after ``max_s`` seconds.  Returns
+    (pairs/s, threads, host CPUs, timed steps, flows_at_init, loss_at_init).  With precision
+    "bf16" the reference outputs come from the oracle with the build's bf16 operand rounding;
+    the timed steps are always the fp32 reference semantics."""
     from oracle import ref_flow as R
     from optical_flow_amd.params import encoder_blocks
-    threads = torch.get_num_threads()
+    threads, total = host_cores()
+    torch.set_num_threads(threads)
     p = {k: torch.tensor(v) for k, v in vals.items()}
     blocks = list(encoder_blocks(levels))
-    x = torch.tensor(pair_np)
+    x = torch.tensor(batch_np)
     R.set_conv_precision(precision)
     try:
         loss0, flows0, _ = R.train_step(x, p, blocks, None)  # warm-up + reference outputs
@@ -193,10 +218,10 @@ def cpu_baseline(pair_np, vals, steps=2, precision="fp32", levels=4):
     while n < steps:
         R.train_step(x, p, blocks, opt)
         n += 1
-        if time.time() - t0 > 25.0:
+        if time.time() - t0 > max_s:
             break
     dt = time.time() - t0
-    return n * x.shape[0] / dt, threads, flows0, float(loss0)
+    return n * x.shape[0] / dt, threads, total, n, flows0, float(loss0)
 
 
 def main():
@@ -208,7 +233,7 @@ def main():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--timing-steps", type=int, default=2,
                     help="steps whose conv launches carry hipEvent pairs: the last ones of the "
                          "timed region (or, with --roofline-window extra, extra steps)")
@@ -247,10 +272,10 @@ def main():
     trainer = Trainer(net, KerasAdam(net.store), LossLayer())
     batch = torch.from_numpy(synthetic_batch(B, H, W, seed=1234, rank=rank)).cuda()
 
-    # ---- parity probe: HIP forward on pair 0 with the initial weights -------------------
+    # ---- parity probe: HIP forward on the whole bench batch with the initial weights -----
     with torch.no_grad():
-        flows_hip = [f.cpu() for f in net(batch[:1].contiguous())]
-        loss_hip = float(LossLayer()(batch[:1].contiguous(), [f.cuda() for f in flows_hip]))
+        flows_hip = [f.cpu() for f in net(batch)]
+        loss_hip = float(LossLayer()(batch, [f.cuda() for f in flows_hip]))
 
     # ---- training throughput --------------------------------------------------------------
     # The roofline timing is taken live in the timed region: over its last --timing-steps
@@ -304,8 +329,8 @@ def main():
         lib.of_timing_enable(0)
     if world > 1:
         dist.barrier()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    if world > 1:
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64)
+    if world > 1:     # control plane (gloo); the gradients went over the C-ABI RCCL comm
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed)
     pairs = world * B * args.steps
@@ -386,22 +411,22 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:     # N=1 only (contract)
-        pair = batch[:1].cpu().numpy()
-        cps, threads, flows_ref, loss_ref = cpu_baseline(pair, vals, args.cpu_steps,
-                                                         args.precision, args.levels)
+        cps, threads, host_cpus, nsteps_cpu, flows_ref, loss_ref = cpu_baseline(
+            batch.cpu().numpy(), vals, args.cpu_steps, args.precision, args.levels)
         cpu = {"value": round(cps, 4), "unit": "image-pairs/s", "cores": threads,
-               "kind": "port",
+               "threads": threads, "host_cpus": host_cpus, "kind": "port",
                "sample": "%d oracle train steps (torch-CPU fp32 restatement of the reference "
-                         "semantics) on 1 pair at %dx%d, after 1 untimed step"
-                         % (args.cpu_steps, H, W)}
+                         "semantics, Keras Adam included) on the bench batch, B=%d at %dx%d, "
+                         "after 1 untimed step; %d threads = the cores this job may use (%d "
+                         "CPUs on the host)" % (nsteps_cpu, B, H, W, threads, host_cpus)}
         epe = [float((a - b.float()).norm(dim=-1).mean()) for a, b in zip(flows_hip, flows_ref)]
         rel = [float((a - b.float()).abs().max() / b.abs().max()) for a, b in
                zip(flows_hip, flows_ref)]
         parity = {"epe": [round(e, 6) for e in epe], "flow_rel_inf": [float("%.3e" % r) for r in rel],
                   "loss_rel": float("%.3e" % (abs(loss_hip - loss_ref) / abs(loss_ref))),
-                  "note": "HIP %s vs CPU oracle (%s operand rounding), same pair and initial "
-                          "weights, flows [H/2 ... H/%d]" % (args.precision, args.precision,
-                                                             2 ** args.levels)}
+                  "note": "HIP %s vs CPU oracle (%s operand rounding), the bench batch (B=%d) "
+                          "and initial weights, flows [H/2 ... H/%d]" % (
+                              args.precision, args.precision, B, 2 ** args.levels)}
 
     gfp = gflop_per_pair(H, W, levels=args.levels)
     if rank == 0:

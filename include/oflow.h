@@ -221,7 +221,10 @@ int of_maxpool2_bwd(const float* x, const float* dy, int n, int h, int w, int c,
 
 /* Cost volume (create_cost_volume, model.py:29-42; P8): out[p][k], k=i*(2d+1)+j =
  * sum_c f1[p][c]*f2[p+(i-d, j-d)][c] with zero padding.  out has ldo >= (2d+1)^2.
- * Channels are reduced in 64-channel slabs; c > 64 needs of_corr_fwd_workspace() bytes. */
+ * The channel reduction may be split into slab groups whose partial sums live in the
+ * workspace (which shapes split depends on the level's tile count and the device's CU
+ * count): always size it with of_corr_fwd_workspace(), which returns 0 when none is needed.
+ * Same rule for of_corr_concat_fwd. */
 size_t of_corr_fwd_workspace(int n, int h, int w, int c, int max_disp);
 int of_corr_fwd(const float* f1, int ld1, const float* f2, int ld2, int n, int h, int w,
                 int c, int max_disp, float* out, int ldo, void* workspace, size_t ws_bytes,
@@ -386,6 +389,27 @@ uint32_t of_crc32c(const void* data, int64_t n, uint32_t crc);
 int of_flow_color(const float* flow, int n, int h, int w, uint8_t* bgr, float* ws, void* stream);
 /* draw_optical_flow_intensity (drawing.py:37-42): min(sqrt(u^2 + u^2) / 20, 1) per pixel. */
 int of_flow_intensity(const float* flow, int64_t npix, float* out, void* stream);
+
+/* ==== SURVEY.md §8 b / §8 e: gradient all-reduce over RCCL (build-added K14) ============= */
+/* The reference is single-process (train.py:47-61); batch data parallelism sums the
+ * gradients tape.gradient() returns (train.py:55) across ranks before the Adam update
+ * (train.py:56).  One communicator per process / GPU; the id is made by rank 0 and handed to
+ * the other ranks by the caller (optical_flow_amd/comm.py: the torch.distributed TCPStore).
+ * librccl.so.1 is dlopen-ed on first use (OF_EUNSUPPORTED if absent). */
+typedef struct of_comm of_comm;
+int of_comm_id_bytes(void);                      /* bytes of a unique id (128) */
+int of_comm_get_unique_id(void* id);
+/* Collective over the nranks processes; binds the communicator to the current HIP device. */
+int of_comm_init(of_comm** comm, const void* id, int nranks, int rank);
+int of_comm_info(const of_comm* comm, int* nranks, int* rank, int* device);
+/* recv = sum over ranks of send (count fp32 elements; send == recv is in place), enqueued on
+ * `stream` and ordered after the work already on it; returns without waiting. */
+int of_comm_allreduce_async(of_comm* comm, const float* send, float* recv, int64_t count,
+                            void* stream);
+/* OF_OK unless the communicator has failed asynchronously. */
+int of_comm_async_error(of_comm* comm);
+/* Frees the communicator (abort != 0: without waiting for in-flight operations). */
+int of_comm_destroy(of_comm* comm, int abort);
 
 #ifdef __cplusplus
 }

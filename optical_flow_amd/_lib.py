@@ -119,6 +119,14 @@ PROTOTYPES = {
     "of_flow_color": (I, [P, I, I, I, P, P, P]),
     "of_flow_intensity": (I, [P, I64, P, P]),
     "of_crc32c": (C.c_uint32, [P, I64, C.c_uint32]),   # checkpoint bundles (row 2)
+    # gradient all-reduce over RCCL (SURVEY §8 b / e)
+    "of_comm_id_bytes": (I, []),
+    "of_comm_get_unique_id": (I, [P]),
+    "of_comm_init": (I, [C.POINTER(P), P, I, I]),
+    "of_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "of_comm_allreduce_async": (I, [P, P, P, I64, P]),
+    "of_comm_async_error": (I, [P]),
+    "of_comm_destroy": (I, [P, I]),
 }
 
 

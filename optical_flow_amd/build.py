@@ -59,7 +59,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             list(ex.map(run, jobs))
     if jobs or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o)
                                                                         for o in objs):
-        run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lpthread"])
+        run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lpthread", "-ldl"])
     return LIB
 
 

@@ -21,6 +21,24 @@ int check_launch(const char* what) {
   return OF_OK;
 }
 
+int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  int v = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+  if (v > 0) return v;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      v <= 0) {
+    (void)hipGetLastError();
+    v = 256;
+  }
+  __atomic_store_n(&cache[dev], v, __ATOMIC_RELAXED);
+  return v;
+}
+
 // ---- timing: hipEvent pairs recorded on the launch stream, read back on demand ----------
 struct TimedLaunch {
   int kind;

@@ -24,6 +24,11 @@ inline int64_t round_up(int64_t a, int64_t b) { return cdiv(a, b) * b; }
 
 constexpr int kWave = 64;
 
+// Compute units of the current device (256 on MI355X; fewer on a partitioned device), cached
+// per device; 256 when no device is visible.  Grid planners size persistent grids and split-K
+// targets from it, and workspace queries use the same value as the launches they size.
+int device_cus();
+
 // XCD-aware bijective block remap (cdna guide T1): the hardware deals workgroups to the 8
 // XCDs round-robin; this maps them so that each XCD gets a contiguous range of work ids,
 // i.e. neighbouring tiles share that XCD's L2.

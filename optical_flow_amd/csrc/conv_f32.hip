@@ -39,7 +39,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 constexpr int BK = 16;
 constexpr int MAX_GROUPS = 4;
-constexpr int kCUs = 256;          // MI355X compute units
 
 // A group = GEMM rows sharing one tap list (dgrad stride-2 phase classes); plain convs have
 // a single identity group.
@@ -3785,9 +3784,9 @@ static int g_split_min_chunks = 12;
 void plan_splits(GemmArgs& a, int kmax, int bk = BK) {
   a.splits = 1;
   a.k_per_split = (int)round_up(kmax, bk);
-  if (a.tiles_total >= 2 * kCUs) return;
+  if (a.tiles_total >= 2 * device_cus()) return;
   const int nchunks = (int)cdiv(kmax, bk);
-  int s = std::max(1, (g_split_wgs * kCUs) / a.tiles_total);
+  int s = std::max(1, (g_split_wgs * device_cus()) / a.tiles_total);
   s = std::min(s, std::max(1, nchunks / (bk == BK ? g_split_min_chunks : g_split_min_chunks / 2)));
   if (s <= 1) return;
   a.k_per_split = (int)round_up(cdiv(kmax, s), bk);
@@ -3931,7 +3930,7 @@ int launch_splitk_epilogue(const GemmArgs& a, hipStream_t s) {
   if (a.res) vec = vec && a.ldr % 4 == 0 && al16(a.res);
   if (MODE == MODE_FWD && a.z) vec = vec && a.ldz % 4 == 0 && al16(a.z);
   if (MODE == MODE_DGRAD && a.act_src) vec = vec && a.ld_act % 4 == 0 && al16(a.act_src);
-  const dim3 grid((unsigned)std::min<int64_t>(cdiv(items, 256), 8 * kCUs));
+  const dim3 grid((unsigned)std::min<int64_t>(cdiv(items, 256), 8 * device_cus()));
   if (vec) hipLaunchKernelGGL((splitk_epilogue_flat<MODE, true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((splitk_epilogue_flat<MODE, false>), grid, dim3(256), 0, s, a);
   return check_launch("conv_splitk_epilogue");
@@ -3979,7 +3978,7 @@ bool tile_ok(const of_conv_desc* d) { return d->kh == 3 && d->kw == 3 && d->stri
 // B tap) when that still leaves >= 4 workgroups per CU, else 4 x 32.
 bool x3_tall(int n, int oh, int ow, int N) {
   const int bn = pick_bn(N);
-  return (bn == 128 || bn == 96) && (int64_t)n * cdiv(oh, X3_TH0) * cdiv(ow, TF_W) >= 4 * kCUs;
+  return (bn == 128 || bn == 96) && (int64_t)n * cdiv(oh, X3_TH0) * cdiv(ow, TF_W) >= 4 * device_cus();
 }
 
 // conv_tile_x3 BN = 128 with 4 x 32 tiles: unsplit grids of >= X3_NB1_MIN tiles take the
@@ -4031,7 +4030,7 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
     // (Measured: enc.l3 384 tiles unsplit, dec1 192 tiles unsplit, enc.l4 96 tiles in 2.)
     // (The single-buffered BN = 128 4 x 32 configuration, used from X3_NB1_MIN tiles, runs
     // two workgroups per CU.)
-    const int slots = x3_nb1_candidate(a, tall) ? 2 * kCUs : kCUs;
+    const int slots = x3_nb1_candidate(a, tall) ? 2 * device_cus() : device_cus();
     int best = 1;
     double best_cost = 1e30;
     for (int sp = 1; sp <= std::min(8, a.K); ++sp) {
@@ -4047,8 +4046,8 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
     }
     a.k_per_split = (int)cdiv(a.K, best);
     a.splits = (int)cdiv(a.K, a.k_per_split);
-  } else if (a.tiles_total < 2 * kCUs) {
-    int sp = std::max(1, (4 * kCUs) / a.tiles_total);
+  } else if (a.tiles_total < 2 * device_cus()) {
+    int sp = std::max(1, (4 * device_cus()) / a.tiles_total);
     sp = std::min(sp, std::max(1, a.K / 2));       // >= 2 chunks (6 tap rows) per slice
     a.k_per_split = (int)cdiv(a.K, sp);
     a.splits = (int)cdiv(a.K, a.k_per_split);
@@ -4130,8 +4129,8 @@ void gemm_x3_plan(GemmArgs& a) {
     const int per = (int)cdiv(chunks, sp);
     if (cdiv(chunks, per) != sp) continue;
     const int64_t w = plan_tiles * sp;
-    const double cost = (double)cdiv(w, kCUs) * (per + 1.0) +
-                        (sp > 1 ? 0.5 * sp * plan_tiles / (double)kCUs : 0.0);
+    const double cost = (double)cdiv(w, device_cus()) * (per + 1.0) +
+                        (sp > 1 ? 0.5 * sp * plan_tiles / (double)device_cus() : 0.0);
     if (cost < best_cost - 1e-9) {
       best_cost = cost;
       best = sp;
@@ -4202,7 +4201,7 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
     wgx3_blocks(d, cib, cob);
     const int chan_tiles = (int)(cdiv(g.cin_p, cib) * cdiv(d->cout, cob));
     const int T = d->n * (int)cdiv(d->ho, wgx3_rows(wgx3_cfg(d))) * (int)cdiv(d->wo, TT_W);
-    int splits = std::max(1, std::min(T, kCUs / chan_tiles));
+    int splits = std::max(1, std::min(T, device_cus() / chan_tiles));
     p.k_per_split = (int)cdiv(T, splits);
     p.splits = (int)cdiv(T, p.k_per_split);
     return p;
@@ -4212,7 +4211,7 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
     // 32-pixel chunks, split to fill the CUs with at least 8 chunks per slice
     const int K = d->n * d->ho * d->wo;
     const int tiles = (int)(cdiv(p.M, 128) * cdiv(d->cout, d->cout > 64 ? 128 : 64));
-    int splits = std::max(1, kCUs / tiles);
+    int splits = std::max(1, device_cus() / tiles);
     splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * BKH)));
     p.k_per_split = (int)round_up(cdiv(K, splits), BKH);
     p.splits = (int)cdiv(K, p.k_per_split);
@@ -4224,7 +4223,7 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
     wgt_blocks(d, cib, cob);
     const int chan_tiles = (int)(cdiv(g.cin_p, cib) * cdiv(d->cout, cob));
     const int T = d->n * (int)cdiv(d->ho, TT_H) * (int)cdiv(d->wo, TT_W);
-    int splits = std::max(1, std::min(T, kCUs / chan_tiles));
+    int splits = std::max(1, std::min(T, device_cus() / chan_tiles));
     p.k_per_split = (int)cdiv(T, splits);
     p.splits = (int)cdiv(T, p.k_per_split);
     return p;
@@ -4234,7 +4233,7 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
   const int tiles = (int)(cdiv(p.M, pick_bm(d->cout)) * cdiv(d->cout, pick_bn(d->cout)));
   // Fill up to g_wgrad_wgs (4) workgroups per CU without overshooting a multiple of the CU
   // count (an overshoot leaves a few CUs with one extra long-running workgroup: a tail).
-  int splits = std::max(1, (g_wgrad_wgs * kCUs) / tiles);
+  int splits = std::max(1, (g_wgrad_wgs * device_cus()) / tiles);
   splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * bk)));
   p.k_per_split = (int)round_up(cdiv(K, splits), bk);
   p.splits = (int)cdiv(K, p.k_per_split);

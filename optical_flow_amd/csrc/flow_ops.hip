@@ -1413,14 +1413,14 @@ extern "C" {
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// Slab groups of the register-blocked forward: the fewest that give >= 512 (tile, group)
-// items, one per workgroup slot of the persistent grid (96x128x64: one group of 768 tiles
+// Slab groups of the register-blocked forward: the fewest that give >= 2 * CUs (512 on
+// MI355X) (tile, group) items, one per workgroup slot of the persistent grid (96x128x64: one group of 768 tiles
 // ran 38 us + no slab sum against 38 + 12 us with two groups).
 static void corr_blk_plan(int n, int h, int w, int c, CorrBlkArgs& p) {
   p.slabs = (int)cdiv(c, CB_SC);
   p.tiles_x = (int)cdiv(w, CB_X), p.tiles_y = (int)cdiv(h, CB_Y);
   const int64_t tiles = (int64_t)n * p.tiles_x * p.tiles_y;
-  const int want = (int)std::min<int64_t>(p.slabs, std::max<int64_t>(1, cdiv(512, tiles)));
+  const int want = (int)std::min<int64_t>(p.slabs, std::max<int64_t>(1, cdiv(2 * device_cus(), tiles)));
   p.spg = (int)cdiv(p.slabs, want);
   p.groups = (int)cdiv(p.slabs, p.spg);
   p.items = (int)(tiles * p.groups);
@@ -1428,7 +1428,7 @@ static void corr_blk_plan(int n, int h, int w, int c, CorrBlkArgs& p) {
 
 // Persistent grid: two workgroups per CU, a multiple of 8 (one partition per XCD) from 64 up.
 static int corr_blk_grid(int items) {
-  const int g = std::min(items, 2 * 256);
+  const int g = std::min(items, 2 * device_cus());
   return g >= 64 ? g & ~7 : g;
 }
 

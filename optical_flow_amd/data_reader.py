@@ -28,30 +28,36 @@ from ._lib import call
 image_means = (np.array([123.0, 117.0, 104.0]) / 255.0).reshape(1, 1, 3)   # data_reader.py:7-9
 
 
+def _drive_dirs(kitti_path: str):
+    """(left camera dir, right camera dir) of every drive, days and drives in os.listdir
+    order; a day's calibration files (names ending in '.txt') are not drives."""
+    for day in os.listdir(kitti_path):
+        day_dir = os.path.join(kitti_path, day)
+        for drive in os.listdir(day_dir):
+            if not drive.endswith(".txt"):
+                cams = [os.path.join(day_dir, drive, cam, "data") for cam in ("image_02", "image_03")]
+                assert all(os.path.isdir(c) for c in cams), "missing camera dir in %s" % drive
+                yield cams
+
+
+def _drive_pairs(left: str, right: str) -> List[List[str]]:
+    """One drive's pairs: consecutive left frames (temporal), then each left frame with the
+    right frame of the same name (stereo); frames in sorted-name order."""
+    names = sorted(os.listdir(left))
+    lpaths = [os.path.join(left, f) for f in names]
+    temporal = [[a, b] for a, b in zip(lpaths, lpaths[1:])]
+    rpaths = [os.path.join(right, f) for f in names]
+    assert all(os.path.isfile(r) for r in rpaths), "right frame missing under %s" % right
+    return temporal + [[a, b] for a, b in zip(lpaths, rpaths)]
+
+
 def read_kitti(kitti_path: str) -> List[List[str]]:
-    """data_reader.py:12-32: per day / drive, temporal pairs (image_02 frame i, i+1) then
-    stereo pairs (image_02 / image_03 frame i).  Days and drives in os.listdir order, frames
-    sorted; entries of a day ending in '.txt' (the calibration files) are skipped."""
-    path_pairs = []
-    for day in os.listdir(os.path.join(kitti_path)):
-        for drive in os.listdir(os.path.join(kitti_path, day)):
-            if drive[-4:] == '.txt':
-                continue
-            images_dir_l = os.path.join(kitti_path, day, drive, 'image_02', 'data')
-            images_dir_r = os.path.join(kitti_path, day, drive, 'image_03', 'data')
-            assert os.path.isdir(images_dir_l)
-            assert os.path.isdir(images_dir_r)
-            frames = os.listdir(images_dir_l)
-            frames.sort()
-            for i in range(len(frames) - 1):
-                path_pairs.append([os.path.join(images_dir_l, frames[i]),
-                                   os.path.join(images_dir_l, frames[i + 1])])
-            for i in range(len(frames)):
-                assert os.path.isfile(os.path.join(images_dir_r, frames[i]))
-                path_pairs.append([os.path.join(images_dir_l, frames[i]),
-                                   os.path.join(images_dir_r, frames[i])])
-    print('Total number of KITTI pairs: ' + str(len(path_pairs)))
-    return path_pairs
+    """The pair list of data_reader.py:12-32 -- per drive, the temporal pairs (image_02
+    frames i, i+1) then the stereo pairs (image_02 / image_03 frame i) -- with the same
+    listing order, asserts and the printed total."""
+    pairs = [p for left, right in _drive_dirs(kitti_path) for p in _drive_pairs(left, right)]
+    print("Total number of KITTI pairs: %d" % len(pairs))
+    return pairs
 
 
 class ReaderOpts:

@@ -1,11 +1,13 @@
-"""Batch-dimension data parallelism: one process per GPU, gradients all-reduced with
-torch.distributed (backend "nccl" = RCCL on ROCm, over xGMI inside an MI355X node).
+"""Batch-dimension data parallelism: one process per GPU, gradients summed over RCCL (the C-ABI
+communicator of comm.py, over xGMI inside an MI355X node).
 
 The reference is single-process; this is the build-added K14.  Buckets are
 contiguous slices of the gradient arena (ordered by backward completion, model.backward_order)
 and each is all-reduced (SUM) as soon as every parameter in it has been written by its
-backward kernel -- RCCL runs on its own stream, ordered after the producing kernels, so the
-reduction of the finest flow head overlaps the backward of the coarser levels and the encoder.
+backward kernels: the reduction is enqueued on the weight-gradient side stream once that has
+waited for the compute stream, so RCCL runs after the producing kernels and the reduction of
+the finest flow head overlaps the backward of the coarser levels and the encoder.  The
+compute stream joins the side stream at the end of the backward (ops._side_join), before Adam.
 The 1/world average is folded into the Adam launch (grad_scale).
 """
 from __future__ import annotations
@@ -20,10 +22,16 @@ from . import ops
 
 
 class GradBucketReducer:
-    def __init__(self, store, bucket_bytes: int = 4 << 20, group=None):
+    """comm: a comm.RcclComm / comm.TorchComm (anything with allreduce_(tensor), wait(),
+    world); None -> comm.TorchComm over the default process group."""
+
+    def __init__(self, store, bucket_bytes: int = 4 << 20, comm=None):
         self.store = store
-        self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if comm is None:
+            from .comm import TorchComm
+            comm = TorchComm()
+        self.comm = comm
+        self.world = comm.world
         # bucket = contiguous arena range covering whole parameters
         self.buckets: List[List[str]] = []
         cur, cur_bytes = [], 0
@@ -46,7 +54,6 @@ class GradBucketReducer:
             for n in names:
                 self.bucket_of[id(store.params[n])] = bi
         self._pending: List[int] = []
-        self._works = []
         self._launched: List[bool] = []
 
     # -- called by ops after a parameter's gradient kernels are enqueued -----------------
@@ -67,41 +74,40 @@ class GradBucketReducer:
         # ordered after both without stalling the input-gradient chain.
         side = in_backward and view.is_cuda and ops.SIDE_STREAM_WGRAD
         with torch.cuda.stream(ops.side_stream()) if side else contextlib.nullcontext():
-            self._works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
-                                               async_op=True))
+            self.comm.allreduce_(view)
         self._launched[bi] = True
 
     def begin(self):
         """Arm for one backward pass."""
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
-        self._works = []
-        ops.set_grad_ready_hook(self._on_grad if self.world > 1 else None)
+        ops.set_grad_ready_hook(self._on_grad)
 
     def finish(self) -> float:
-        """Launch buckets that never completed (unused params), make the current stream wait
-        for every reduction; returns the grad scale (1/world) for the optimizer."""
+        """Launch buckets that never completed (unused params) on the current stream, join
+        the reductions (TorchComm: wait on the works; RCCL: stream-ordered, the current stream
+        already joined the side stream at the end of the backward, so only an asynchronous
+        communicator failure is checked); returns the grad scale (1/world) for the optimizer."""
         ops.set_grad_ready_hook(None)
-        if self.world > 1:
-            for bi in range(len(self.buckets)):
-                if not self._launched[bi]:
-                    self._launch(bi, in_backward=False)
-            for w in self._works:
-                w.wait()
-        self._works = []
+        for bi in range(len(self.buckets)):
+            if not self._launched[bi]:
+                self._launch(bi, in_backward=False)
+        ops.side_join_now()
+        self.comm.wait()
         return 1.0 / self.world
 
 
 def init_from_env(backend: Optional[str] = None):
-    """torch.distributed.run environment -> (rank, world, local_rank); initialises the
-    process group when WORLD_SIZE > 1."""
+    """torch.distributed.run environment -> (rank, world, local_rank).  With WORLD_SIZE > 1 the
+    default process group is the control plane only -- rendezvous store (which carries the
+    RCCL unique id, comm.RcclComm) and barriers -- on gloo unless ``backend`` says otherwise;
+    gradients go over the C-ABI RCCL communicator."""
     import os
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = backend or "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group(backend, device_id=torch.device("cuda", local))

@@ -93,36 +93,40 @@ def arrowed_line(image, start, end, color, tip_length=0.1):
         _line(image, p, end, color)
 
 
+ARROW_COLOR = (1.0, 0.0, 0.0)      # blue in BGR (drawing.py:14)
+ARROW_GRID = (8, 15)               # arrow rows x columns (drawing.py:26-27)
+
+
+def _arrow_end(x, y, flow, width, height):
+    """Tip of the arrow at (x, y): the displaced point rounded half-to-even (np.round) and
+    clamped into the picture."""
+    tip = np.rint(np.asarray([x, y], np.float64) + np.asarray(flow, np.float64))
+    return (int(min(max(tip[0], 0), width - 1)), int(min(max(tip[1], 0), height - 1)))
+
+
 def draw_arrow(image, x, y, optical_flow):
-    """drawing.py:5-14: an arrow from (x, y) to (x, y) + flow, end rounded and clipped."""
-    height, width, _ = image.shape
-    start_point = np.array([x, y])
-    end_point = start_point + optical_flow
-    end_point = np.round(end_point).astype(np.int32)
-    end_point = np.clip(end_point, 0, [width - 1, height - 1])
-    assert end_point[0] < width
-    assert end_point[1] < height
-    arrowed_line(image, tuple(start_point), tuple(end_point), (1.0, 0.0, 0.0))
+    """The arrow of drawing.py:5-14: from (x, y) to (x, y) + flow, tip rounded and clipped
+    to the picture, drawn in place."""
+    h, w = image.shape[:2]
+    arrowed_line(image, (int(x), int(y)), _arrow_end(x, y, optical_flow, w, h), ARROW_COLOR)
+
+
+def _arrow_anchors(height, width):
+    """Arrow origins of drawing.py:28-32: every height//8-th row and width//15-th column."""
+    rows, cols = ARROW_GRID
+    return [(x, y) for y in range(0, height, height // rows) for x in range(0, width, width // cols)]
 
 
 def draw_all_arrows(img1, img2, optical_flow):
-    """drawing.py:17-34: the average of the two images with a 15 x 8 grid of flow arrows."""
-    assert img1.shape == img2.shape
-    height, width, _ = img1.shape
-    assert optical_flow.shape[0] == height
-    assert optical_flow.shape[1] == width
-    assert optical_flow.shape[2] == 2
-    assert img1.max() <= 1
-    assert img2.max() <= 1
-    blended_image = (img1 + img2) * 0.5
-    narrows_per_row = 15
-    narrows_per_col = 8
-    for y in np.arange(0, height, height // narrows_per_col):
-        assert y < height
-        for x in np.arange(0, width, width // narrows_per_row):
-            assert x < width
-            draw_arrow(blended_image, x, y, optical_flow[y, x, :])
-    return blended_image
+    """drawing.py:17-34: the mean of the two pictures (values <= 1) with the flow drawn as an
+    8 x 15 grid of arrows; returns the new picture."""
+    assert img1.shape == img2.shape and img1.max() <= 1 and img2.max() <= 1
+    height, width = img1.shape[:2]
+    assert tuple(optical_flow.shape) == (height, width, 2)
+    picture = 0.5 * (img1 + img2)
+    for x, y in _arrow_anchors(height, width):
+        draw_arrow(picture, x, y, optical_flow[y, x])
+    return picture
 
 
 def resize_linear(img: np.ndarray, out_h: int, out_w: int) -> np.ndarray:

@@ -63,14 +63,27 @@ class Trainer:
     hot loop body of train.py:72-82."""
 
     def __init__(self, flow_net: FlowNet, optimizer: KerasAdam = None, loss_layer=None,
-                 data_parallel: bool = None):
+                 data_parallel: bool = None, comm=None):
+        """data_parallel: sum the gradients over ranks before Adam (default: when a
+        torch.distributed group of > 1 ranks exists).  comm: a communicator (comm.py), or
+        "rccl" / "torch" to create one; default "rccl" for a GPU model (the C-ABI RCCL
+        communicator over all ranks of the default group), "torch" otherwise."""
         self.flow_net = flow_net
         self.optimizer = optimizer or KerasAdam(flow_net.store)
         self.loss_layer = loss_layer or LossLayer()
         if data_parallel is None:
-            data_parallel = torch.distributed.is_initialized() and \
-                torch.distributed.get_world_size() > 1
-        self.reducer = GradBucketReducer(flow_net.store) if data_parallel else None
+            data_parallel = comm is not None or (torch.distributed.is_initialized() and
+                                                 torch.distributed.get_world_size() > 1)
+        self.reducer = None
+        if data_parallel:
+            if comm is None or isinstance(comm, str):
+                from .comm import make_comm
+                dist = torch.distributed
+                rank, world = ((dist.get_rank(), dist.get_world_size())
+                               if dist.is_initialized() else (0, 1))
+                kind = comm or ("rccl" if flow_net.store.arena.is_cuda else "torch")
+                comm = make_comm(kind, rank, world)
+            self.reducer = GradBucketReducer(flow_net.store, comm=comm)
 
     def train_step(self, batch_imgs, step_count=0):
         store = self.flow_net.store

@@ -221,18 +221,21 @@ def upscale_flow(flow):
     return resize_bilinear(flow, flow.shape[1] * 2, flow.shape[2] * 2) * 2.0
 
 
-def flow_head(x, p, prefix):
-    """model.py:104-114: 6 convs 3x3 'same', LeakyReLU(0.3) after the first five."""
+def flow_head(x, p, prefix, masks=None):
+    """model.py:104-114: 6 convs 3x3 'same', LeakyReLU(0.3) after the first five.
+    masks (tests only): per LeakyReLU, a boolean tensor choosing the slope-1 side instead of
+    the sign of the pre-activation -- the slopes another implementation took, so that a
+    comparison is not dominated by pre-activations within rounding of the kink at 0."""
     for i in range(6):
         x = conv2d_same(x, p["%s/conv%d/kernel" % (prefix, i)],
                         p["%s/conv%d/bias" % (prefix, i)], 1)
         if i < 5:
-            x = leaky_relu(x)
+            x = leaky_relu(x) if masks is None else torch.where(masks[i], x, LEAKY_ALPHA * x)
     return x
 
 
-def flow_module(f1, f2, prev, max_disp, p, prefix):
-    """model.py:80-116."""
+def flow_module(f1, f2, prev, max_disp, p, prefix, masks=None):
+    """model.py:80-116 (masks: see flow_head)."""
     if prev is not None:
         flow_up = upscale_flow(prev)
         f2w = warp_features(flow_up, f2)
@@ -243,7 +246,7 @@ def flow_module(f1, f2, prev, max_disp, p, prefix):
         x = torch.cat([f1, cv, flow_up], -1)
     else:
         x = torch.cat([f1, cv], -1)
-    return flow_head(x, p, prefix)
+    return flow_head(x, p, prefix, masks)
 
 
 def flow_net(batch_imgs, p, blocks, max_disp=3):

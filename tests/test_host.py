@@ -97,3 +97,25 @@ def test_bench_kernel_symbols_match_pmc_keys():
     names.add(bench.kernel_symbol(bench.KIND_STEM_X3))
     x3_keys = {k for k in keys if "_x3<" in k or "_x3b<" in k}
     assert x3_keys and x3_keys <= names, sorted(x3_keys - names)
+
+
+def test_draw_all_arrows_geometry():
+    """drawing.py:17-34 arrow grid: 8 rows x 15 columns of anchors, the tip at the rounded,
+    clamped displaced point, the blend (img1 + img2) / 2 elsewhere."""
+    from optical_flow_amd.drawing import ARROW_COLOR, _arrow_anchors, _arrow_end, draw_all_arrows
+    h, w = 32, 60
+    img1 = np.full((h, w, 3), 0.2, np.float32)
+    img2 = np.full((h, w, 3), 0.6, np.float32)
+    flow = np.zeros((h, w, 2), np.float32)
+    flow[..., 0] = 2.5                       # rounds half-to-even: tip at x + 2
+    flow[..., 1] = 100.0                     # clamped to the last row
+    pic = draw_all_arrows(img1, img2, flow)
+    anchors = _arrow_anchors(h, w)
+    assert len(anchors) == 8 * 15 and anchors[0] == (0, 0) and anchors[-1] == (56, 28)
+    assert _arrow_end(4, 8, flow[8, 4], w, h) == (6, h - 1)
+    assert _arrow_end(58, 0, (5.0, -3.0), w, h) == (w - 1, 0)
+    for x, y in anchors:
+        tx, ty = _arrow_end(x, y, flow[y, x], w, h)
+        np.testing.assert_array_equal(pic[ty, tx], ARROW_COLOR)
+    untouched = pic[(pic != np.array(ARROW_COLOR, np.float32)).any(-1)]
+    np.testing.assert_allclose(untouched, 0.4, rtol=1e-6)
