@@ -21,6 +21,7 @@ Prints ONE JSON line (rank 0) with the contract fields plus:
 from __future__ import annotations
 
 import argparse
+import contextlib
 import ctypes as C
 import json
 import os
@@ -54,6 +55,8 @@ def kind_parts(kind):
     implicit GEMM (other shapes) 160 + mode*8 + cfg (optical_flow_amd/csrc/conv_f32.hip)."""
     if kind == KIND_STEM_X3:
         return 0, 0, "stem_x3"
+    if kind >= 192:                               # conv_tile_b16 (bf16 on the x3 structure)
+        return (kind - 192) // 8, (kind - 192) % 8, "tile_b16"
     fam = ("gemm_x3" if kind >= 160 else "tile_x3" if kind >= 128 else "tile_bf16" if kind >= 96 else
            "bf16" if kind >= 64 else
            "tile_f32" if kind >= 32 else "f32")
@@ -101,7 +104,9 @@ def kind_name(kind):
     if fam == "stem_x3":
         return "fwd_stem_x3"
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
-           "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3"}[fam]
+           "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3", "tile_b16": "_tile_b16"}[fam]
+    if fam == "tile_b16":
+        return "%s%s<%s, %d>" % (MODE_NAMES[mode], sfx, X3_BN[cfg], X3_TH[cfg])
     if fam == "gemm_x3":
         return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (GX3_WG if mode == 2 else GX3)[cfg])
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
@@ -121,6 +126,9 @@ def kernel_symbol(kind):
         return "void oflow::conv_stem_x3<32>(oflow::GemmArgs)"   # of_set_tuning key 8 default
     if cfg == 7 and fam == "f32":
         return NARROW_SYMBOLS[mode]
+    if fam == "tile_b16":
+        return "void oflow::conv_tile_b16<%s, %d, %d>(oflow::GemmArgs)" % (X3_BN[cfg], mode,
+                                                                            X3_TH[cfg])
     if fam == "gemm_x3":
         if mode == 2:
             return "void oflow::conv_wgrad_x3<%s>(oflow::GemmArgs)" % GX3_WG[cfg]
@@ -246,6 +254,9 @@ def main():
                     help="fp32: config 2 (headline); bf16: configs 3-5 conv contractions on "
                          "bf16 MFMA with fp32 accumulation")
     ap.add_argument("--tune", default=None, help="key=value[,...] of_set_tuning (experiments)")
+    ap.add_argument("--graph", type=int, choices=[0, 1], default=1,
+                    help="1: capture the train step once as a HIP graph and replay it (the "
+                         "timed steps); 0: eager launches through the Python glue")
     ap.add_argument("--side-stream", type=int, choices=[0, 1], default=1,
                     help="1: weight-gradient kernels on a second HIP stream (ops.side_stream)")
     args = ap.parse_args()
@@ -309,12 +320,42 @@ def main():
             pdom = max(prof_per, key=lambda k: prof_per[k][1])
             prof_only = {ptags[i] for i in range(pn) if pk[i] == pdom}
     torch.cuda.synchronize()
+    graphed = None
+    if args.graph:
+        # The whole step captured once as a HIP graph (Trainer.graphed) and replayed: the
+        # roofline's event pairs are captured with it (hipEventRecordExternal nodes around the
+        # dominant kernel's launches), so every replay re-records them and of_timing_read()
+        # returns the durations of the last timed replay.
+        @contextlib.contextmanager
+        def timed_capture():
+            lib.of_timing_read(0, None, None, None)     # drop the warm-up step's records
+            if live:
+                ops.TIMING_TAGS = []
+                if prof_only is not None:
+                    ops.TIMING_ONLY = prof_only
+                else:
+                    lib.of_timing_enable(1)
+            try:
+                yield
+            finally:
+                ops.TIMING_ONLY = None
+                lib.of_timing_enable(0)
+
+        graphed = trainer.graphed(batch, warmup=1, capture_ctx=timed_capture)
+        for _ in range(2):                              # upload + first replays, untimed
+            graphed()
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     timed_from = max(0, args.steps - args.timing_steps)      # the last timing_steps steps
+    if graphed is not None:
+        timed_from = args.steps - 1                           # the last replay's events
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if graphed is not None:
+            loss, flows = graphed()
+            continue
         if live and i == timed_from:
             ops.TIMING_TAGS = []
             if prof_only is not None:
@@ -449,6 +490,8 @@ def main():
                        "parallelism": "dp%d" % world,
                        "params": sum(p.numel() for p in net.trainable_weights),
                        "conv_math": conv_math(args.precision),
+                       "execution": ("HIP graph: the train step captured once, replayed per step"
+                                     if graphed is not None else "eager launches"),
                        **({"levels": args.levels} if args.levels != 4 else {})},
             "algorithmic_gflop_per_pair": round(gfp, 2),
             "model_tflops": round(gfp * value / 1e3, 2),

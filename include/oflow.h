@@ -294,6 +294,13 @@ int of_sum_partials(const float* const* parts, const int* counts, const float* c
  * m += (g'-m)(1-b1); v += (g'^2-v)(1-b2); p -= lr_t * m / (sqrt(v) + eps). */
 int of_adam_keras(float* p, const float* g, float* m, float* v, int64_t n, float lr_t,
                   float beta1, float beta2, float eps, float gscale, void* stream);
+/* The same update with its schedule in device memory, so a captured step (HIP graph) replays
+ * correctly: one thread first sets t = ++*iter and sched[1] = sched[0] * sqrt(1-b2^t) /
+ * (1-b1^t) (sched[0] = lr, written by the host, e.g. the epoch-15 drop of train.py:69-70),
+ * then the arena update reads lr_t = sched[1]. */
+int of_adam_keras_dev(float* p, const float* g, float* m, float* v, int64_t n, float* sched,
+                      int32_t* iter, float beta1, float beta2, float eps, float gscale,
+                      void* stream);
 
 /* Elementwise helpers used by the host glue. */
 int of_add_inplace(float* y, const float* x, int64_t n, void* stream);        /* y += x */
@@ -323,7 +330,9 @@ int of_timing_enable(int on);
  * (default 1), bit 1 the register-blocked backward (default off: measured slower), key 10 =
  * the fp32 / bf16 GEMM weight gradients' split-K target workgroups per CU (1-16, default 4),
  * key 11 = the split weight gradient of Cout-64 layers whose Cin is not a multiple of 64 on
- * 32 x 64 channel blocks (1, default) or on 64 x 64 blocks (0). */
+ * 32 x 64 channel blocks (1, default) or on 64 x 64 blocks (0);
+ * key 12 = bf16 3x3 stride-1 fwd / dgrad on the single-plane halo kernel conv_tile_b16 (1,
+ * default; timing kinds 192 + 8 mode + cfg) or the round-1 conv_tile_bf16 (0). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

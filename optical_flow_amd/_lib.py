@@ -97,6 +97,7 @@ PROTOTYPES = {
     "of_photo_l1_bwd": (I, [P, P, I, I, I, F, P, P, P]),
     "of_sum_partials": (I, [C.POINTER(P), C.POINTER(I), C.POINTER(F), I, P, P]),
     "of_adam_keras": (I, [P, P, P, P, I64, F, F, F, F, F, P]),
+    "of_adam_keras_dev": (I, [P, P, P, P, I64, P, P, F, F, F, F, P]),
     "of_add_inplace": (I, [P, P, I64, P]),
     "of_copy_strided": (I, [P, I, P, I, I64, I, P]),
     "of_fill": (I, [P, F, I64, P]),

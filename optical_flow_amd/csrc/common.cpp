@@ -66,10 +66,23 @@ static hipEvent_t get_event() {
 
 bool timing_on() { return g_timing; }
 
+// Inside a stream capture (HIP graph) a plain hipEventRecord only expresses a dependency;
+// hipEventRecordExternal makes it an event-record node, so every replay of the graph
+// re-records the pair and of_timing_read() returns the durations of the latest replay.
+static void record(hipEvent_t e, hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive) {
+    if (hipEventRecordWithFlags(e, s, hipEventRecordExternal) != hipSuccess)
+      (void)hipGetLastError();   // not recorded: leave no sticky error for the next launch check
+  } else {
+    (void)hipEventRecord(e, s);
+  }
+}
+
 void timing_begin(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_tmu);
   g_pending_start = get_event();
-  if (g_pending_start) (void)hipEventRecord(g_pending_start, s);
+  if (g_pending_start) record(g_pending_start, s);
 }
 
 void timing_end(hipStream_t s, int kind, double flops) {
@@ -77,7 +90,7 @@ void timing_end(hipStream_t s, int kind, double flops) {
   if (!g_pending_start) return;
   hipEvent_t stop = get_event();
   if (!stop) return;
-  (void)hipEventRecord(stop, s);
+  record(stop, s);
   g_launches.push_back({kind, flops, g_pending_start, stop});
   g_pending_start = nullptr;
   if (g_timing_oneshot) g_timing = g_timing_oneshot = false;

@@ -1259,9 +1259,24 @@ __device__ __forceinline__ void dma16_to_lds(rsrc_t r, uint4* dst, uint32_t voff
                                            voff, soff, 0, 0);
 }
 
-template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int NB = 2>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_tile_x3(GemmArgs a) {
-  constexpr int BM = TH * TF_W, KS = 3, NP = 3;
+// 4 fp32 -> 4 bf16 (RNE, v_cvt_pk_bf16_f32), element 0 in the low half of .x
+__device__ __forceinline__ uint2 pack_bf16x4(const float4& v) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 r;
+  r[0] = (__bf16)v.x;
+  r[1] = (__bf16)v.y;
+  r[2] = (__bf16)v.z;
+  r[3] = (__bf16)v.w;
+  return __builtin_bit_cast(uint2, r);
+}
+
+// The halo-tiled 3x3 stride-1 body shared by the fp32 split kernel (NP = 3 planes: hi / mid /
+// lo, six MFMAs per fragment pair) and the bf16 one (NP = 1: activations rounded to bf16 RNE
+// while staged, the bf16 packed weights, one MFMA per fragment pair).
+template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int NB, int NP>
+__device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
+  constexpr int BM = TH * TF_W, KS = 3;
+  static_assert(NP == 1 || NP == 3, "planes");
   constexpr int HH = TH + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int SM = WM / 16, SN = WN / 16;                    // 16 x 16 MFMA tiles per wave
@@ -1275,12 +1290,16 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
   // rows 4 apart share a bank-slot base, and the float4 reads of a ds_read_b128 lane group
   // (4 EJ lanes per row) cover 16 distinct slots; the 2-way ds_write_b32 conflict is free).
   constexpr int AH_U4 = NP * HP * 4, BS_U4 = NB * NP * BN * 4;
-  constexpr int LDS_B = (AH_U4 + BS_U4) * 16;
+  // (one plane can leave the loop's images smaller than one 16-column epilogue pass: the
+  // array is then sized for that pass)
+  constexpr int EP1_U4 = (NT / 64) * WM * 16 * 4 / 16;
+  constexpr int SM_U4 = AH_U4 + BS_U4 > EP1_U4 ? AH_U4 + BS_U4 : EP1_U4;
+  constexpr int LDS_B = SM_U4 * 16;
   constexpr int EJ = (NT / 64) * WM * 16 * SN * 4 <= LDS_B ? SN
                      : (NT / 64) * WM * 8 * SN * 4 <= LDS_B ? SN / 2 : 1;
   constexpr int EPW = 16 * EJ;
   static_assert(SN % EJ == 0 && (NT / 64) * WM * EPW * 4 <= LDS_B, "epilogue image fits LDS");
-  __shared__ uint4 smem[AH_U4 + BS_U4];
+  __shared__ uint4 smem[SM_U4];
   uint4* Ah = smem;                      // [plane][halo pixel][4 octets]
   uint4* Bs = smem + AH_U4;              // [buf][plane][BN rows][4 octets]
 
@@ -1332,14 +1351,18 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
     for (int j = 0; j < HS; ++j) {
       const int q = tid + NT * j;
       if (q < HQ) {
-        uint2 h, m, l;
-        split3x4(hv[j], h, m, l);
         const int hp = q >> 3;
         const int off = hp * 64 + ((((q & 7) >> 1) ^ x3_sw(hp)) << 4) + 8 * (q & 1);
         char* base = reinterpret_cast<char*>(Ah);
-        *reinterpret_cast<uint2*>(base + off) = h;
-        *reinterpret_cast<uint2*>(base + HP * 64 + off) = m;
-        *reinterpret_cast<uint2*>(base + 2 * HP * 64 + off) = l;
+        if constexpr (NP == 1) {
+          *reinterpret_cast<uint2*>(base + off) = pack_bf16x4(hv[j]);
+        } else {
+          uint2 h, m, l;
+          split3x4(hv[j], h, m, l);
+          *reinterpret_cast<uint2*>(base + off) = h;
+          *reinterpret_cast<uint2*>(base + HP * 64 + off) = m;
+          *reinterpret_cast<uint2*>(base + 2 * HP * 64 + off) = l;
+        }
       }
     }
   };
@@ -1459,6 +1482,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
 #pragma unroll
         for (int j = 0; j < SN; ++j) {
           f32x4 x = acc4[i][j];
+          if constexpr (NP == 1) {
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+            continue;
+          } else {
           if (X3_ABL & 8) {      // ablation: one product (the MFMA count of a bf16 conv)
             asm volatile("" ::"v"(av[1][i]), "v"(av[2][i]), "v"(bv[1][j]), "v"(bv[2][j]));
             acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
@@ -1470,6 +1497,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
           x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
           x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
           acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+          }
         }
       __builtin_amdgcn_sched_barrier(0);   // the stores wait for the prefetch: after the MFMAs
       // single B buffer: every wave must be done with it; double: only with the halo
@@ -1557,6 +1585,28 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_
         epilogue_store<MODE>(a, row, n, v, bias, scale, shift, aux[q]);
     }
   }
+}
+
+template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int NB = 2>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NB == 1 ? 2 : 1) void conv_tile_x3(GemmArgs a) {
+  tile_x3_body<BN, WAVES_M, WAVES_N, MODE, TH, NB, 3>(a);
+}
+
+// bf16 (configs 3-5) 3x3 stride-1 fwd / dgrad on the same structure, one plane: 16x16x32
+// fragments on 64-byte swizzled rows, B by LDS DMA one tap ahead, the 16-byte epilogue.  One
+// plane takes a third of the split kernel's LDS (38 KB at 8 x 32 x 128), so two workgroups
+// share a CU and one's staging / barrier / epilogue overlaps the other's MFMAs.
+// (__launch_bounds__'s second argument is the minimum waves per SIMD: two workgroups of W
+// waves per CU need W / 2.  Waves with more than 48 accumulator registers (the 8 x 32 x 128
+// tile: 64) spill under that bound, and the 12-wave form exceeds 32 waves per CU: those keep
+// one workgroup per CU.)
+constexpr int b16_min_waves(int w, int acc) { return w <= 8 && acc <= 48 ? (w + 1) / 2 : (w + 3) / 4; }
+template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N,
+                             b16_min_waves(WAVES_M * WAVES_N,
+                                           (TH * TF_W / WAVES_M / 16) * (BN / WAVES_N / 16) * 4))
+void conv_tile_b16(GemmArgs a) {
+  tile_x3_body<BN, WAVES_M, WAVES_N, MODE, TH, 2, 1>(a);
 }
 
 // ---- the stem (7x7 stride 2, 3 -> 4 padded input channels, 64 outputs) on the split-bf16
@@ -3909,6 +3959,9 @@ static int g_wgx3_c4 = 1;
 // of_set_tuning key 6: the other shapes' fp32 weight gradient on the split-bf16 implicit GEMM
 // (conv_wgrad_x3, 1) or on the fp32 MFMA GEMM (0).
 static int g_wgx3_gemm = 1;
+// of_set_tuning key 12: bf16 3x3 stride-1 fwd / dgrad on conv_tile_b16 (1, default) or on the
+// round-1 conv_tile_bf16 (0).
+static int g_tile_b16 = 1;
 bool vec_ep_ok(const GemmArgs& a) {
   if (!g_vec_ep || a.N % 4) return false;
   if (a.slab && !(a.slab_ld % 4 == 0 && a.split_stride % 4 == 0 && al16(a.slab))) return false;
@@ -3995,7 +4048,8 @@ bool x3_nb1(const GemmArgs& a) {
   return a.bm != X3_TH0 * TF_W && a.splits == 1 && x3_nb1_candidate(a, false);
 }
 
-GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false) {
+GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false,
+                   bool b16 = false) {
   GemmArgs a = base_args(d);
   const bool fwd = mode == MODE_FWD;
   a.kc = fwd ? g.cin_p : g.cout_p;
@@ -4004,8 +4058,8 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   a.ldb = fwd ? g.kf16 : (int)g.kd16;
   const int OH = fwd ? d->ho : d->h, OW = fwd ? d->wo : d->w;
   // bf16: fwd only (8 x 32 tiles measured +5 % on dec3 fwd, -2 % on dgrad)
-  const bool tall = x3 ? x3_tall(d->n, OH, OW, a.N)
-                       : fwd && pick_bn(a.N) == 128 && x3_tall(d->n, OH, OW, a.N);
+  const bool tall = x3 || b16 ? x3_tall(d->n, OH, OW, a.N)
+                             : fwd && pick_bn(a.N) == 128 && x3_tall(d->n, OH, OW, a.N);
   const int th = tall ? X3_TH0 : TF_H;
   const int m_tiles = d->n * (int)cdiv(OH, th) * (int)cdiv(OW, TF_W);
   a.bm = th * TF_W;
@@ -4023,14 +4077,14 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   G.K = a.K;
   a.splits = 1;
   a.k_per_split = a.K;
-  if (x3) {
-    // One workgroup per CU: choose the K split with the least modelled time, in units of one
+  if (x3 || b16) {
+    // One workgroup per CU (conv_tile_b16: two): choose the K split with the least modelled time, in units of one
     // chunk (9 taps): rounds of 256 workgroups x (chunks per slice + 1 for prologue and
     // epilogue), plus 0.5 per slice and tile round for the slab write and epilogue pass.
     // (Measured: enc.l3 384 tiles unsplit, dec1 192 tiles unsplit, enc.l4 96 tiles in 2.)
     // (The single-buffered BN = 128 4 x 32 configuration, used from X3_NB1_MIN tiles, runs
     // two workgroups per CU.)
-    const int slots = x3_nb1_candidate(a, tall) ? 2 * device_cus() : device_cus();
+    const int slots = (b16 && !tall) || x3_nb1_candidate(a, tall) ? 2 * device_cus() : device_cus();
     int best = 1;
     double best_cost = 1e30;
     for (int sp = 1; sp <= std::min(8, a.K); ++sp) {
@@ -4096,6 +4150,27 @@ int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
   else hipLaunchKernelGGL((conv_tile_x3<32, 4, 1, MODE, 4>), grid, block, 0, s, a);
   if (timing_on()) timing_end(s, 128 + MODE * 8 + cfg, flops);
   int st = check_launch("conv_tile_x3");
+  if (st || a.splits == 1) return st;
+  return launch_splitk_epilogue<MODE>(a, s);
+}
+
+// bf16 3x3 stride-1 fwd / dgrad on conv_tile_b16: timing kinds 192 + mode * 8 + cfg (the
+// conv_tile_x3 configurations; cfg 4, the single-buffered one, is not used).
+template <int MODE>
+int launch_tile_b16(const GemmArgs& a, hipStream_t s, double flops) {
+  const int bn = pick_bn(a.N);
+  dim3 grid(a.tiles_total * a.splits);
+  const bool tall = a.bm == X3_TH0 * TF_W;
+  const int cfg = bn == 128 ? (tall ? 0 : 6) : bn == 96 ? (tall ? 5 : 1) : bn == 64 ? 2 : 3;
+  if (timing_on()) timing_begin(s);
+  if (cfg == 0) hipLaunchKernelGGL((conv_tile_b16<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);
+  else if (cfg == 6) hipLaunchKernelGGL((conv_tile_b16<128, 2, 4, MODE, 4>), grid, dim3(512), 0, s, a);
+  else if (cfg == 5) hipLaunchKernelGGL((conv_tile_b16<96, 4, 3, MODE, X3_TH0>), grid, dim3(768), 0, s, a);
+  else if (cfg == 1) hipLaunchKernelGGL((conv_tile_b16<96, 2, 3, MODE, 4>), grid, dim3(384), 0, s, a);
+  else if (cfg == 2) hipLaunchKernelGGL((conv_tile_b16<64, 4, 2, MODE, 4>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((conv_tile_b16<32, 4, 1, MODE, 4>), grid, dim3(256), 0, s, a);
+  if (timing_on()) timing_end(s, 192 + MODE * 8 + cfg, flops);
+  int st = check_launch("conv_tile_b16");
   if (st || a.splits == 1) return st;
   return launch_splitk_epilogue<MODE>(a, s);
 }
@@ -4348,6 +4423,7 @@ int of_set_tuning(int key, int value) {
   if (key == 4 && value >= 0 && value <= 2) { g_wgx3b = value; return OF_OK; }
   if (key == 5 && (value == 1 || value == 2)) { g_wgx3b_mi = value; return OF_OK; }
   if (key == 6 && (value == 0 || value == 1)) { g_wgx3_gemm = value; return OF_OK; }
+  if (key == 12 && (value == 0 || value == 1)) { g_tile_b16 = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -4414,12 +4490,13 @@ size_t of_conv2d_dgrad_workspace(const of_conv_desc* d) {
 
 size_t of_conv2d_fwd_bf16_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
-  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_FWD) : fwd_args(d, geo(d), true));
+  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_FWD, false, g_tile_b16 != 0)
+                                 : fwd_args(d, geo(d), true));
 }
 
 size_t of_conv2d_dgrad_bf16_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
-  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_DGRAD)
+  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_DGRAD, false, g_tile_b16 != 0)
                                  : dgrad_args(d, geo(d), true));
 }
 
@@ -4456,7 +4533,8 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   }
   Geo g = geo(d);
   const bool tile = (bf16 || x3) && tile_ok(d);
-  GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3) : fwd_args(d, g, bf16 || x3);
+  const bool b16 = tile && bf16 && g_tile_b16;
+  GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3, b16) : fwd_args(d, g, bf16 || x3);
   bool stem = x3 && !tile && g_stem_x3 && stem_x3_ok(d);
   if (stem) {                            // conv_stem_x3: one workgroup per output tile, no split
     a.splits = 1;
@@ -4509,6 +4587,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
     return check_launch("conv_stem_x3");
   }
   st = x3     ? (tile ? launch_tile_x3<MODE_FWD>(a, s, flops) : launch_gemm_x3<MODE_FWD>(a, s, flops))
+       : b16  ? launch_tile_b16<MODE_FWD>(a, s, flops)
        : tile ? launch_tile_bf16<MODE_FWD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops)
               : launch_gemm<MODE_FWD>(a, s, flops);
@@ -4563,7 +4642,9 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   }
   const bool tile = (bf16 || x3) && tile_ok(d);
   const bool in_place = add && add == dx && ld_add == lddx;
-  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3) : dgrad_args(d, g, bf16 || x3, in_place);
+  const bool b16 = tile && bf16 && g_tile_b16;
+  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3, b16)
+                    : dgrad_args(d, g, bf16 || x3, in_place);
   if (x3 && !tile) gemm_x3_plan(a);
   if (a.tiles_total == 0) return OF_OK;                 // every output already final
   attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
@@ -4588,6 +4669,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   a.vec_ep = vec_ep_ok(a);
   st = x3     ? (tile ? launch_tile_x3<MODE_DGRAD>(a, s, flops)
                      : launch_gemm_x3<MODE_DGRAD>(a, s, flops))
+       : b16  ? launch_tile_b16<MODE_DGRAD>(a, s, flops)
        : tile ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops)
               : launch_gemm<MODE_DGRAD>(a, s, flops);

@@ -415,6 +415,51 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
   }
 }
 
+// Device-resident schedule for a graph-captured step: sched[0] = lr (set by the host between
+// steps), sched[1] <- lr_t of the step about to run; *iter counts applied updates.  One
+// thread, launched right before adam_dev_kernel, so a replayed graph advances t by itself.
+__global__ void adam_sched_kernel(float* __restrict__ sched, int32_t* __restrict__ iter,
+                                  float b1, float b2) {
+  const int t = *iter + 1;
+  *iter = t;
+  const double lr = sched[0];
+  sched[1] = (float)(lr * sqrt(1.0 - pow((double)b2, (double)t)) / (1.0 - pow((double)b1, (double)t)));
+}
+
+__global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p,
+                                                       const float* __restrict__ g,
+                                                       float* __restrict__ m,
+                                                       float* __restrict__ v, int64_t n,
+                                                       const float* __restrict__ sched, float b1,
+                                                       float b2, float eps, float gs) {
+  const float lr_t = sched[1];
+  const int64_t nq = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (int64_t i = tid; i < nq; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    gg.x *= gs; gg.y *= gs; gg.z *= gs; gg.w *= gs;
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+#define OF_ADAM1(c)                                  \
+  mm.c += (gg.c - mm.c) * (1.f - b1);                \
+  vv.c += (gg.c * gg.c - vv.c) * (1.f - b2);         \
+  pp.c -= lr_t * mm.c / (sqrtf(vv.c) + eps);
+    OF_ADAM1(x) OF_ADAM1(y) OF_ADAM1(z) OF_ADAM1(w)
+#undef OF_ADAM1
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  for (int64_t i = 4 * nq + tid; i < n; i += stride) {
+    const float gi = g[i] * gs;
+    m[i] += (gi - m[i]) * (1.f - b1);
+    v[i] += (gi * gi - v[i]) * (1.f - b2);
+    p[i] -= lr_t * m[i] / (sqrtf(v[i]) + eps);
+  }
+}
+
 // ---------------------------------------------------------------------- elementwise ----
 __global__ __launch_bounds__(256) void add_kernel(float* __restrict__ y,
                                                   const float* __restrict__ x, int64_t n) {
@@ -579,6 +624,21 @@ int of_adam_keras(float* p, const float* g, float* m, float* v, int64_t n, float
   hipLaunchKernelGGL(adam_kernel, dim3(std::min<int64_t>(grid_of(n / 4 + 1), 2048)), dim3(256),
                      0, as_stream(stream), p, g, m, v, n, lr_t, beta1, beta2, eps, gscale);
   return check_launch("adam");
+}
+
+int of_adam_keras_dev(float* p, const float* g, float* m, float* v, int64_t n, float* sched,
+                      int32_t* iter, float beta1, float beta2, float eps, float gscale,
+                      void* stream) {
+  OF_CHECK_ARG(p && g && m && v && sched && iter && n >= 0, "adam dev: args");
+  OF_CHECK_ARG((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0,
+               "adam: arenas must be 16-byte aligned");
+  hipLaunchKernelGGL(adam_sched_kernel, dim3(1), dim3(1), 0, as_stream(stream), sched, iter,
+                     beta1, beta2);
+  if (n > 0)
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(std::min<int64_t>(grid_of(n / 4 + 1), 2048)),
+                       dim3(256), 0, as_stream(stream), p, g, m, v, n, sched, beta1, beta2, eps,
+                       gscale);
+  return check_launch("adam dev");
 }
 
 int of_act_bwd(const float* dy, const float* y, int act, float alpha, float* dz, int64_t n,

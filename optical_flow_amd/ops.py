@@ -387,7 +387,9 @@ class ConvPacker:
 
     def ensure(self):
         v = self.version_of()
-        if v == self._version:
+        # inside a HIP-graph capture the pack is always recorded: every replay follows an
+        # optimizer update that the host-side version counter does not see
+        if v == self._version and not torch.cuda.is_current_stream_capturing():
             return
         call("of_conv_pack_many", C.c_void_p(self.table.data_ptr()), self.total, _stream())
         for L in self.layers:

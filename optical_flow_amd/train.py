@@ -16,6 +16,7 @@ Run:  python -m optical_flow_amd.train --height 384 --width 512 --batch 8 --step
 from __future__ import annotations
 
 import argparse
+import contextlib
 import ctypes as C
 import json
 import math
@@ -36,25 +37,42 @@ from .model import FlowNet, build_flow_net
 
 class KerasAdam:
     """tf.keras.optimizers.Adam (train.py:34): beta_1 0.9, beta_2 0.999, epsilon 1e-7,
-    ResourceApplyAdam update with lr_t = lr*sqrt(1-b2^t)/(1-b1^t) (P13).  One fused launch
-    over the model's parameter arena."""
+    ResourceApplyAdam update with lr_t = lr*sqrt(1-b2^t)/(1-b1^t) (P13).  Two launches over
+    the model's parameter arena: the step counter t and lr_t live in device memory
+    (of_adam_keras_dev), so the same update also runs inside a captured HIP graph
+    (Trainer.graphed).  ``learning_rate`` may be set between steps (train.py:69-70)."""
 
     def __init__(self, store, learning_rate=1e-4, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
         self.store = store
-        self.learning_rate = learning_rate
         self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
-        self.iterations = 0
+        dev = store.arena.device
         self.m = torch.zeros_like(store.arena)
         self.v = torch.zeros_like(store.arena)
+        self._sched = torch.zeros(2, device=dev)              # [lr, lr_t of the last step]
+        self._iter = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.learning_rate = learning_rate
+
+    @property
+    def learning_rate(self):
+        return self._lr
+
+    @learning_rate.setter
+    def learning_rate(self, lr):
+        self._lr = float(lr)
+        self._sched[0].fill_(self._lr)
+
+    @property
+    def iterations(self):
+        """Updates applied so far (device counter: replays of a captured step count too)."""
+        return int(self._iter.item())
 
     def apply_gradients(self, grad_scale: float = 1.0):
-        t = self.iterations + 1
-        lr_t = self.learning_rate * math.sqrt(1.0 - self.beta_2 ** t) / (1.0 - self.beta_1 ** t)
         s = self.store
-        call("of_adam_keras", C.c_void_p(s.arena.data_ptr()), C.c_void_p(s.grad_arena.data_ptr()),
-             C.c_void_p(self.m.data_ptr()), C.c_void_p(self.v.data_ptr()), s.numel, lr_t,
-             self.beta_1, self.beta_2, self.epsilon, grad_scale, ops._stream())
-        self.iterations += 1
+        call("of_adam_keras_dev", C.c_void_p(s.arena.data_ptr()),
+             C.c_void_p(s.grad_arena.data_ptr()), C.c_void_p(self.m.data_ptr()),
+             C.c_void_p(self.v.data_ptr()), s.numel, C.c_void_p(self._sched.data_ptr()),
+             C.c_void_p(self._iter.data_ptr()), self.beta_1, self.beta_2, self.epsilon,
+             grad_scale, ops._stream())
         s.version += 1       # packed conv weights are refreshed lazily on next use
 
 
@@ -96,6 +114,50 @@ class Trainer:
         scale = self.reducer.finish() if self.reducer is not None else 1.0
         self.optimizer.apply_gradients(grad_scale=scale)
         return loss_value.detach(), [f.detach() for f in flows]
+
+    def graphed(self, batch_imgs, warmup: int = 2, capture_ctx=None):
+        """The step captured once as a HIP graph over a static input batch (train.py:47-48
+        traces train_step once as a tf.function; this is the MI355X counterpart): returns a
+        GraphedStep whose call copies nothing and replays every kernel of forward, loss,
+        backward, bucket all-reduce (RCCL) and Adam with no host work per launch.
+        ``warmup`` eager steps run first (they train, like any step)."""
+        return GraphedStep(self, batch_imgs, warmup, capture_ctx)
+
+
+class GraphedStep:
+    """A captured Trainer.train_step.  ``batch`` is the static input: write the next batch
+    into it (``load``) before calling.  Returns the static (loss, flows) tensors, overwritten
+    by every replay."""
+
+    def __init__(self, trainer: "Trainer", batch_imgs, warmup: int = 2, capture_ctx=None):
+        """capture_ctx: optional context-manager factory entered around the capture only (the
+        bench arms its kernel timing there)."""
+        if trainer.reducer is not None and getattr(trainer.reducer.comm, "kind", "") != "rccl":
+            raise RuntimeError("graph capture needs the RCCL communicator (gloo collectives "
+                               "cannot be captured)")
+        self.trainer = trainer
+        self.batch = batch_imgs
+        cur = torch.cuda.current_stream()
+        s = torch.cuda.Stream()
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):                   # warm-up off the default stream (torch
+            for i in range(warmup):                  # capture rule), creates the side streams
+                trainer.train_step(batch_imgs, i)
+        cur.wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with capture_ctx() if capture_ctx is not None else contextlib.nullcontext():
+            with torch.cuda.graph(self.graph):
+                self.loss, self.flows = trainer.train_step(batch_imgs)
+
+    def load(self, batch_imgs):
+        self.batch.copy_(batch_imgs, non_blocking=True)
+
+    def __call__(self, batch_imgs=None, step_count=0):
+        if batch_imgs is not None and batch_imgs.data_ptr() != self.batch.data_ptr():
+            self.load(batch_imgs)
+        self.graph.replay()
+        self.trainer.flow_net.store.version += 1
+        return self.loss, self.flows
 
 
 def main(argv=None):

@@ -73,7 +73,7 @@ def _run(H, W, B, precision="fp32", seed=0):
         for d in L._descs.values():
             if L.fwd_entry(d)[1] > 0:
                 split.add((L.name, 0))
-            if L.cout > 4 and L.dgrad_entry(d)[1] > 0:
+            if L.cout > 4 and L.name != "conv1" and L.dgrad_entry(d)[1] > 0:   # images: no dgrad
                 split.add((L.name, 1))
     del net, flows, loss, bd
     torch.cuda.empty_cache()

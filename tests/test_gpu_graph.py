@@ -1,0 +1,91 @@
+"""The train step captured as a HIP graph (Trainer.graphed; train.py:47-48 traces train_step
+once as a tf.function, this is the MI355X counterpart): the replays must train exactly like the
+eager step -- against the oracle's Keras-Adam trajectory, and against the eager HIP step in
+both precisions and with the RCCL bucket all-reduce captured inside the graph."""
+import pytest
+import torch
+
+from helpers import REL_TOL, dev, rel_l2
+from oracle import ref_flow as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(H, W, precision="fp32", seed=3, comm=None, lr=1e-4):
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import flow_net_spec, init_params, perturb_params
+    from optical_flow_amd.train import KerasAdam, Trainer
+    vals = perturb_params(init_params(flow_net_spec(), seed), seed + 1)
+    net = FlowNet(H, W, values=vals, precision=precision)
+    return Trainer(net, KerasAdam(net.store, learning_rate=lr), data_parallel=comm is not None,
+                   comm=comm), vals
+
+
+def test_graph_trajectory_vs_oracle():
+    """10 Keras-Adam steps: 1 eager warm-up step, then 9 replays of the captured step; loss
+    per replayed step and the final weights within 1e-3 of the oracle's (SURVEY.md §8 d)."""
+    from optical_flow_amd.data import synthetic_batch
+    from optical_flow_amd.params import encoder_blocks
+    H, W, B = 64, 128, 2
+    trainer, vals = _trainer(H, W)
+    batch = synthetic_batch(B, H, W, seed=3)
+    p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+    opt_o = R.KerasAdam(lr=1e-4)
+    bo = torch.tensor(batch, dtype=torch.float64)
+    losses_o = [R.train_step(bo, p, list(encoder_blocks()), opt_o)[0].item() for _ in range(10)]
+    step = trainer.graphed(dev(torch.from_numpy(batch)), warmup=1)
+    for k in range(1, 10):
+        loss, _ = step()
+        lv = loss.item()
+        rel = abs(lv - losses_o[k]) / abs(losses_o[k])
+        print("graph step %d loss %.6e oracle %.6e rel %.2e" % (k, lv, losses_o[k], rel))
+        assert rel < REL_TOL
+    assert trainer.optimizer.iterations == 10
+    net = trainer.flow_net
+    for name in net.weight_names:
+        assert rel_l2(net.store.params[name], p[name]) < REL_TOL, name
+
+
+def _sync_state(dst, src):
+    """Copy weights, Adam moments and the Adam step counter of trainer src into dst."""
+    dst.flow_net.store.arena.copy_(src.flow_net.store.arena)
+    dst.flow_net.store.version += 1
+    for name in ("m", "v", "_iter", "_sched"):
+        getattr(dst.optimizer, name).copy_(getattr(src.optimizer, name))
+
+
+@pytest.mark.parametrize("precision,comm", [("fp32", None), ("bf16", None), ("fp32", "rccl")],
+                         ids=["fp32", "bf16", "fp32_rccl_world1"])
+def test_graph_matches_eager(precision, comm):
+    """Each replay of the captured step (a new batch loaded into the static input first) does
+    what one eager step does from the same state: before every replay an eager trainer takes
+    the graphed trainer's weights, Adam moments and step counter and runs train_step on the
+    same batch; loss, every gradient and the updated weights agree up to the feature-warp
+    backward's atomic-order noise.  (Comparing whole trajectories instead would measure
+    Adam's amplification of that noise: a gradient near 0 whose sign flips moves its weight
+    by 2 lr.)  With comm="rccl" the bucket all-reduces of a one-rank RCCL communicator are
+    inside the captured graph."""
+    from optical_flow_amd.comm import RcclComm
+    from optical_flow_amd.data import synthetic_batch
+    H, W, B = 128, 256, 2
+    batches = [dev(torch.from_numpy(synthetic_batch(B, H, W, seed=40 + i))) for i in range(5)]
+    c = RcclComm(0, 1) if comm == "rccl" else None
+    gt, _ = _trainer(H, W, precision, comm=c)
+    eager, _ = _trainer(H, W, precision)
+    step = gt.graphed(batches[0].clone(), warmup=1)
+    for k, b in enumerate(batches[1:]):
+        _sync_state(eager, gt)
+        le, _ = eager.train_step(b)
+        lg, _ = step(b)
+        torch.cuda.synchronize()
+        ge, gg = eager.flow_net.store.grad_arena, gt.flow_net.store.grad_arena
+        eg = rel_l2(gg, ge)
+        ew = rel_l2(gt.flow_net.store.arena, eager.flow_net.store.arena)
+        print("%s %s replay %d: loss %.7e vs eager %.7e, grads rel_l2 %.2e, weights %.2e" % (
+            precision, comm, k, float(lg), float(le), eg, ew))
+        assert abs(float(lg) - float(le)) <= 1e-6 * abs(float(le))
+        assert eg < 1e-4, eg
+        assert ew < 1e-5, ew
+    assert gt.optimizer.iterations == 5
+    if c is not None:
+        c.close()
