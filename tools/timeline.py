@@ -30,7 +30,7 @@ def main():
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    adam = [i for i, r in enumerate(rows) if "adam_kernel" in r[2]]
+    adam = [i for i, r in enumerate(rows) if re.search(r"adam_(dev_)?kernel", r[2])]
     if len(adam) < args.steps + 1:
         raise SystemExit("need %d adam launches, got %d" % (args.steps + 1, len(adam)))
     spans = []
