@@ -401,6 +401,48 @@ int of_flow_color(const float* flow, int n, int h, int w, uint8_t* bgr, float* w
 /* draw_optical_flow_intensity (drawing.py:37-42): min(sqrt(u^2 + u^2) / 20, 1) per pixel. */
 int of_flow_intensity(const float* flow, int64_t npix, float* out, void* stream);
 
+/* ==== Inference BatchNorm folded into the backward (FusedBatchNormGrad, model.py:14 and the
+ * resnet blocks; P5).  With y = act(BN(z) + res), BN(z) = gamma zhat + beta, zhat = (z - mean) /
+ * sqrt(var + eps), and t = dL/dy * act'(y):  dbeta = sum t, dgamma = sum t zhat, dbias = s sum t
+ * and dz = t s with s = gamma / sqrt(var + eps).  dz is never formed: s is folded into the
+ * conv's packed input-gradient weights (of_conv_pack_weights_bn / of_conv_pack_table_bn) and its
+ * weight-gradient reduction (of_conv2d_wgrad_bn), both then take t.  z is not stored either:
+ * zhat is recovered from y where t != 0, zhat = (y - res - beta) / gamma (gamma != 0). */
+int of_conv_pack_weights_bn(const of_conv_desc* d, int precision, const float* w_hwio,
+                            void* w_fwd, void* w_bwd, const float* bn_gamma,
+                            const float* bn_var, float bn_eps, void* stream);
+/* precision[i]: 0 fp32, 1 bf16, 2 fp32 split planes; bn_gamma[i] == NULL: no BN on conv i. */
+int of_conv_pack_table_bn(int nconv, const of_conv_desc* descs, const float* const* w_hwio,
+                          void* const* w_fwd, void* const* w_bwd, const int* precision,
+                          const float* const* bn_gamma, const float* const* bn_var,
+                          float bn_eps, void* host_table);
+/* dw = s * (x^T t) (HWIO; accumulate != 0 adds); precision as above, workspace of
+ * of_conv2d_wgrad_bn_workspace(d, precision) bytes. */
+size_t of_conv2d_wgrad_bn_workspace(const of_conv_desc* d, int precision);
+int of_conv2d_wgrad_bn(const of_conv_desc* d, int precision, const float* x, int ldx,
+                       const float* t, int ldt, float* dw, int accumulate, const float* bn_gamma,
+                       const float* bn_var, float bn_eps, void* workspace, size_t ws_bytes,
+                       void* stream);
+/* Input gradient of a layer whose input x = relu(u) has several consumers:
+ * dx = act'(act_src) * (dgrad(dy) + add), the derivative applied after the sum (add may be
+ * NULL; add == dx in place).  The producer-side t of the layer before. */
+int of_conv2d_dgrad_add_act(const of_conv_desc* d, int precision, const float* dy, int lddy,
+                            const void* w_bwd, const float* add, int ld_add,
+                            const float* act_src, int ld_act, int act, float alpha, float* dx,
+                            int lddx, void* workspace, size_t ws_bytes, void* stream);
+/* BN backward reductions from t (act NONE: dy is t) or from dy (act RELU: t = dy [y > 0],
+ * written to t_out if non-NULL); res: the residual added before the activation, or NULL.
+ * dgamma / dbeta / dbias: [c] (NULL to skip).  Workspace: of_bn_act_bwd_workspace(npix, c). */
+int of_bn_bwd_reduce(int64_t npix, int c, int act, const float* dy, const float* y,
+                     const float* res, const float* gamma, const float* beta, const float* var,
+                     float eps, float* t_out, float* dgamma, float* dbeta, float* dbias,
+                     int accumulate, void* workspace, void* stream);
+/* of_maxpool_bn_act_bwd without z (zhat from y) for the stem: conv1 -> BN -> ReLU -> max-pool. */
+int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const float* g,
+                           const float* y, const float* gamma, const float* beta,
+                           const float* var, float eps, float* dz, float* dgamma, float* dbeta,
+                           float* dbias, int accumulate, void* workspace, void* stream);
+
 /* ==== SURVEY.md §8 b / §8 e: gradient all-reduce over RCCL (build-added K14) ============= */
 /* The reference is single-process (train.py:47-61); batch data parallelism sums the
  * gradients tape.gradient() returns (train.py:55) across ranks before the Adam update

@@ -120,6 +120,15 @@ PROTOTYPES = {
     "of_flow_color": (I, [P, I, I, I, P, P, P]),
     "of_flow_intensity": (I, [P, I64, P, P]),
     "of_crc32c": (C.c_uint32, [P, I64, C.c_uint32]),   # checkpoint bundles (row 2)
+    # inference BN folded into the backward
+    "of_conv_pack_weights_bn": (I, [PD, I, P, P, P, P, P, F, P]),
+    "of_conv_pack_table_bn": (I, [I, PD, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(I),
+                                  C.POINTER(P), C.POINTER(P), F, P]),
+    "of_conv2d_wgrad_bn_workspace": (SZ, [PD, I]),
+    "of_conv2d_wgrad_bn": (I, [PD, I, P, I, P, I, P, I, P, P, F, P, SZ, P]),
+    "of_conv2d_dgrad_add_act": (I, [PD, I, P, I, P, P, I, P, I, I, F, P, I, P, SZ, P]),
+    "of_bn_bwd_reduce": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
+    "of_maxpool_bn_relu_bwd": (I, [I, I, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     # gradient all-reduce over RCCL (SURVEY §8 b / e)
     "of_comm_id_bytes": (I, []),
     "of_comm_get_unique_id": (I, [P]),

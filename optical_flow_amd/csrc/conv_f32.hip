@@ -82,8 +82,17 @@ struct GemmArgs {
   int ngroups;
   int vec_ep;             // tile kernels: 4-column epilogue (N, every ld a multiple of 4,
                           // every row pointer 16-byte aligned)
+  int act_post;           // dgrad: dx = act'(act_src) * (sum + res) instead of act' * sum + res
   Group grp[MAX_GROUPS];
 };
+
+// dgrad epilogue value: the input gradient v times the producer's activation derivative at s,
+// plus an added gradient r -- or, with act_post, the derivative applied to the sum (the
+// gradient of a ReLU output that has several consumers: encoder block inputs).
+__device__ __forceinline__ float dgrad_ep(const GemmArgs& a, float v, float s, float r) {
+  const float d = s > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
+  return a.act_post ? (v + r) * d : v * d + r;
+}
 
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
   a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
@@ -144,8 +153,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& a, int64_t row, i
     v += aux.s;
     v = act_fwd(v, a.act, a.alpha);
   } else if (MODE == MODE_DGRAD) {
-    v *= aux.s > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
-    v += aux.r;
+    v = dgrad_ep(a, v, aux.s, aux.r);
   }
   a.C[row * a.ldc + n] = v;
 }
@@ -193,20 +201,13 @@ __device__ __forceinline__ void epilogue_store4(const GemmArgs& a, int split, in
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], a.act, a.alpha);
   } else if (MODE == MODE_DGRAD) {
-    if (a.act_src) {
-      const float4 s4 = *reinterpret_cast<const float4*>(&a.act_src[row * a.ld_act + n]);
-      const float s[4] = {s4.x, s4.y, s4.z, s4.w};
-      const float neg = a.act == OF_ACT_LEAKY ? a.alpha : 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= s[e] > 0.f ? 1.f : neg;
-    }
-    if (a.res) {
-      const float4 r = *reinterpret_cast<const float4*>(&a.res[row * a.ldr + n]);
-      v[0] += r.x;
-      v[1] += r.y;
-      v[2] += r.z;
-      v[3] += r.w;
-    }
+    float4 s4 = make_float4(1.f, 1.f, 1.f, 1.f), r4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.act_src) s4 = *reinterpret_cast<const float4*>(&a.act_src[row * a.ld_act + n]);
+    if (a.res) r4 = *reinterpret_cast<const float4*>(&a.res[row * a.ldr + n]);
+    v[0] = dgrad_ep(a, v[0], s4.x, r4.x);
+    v[1] = dgrad_ep(a, v[1], s4.y, r4.y);
+    v[2] = dgrad_ep(a, v[2], s4.z, r4.z);
+    v[3] = dgrad_ep(a, v[3], s4.w, r4.w);
   }
   *reinterpret_cast<float4*>(&a.C[row * a.ldc + n]) = make_float4(v[0], v[1], v[2], v[3]);
 }
@@ -3518,8 +3519,7 @@ __global__ __launch_bounds__(256) void splitk_epilogue_flat(GemmArgs a) {
           if (a.bn_g) v[e] = v[e] * scale + shift;
           v[e] = act_fwd(v[e] + s[e], a.act, a.alpha);
         } else {
-          v[e] *= s[e] > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
-          v[e] += r[e];
+          v[e] = dgrad_ep(a, v[e], s[e], r[e]);
         }
       }
       if (MODE == MODE_FWD && a.z)
@@ -3599,8 +3599,15 @@ struct PackEntry {
   int kf16;
   int64_t kd16;
   int64_t work_begin;      // cumulative elements (fwd then bwd) before this entry
+  const float* bn_g;       // non-NULL: the input-gradient image is scaled per output channel
+  const float* bn_v;       // by gamma / sqrt(var + eps) (inference BN folded into the dgrad)
+  float bn_eps;
   PackGroups pg;
 };
+
+__device__ __forceinline__ float bn_fold(const PackEntry& E, int co) {
+  return E.bn_g ? E.bn_g[co] * rsqrtf(E.bn_v[co] + E.bn_eps) : 1.f;
+}
 
 struct PackTableHeader {
   int nconv;
@@ -3652,7 +3659,7 @@ __device__ void pack_elem(const PackEntry& E, int k) {
       if (t < pg.ntaps[g] && co < E.cout && ci < E.cin) {
         const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
         const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
-        v = E.w[((r * E.kw + ss) * E.cin + ci) * E.cout + co];
+        v = E.w[((r * E.kw + ss) * E.cin + ci) * E.cout + co] * bn_fold(E, co);
       }
       put16(E.bf16, E.wd, k, E.kd16 * E.nd, v);
     }
@@ -3680,7 +3687,7 @@ __device__ void pack_elem(const PackEntry& E, int k) {
     if (t < pg.ntaps[g] && co < E.cout && nn < E.cin) {
       const int r = pg.r0[g] + pg.dt * (t / pg.ns[g]);
       const int ss = pg.s0[g] + pg.dt * (t % pg.ns[g]);
-      v = E.w[((r * E.kw + ss) * E.cin + nn) * E.cout + co];
+      v = E.w[((r * E.kw + ss) * E.cin + nn) * E.cout + co] * bn_fold(E, co);
     }
     E.wd[k] = v;
   }
@@ -3728,7 +3735,10 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
                                                            int splits, int64_t split_stride,
                                                            int taps, int kc, int cin, int cout,
                                                            int ldc, float* __restrict__ dw,
-                                                           float* __restrict__ db, int accum) {
+                                                           float* __restrict__ db, int accum,
+                                                           const float* __restrict__ bn_g,
+                                                           const float* __restrict__ bn_v,
+                                                           float bn_eps) {
   __shared__ float4 red[EP_LANES][EP_ITEMS];
   const int it = threadIdx.x % EP_ITEMS, sl = threadIdx.x / EP_ITEMS;
   const int cq = (cout + 3) / 4;
@@ -3753,9 +3763,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   __syncthreads();
   if (sl != 0 || !live) return;
   for (int k = 1; k < EP_LANES; ++k) add4(acc, red[k][it]);
-  const float v[4] = {acc.x, acc.y, acc.z, acc.w};
+  float v[4] = {acc.x, acc.y, acc.z, acc.w};
   float* dst = is_bias ? db + 4 * q : dw + (int64_t)row * cout + 4 * q;
   const int nv = min(4, cout - 4 * q);
+  if (bn_g)                       // dL/dz = t * gamma / sqrt(var + eps), folded per column
+    for (int e = 0; e < nv; ++e) v[e] *= bn_g[4 * q + e] * rsqrtf(bn_v[4 * q + e] + bn_eps);
   for (int e = 0; e < nv; ++e) dst[e] = accum ? dst[e] + v[e] : v[e];
 }
 
@@ -4657,7 +4669,7 @@ int of_conv2d_fwd_bf16(const of_conv_desc* d, const float* x, int ldx, const voi
 static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int lddy,
                            const void* w_bwd, const float* act_src, int ld_act, int act,
                            float alpha, const float* add, int ld_add, float* dx, int lddx,
-                           void* workspace, size_t ws_bytes, void* stream) {
+                           void* workspace, size_t ws_bytes, void* stream, int act_post = 0) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
@@ -4672,7 +4684,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
                "conv dgrad: dy / w must be 16-byte aligned");
   OF_CHECK_ARG(d->stride == 1 || d->stride == 2, "conv dgrad: stride must be 1 or 2");
   if (!prec && narrow_ok(d)) {
-    OF_CHECK_ARG(!add, "conv dgrad: the Cout <= 4 kernels take no added gradient");
+    OF_CHECK_ARG(!add && !act_post, "conv dgrad: the Cout <= 4 kernels take no added gradient");
     hipStream_t s = as_stream(stream);
     if (timing_on()) timing_begin(s);
     st = narrow_dgrad(d, dy, lddy, static_cast<const float*>(w_bwd), act_src, ld_act, act,
@@ -4704,6 +4716,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   a.alpha = alpha;
   a.res = add;
   a.ldr = ld_add;
+  a.act_post = act_post;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   a.vec_ep = vec_ep_ok(a);
@@ -4821,7 +4834,9 @@ size_t of_conv2d_wgrad_x3_workspace(const of_conv_desc* d) {
 // prec: 0 fp32 MFMA, 1 bf16, 2 fp32 with conv_wgrad_tile_x3 where wgx3_ok (else as 0).
 static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int ldx,
                            const float* dy, int lddy, float* dw, float* db, int accumulate,
-                           void* workspace, size_t ws_bytes, void* stream) {
+                           void* workspace, size_t ws_bytes, void* stream,
+                           const float* bn_g = nullptr, const float* bn_v = nullptr,
+                           float bn_eps = 0.f) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
@@ -4832,6 +4847,7 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv wgrad: lddy");
   if (narrow_ok(d)) {
+    OF_CHECK_ARG(!bn_g, "conv wgrad: the Cout <= 4 kernels take no BN scale");
     OF_CHECK_ARG(ws_bytes >= narrow_wgrad_ws(d), "conv wgrad: workspace too small");
     hipStream_t s = as_stream(stream);
     if (timing_on()) timing_begin(s);
@@ -4959,7 +4975,7 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   const int64_t items = ((int64_t)g.taps * d->cin + (db ? 1 : 0)) * cdiv(d->cout, 4);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
                      static_cast<const float*>(workspace), p.splits, p.split_stride, g.taps,
-                     g.cin_p, d->cin, d->cout, p.ldc, dw, db, accumulate);
+                     g.cin_p, d->cin, d->cout, p.ldc, dw, db, accumulate, bn_g, bn_v, bn_eps);
   return check_launch("wgrad_reduce");
 }
 
@@ -4982,6 +4998,71 @@ int of_conv2d_wgrad_x3(const of_conv_desc* d, const float* x, int ldx, const flo
                        size_t ws_bytes, void* stream) {
   return conv_wgrad_impl(2, d, x, ldx, dy, lddy, dw, db, accumulate, workspace, ws_bytes,
                          stream);
+}
+
+
+// ---- inference-BN folded into the backward (FusedBatchNormGrad) --------
+int of_conv_pack_weights_bn(const of_conv_desc* d, int precision, const float* w_hwio,
+                            void* w_fwd, void* w_bwd, const float* bn_gamma,
+                            const float* bn_var, float bn_eps, void* stream) {
+  int st = validate(d);
+  if (st) return st;
+  OF_CHECK_ARG(precision >= 0 && precision <= 2, "pack bn: precision 0, 1 or 2");
+  OF_CHECK_ARG(w_hwio && w_fwd && w_bwd, "pack bn: NULL pointer");
+  OF_CHECK_ARG(!bn_gamma || bn_var, "pack bn: gamma without var");
+  const int64_t total = pack_work(d, precision ? 1 : 0);
+  OF_CHECK_ARG(total < INT32_MAX, "pack: layer too large");
+  PackEntry E = pack_entry(d, w_hwio, w_fwd, w_bwd, precision);
+  E.bn_g = bn_gamma;
+  E.bn_v = bn_var;
+  E.bn_eps = bn_eps;
+  const int blocks = (int)std::min<int64_t>(cdiv(total, 256), 4096);
+  hipLaunchKernelGGL(pack_one_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), E, total);
+  return check_launch("pack_bn");
+}
+
+int of_conv_pack_table_bn(int nconv, const of_conv_desc* descs, const float* const* w_hwio,
+                          void* const* w_fwd, void* const* w_bwd, const int* precision,
+                          const float* const* bn_gamma, const float* const* bn_var,
+                          float bn_eps, void* host_table) {
+  int st = of_conv_pack_table_ex(nconv, descs, w_hwio, w_fwd, w_bwd, precision, host_table);
+  if (st || !bn_gamma) return st;
+  OF_CHECK_ARG(bn_var != nullptr, "pack table bn: gamma without var");
+  PackEntry* e = reinterpret_cast<PackEntry*>(static_cast<char*>(host_table) +
+                                              sizeof(PackTableHeader));
+  for (int i = 0; i < nconv; ++i) {
+    OF_CHECK_ARG(!bn_gamma[i] || bn_var[i], "pack table bn: gamma without var");
+    e[i].bn_g = bn_gamma[i];
+    e[i].bn_v = bn_var[i];
+    e[i].bn_eps = bn_eps;
+  }
+  return OF_OK;
+}
+
+size_t of_conv2d_wgrad_bn_workspace(const of_conv_desc* d, int precision) {
+  return precision == 1 ? of_conv2d_wgrad_bf16_workspace(d)
+         : precision == 2 ? of_conv2d_wgrad_x3_workspace(d) : of_conv2d_wgrad_workspace(d);
+}
+
+int of_conv2d_wgrad_bn(const of_conv_desc* d, int precision, const float* x, int ldx,
+                       const float* t, int ldt, float* dw, int accumulate, const float* bn_gamma,
+                       const float* bn_var, float bn_eps, void* workspace, size_t ws_bytes,
+                       void* stream) {
+  OF_CHECK_ARG(precision >= 0 && precision <= 2, "wgrad bn: precision 0, 1 or 2");
+  OF_CHECK_ARG(bn_gamma && bn_var, "wgrad bn: gamma / var");
+  return conv_wgrad_impl(precision, d, x, ldx, t, ldt, dw, nullptr, accumulate, workspace,
+                         ws_bytes, stream, bn_gamma, bn_var, bn_eps);
+}
+
+int of_conv2d_dgrad_add_act(const of_conv_desc* d, int precision, const float* dy, int lddy,
+                            const void* w_bwd, const float* add, int ld_add,
+                            const float* act_src, int ld_act, int act, float alpha, float* dx,
+                            int lddx, void* workspace, size_t ws_bytes, void* stream) {
+  OF_CHECK_ARG(precision >= 0 && precision <= 2, "dgrad add act: precision 0, 1 or 2");
+  OF_CHECK_ARG(act_src && (act == OF_ACT_RELU || act == OF_ACT_LEAKY),
+               "dgrad add act: act_src and a relu / leaky act");
+  return conv_dgrad_impl(precision, d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, add,
+                         ld_add, dx, lddx, workspace, ws_bytes, stream, 1);
 }
 
 }  // extern "C"

@@ -132,9 +132,16 @@ __global__ __launch_bounds__(256) void rows_final_kernel(const float* __restrict
 // BN(inference)+residual+act backward, fused with its channel reductions:
 // dt = dy*act'(y); dz = dt*gamma*invstd; dres = dt; partial sums of dt and dt*(z-mean)*invstd.
 // Dense [npix][c] tensors, c % 4 == 0.
+// FROM_Y: z (the conv output before BN) is not stored; the normalised value is recovered from
+// the layer output y wherever the gradient is non-zero: y = act(gamma zhat + beta + res), so
+// zhat = (y - res - beta) / gamma where act' != 0 (ReLU: y > 0; none: everywhere).  dz may
+// then be NULL (the BN scale is folded into the conv's packed dgrad weights and its weight-
+// gradient reduction: of_conv_pack_weights_bn, of_conv2d_wgrad_bn), dres receives t.
+template <bool FROM_Y>
 __global__ __launch_bounds__(256) void bn_act_bwd_partial(
     int64_t npix, int c, int act, const float* __restrict__ dy, const float* __restrict__ y,
-    const float* __restrict__ z, const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ z, const float* __restrict__ res, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ mean,
     const float* __restrict__ var, float eps, float* __restrict__ dz, float* __restrict__ dres,
     int qw, int rows, int64_t ppb, float* __restrict__ part) {
   __shared__ float4 red[256];
@@ -151,26 +158,42 @@ __global__ __launch_bounds__(256) void bn_act_bwd_partial(
     const float4 is = make_float4(rsqrtf(vr.x + eps), rsqrtf(vr.y + eps), rsqrtf(vr.z + eps),
                                   rsqrtf(vr.w + eps));
     const float4 sc = make_float4(gm.x * is.x, gm.y * is.y, gm.z * is.z, gm.w * is.w);
+    float4 bt = make_float4(0.f, 0.f, 0.f, 0.f), ig = bt;
+    if (FROM_Y) {
+      bt = *reinterpret_cast<const float4*>(beta + ch);
+      ig = make_float4(1.f / gm.x, 1.f / gm.y, 1.f / gm.z, 1.f / gm.w);
+    }
     const bool relu = act == OF_ACT_RELU;
 #pragma unroll BNP_UNROLL
     for (int64_t p = p0 + r; p < p1; p += rows) {
       const int64_t o = p * c + ch;
       const float4 g = *reinterpret_cast<const float4*>(dy + o);
       const float4 yy = *reinterpret_cast<const float4*>(y + o);
-      const float4 zz = *reinterpret_cast<const float4*>(z + o);
+      float4 zh;                                   // normalised pre-BN value
+      if (FROM_Y) {
+        const float4 rr = res ? *reinterpret_cast<const float4*>(res + o)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        zh = make_float4((yy.x - rr.x - bt.x) * ig.x, (yy.y - rr.y - bt.y) * ig.y,
+                         (yy.z - rr.z - bt.z) * ig.z, (yy.w - rr.w - bt.w) * ig.w);
+      } else {
+        const float4 zz = *reinterpret_cast<const float4*>(z + o);
+        zh = make_float4((zz.x - mu.x) * is.x, (zz.y - mu.y) * is.y, (zz.z - mu.z) * is.z,
+                         (zz.w - mu.w) * is.w);
+      }
       float4 t;
       t.x = (!relu || yy.x > 0.f) ? g.x : 0.f;
       t.y = (!relu || yy.y > 0.f) ? g.y : 0.f;
       t.z = (!relu || yy.z > 0.f) ? g.z : 0.f;
       t.w = (!relu || yy.w > 0.f) ? g.w : 0.f;
-      *reinterpret_cast<float4*>(dz + o) =
-          make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
+      if (dz)
+        *reinterpret_cast<float4*>(dz + o) =
+            make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
       if (dres) *reinterpret_cast<float4*>(dres + o) = t;
       add4(sb, t);
-      sg.x += t.x * (zz.x - mu.x) * is.x;
-      sg.y += t.y * (zz.y - mu.y) * is.y;
-      sg.z += t.z * (zz.z - mu.z) * is.z;
-      sg.w += t.w * (zz.w - mu.w) * is.w;
+      sg.x += t.x * zh.x;
+      sg.y += t.y * zh.y;
+      sg.z += t.z * zh.z;
+      sg.w += t.w * zh.w;
     }
   }
   sb = rows_reduce(sb, q, r, qw, rows, red);
@@ -189,12 +212,13 @@ __global__ __launch_bounds__(256) void bn_act_bwd_partial(
 // BN(inference)+ReLU backward and its channel sums -- one read of y, z, g and the pooled dy,
 // one write of dz, instead of max-pool backward + add + bn_act_bwd (three passes over the
 // largest activation of the encoder).  Pixels are 2x2 windows: npix = n*(h/2)*(w/2).
+template <bool FROM_Y>     // (z not stored: zhat = (y - beta) / gamma where y > 0, as above)
 __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
     int64_t npix, int h, int w, int c, const float* __restrict__ dyp,
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ z,
-    const float* __restrict__ gamma, const float* __restrict__ mean,
-    const float* __restrict__ var, float eps, float* __restrict__ dz, int qw, int rows,
-    int64_t ppb, float* __restrict__ part) {
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ mean, const float* __restrict__ var, float eps,
+    float* __restrict__ dz, int qw, int rows, int64_t ppb, float* __restrict__ part) {
   __shared__ float4 red[256];
   const int q = threadIdx.x % qw, r = threadIdx.x / qw;
   const int ch = (blockIdx.y * qw + q) * 4;
@@ -210,6 +234,11 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
     const float4 is = make_float4(rsqrtf(vr.x + eps), rsqrtf(vr.y + eps), rsqrtf(vr.z + eps),
                                   rsqrtf(vr.w + eps));
     const float4 sc = make_float4(gm.x * is.x, gm.y * is.y, gm.z * is.z, gm.w * is.w);
+    float4 bt = make_float4(0.f, 0.f, 0.f, 0.f), ig = bt;
+    if (FROM_Y) {
+      bt = *reinterpret_cast<const float4*>(beta + ch);
+      ig = make_float4(1.f / gm.x, 1.f / gm.y, 1.f / gm.z, 1.f / gm.w);
+    }
     for (int64_t p = p0 + r; p < p1; p += rows) {
       const int ox = (int)(p % wo);
       const int64_t t2 = p / wo;
@@ -221,8 +250,18 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         yv[k] = *reinterpret_cast<const float4*>(y + offs[k]);
-        zv[k] = *reinterpret_cast<const float4*>(z + offs[k]);
         gv[k] = g ? *reinterpret_cast<const float4*>(g + offs[k]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {   // zv: the normalised pre-BN values
+        if (FROM_Y) {
+          zv[k] = make_float4((yv[k].x - bt.x) * ig.x, (yv[k].y - bt.y) * ig.y,
+                              (yv[k].z - bt.z) * ig.z, (yv[k].w - bt.w) * ig.w);
+        } else {
+          const float4 zz = *reinterpret_cast<const float4*>(z + offs[k]);
+          zv[k] = make_float4((zz.x - mu.x) * is.x, (zz.y - mu.y) * is.y, (zz.z - mu.z) * is.z,
+                              (zz.w - mu.w) * is.w);
+        }
       }
       const float4 d = *reinterpret_cast<const float4*>(dyp + p * c + ch);
       // first maximum per channel
@@ -244,10 +283,10 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
         *reinterpret_cast<float4*>(dz + offs[k]) =
             make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
         add4(sb, t);
-        sg.x += t.x * (zv[k].x - mu.x) * is.x;
-        sg.y += t.y * (zv[k].y - mu.y) * is.y;
-        sg.z += t.z * (zv[k].z - mu.z) * is.z;
-        sg.w += t.w * (zv[k].w - mu.w) * is.w;
+        sg.x += t.x * zv[k].x;
+        sg.y += t.y * zv[k].y;
+        sg.z += t.z * zv[k].z;
+        sg.w += t.w * zv[k].w;
       }
     }
   }
@@ -558,9 +597,9 @@ int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
   hipStream_t s = as_stream(stream);
   const RedGeo g = red_geo(npix, c);
   float* part = static_cast<float*>(workspace);
-  hipLaunchKernelGGL(bn_act_bwd_partial, dim3(g.nblk, cdiv(c / 4, g.qw)), dim3(256), 0, s, npix,
-                     c, act, dy, y, z, gamma, mean, var, eps, dz, dres, g.qw, g.rows, g.ppb,
-                     part);
+  hipLaunchKernelGGL(bn_act_bwd_partial<false>, dim3(g.nblk, cdiv(c / 4, g.qw)), dim3(256), 0, s,
+                     npix, c, act, dy, y, z, nullptr, gamma, nullptr, mean, var, eps, dz, dres,
+                     g.qw, g.rows, g.ppb, part);
   int st = check_launch("bn_act_bwd_partial");
   if (st) return st;
   hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c / 4, BNF_Q)), dim3(BNF_Q * BNF_G), 0, s, part,
@@ -588,10 +627,57 @@ int of_maxpool_bn_act_bwd(int n, int h, int w, int c, const float* dyp, const fl
   const int64_t npix = (int64_t)n * (h / 2) * (w / 2);
   const RedGeo geo = red_geo(npix, c);
   float* part = static_cast<float*>(workspace);
-  hipLaunchKernelGGL(maxpool_bn_act_bwd_partial, dim3(geo.nblk, cdiv(c / 4, geo.qw)), dim3(256),
-                     0, s, npix, h, w, c, dyp, g, y, z, gamma, mean, var, eps, dz, geo.qw,
-                     geo.rows, geo.ppb, part);
+  hipLaunchKernelGGL(maxpool_bn_act_bwd_partial<false>, dim3(geo.nblk, cdiv(c / 4, geo.qw)),
+                     dim3(256), 0, s, npix, h, w, c, dyp, g, y, z, gamma, nullptr, mean, var, eps,
+                     dz, geo.qw, geo.rows, geo.ppb, part);
   int st = check_launch("maxpool_bn_act_bwd_partial");
+  if (st) return st;
+  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c / 4, BNF_Q)), dim3(BNF_Q * BNF_G), 0, s, part,
+                     geo.nblk, c, gamma, var, eps, dgamma, dbeta, dbias, accumulate);
+  return check_launch("bn_act_bwd_final");
+}
+
+int of_bn_bwd_reduce(int64_t npix, int c, int act, const float* dy, const float* y,
+                     const float* res, const float* gamma, const float* beta, const float* var,
+                     float eps, float* t_out, float* dgamma, float* dbeta, float* dbias,
+                     int accumulate, void* workspace, void* stream) {
+  OF_CHECK_ARG(dy && y && gamma && beta && var && workspace, "bn_bwd_reduce: args");
+  OF_CHECK_ARG(act == OF_ACT_NONE || act == OF_ACT_RELU, "bn_bwd_reduce: act must be none/relu");
+  OF_CHECK_ARG(c % 4 == 0 && npix > 0, "bn_bwd_reduce: c must be a multiple of 4");
+  OF_CHECK_ARG((((uintptr_t)dy | (uintptr_t)y | (uintptr_t)res | (uintptr_t)t_out |
+                 (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)var) & 15) == 0,
+               "bn_bwd_reduce: 16-byte alignment");
+  hipStream_t s = as_stream(stream);
+  const RedGeo g = red_geo(npix, c);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(bn_act_bwd_partial<true>, dim3(g.nblk, cdiv(c / 4, g.qw)), dim3(256), 0, s,
+                     npix, c, act, dy, y, nullptr, res, gamma, beta, nullptr, var, eps, nullptr,
+                     t_out, g.qw, g.rows, g.ppb, part);
+  int st = check_launch("bn_bwd_reduce");
+  if (st) return st;
+  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c / 4, BNF_Q)), dim3(BNF_Q * BNF_G), 0, s, part,
+                     g.nblk, c, gamma, var, eps, dgamma, dbeta, dbias, accumulate);
+  return check_launch("bn_act_bwd_final");
+}
+
+int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const float* g,
+                           const float* y, const float* gamma, const float* beta,
+                           const float* var, float eps, float* dz, float* dgamma, float* dbeta,
+                           float* dbias, int accumulate, void* workspace, void* stream) {
+  OF_CHECK_ARG(dyp && y && gamma && beta && var && dz && workspace, "maxpool_bn_relu_bwd: args");
+  OF_CHECK_ARG(n > 0 && h % 2 == 0 && w % 2 == 0 && h > 0 && w > 0 && c % 4 == 0,
+               "maxpool_bn_relu_bwd: even h, w and c % 4 == 0");
+  OF_CHECK_ARG((((uintptr_t)dyp | (uintptr_t)g | (uintptr_t)y | (uintptr_t)dz |
+                 (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)var) & 15) == 0,
+               "maxpool_bn_relu_bwd: 16-byte alignment");
+  hipStream_t s = as_stream(stream);
+  const int64_t npix = (int64_t)n * (h / 2) * (w / 2);
+  const RedGeo geo = red_geo(npix, c);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(maxpool_bn_act_bwd_partial<true>, dim3(geo.nblk, cdiv(c / 4, geo.qw)),
+                     dim3(256), 0, s, npix, h, w, c, dyp, g, y, nullptr, gamma, beta, nullptr,
+                     var, eps, dz, geo.qw, geo.rows, geo.ppb, part);
+  int st = check_launch("maxpool_bn_relu_bwd_partial");
   if (st) return st;
   hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c / 4, BNF_Q)), dim3(BNF_Q * BNF_G), 0, s, part,
                      geo.nblk, c, gamma, var, eps, dgamma, dbeta, dbias, accumulate);

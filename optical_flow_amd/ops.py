@@ -314,9 +314,14 @@ class ConvLayer:
         if self._wf is None:
             self.alloc_packed(d)
         if key != self._pack_key or self.version_of is None:
-            call(("of_conv_pack_weights", "of_conv_pack_weights_bf16",
-                  "of_conv_pack_weights_x3")[self.mode(d)],
-                 C.byref(d), _ptr(self.kernel), _ptr(self._wf), _ptr(self._wd), _stream())
+            if self.bn is not None:       # BN scale folded into the dgrad image (see _bn_backward)
+                call("of_conv_pack_weights_bn", C.byref(d), self.mode(d), _ptr(self.kernel),
+                     _ptr(self._wf), _ptr(self._wd), _ptr(self.bn[0]), _ptr(self.bn[3]),
+                     BN_EPS, _stream())
+            else:
+                call(("of_conv_pack_weights", "of_conv_pack_weights_bf16",
+                      "of_conv_pack_weights_x3")[self.mode(d)],
+                     C.byref(d), _ptr(self.kernel), _ptr(self._wf), _ptr(self._wd), _stream())
             self._pack_key = key
         return self._wf, self._wd
 
@@ -377,9 +382,13 @@ class ConvPacker:
             L.alloc_packed(d)
             flags[i] = L.mode(d)
             wp[i], fp[i], bp[i] = L.kernel.data_ptr(), L._wf.data_ptr(), L._wd.data_ptr()
+        gp, vp = (C.c_void_p * n)(), (C.c_void_p * n)()
+        for i, L in enumerate(self.layers):
+            if L.bn is not None:
+                gp[i], vp[i] = L.bn[0].data_ptr(), L.bn[3].data_ptr()
         nbytes = lib.of_conv_pack_table_bytes(n)
         host = (C.c_char * nbytes)()
-        call("of_conv_pack_table_ex", n, descs, wp, fp, bp, flags, host)
+        call("of_conv_pack_table_bn", n, descs, wp, fp, bp, flags, gp, vp, BN_EPS, host)
         self.total = C.c_int64.from_buffer(host, 8).value
         self.table = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(
             self.layers[0].kernel.device)
@@ -421,7 +430,7 @@ def _conv_forward(layer: "ConvLayer", x, residual=None):
     d = layer.desc(n, h, w)
     wf, _ = layer.packed(d)
     y = torch.empty((n, d.ho, d.wo, layer.cout), device=x.device)
-    z = torch.empty_like(y) if layer.bn is not None else None
+    z = None      # BN layers: z is not stored, the backward recovers zhat from y (_conv_backward)
     bn = layer.bn
     if residual is not None:
         residual = residual.contiguous()
@@ -438,14 +447,25 @@ def _conv_forward(layer: "ConvLayer", x, residual=None):
 
 
 def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx_out=None,
-                   dz_given=None):
+                   dz_given=None, t_given=False, res_src=None, in_act=None):
     """Backward of _conv_forward: BN/activation backward (with the residual gradient), weight
     and bias gradients, input gradient.  needs = (x, kernel, bias, gamma, beta, residual).
     add: a gradient summed into dx by the input-gradient kernel's epilogue (dx_out may be
     that same buffer).  dz_given: the pre-activation gradient already computed, with the BN
-    and bias gradients, by a fused kernel (the stem, of_maxpool_bn_act_bwd).  Returns (dx,
-    d_kernel, d_bias, d_gamma, d_beta, d_residual) with None for gradients written straight
-    into the gradient arena."""
+    and bias gradients, by a fused kernel (the stem, of_maxpool_bn_relu_bwd).
+
+    BN layers (FusedBatchNormGrad, inference mode, P5) never form dz: with t = dy * act'(y)
+    the BN scale s = gamma / sqrt(var + eps) is folded into the packed input-gradient weights
+    (ConvLayer.packed, ConvPacker) and the weight-gradient reduction (of_conv2d_wgrad_bn), and
+    one reduction pass (of_bn_bwd_reduce) gives dgamma, dbeta and the bias gradient, reading t
+    and y (z is recovered from y; res_src = the residual added before the activation).
+    t_given: dy already is t (the producing input-gradient kernel applied act' in its
+    epilogue).  in_act = (act_src, act): multiply this layer's input gradient by the
+    derivative of the activation that produced x (after the add, if any), so the layer before
+    receives its t.
+
+    Returns (dx, d_kernel, d_bias, d_gamma, d_beta, d_residual) with None for gradients
+    written straight into the gradient arena."""
     n, h, w, cx = x.shape
     d = layer.desc(n, h, w)
     _, wd = layer.packed(d)
@@ -454,14 +474,13 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
     need_x, need_k, need_b, need_g, need_be, need_res = needs
     ret_k = ret_b = ret_g = ret_be = dres = dx = None
     npix = n * d.ho * d.wo
+    bn_fold = False
     # ---- pre-activation gradient dz -----------------------------------------------------
     if dz_given is not None:
         dz = dz_given
         bias_done = True
     elif layer.bn is not None:
         gamma, beta, mean, var = layer.bn
-        dz = torch.empty_like(dy)
-        dres = torch.empty_like(dy) if (has_res and need_res) else None
         tg = grad_target(gamma) if need_g else (None, 0, None)
         tb = grad_target(beta) if need_be else (None, 0, None)
         tbias = grad_target(layer.bias) if need_b else (None, 0, None)
@@ -471,10 +490,20 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
         assert all(t[0] is None or t[1] == acc for t in (tg, tb, tbias))
         ws = torch.empty(_lib.lib().of_bn_act_bwd_workspace(npix, layer.cout) // 4 + 1,
                          device=dy.device)
-        call("of_bn_act_bwd", npix, layer.cout, layer.act, _ptr(dy), _ptr(y), _ptr(z),
-             _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, _ptr(dz), _ptr(dres),
-             _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
+        if t_given or layer.act == ACT_NONE:
+            dz = dy                     # already t
+            call("of_bn_bwd_reduce", npix, layer.cout, ACT_NONE, _ptr(dz), _ptr(y),
+                 _ptr(res_src), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, None,
+                 _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
+        else:
+            dz = torch.empty_like(dy)    # t = dy * act'(y)
+            call("of_bn_bwd_reduce", npix, layer.cout, layer.act, _ptr(dy), _ptr(y),
+                 _ptr(res_src), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, _ptr(dz),
+                 _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
+        if has_res and need_res:
+            dres = dz                   # the residual branch's gradient is t itself
         bias_done = True
+        bn_fold = True
     else:
         if layer.act != ACT_NONE:
             dz = torch.empty_like(dy)
@@ -494,7 +523,18 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
             dx = dx_out if dx_out is not None else torch.empty((n, h, w, cx), device=dz.device)
             res["dx"] = dx
             _tag(layer, 1)
-            if add is not None:
+            if in_act is not None:
+                src, iact = in_act
+                src = src.contiguous()
+                addc = add.contiguous() if add is not None else None
+                if addc is not None:
+                    assert addc.shape == dx.shape
+                _, wsz = layer.dgrad_add_entry(d)
+                wsk, wsp, wsb = _workspace(wsz, dy.device if dy is not None else dz.device)
+                call("of_conv2d_dgrad_add_act", C.byref(d), layer.mode(d), _ptr(dzp),
+                     dzp.shape[-1], _ptr(wd), _ptr(addc), cx, _ptr(src), cx, iact,
+                     LEAKY_ALPHA, _ptr(dx), cx, wsp, wsb, s)
+            elif add is not None:
                 addc = add.contiguous()
                 assert addc.shape == dx.shape
                 entry, wsz = layer.dgrad_add_entry(d)
@@ -517,6 +557,16 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
                     d.n * d.ho * d.wo <= _side_max_pix(layer))
             with torch.cuda.stream(side_stream(x, dzp)) if side else contextlib.nullcontext():
                 ss = _stream()
+                if bn_fold:                 # dw = s * (x^T t): the BN scale in the reduction
+                    wsb = _lib.lib().of_conv2d_wgrad_bn_workspace(C.byref(d), layer.mode(d))
+                    ws = torch.empty(wsb // 4 + 1, device=dz.device)
+                    gamma, _, _, var = layer.bn
+                    _tag(layer, 2)
+                    call("of_conv2d_wgrad_bn", C.byref(d), layer.mode(d), _ptr(x), cx, _ptr(dzp),
+                         dzp.shape[-1], _ptr(tk[0]), tk[1], _ptr(gamma), _ptr(var), BN_EPS,
+                         _ptr(ws), wsb, ss)
+                    res["k"] = tk[2] if need_k else None
+                    return
                 ws = torch.empty(wsb // 4 + 1, device=dz.device)
                 if tbias[0] is not None and tbias[1] != tk[1]:
                     # mixed arena / fresh targets: compute the bias into a temp, then place it
@@ -562,13 +612,15 @@ class _ConvFn(torch.autograd.Function):
         y, z = _conv_forward(layer, x.contiguous(), residual)
         ctx.layer = layer
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x.contiguous(), y, z)
+        ctx.save_for_backward(x.contiguous(), y, z,
+                              residual.contiguous() if residual is not None else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, z = ctx.saved_tensors
-        out = _conv_backward(ctx.layer, x, y, z, dy, ctx.has_res, ctx.needs_input_grad[:6])
+        x, y, z, r = ctx.saved_tensors
+        out = _conv_backward(ctx.layer, x, y, z, dy, ctx.has_res, ctx.needs_input_grad[:6],
+                             res_src=r)
         return (*out, None)
 
 
@@ -600,31 +652,41 @@ class _ResBlockFn(torch.autograd.Function):
         return (dx, *grads, None)
 
 
-def _res_block_backward(block, saved, dy, need, extra=None):
+def _res_block_backward(block, saved, dy, need, extra=None, t_given=False, in_act=None):
     """Backward of one residual block.  need: needs_input_grad of (x, then kernel, bias,
     gamma, beta per layer a, b, p).  extra: a further gradient of the block input x (its
     other consumer) summed by the shortcut's input-gradient epilogue -- no separate add.
-    Returns (dx, [param grads of a, b, p])."""
+    t_given: dy already carries the block's output ReLU derivative (the next block's
+    input-gradient epilogue applied it).  in_act = (x, ACT_RELU) when x is a ReLU output: the
+    returned dx is then the previous block's t.  conv_b's input gradient always carries
+    conv_a's ReLU derivative (t of conv_a).  Returns (dx, [param grads of a, b, p])."""
     x, ya, za, y, zb, yp, zp = saved
     a, b, p = block
     need_x = need[0]
     nb = lambda k: tuple(need[1 + 4 * k:5 + 4 * k])     # kernel, bias, gamma, beta of layer k
-    dya, *gb = _conv_backward(b, ya, y, zb, dy, True, (True, *nb(1), True))
-    dres = gb[-1]
+    sc = yp if p is not None else x                      # residual added before b's ReLU
+    dya, *gb = _conv_backward(b, ya, y, zb, dy, True, (True, *nb(1), True), t_given=t_given,
+                              res_src=sc, in_act=(ya, ACT_RELU))
+    dres = gb[-1]                                        # = t of conv_b
     gb = gb[:-1]
     if p is not None:
         dxp, *gp = _conv_backward(p, x, yp, zp, dres, False, (need_x, *nb(2), False),
                                   add=extra if need_x else None,
-                                  dx_out=extra if need_x else None)   # in place: see below
+                                  dx_out=extra if need_x else None,   # in place: see below
+                                  t_given=True)
         gp = gp[:-1]
         add, dx_out = dxp, dxp
     else:
         gp = []
-        if extra is not None and need_x:
-            call("of_add_inplace", _ptr(dres), _ptr(extra.contiguous()), dres.numel(), _stream())
         add, dx_out = dres, None
+        if extra is not None and need_x:
+            # (dres is also conv_b's weight-gradient input, possibly still being read on the
+            # side stream: sum into a copy)
+            add = dres.clone()
+            call("of_add_inplace", _ptr(add), _ptr(extra.contiguous()), add.numel(), _stream())
     dx, *ga = _conv_backward(a, x, ya, za, dya, False, (need_x, *nb(0), False),
-                             add=add if need_x else None, dx_out=dx_out)
+                             add=add if need_x else None, dx_out=dx_out, t_given=True,
+                             in_act=in_act if need_x else None)
     ga = ga[:-1]
     return dx, list(ga) + list(gb) + list(gp)
 
@@ -684,7 +746,11 @@ class _EncoderFn(torch.autograd.Function):
             blk = saved[3 + 7 * i:3 + 7 * (i + 1)]
             extra = gouts[i // 2] if (i % 2 == 0 and i > 0) else None
             nd = (True,) + tuple(need[pos[i]:pos[i] + 4 * (3 if blocks[i][2] is not None else 2)])
-            dy, g = _res_block_backward(blocks[i], blk, dy, nd, extra=extra)
+            # block i > 0 takes a ReLU output (block i - 1's) as input: its input gradient
+            # is returned as that block's t; block 0's input is the max-pooled stem output
+            dy, g = _res_block_backward(blocks[i], blk, dy, nd, extra=extra,
+                                        t_given=i < nbk - 1,
+                                        in_act=(blk[0], ACT_RELU) if i > 0 else None)
             grads = list(g) + grads
         # stem: max-pool backward + out0's decoder gradient + BN/ReLU backward, one pass
         n, h, w, c = y0.shape
@@ -698,8 +764,8 @@ class _EncoderFn(torch.autograd.Function):
         dz0 = torch.empty_like(y0)
         ws = torch.empty(_lib.lib().of_maxpool_bn_act_bwd_workspace(n, h, w, c) // 4 + 1,
                          device=y0.device)
-        call("of_maxpool_bn_act_bwd", n, h, w, c, _ptr(dy.contiguous()), _ptr(gouts[0]), _ptr(y0),
-             _ptr(z0), _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, _ptr(dz0), _ptr(tg[0]),
+        call("of_maxpool_bn_relu_bwd", n, h, w, c, _ptr(dy.contiguous()), _ptr(gouts[0]),
+             _ptr(y0), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, _ptr(dz0), _ptr(tg[0]),
              _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
         _, gk, _, _, _, _ = _conv_backward(conv1, x4, y0, z0, None, False,
                                            (False, nk, nbias, ng, nbe, False), dz_given=dz0)

@@ -102,6 +102,40 @@ def _conv2d_same_exact(x, w, b, stride=1):
     return y.permute(0, 2, 3, 1)
 
 
+class _Bf16ConvBN(torch.autograd.Function):
+    """bf16 mode, conv + inference BN (the encoder's conv_a / conv_b / proj): the operand
+    rounding points of the build's folded BN backward (ops._conv_backward): with t = dL/du the
+    gradient of the BN output u and s = gamma / sqrt(var + eps), the input gradient is
+    conv^T(bf16(t), bf16(W s)) and the weight gradient s * (bf16(x)^T bf16(t)); the bias,
+    gamma and beta gradients are exact.  (The stem keeps dz = t s: its fused max-pool / BN
+    backward forms dz, see encoder().)"""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, mean, var, stride):
+        ctx.save_for_backward(x, w, gamma, mean, var)
+        ctx.stride = stride
+        z = _conv2d_same_exact(bf16_round(x), bf16_round(w), b, stride)
+        ctx.zhat = (z - mean) / torch.sqrt(var + BN_EPS)
+        return ctx.zhat * gamma + beta
+
+    @staticmethod
+    def backward(ctx, t):
+        x, w, gamma, mean, var = [v.detach() for v in ctx.saved_tensors]
+        sc = gamma / torch.sqrt(var + BN_EPS)
+        tr = bf16_round(t)
+        with torch.enable_grad():
+            xv = x.clone().requires_grad_(True)
+            (_conv2d_same_exact(xv, bf16_round(w * sc), None, ctx.stride) * tr).sum().backward()
+            wv = w.clone().requires_grad_(True)
+            (_conv2d_same_exact(bf16_round(x), wv, None, ctx.stride) * tr).sum().backward()
+        dw = wv.grad * sc
+        red = tuple(range(t.dim() - 1))
+        db = t.sum(dim=red) * sc
+        dgamma = (t * ctx.zhat).sum(dim=red)
+        dbeta = t.sum(dim=red)
+        return xv.grad, dw, db, dgamma, dbeta, None, None, None
+
+
 def batchnorm_inference(x, p: Dict[str, torch.Tensor], prefix: str):
     """keras BatchNormalization called with training unset -> inference mode: moving
     statistics, eps=1e-3, no statistic update; gamma/beta trainable (P5; train.py:51)."""
@@ -121,6 +155,10 @@ def maxpool2(x):
 
 # -------------------------------------------------------------------------- encoder ----
 def _conv_bn(x, p, conv, bn, stride):
+    if CONV_PRECISION == "bf16":
+        return _Bf16ConvBN.apply(x, p[conv + "/kernel"], p[conv + "/bias"], p[bn + "/gamma"],
+                                 p[bn + "/beta"], p[bn + "/moving_mean"],
+                                 p[bn + "/moving_variance"], stride)
     y = conv2d_same(x, p[conv + "/kernel"], p[conv + "/bias"], stride)
     return batchnorm_inference(y, p, bn)
 

@@ -147,11 +147,10 @@ def test_conv_bf16(case):
     mu = rng_tensor((cout,), seed + 5, scale=0.1)
     var = rng_tensor((cout,), seed + 6, lo=0.5, hi=1.5)
     xo, wo_, bo = [f64(t).requires_grad_(True) for t in (x, wt, b)]
-    yo = R._Bf16Conv.apply(xo, wo_, bo, s)
-    p = {"bn/gamma": f64(g), "bn/beta": f64(be), "bn/moving_mean": f64(mu),
-         "bn/moving_variance": f64(var)}
-    if use_bn:
-        yo = R.batchnorm_inference(yo, p, "bn")
+    if use_bn:     # the folded-BN rounding points of the build (oracle _Bf16ConvBN)
+        yo = R._Bf16ConvBN.apply(xo, wo_, bo, f64(g), f64(be), f64(mu), f64(var), s)
+    else:
+        yo = R._Bf16Conv.apply(xo, wo_, bo, s)
     res = rng_tensor(tuple(yo.shape), seed + 7) if use_res else None
     if use_res:
         yo = yo + f64(res)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# full GPU suite + bench after the BN-fold rework
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+export TMPDIR=/tmp
+OUT=${1:-gpurun_out/r3i}
+mkdir -p "$OUT"
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_all.log" 2>&1
+rc=$?
+grep -E "FAILED|ERROR|Error" "$OUT/pytest_all.log" | head -8; tail -2 "$OUT/pytest_all.log"
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+for i in 1 2; do
+timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 --warmup 5 > "$OUT/bench_$i.log" 2>&1 || { echo bench failed; tail -5 "$OUT/bench_$i.log"; exit 1; }
+grep '^{' "$OUT/bench_$i.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('fp32', d['value'], d['ms_per_step'], r['frac'])"
+done
+timeout -k 10 300 python bench.py --precision bf16 --batch 32 --no-cpu-baseline > "$OUT/bench_bf16.log" 2>&1 || { echo bench failed; tail -5 "$OUT/bench_bf16.log"; exit 1; }
+grep '^{' "$OUT/bench_bf16.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('bf16', d['value'], d['ms_per_step'], r['frac'])"
+exit $rc

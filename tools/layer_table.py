@@ -11,7 +11,7 @@ from collections import defaultdict
 
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(
     __import__("os").path.abspath(__file__))))
-from bench import kind_name  # noqa: E402
+from bench import kind_name, kind_parts  # noqa: E402
 
 
 def main():
@@ -20,7 +20,7 @@ def main():
     ceil = float(sys.argv[3]) if len(sys.argv) > 3 else 118.0
     acc = defaultdict(lambda: [0.0, 0.0, 0, None])
     for r in rows:
-        mode = ("fwd", "dgrad", "wgrad")[(r["kind"] % 32) // 8]
+        mode = ("fwd", "dgrad", "wgrad")[kind_parts(r["kind"])[0]]
         a = acc[(r["layer"], mode)]
         a[0] += r["gflop"]
         a[1] += r["ms"]
