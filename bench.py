@@ -415,9 +415,10 @@ def main():
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
-                pmc = json.load(f)
+                db = json.load(f)
+            pmc = db.get("entries", {}).get("%s:%dx%dx%d" % (args.precision, H, W, B), {})
             same_math = args.precision != "fp32" or pmc.get("f32_split", True) == ops.F32_SPLIT
-            if pmc.get("config") == [H, W, B] and same_math and sym in pmc.get("kernels", {}):
+            if same_math and sym in pmc.get("kernels", {}):
                 traffic = pmc["kernels"][sym]["hbm_bytes_per_launch"]
         allconv = sum(v[0] for v in table.values()) / (sum(v[1] for v in table.values()) * 1e-3) / 1e12
         fam = kind_parts(dom)[2]

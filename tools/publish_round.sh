@@ -16,7 +16,12 @@ python tools/make_summary.py "$IN/bench.log" "$IN/prof/bench_kernel_stats.csv" \
   "python bench.py --no-cpu-baseline" > profiles/${R}_summary.md
 python tools/make_summary.py "$IN/bench_bf16.log" "$IN/prof_bf16/bench_kernel_stats.csv" \
   "python bench.py --precision bf16 --batch 32 --no-cpu-baseline" > profiles/${R}_bf16_summary.md
-python tools/pmc_traffic.py "$IN/fetch/bench_counter_collection.csv" "$IN/write/bench_counter_collection.csv" 384 512 8
+if [ -f "$IN/pmc_traffic.json" ]; then
+  cp "$IN/pmc_traffic.json" profiles/pmc_traffic.json
+else
+  python tools/pmc_traffic.py "$IN/fetch/bench_counter_collection.csv" "$IN/write/bench_counter_collection.csv" 384 512 8
+fi
 for f in conv_bench conv_bench_bf16 conv_bench_f32mfma flow_bench x3_accuracy; do
-  grep -v amdgpu.ids "$IN/$f.txt" > profiles/${R}_$f.txt
+  [ -f "$IN/$f.txt" ] && grep -v amdgpu.ids "$IN/$f.txt" > profiles/${R}_$f.txt
 done
+true
