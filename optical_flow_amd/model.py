@@ -8,6 +8,8 @@ Same public names and argument meaning as ``/root/reference/model.py``:
 * ``upscale_flow(flow)``                                          (model.py:76-77)
 * ``flow_module(features1, features2, previous_flow, max_disp)``  (model.py:80-116)
 * ``build_flow_net(height, width, pretrained_weights_path, max_disp=3)`` (model.py:119-143)
+* ``resnet_layer_simple(x, nblocks, downsample, idx)`` (the un-vendored ``resnet`` submodule's
+  stage, model.py:2,18,20,22; assumed basic blocks)
 
 Tensors are torch NHWC float32 on the GPU; every op runs as HIP kernels (``ops.py``).  The
 returned ``FlowNet`` keeps the Keras ``Model`` surface the driver uses: ``__call__`` ->
@@ -31,8 +33,8 @@ import torch
 
 from . import ops
 from ._lib import ACT_LEAKY, ACT_NONE, ACT_RELU, call
-from .params import (ENC_CHANNELS, HEAD_WIDTHS, encoder_blocks, encoder_spec, flow_net_spec,
-                     head_cin, head_spec, init_params)
+from .params import (ENC_CHANNELS, HEAD_WIDTHS, blocks_spec, encoder_blocks, encoder_spec,
+                     flow_net_spec, head_cin, head_spec, init_params, stage_blocks)
 
 
 # =================================================================== parameter arena ====
@@ -135,30 +137,13 @@ class Encoder:
         self.store = store
         self.name = name
         self.levels = levels
-        ver = lambda: store.version
         P = store.params
-
-        def bn(prefix):
-            return (P[prefix + "/gamma"], P[prefix + "/beta"], P[prefix + "/moving_mean"],
-                    P[prefix + "/moving_variance"])
-
+        stem_bn = tuple(P["ResNet18/layer1_bn/" + k]
+                        for k in ("gamma", "beta", "moving_mean", "moving_variance"))
         self.conv1 = ops.ConvLayer(P["ResNet18/conv1/kernel"], P["ResNet18/conv1/bias"], stride=2,
-                                   act=ACT_RELU, bn=bn("ResNet18/layer1_bn"), cin_p=4,
-                                   version_of=ver, name="conv1")
-        self.blocks = []
-        for prefix, cin, cout, stride, proj in encoder_blocks(levels):
-            a = ops.ConvLayer(P[prefix + "/conv_a/kernel"], P[prefix + "/conv_a/bias"],
-                              stride=stride, act=ACT_RELU, bn=bn(prefix + "/bn_a"),
-                              version_of=ver, name=prefix + "/conv_a")
-            b = ops.ConvLayer(P[prefix + "/conv_b/kernel"], P[prefix + "/conv_b/bias"], stride=1,
-                              act=ACT_RELU, bn=bn(prefix + "/bn_b"), version_of=ver,
-                              name=prefix + "/conv_b")
-            p = None
-            if proj:
-                p = ops.ConvLayer(P[prefix + "/proj/kernel"], P[prefix + "/proj/bias"],
-                                  stride=stride, act=ACT_NONE, bn=bn(prefix + "/bn_proj"),
-                                  version_of=ver, name=prefix + "/proj")
-            self.blocks.append((a, b, p))
+                                   act=ACT_RELU, bn=stem_bn, cin_p=4,
+                                   version_of=lambda: store.version, name="conv1")
+        self.blocks = block_layers(store, encoder_blocks(levels))
 
     def forward4(self, x4):
         """x4: (N, H, W, 4) images with a zero 4th channel -> 4 feature maps."""
@@ -180,6 +165,55 @@ class Encoder:
     def __call__(self, images):
         """images: (N, H, W, 3) -> [H/2 x64, H/4 x64, H/8 x128, H/16 x256]."""
         return self.forward4(ops._pad_channels(images, 4))
+
+
+def block_layers(store: ParamStore, blocks):
+    """(conv_a, conv_b, proj or None) ConvLayers of residual blocks whose weights live in
+    ``store`` under the block prefixes of params.encoder_blocks / params.stage_blocks."""
+    P = store.params
+    ver = lambda: store.version
+
+    def bn(prefix):
+        return (P[prefix + "/gamma"], P[prefix + "/beta"], P[prefix + "/moving_mean"],
+                P[prefix + "/moving_variance"])
+
+    out = []
+    for prefix, cin, cout, stride, proj in blocks:
+        a = ops.ConvLayer(P[prefix + "/conv_a/kernel"], P[prefix + "/conv_a/bias"],
+                          stride=stride, act=ACT_RELU, bn=bn(prefix + "/bn_a"),
+                          version_of=ver, name=prefix + "/conv_a")
+        b = ops.ConvLayer(P[prefix + "/conv_b/kernel"], P[prefix + "/conv_b/bias"], stride=1,
+                          act=ACT_RELU, bn=bn(prefix + "/bn_b"), version_of=ver,
+                          name=prefix + "/conv_b")
+        p = None
+        if proj:
+            p = ops.ConvLayer(P[prefix + "/proj/kernel"], P[prefix + "/proj/bias"],
+                              stride=stride, act=ACT_NONE, bn=bn(prefix + "/bn_proj"),
+                              version_of=ver, name=prefix + "/proj")
+        out.append((a, b, p))
+    return out
+
+
+def resnet_layer_simple(x, nblocks, downsample, idx, store: Optional[ParamStore] = None,
+                        seed: int = 0):
+    """``resnet.models.resnet_layer_simple(x, nblocks, downsample, idx)`` (model.py:2,18,20,22).
+    The ``resnet`` submodule is not vendored, so this is the assumed ResNet-18 basic stage
+    (parity unpinned): ``nblocks`` blocks of [conv3x3(s) + BN + ReLU,
+    conv3x3 + BN] + shortcut (1x1/s conv + BN when downsampling or when the channel count
+    changes) -> add -> ReLU, with 64 * 2^(idx-2) output channels; BN in inference mode (P5).
+
+    x: (N, H, W, C) NHWC float32 on the GPU.  Like the Keras functional call, a call with no
+    ``store`` creates fresh layers (Keras-default init from ``seed``; the store is kept on
+    the returned tensor as ``_resnet_store``); a ``store`` holding the stage's weights under
+    ``ResNet18/res{idx}_{j}/...`` (e.g. a FlowNet's) reuses them."""
+    assert x.dim() == 4, "NHWC input"
+    blocks = stage_blocks(idx, x.shape[-1], nblocks, downsample)
+    if store is None:
+        store = ParamStore(blocks_spec(blocks), seed=seed, device=x.device)
+    for a, b, p in block_layers(store, blocks):
+        x = ops.res_block(x, a, b, p)
+    x._resnet_store = store
+    return x
 
 
 def reset18_encoder(height, width, name="ResNet18", seed=0, device="cuda"):

@@ -64,21 +64,39 @@ def encoder_blocks(levels: int = 4):
     assert levels in LEVELS, levels
     cin = 64
     for idx, down, cout in ENC_STAGES[:levels - 1]:
-        for j in range(2):
-            stride = 2 if (down and j == 0) else 1
-            proj = (j == 0 and (down or cin != cout))
-            yield ("ResNet18/res%d_%d" % (idx, j), cin, cout, stride, proj)
-            cin = cout
+        for blk in stage_blocks(idx, cin, 2, down):
+            yield blk
+        cin = cout
 
 
-def encoder_spec(levels: int = 4) -> List[PSpec]:
-    s = _conv("ResNet18/conv1", 7, 3, 64) + _bn("ResNet18/layer1_bn", 64)
-    for prefix, cin, cout, stride, proj in encoder_blocks(levels):
+def stage_blocks(idx: int, cin: int, nblocks: int = 2, downsample: bool = False):
+    """The blocks one ``resnet_layer_simple(x, nblocks, downsample, idx)`` call creates
+    (model.py:18,20,22; assumed basic stage): output channels 64 * 2^(idx-2)
+    (the shape comments of model.py:19,21,23), the first block strided by 2 when downsampling
+    and projected when downsampling or when the channel count changes."""
+    cout = 64 << (idx - 2)
+    out = []
+    for j in range(nblocks):
+        stride = 2 if (downsample and j == 0) else 1
+        proj = j == 0 and (downsample or cin != cout)
+        out.append(("ResNet18/res%d_%d" % (idx, j), cin, cout, stride, proj))
+        cin = cout
+    return out
+
+
+def blocks_spec(blocks) -> List[PSpec]:
+    s = []
+    for prefix, cin, cout, stride, proj in blocks:
         s += _conv(prefix + "/conv_a", 3, cin, cout) + _bn(prefix + "/bn_a", cout)
         s += _conv(prefix + "/conv_b", 3, cout, cout) + _bn(prefix + "/bn_b", cout)
         if proj:
             s += _conv(prefix + "/proj", 1, cin, cout) + _bn(prefix + "/bn_proj", cout)
     return s
+
+
+def encoder_spec(levels: int = 4) -> List[PSpec]:
+    return (_conv("ResNet18/conv1", 7, 3, 64) + _bn("ResNet18/layer1_bn", 64) +
+            blocks_spec(encoder_blocks(levels)))
 
 
 def head_cin(level: int, max_disp: int = 3, levels: int = 4) -> int:

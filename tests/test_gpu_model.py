@@ -193,3 +193,55 @@ def test_save_load_weights_tf_checkpoint(tmp_path):
     fresh = build_flow_net(64, 128, None, seed=9).store.state()
     np.testing.assert_array_equal(st["flow_module_0/conv0/kernel"],
                                   fresh["flow_module_0/conv0/kernel"])   # heads not loaded
+
+
+@pytest.mark.parametrize("idx,nblocks,down,cin", [(2, 2, False, 64), (3, 2, True, 64),
+                                                  (4, 3, False, 128)],
+                         ids=["res2", "res3_down", "res4_proj_s1"])
+def test_resnet_layer_simple(idx, nblocks, down, cin):
+    """model.resnet_layer_simple(x, nblocks, downsample, idx) -- the reference's stage call
+    (model.py:18,20,22) -- against the oracle's chain of resnet_block: output, input gradient
+    and every weight gradient within 1e-3 (assumed basic stage, parity unpinned).
+    Covers a stride-2 projected first block, an identity stage, and a stride-1 projection
+    (channel change without downsampling)."""
+    from optical_flow_amd.model import ParamStore, resnet_layer_simple
+    from optical_flow_amd.params import blocks_spec, init_params, perturb_params, stage_blocks
+    blocks = stage_blocks(idx, cin, nblocks, down)
+    spec = blocks_spec(blocks)
+    vals = perturb_params(init_params(spec, 5), 6)
+    store = ParamStore(spec, values=vals, device="cuda")
+    g = torch.Generator().manual_seed(idx)
+    x0 = torch.randn(2, 32, 48, cin, generator=g, dtype=torch.float64)
+    x = dev(x0.float()).requires_grad_(True)
+    store.zero_grad()
+    y = resnet_layer_simple(x, nblocks, down, idx, store=store)
+    assert y._resnet_store is store
+    dy0 = torch.randn(tuple(y.shape), generator=g, dtype=torch.float64)
+    y.backward(dev(dy0.float()))
+    torch.cuda.synchronize()
+
+    p = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in vals.items()}
+    xo = x0.clone().requires_grad_(True)
+    yo = xo
+    for prefix, _, _, stride, proj in blocks:
+        yo = R.resnet_block(yo, p, prefix, stride, proj)
+    yo.backward(dy0)
+    assert tuple(y.shape) == tuple(yo.shape) == (2, 32 // (2 if down else 1),
+                                                   48 // (2 if down else 1), 64 << (idx - 2))
+    assert rel_inf(y, yo) < REL_TOL
+    assert rel_l2(x.grad, xo.grad) < REL_TOL
+    for name, gr in store.grads().items():
+        e = rel_l2(gr, p[name].grad)
+        assert e < REL_TOL, "grad %s rel_l2 %.3e" % (name, e)
+
+
+def test_resnet_layer_simple_fresh_layers():
+    """Without a store the call creates fresh layers (Keras functional semantics), seeded."""
+    from optical_flow_amd.model import resnet_layer_simple
+    x = dev(torch.randn(1, 16, 16, 64))
+    y1 = resnet_layer_simple(x, 2, True, 3, seed=1)
+    y2 = resnet_layer_simple(x, 2, True, 3, seed=1)
+    assert y1.shape == (1, 8, 8, 128)
+    assert set(y1._resnet_store.params) >= {"ResNet18/res3_0/proj/kernel",
+                                            "ResNet18/res3_1/conv_b/kernel"}
+    assert torch.equal(y1, y2)

@@ -18,6 +18,17 @@ def test_param_count_and_layout():
     assert [b[4] for b in blocks] == [False, False, True, False, True, False]
 
 
+def test_stage_blocks_match_encoder():
+    """resnet_layer_simple's stage layout (model.py:18,20,22) composes into the encoder's."""
+    stages = (P.stage_blocks(2, 64, 2, False) + P.stage_blocks(3, 64, 2, True) +
+              P.stage_blocks(4, 128, 2, True))
+    assert stages == list(P.encoder_blocks())
+    assert P.blocks_spec(stages) == P.encoder_spec()[6:]     # after conv1 + layer1_bn
+    s = P.stage_blocks(4, 128, 3, False)                    # channel change, no downsample
+    assert [(b[3], b[4]) for b in s] == [(1, True), (1, False), (1, False)]
+    assert s[-1][0] == "ResNet18/res4_2" and s[0][2] == 256
+
+
 def test_glorot_init_deterministic():
     a = P.init_params(P.head_spec(3), 0)
     b = P.init_params(P.head_spec(3), 0)
@@ -82,7 +93,8 @@ def test_bench_kernel_symbols_match_pmc_keys():
     import os
     import bench
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    keys = set(json.load(open(os.path.join(root, "profiles", "pmc_traffic.json")))["kernels"])
+    entries = json.load(open(os.path.join(root, "profiles", "pmc_traffic.json")))["entries"]
+    keys = set().union(*(e["kernels"] for e in entries.values()))
     names = set()
     for mode in (0, 1):
         for cfg in bench.X3_BN:
