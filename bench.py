@@ -55,6 +55,8 @@ def kind_parts(kind):
     implicit GEMM (other shapes) 160 + mode*8 + cfg (optical_flow_amd/csrc/conv_f32.hip)."""
     if kind == KIND_STEM_X3:
         return 0, 0, "stem_x3"
+    if kind == KIND_STEM_WG_X3:
+        return 2, 0, "stem_x3"
     if kind >= 216:                               # conv_wgrad_tile_b16 (x3b configs, 1 plane)
         return 2, kind - 216, "wgrad_b16"
     if kind >= 192:                               # conv_tile_b16 (bf16 on the x3 structure)
@@ -100,12 +102,13 @@ def conv_math(precision):
 
 
 KIND_STEM_X3 = 184   # conv_stem_x3 (the 7x7 stride-2 stem forward on the split-bf16 MFMA)
+KIND_STEM_WG_X3 = 185   # conv_wgrad_stem_x3 (its weight gradient)
 
 
 def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
     if fam == "stem_x3":
-        return "fwd_stem_x3"
+        return "wgrad_stem_x3" if mode == 2 else "fwd_stem_x3"
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
            "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3", "tile_b16": "_tile_b16",
            "wgrad_b16": ""}[fam]
@@ -129,6 +132,8 @@ def kernel_symbol(kind):
     """rocprofv3 name of the conv kernel instance behind a timing kind."""
     mode, cfg, fam = kind_parts(kind)
     if fam == "stem_x3":
+        if mode == 2:
+            return "oflow::conv_wgrad_stem_x3(oflow::GemmArgs)"
         return "void oflow::conv_stem_x3<32>(oflow::GemmArgs)"   # of_set_tuning key 8 default
     if cfg == 7 and fam == "f32":
         return NARROW_SYMBOLS[mode]

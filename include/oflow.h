@@ -307,6 +307,11 @@ int of_add_inplace(float* y, const float* x, int64_t n, void* stream);        /*
 int of_copy_strided(const float* src, int lds, float* dst, int ldd, int64_t npix, int c,
                     void* stream);                                             /* per pixel */
 int of_fill(float* y, float v, int64_t n, void* stream);
+/* Order stream `waiter` after everything enqueued so far on stream `signaller` (same device):
+ * a hipEvent created with hipEventDisableSystemFence, so the record / wait pair fences at
+ * device scope only (the side-stream forks and joins of the backward; torch's
+ * Stream.wait_stream records a default event).  Works inside a stream capture. */
+int of_stream_wait(void* waiter, void* signaller);
 
 /* Per-launch timing of the conv kernels (bench instrumentation): when enabled (on = 1), every
  * conv launch records a hipEvent pair on its stream; on = 2 times the next conv launch only
@@ -334,7 +339,9 @@ int of_timing_enable(int on);
  * key 12 = bf16 3x3 stride-1 fwd / dgrad on the single-plane halo kernel conv_tile_b16 (1;
  * timing kinds 192 + 8 mode + cfg) or the round-1 conv_tile_bf16 (0, default);
  * key 13 = bf16 3x3 stride-1 weight gradient on the single-plane 9-tap kernel
- * conv_wgrad_tile_b16 (1; timing kinds 216 + cfg) or conv_wgrad_tile_bf16 (0, default). */
+ * conv_wgrad_tile_b16 (1; timing kinds 216 + cfg) or conv_wgrad_tile_bf16 (0, default);
+ * key 14 = the stem's fp32 weight gradient (7x7 stride 2, 3 input channels padded to 4, 64
+ * outputs) on conv_wgrad_stem_x3 (1, default; timing kind 185) or the fp32 MFMA GEMM (0). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -2,6 +2,7 @@
 #include "common.h"
 
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 namespace oflow {
@@ -96,6 +97,19 @@ void timing_end(hipStream_t s, int kind, double flops) {
   if (g_timing_oneshot) g_timing = g_timing_oneshot = false;
 }
 
+// ---- cross-stream ordering --------------------------------------------------------------
+// A default hipEvent releases at system scope when it is recorded and its waiters acquire at
+// system scope; ordering two streams of one device needs device scope only.  A ring of
+// fence-light events per device (hipStreamWaitEvent binds the record current at the call,
+// so re-recording a ring slot later is safe).
+static std::mutex g_wmu;
+struct WaitRing {
+  std::vector<hipEvent_t> ev;
+  size_t next = 0;
+};
+static std::unordered_map<int, WaitRing> g_wait_rings;
+constexpr int kWaitRing = 64;
+
 }  // namespace oflow
 
 using namespace oflow;
@@ -114,6 +128,32 @@ int of_same_pads(int n, int k, int s, int* before, int* after, int* out) {
   *before = total / 2;
   *after = total - total / 2;
   *out = o;
+  return OF_OK;
+}
+
+int of_stream_wait(void* waiter, void* signaller) {
+  OF_CHECK_ARG(waiter != signaller, "stream_wait: waiter and signaller are one stream");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return check_launch("stream_wait: hipGetDevice");
+  hipEvent_t e = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_wmu);
+    WaitRing& r = g_wait_rings[dev];
+    if (r.ev.empty()) {
+      for (int i = 0; i < kWaitRing; ++i) {
+        hipEvent_t x = nullptr;
+        if (hipEventCreateWithFlags(&x, hipEventDisableTiming | hipEventDisableSystemFence) !=
+            hipSuccess)
+          return check_launch("stream_wait: hipEventCreateWithFlags");
+        r.ev.push_back(x);
+      }
+    }
+    e = r.ev[r.next++ % r.ev.size()];
+  }
+  if (hipEventRecord(e, static_cast<hipStream_t>(signaller)) != hipSuccess)
+    return check_launch("stream_wait: hipEventRecord");
+  if (hipStreamWaitEvent(static_cast<hipStream_t>(waiter), e, 0) != hipSuccess)
+    return check_launch("stream_wait: hipStreamWaitEvent");
   return OF_OK;
 }
 

@@ -2495,6 +2495,195 @@ __device__ __forceinline__ void split3x8(const float* v, bf16x8& h, bf16x8& m, b
   l = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
 }
 
+// ---- the stem's weight gradient (7x7 stride 2, 4 padded input channels, 64 outputs) on the
+// split-bf16 MFMA.  dW[(r, s, ci)][co] = sum over output pixels p of
+// x[2 py + r - pt][2 px + s - pl][ci] * dz[p][co]: GEMM M = (r, s, ci) over the 147 real rows
+// (10 M tiles of 16), N = 64, K = output pixels.  The implicit GEMM gathers 49 taps x 16 bytes
+// per pixel from global memory for every K step; here a workgroup owns 4 x 32-pixel output
+// tiles: the tile's input halo (13 rows x 69 pixels x 4 channels) goes to LDS once, fp32,
+// split by column parity ([row][ci][parity][col / 2]) so that kernel column s of 8 consecutive
+// output pixels is 8 consecutive floats at a per-lane offset (each lane gathers its own A row
+// with ds_read_b32, so the rows need no (r, s, ci) padding); it is prefetched one tile ahead
+// into a second buffer.  Each 32-pixel output row is one K chunk whose dz (32 px x 64 co) is
+// loaded two chunks ahead, cut into hi / mid / lo bf16 planes in B-fragment order ([plane]
+// [k octet][co], conflict-free ds_read_b128) and double-buffered.  Wave w (5 waves) owns M
+// tiles 2w, 2w + 1 x 4 N tiles, six v_mfma_f32_16x16x32_bf16 per fragment pair (rows 147-159
+// compute discarded values).  Workgroups (three per CU) are persistent over a contiguous range
+// of a.k_per_split tiles (a.K tiles in all) and write one split-K slab each (with a.colsum the
+// bias column sums in slab row 196), reduced by wgrad_reduce_kernel.
+constexpr int SW_TH = 4, SW_TW = 32, SW_HH = 2 * SW_TH + 5, SW_HX = 2 * SW_TW + 5, SW_HC = 36;
+constexpr int SW_HP = SW_HH * 4 * 2 * SW_HC;             // floats per halo buffer
+constexpr int SW_NW = 5, SW_NT = 64 * SW_NW;
+constexpr int SW_HQ = (SW_HH * SW_HX + SW_NT - 1) / SW_NT; // halo pixels per thread
+constexpr int SW_WGS_PER_CU = 3;
+
+__global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
+  constexpr int NT = SW_NT, NP = 3;
+  __shared__ float Hs[2][SW_HP];                       // 2 x 14.6 KB
+  __shared__ uint4 Ds[2][NP * 4 * 64];                 // 2 x 12 KB
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int split = xcd_remap(blockIdx.x, gridDim.x);
+  const int t_begin = split * a.k_per_split;
+  const int t_end = min(a.K, t_begin + a.k_per_split);
+  const int ntiles = max(0, t_end - t_begin);
+  const int nchunks = ntiles * SW_TH;
+  const int tiles_x = (a.wo + SW_TW - 1) / SW_TW, tiles_y = (a.ho + SW_TH - 1) / SW_TH;
+  const rsrc_t rx = make_rsrc(a.A, a.a_bytes);
+  const rsrc_t rd = make_rsrc(a.B, a.b_bytes);
+  auto tile_of = [&](int t, int& b, int& oy0, int& ox0) {
+    b = t / (tiles_x * tiles_y);
+    const int rem = t - b * tiles_x * tiles_y;
+    oy0 = (rem / tiles_x) * SW_TH;
+    ox0 = (rem % tiles_x) * SW_TW;
+  };
+
+  // ---- dz (waves 0-3): thread (co, k octet) loads 8 consecutive pixels of one channel (each
+  // load instruction reads 64 channels of 4 pixels: 4 x 64-byte segments); two chunks in flight
+  const int d_co = tid & 63, d_kg = (tid >> 6) & 3;
+  const bool d_on = tid < 256 && d_co < a.N;
+  const uint32_t d_step = (uint32_t)a.ldb * 4;        // bytes between consecutive pixels
+  float dv[2][8], csum = 0.f;
+  auto load_dz = [&](int c, float* v) {
+    int b, oy0, ox0;
+    tile_of(t_begin + c / SW_TH, b, oy0, ox0);
+    const int oy = oy0 + c % SW_TH, px0 = ox0 + 8 * d_kg;
+    const int lim = d_on && oy < a.ho ? a.wo - px0 : 0;   // pixels of this octet in the row
+    const uint32_t base = (uint32_t)((((int64_t)b * a.ho + oy) * a.wo + px0) * a.ldb + d_co) * 4;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bload1(rd, e < lim ? base + e * d_step : kOOB);
+  };
+  auto store_dz = [&](int buf, const float* v) {
+    if (tid >= 256) return;
+    bf16x8 h, m, l;
+    split3x8(v, h, m, l);
+    Ds[buf][(0 * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, h);
+    Ds[buf][(1 * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, m);
+    Ds[buf][(2 * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, l);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum += v[e];
+  };
+  // ---- input halo ([row][ci][parity][col / 2] fp32), loaded one tile ahead
+  float4 hv[SW_HQ];
+  auto load_halo = [&](int t) {
+    int b, oy0, ox0;
+    tile_of(t, b, oy0, ox0);
+    const int iy0 = 2 * oy0 - a.pt, ix0 = 2 * ox0 - a.pl;
+#pragma unroll
+    for (int k = 0; k < SW_HQ; ++k) {
+      const int q = tid + NT * k;
+      const int hy = q / SW_HX, hx = q - hy * SW_HX;
+      const int iy = iy0 + hy, ix = ix0 + hx;
+      const bool ok = q < SW_HH * SW_HX && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+      hv[k] = bload4(rx, ok ? (uint32_t)((((int64_t)b * a.h + iy) * a.w + ix) * a.lda * 4) : kOOB);
+    }
+  };
+  auto store_halo = [&](int hb) {
+#pragma unroll
+    for (int k = 0; k < SW_HQ; ++k) {
+      const int q = tid + NT * k;
+      if (q >= SW_HH * SW_HX) continue;
+      const int hy = q / SW_HX, hx = q - hy * SW_HX;
+      float* dst = Hs[hb] + hy * 8 * SW_HC + (hx & 1) * SW_HC + (hx >> 1);
+      dst[0] = hv[k].x;
+      dst[2 * SW_HC] = hv[k].y;
+      dst[4 * SW_HC] = hv[k].z;
+      dst[6 * SW_HC] = hv[k].w;
+    }
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+  // A row of this lane in M tile mt: m = 16 (2 wave + mt) + l16 = (tap = r * 7 + s) * 3 + ci
+  const int l16 = lane & 15, kg = lane >> 4;
+  int a_off[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int m = min(16 * (2 * wave + mt) + l16, 146);
+    const int tap = m / 3, ci = m - 3 * tap, r = tap / 7, sc = tap - 7 * r;
+    a_off[mt] = (r * 8 + ci * 2 + (sc & 1)) * SW_HC + 8 * kg + (sc >> 1);
+  }
+
+  if (nchunks > 0) {
+    load_halo(t_begin);
+    load_dz(0, dv[0]);
+    if (nchunks > 1) load_dz(1, dv[1]);
+    store_halo(0);
+  }
+  // chunk c uses dz register set c & 1 (static: the body is instantiated for both sets)
+  auto chunk = [&](int c, float* dvc) {
+    const int j = c % SW_TH, tl = c / SW_TH;
+    const int buf = c & 1;
+    // The halo of tile tl + 1 is stored into the other buffer at j = 1: every wave passed this
+    // chunk's barrier, so none still reads that buffer (tile tl - 1, last read at chunk c - 2).
+    if (j == 0 && tl + 1 < ntiles) load_halo(t_begin + tl + 1);
+    store_dz(buf, dvc);
+    __syncthreads();                               // this chunk's dz (and its tile's halo)
+    if (c + 2 < nchunks) load_dz(c + 2, dvc);      // two chunks in flight
+    if (j == 1 && tl + 1 < ntiles) store_halo((tl + 1) & 1);
+    const float* hrow = Hs[tl & 1] + 2 * j * 8 * SW_HC;
+    bf16x8 av[2][NP];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = hrow[a_off[mt] + e];
+      split3x8(v, av[mt][0], av[mt][1], av[mt][2]);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      bf16x8 bv[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        bv[p] = __builtin_bit_cast(bf16x8, Ds[buf][(p * 4 + kg) * 64 + nt * 16 + l16]);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        f32x4 x = acc[mt][nt];
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][2], bv[0], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][0], bv[2], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][1], bv[1], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][1], bv[0], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][0], bv[1], x, 0, 0, 0);
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][0], bv[0], x, 0, 0, 0);
+      }
+    }
+  };
+  for (int c = 0; c < nchunks; c += 2) {
+    chunk(c, dv[0]);
+    if (c + 1 < nchunks) chunk(c + 1, dv[1]);
+  }
+
+  // ---- this workgroup's slab: lane's value rr of (mt, nt) is row m = 16 (2 wave + mt) +
+  // 4 kg + rr = tap * 3 + ci, column 16 nt + l16; slab row = tap * 4 + ci
+  float* slab = a.slab + (int64_t)split * a.split_stride;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = 16 * (2 * wave + mt) + 4 * kg + rr;
+      if (m >= 147) continue;
+      const int tap = m / 3, ci = m - 3 * tap;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int co = nt * 16 + l16;
+        if (co < a.N) slab[(int64_t)(tap * 4 + ci) * a.slab_ld + co] = acc[mt][nt][rr];
+      }
+    }
+  if (a.colsum) {                                  // bias: column sums of dz, fixed order
+    float* Cs = reinterpret_cast<float*>(&Ds[0][0]);
+    __syncthreads();                               // every wave is done with Ds
+    if (tid < 256) Cs[d_kg * 64 + d_co] = csum;
+    __syncthreads();
+    if (tid < 64 && tid < a.N)
+      slab[(int64_t)196 * a.slab_ld + tid] = (Cs[tid] + Cs[64 + tid]) + (Cs[128 + tid] + Cs[192 + tid]);
+  }
+}
+
 template <int WAVES_CI, int WAVES_CO, int WAVES_R, int XH>
 __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO * WAVES_R, 1) void conv_wgrad_tile_x3(GemmArgs a) {
   constexpr int NT = 64 * WAVES_CI * WAVES_CO * WAVES_R;
@@ -4312,6 +4501,15 @@ void wgx3_blocks(const of_conv_desc* d, int& cib, int& cob) {
   cob = c == 0 ? 128 : c == 1 ? 96 : c == 2 || c == 4 ? 64 : 32;
 }
 
+// of_set_tuning key 14: the stem's fp32 weight gradient (3 input channels) on
+// conv_wgrad_stem_x3 (1, default) or on the fp32 MFMA GEMM (0).
+static int g_stem_wg = 1;
+// (3 real input channels: the kernel's M rows are the 49 x 3 real (tap, ci) pairs)
+bool stem_wg_ok(const of_conv_desc* d) { return g_stem_wg && stem_x3_ok(d) && d->cin == 3; }
+int stem_wg_tiles(const of_conv_desc* d) {
+  return d->n * (int)cdiv(d->ho, SW_TH) * (int)cdiv(d->wo, SW_TW);
+}
+
 // of_set_tuning key 10: fp32 / bf16 GEMM weight-gradient split-K target workgroups per CU.
 static int g_wgrad_wgs = 4;
 
@@ -4321,6 +4519,14 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
   p.M = g.taps * g.cin_p;
   p.ldc = g.cout_p;
   p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
+  if (!bf16 && stem_wg_ok(d)) {
+    // conv_wgrad_stem_x3: K = 4 x 32 output tiles, persistent workgroups (3 per CU)
+    const int T = stem_wg_tiles(d);
+    int splits = std::max(1, std::min(T, SW_WGS_PER_CU * device_cus()));
+    p.k_per_split = (int)cdiv(T, splits);
+    p.splits = (int)cdiv(T, p.k_per_split);
+    return p;
+  }
   if ((x3 || (bf16 && g_wgrad_b16)) && wgx3_ok(d)) {
     // K = 4 x 16 pixel tiles; one workgroup per CU, equal slices
     int cib, cob;
@@ -4476,6 +4682,7 @@ int of_set_tuning(int key, int value) {
   if (key == 6 && (value == 0 || value == 1)) { g_wgx3_gemm = value; return OF_OK; }
   if (key == 12 && (value == 0 || value == 1)) { g_tile_b16 = value; return OF_OK; }
   if (key == 13 && (value == 0 || value == 1)) { g_wgrad_b16 = value; return OF_OK; }
+  if (key == 14 && (value == 0 || value == 1)) { g_stem_wg = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -4882,7 +5089,14 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   a.vec_ep = vec_ep_ok(a);
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
-  if (b16) {
+  if (!bf16 && stem_wg_ok(d)) {
+    a.K = stem_wg_tiles(d);
+    a.lda = ldx;
+    if (timing_on()) timing_begin(s);
+    hipLaunchKernelGGL(conv_wgrad_stem_x3, dim3(a.splits), dim3(SW_NT), 0, s, a);
+    if (timing_on()) timing_end(s, 185, flops);     // bench.py KIND_STEM_WG_X3
+    st = check_launch("conv_wgrad_stem_x3");
+  } else if (b16) {
     // the x3b configurations, all 9-tap: timing kinds 216 + cfg (bench.py X3_WGT 4 + cfg)
     const int cfg = wgx3_cfg(d);
     a.K = d->n * (int)cdiv(d->ho, wgx3_rows(cfg)) * (int)cdiv(d->wo, TT_W);

@@ -129,12 +129,30 @@ def _side_max_pix(layer) -> int:
     return SIDE_MAX_PIX_DEFAULT[layer.precision]
 _SIDE = {}
 _side_armed = False
+# The BN reduction of a layer whose t = dL/dz the input-gradient kernel already produced
+# (of_bn_bwd_reduce without t_out: dgamma, dbeta and the bias gradient only) runs on the side
+# stream too; OFLOW_BN_SIDE=0 keeps it on the current stream for A/B.
+BN_REDUCE_SIDE = os.environ.get("OFLOW_BN_SIDE", "1") == "1"
 # Launch order inside a conv's backward.  Weight gradient first (default): a side-stream
 # weight gradient then forks before the input gradient is enqueued and overlaps it.  Input
 # gradient first (OFLOW_DGRAD_FIRST=1, the critical path queued earlier where the host is
 # slower than the GPU) measured 2 % slower (A/B, one box: 590-593 vs 602-606 pairs/s): the
 # side stream's fork then waits for the dgrad.
 DGRAD_FIRST = os.environ.get("OFLOW_DGRAD_FIRST", "0") == "1"
+
+
+# Cross-stream waits through of_stream_wait (device-scope event fences) instead of torch's
+# Stream.wait_stream (a default event: system-scope release / acquire).  OFLOW_STREAM_WAIT=torch
+# keeps torch's for A/B.
+NATIVE_STREAM_WAIT = os.environ.get("OFLOW_STREAM_WAIT", "native") != "torch"
+
+
+def stream_wait(waiter, signaller):
+    """Order stream ``waiter`` after the work enqueued so far on ``signaller``."""
+    if NATIVE_STREAM_WAIT:
+        call("of_stream_wait", C.c_void_p(waiter.cuda_stream), C.c_void_p(signaller.cuda_stream))
+    else:
+        waiter.wait_stream(signaller)
 
 
 def _side_join():
@@ -147,7 +165,7 @@ def side_join_now():
     """Order each device's current stream after everything enqueued so far on its side
     streams (the end-of-backward join, also used after work launched outside a backward)."""
     for dev, s in list(_SIDE.items()) + list(_CORR_SIDE.items()):
-        torch.cuda.current_stream(dev).wait_stream(s)
+        stream_wait(torch.cuda.current_stream(dev), s)
 
 
 def side_stream(*tensors):
@@ -159,7 +177,7 @@ def side_stream(*tensors):
     s = _SIDE.get(cur.device)
     if s is None:
         s = _SIDE[cur.device] = torch.cuda.Stream(cur.device)
-    s.wait_stream(cur)
+    stream_wait(s, cur)
     for t in tensors:
         if t is not None:
             t.record_stream(s)
@@ -187,7 +205,7 @@ def corr_side_stream(*tensors):
     s = _CORR_SIDE.get(cur.device)
     if s is None:
         s = _CORR_SIDE[cur.device] = torch.cuda.Stream(cur.device)
-    s.wait_stream(cur)
+    stream_wait(s, cur)
     for t in tensors:
         if t is not None:
             t.record_stream(s)
@@ -201,7 +219,7 @@ def corr_side_wait(device):
     """Order the current stream after the df1 stream (before anything reads a df1)."""
     s = _CORR_SIDE.get(torch.device(device))
     if s is not None:
-        torch.cuda.current_stream(device).wait_stream(s)
+        stream_wait(torch.cuda.current_stream(device), s)
 
 
 def grad_target(param: torch.Tensor):
@@ -492,9 +510,13 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
                          device=dy.device)
         if t_given or layer.act == ACT_NONE:
             dz = dy                     # already t
-            call("of_bn_bwd_reduce", npix, layer.cout, ACT_NONE, _ptr(dz), _ptr(y),
-                 _ptr(res_src), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, None,
-                 _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
+            # only parameter gradients come out: off the critical path (BN_REDUCE_SIDE)
+            side = BN_REDUCE_SIDE and SIDE_STREAM_WGRAD and acc == 1
+            with torch.cuda.stream(side_stream(dz, y, res_src, ws)) if side else \
+                    contextlib.nullcontext():
+                call("of_bn_bwd_reduce", npix, layer.cout, ACT_NONE, _ptr(dz), _ptr(y),
+                     _ptr(res_src), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, None,
+                     _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
         else:
             dz = torch.empty_like(dy)    # t = dy * act'(y)
             call("of_bn_bwd_reduce", npix, layer.cout, layer.act, _ptr(dy), _ptr(y),

@@ -30,9 +30,9 @@ pytestmark = pytest.mark.gpu
 # timing kinds (bench.py kind_parts) of the forms the config-2 bench line reports
 # (BENCH_r02.json roofline.per_kernel): fwd / dgrad on 8 x 32 tiles of conv_tile_x3<128, 4, 2,
 # 8> (128, 136), the 9-tap weight gradient conv_wgrad_tile_x3b<2, 4, 8, 1> (148), the stem
-# conv_stem_x3 (184) and its weight gradient on the fp32 GEMM (18), the split implicit GEMMs
+# conv_stem_x3 (184) and its weight gradient conv_wgrad_stem_x3 (185), the split implicit GEMMs
 # of the stride-2 / 1x1 layers (160 + mode * 8 + cfg) and the narrow flow convs (7, 15, 23).
-CFG2_KINDS = {128, 136, 148, 184, 7, 15, 23, 18}
+CFG2_KINDS = {128, 136, 148, 184, 7, 15, 23, 185}
 GEMM_X3_FWD, GEMM_X3_DGRAD, GEMM_X3_WGRAD = range(160, 168), range(168, 176), range(176, 184)
 
 

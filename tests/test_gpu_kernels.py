@@ -331,6 +331,62 @@ def test_conv_stem_x3(n, h, w):
     assert rel_l2(outs[0][0], yref) < 3 * rel_l2(outs[2][0], yref) + 1e-7
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (3, 38, 130), (8, 384, 512)])
+def test_conv_stem_wgrad_x3(n, h, w):
+    """The stem's weight gradient on its own split-bf16 kernel (conv_wgrad_stem_x3: 4 x 32
+    output tiles, the input halo split by column parity in LDS, persistent workgroups, one
+    slab each) against fp64 and against the fp32 MFMA GEMM (of_set_tuning key 14 = 0): the
+    kernel and bias gradients, accumulate, ragged tiles, and the bench's full size (B = 8,
+    384 x 512); as accurate as one fp32 rounding per product; the timing kind says which
+    kernel ran."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_RELU, call
+    lib = _lib.lib()
+    cin, cout = 4, 64
+    xc = rng_tensor((n, h, w, 3), 71)
+    x = torch.cat([xc, torch.zeros(n, h, w, 1)], -1)
+    wt = rng_tensor((7, 7, 3, cout), 72, scale=(2.0 / 147) ** 0.5)
+    layer = ops.ConvLayer(dev(wt), dev(torch.zeros(cout)), stride=2, act=ACT_RELU, cin_p=cin,
+                          f32_split=True)
+    d = layer.desc(n, h, w)
+    dz = rng_tensor((n, d.ho, d.wo, cout), 73)
+    went, _ = layer.wgrad_entry(d)
+    xd, dzd = dev(x), dev(dz)
+    P, st = ops._ptr, ops._stream()
+    prior_w = rng_tensor((7, 7, 3, cout), 74)
+    prior_b = rng_tensor((cout,), 75)
+    res = {}
+    try:
+        for form in (1, 0):
+            assert lib.of_set_tuning(14, form) == 0
+            wws = getattr(lib, went + "_workspace")(C.byref(d))
+            ws = torch.empty(wws // 4 + 4, device="cuda")
+            dw, db = dev(prior_w.clone()), dev(prior_b.clone())
+            lib.of_timing_enable(1)
+            call(went, C.byref(d), P(xd), cin, P(dzd), cout, P(dw), P(db), 1, P(ws), wws, st)
+            torch.cuda.synchronize()
+            lib.of_timing_enable(0)
+            kk = (C.c_int * 16)()
+            cnt = lib.of_timing_read(16, kk, None, None)
+            res[form] = (dw.cpu().double() - f64(prior_w), db.cpu().double() - f64(prior_b),
+                         {kk[i] for i in range(cnt)})
+    finally:
+        lib.of_set_tuning(14, 1)
+        lib.of_timing_enable(0)
+    assert res[1][2] == {185} and 185 not in res[0][2], (res[1][2], res[0][2])
+    wo = f64(wt).requires_grad_(True)
+    (R.conv2d_same(f64(xc), wo, None, 2) * f64(dz)).sum().backward()
+    dbref = f64(dz).sum((0, 1, 2))
+    e_new = [rel_l2(res[1][0], wo.grad), rel_l2(res[1][1], dbref)]
+    e_old = [rel_l2(res[0][0], wo.grad), rel_l2(res[0][1], dbref)]
+    print("stem wgrad rel_l2 new %s, fp32 GEMM %s" % (e_new, e_old))
+    # (the accumulate subtraction leaves fp32 rounding of the prior values: 1e-6 relative)
+    assert e_new[0] < 3 * e_old[0] + 1e-6 and e_new[0] < 5e-6, (e_new, e_old)
+    assert e_new[1] < 5e-6, (e_new, e_old)
+
+
 @pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
     # kinds: 128 + 8 mode + cfg; wgrad 144 + cfg (3-tap form) / 148 + cfg (9-tap x3b form)
     ("tall128", 8, 128, 256, 128, 128, {128, 136, 148}),  # 8 x 32 tiles, BN 128 (1024 tiles)
