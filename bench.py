@@ -57,6 +57,8 @@ def kind_parts(kind):
         return 0, 0, "stem_x3"
     if kind == KIND_STEM_WG_X3:
         return 2, 0, "stem_x3"
+    if kind >= 224:                               # conv_tile_ws (warp-specialised bf16 3x3)
+        return (kind - 224) // 8, (kind - 224) % 8, "tile_ws"
     if kind >= 216:                               # conv_wgrad_tile_b16 (x3b configs, 1 plane)
         return 2, kind - 216, "wgrad_b16"
     if kind >= 192:                               # conv_tile_b16 (bf16 on the x3 structure)
@@ -83,6 +85,7 @@ X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4",   
 
 
 WGT_WAVES = {0: "1, 4", 2: "2, 2"}   # conv_wgrad_tile_bf16<WAVES_CI, WAVES_CO>
+WS_BN = {0: "128, 8, 2, 2", 1: "96, 8, 2, 2"}   # conv_tile_ws<BN, TH, CWM, CWN>
 B16_WGT = {0: "2, 4, 8", 1: "2, 3, 8", 2: "4, 2, 4", 3: "4, 1, 4", 4: "2, 2, 8"}   # conv_wgrad_tile_b16
 
 
@@ -111,7 +114,9 @@ def kind_name(kind):
         return "wgrad_stem_x3" if mode == 2 else "fwd_stem_x3"
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
            "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3", "tile_b16": "_tile_b16",
-           "wgrad_b16": ""}[fam]
+           "wgrad_b16": "", "tile_ws": "_tile_ws"}[fam]
+    if fam == "tile_ws":
+        return "%s%s<%s>" % (MODE_NAMES[mode], sfx, WS_BN[cfg])
     if fam == "tile_b16":
         return "%s%s<%s, %d>" % (MODE_NAMES[mode], sfx, X3_BN[cfg], X3_TH[cfg])
     if fam == "wgrad_b16":
@@ -142,6 +147,8 @@ def kernel_symbol(kind):
                                                                             X3_TH[cfg])
     if fam == "wgrad_b16":
         return "void oflow::conv_wgrad_tile_b16<%s>(oflow::GemmArgs)" % B16_WGT[cfg]
+    if fam == "tile_ws":
+        return "void oflow::conv_tile_ws<%s, %d>(oflow::GemmArgs)" % (WS_BN[cfg], mode)
     if fam == "gemm_x3":
         if mode == 2:
             return "void oflow::conv_wgrad_x3<%s>(oflow::GemmArgs)" % GX3_WG[cfg]

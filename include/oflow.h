@@ -337,7 +337,9 @@ int of_timing_enable(int on);
  * key 11 = the split weight gradient of Cout-64 layers whose Cin is not a multiple of 64 on
  * 32 x 64 channel blocks (1, default) or on 64 x 64 blocks (0);
  * key 12 = bf16 3x3 stride-1 fwd / dgrad on the single-plane halo kernel conv_tile_b16 (1;
- * timing kinds 192 + 8 mode + cfg) or the round-1 conv_tile_bf16 (0, default);
+ * timing kinds 192 + 8 mode + cfg), on the warp-specialised conv_tile_ws for N tiles of 128 /
+ * 96 (2: fwd and dgrad, 3: fwd only; timing kinds 224 + 8 mode + cfg) or the round-1
+ * conv_tile_bf16 (0, default);
  * key 13 = bf16 3x3 stride-1 weight gradient on the single-plane 9-tap kernel
  * conv_wgrad_tile_b16 (1; timing kinds 216 + cfg) or conv_wgrad_tile_bf16 (0, default);
  * key 14 = the stem's fp32 weight gradient (7x7 stride 2, 3 input channels padded to 4, 64

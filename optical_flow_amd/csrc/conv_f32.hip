@@ -27,230 +27,14 @@
 // the producer layer's activation derivative (dgrad).  Work-group ids are remapped so that
 // consecutive tiles (and all tiles of one K slice) run on one XCD and share its L2.
 #include "common.h"
+#include "conv_dev.h"
 #include "conv_narrow.h"
 
 #include <algorithm>
 
 namespace oflow {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
-constexpr int BK = 16;
-constexpr int MAX_GROUPS = 4;
-
-// A group = GEMM rows sharing one tap list (dgrad stride-2 phase classes); plain convs have
-// a single identity group.
-struct Group {
-  int tiles_begin;   // first m-tile of this group in the flattened tile space
-  int m_tiles;
-  int M;             // rows of the group
-  int hc, wc;        // phase mode: rows are (b, u, v), input pixel (2u+ry, 2v+rx)
-  int ry, rx;
-  int r0, s0, ns;    // taps (r0 + dt*(t/ns), s0 + dt*(t%ns)), t < ntaps
-  int ntaps;
-  int K;             // K of the group (multiple of BK)
-  int64_t b_off;     // first packed-B row of the group
-};
-
-struct GemmArgs {
-  int n, h, w, ho, wo;
-  int kh, kw, stride, pt, pl;
-  int kc;                 // channels per tap along K (fwd: cin_p, dgrad: cout_p) / M (wgrad)
-  int dt;                 // tap step inside a group (1, or 2 for phase groups)
-  int phase;              // dgrad phase-group mode (stride 2)
-  int M, N, K;            // wgrad: M = taps*cin_p, K = output pixels
-  const float* A; int lda; int64_t a_bytes;
-  const float* B; int ldb; int nb; int64_t b_bytes;
-  int64_t b_plane;        // conv_tile_x3: elements between the hi / mid / lo weight planes
-  float* C; int ldc;      // final output (epilogue)
-  const float* bias;
-  const float* bn_g; const float* bn_b; const float* bn_m; const float* bn_v; float bn_eps;
-  const float* res; int ldr;
-  float* z; int ldz;
-  int act; float alpha;
-  const float* act_src; int ld_act;
-  int splits;             // K slices over workgroups
-  int k_per_split;        // elements of K per slice (multiple of BK)
-  float* slab; int slab_ld;   // partials (wgrad always; fwd/dgrad when splits > 1)
-  int64_t split_stride;
-  int n_tiles;
-  int tiles_total;        // sum over groups of m_tiles * n_tiles
-  int colsum;             // wgrad: column sums of B (bias grad) into slab row M
-  int bm;                 // M tile of the launched configuration
-  int ngroups;
-  int vec_ep;             // tile kernels: 4-column epilogue (N, every ld a multiple of 4,
-                          // every row pointer 16-byte aligned)
-  int act_post;           // dgrad: dx = act'(act_src) * (sum + res) instead of act' * sum + res
-  Group grp[MAX_GROUPS];
-};
-
-// dgrad epilogue value: the input gradient v times the producer's activation derivative at s,
-// plus an added gradient r -- or, with act_post, the derivative applied to the sum (the
-// gradient of a ReLU output that has several consumers: encoder block inputs).
-__device__ __forceinline__ float dgrad_ep(const GemmArgs& a, float v, float s, float r) {
-  const float d = s > 0.f ? 1.f : (a.act == OF_ACT_LEAKY ? a.alpha : 0.f);
-  return a.act_post ? (v + r) * d : v * d + r;
-}
-
-__device__ __forceinline__ void add4(float4& a, const float4& b) {
-  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-}
-
-__device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
-  if (act == OF_ACT_RELU) return v > 0.f ? v : 0.f;
-  if (act == OF_ACT_LEAKY) return v > 0.f ? v : alpha * v;
-  return v;
-}
-
-// Output pixel row of group-local GEMM row m (identity unless dgrad phase groups).
-__device__ __forceinline__ int64_t out_row(const GemmArgs& a, const Group& g, int m) {
-  if (!a.phase) return m;
-  const int hw = g.hc * g.wc;
-  const int b = m / hw, rem = m - b * hw;
-  const int u = rem / g.wc, v = rem - u * g.wc;
-  return ((int64_t)b * a.h + 2 * u + g.ry) * a.w + 2 * v + g.rx;
-}
-
-// The epilogue's second input for one element: the residual (fwd) or the producer's output
-// whose activation derivative scales dx (dgrad).  Call sites gather all of a lane's values
-// before the first store: interleaved, every load would wait behind the previous store (the
-// compiler cannot prove a.C does not alias them).
-// dgrad: s = the producer's output (activation derivative), r = a gradient to add (the
-// residual branch's, so the autograd sum of the two input gradients needs no extra pass).
-struct EpAux {
-  float s, r;
-};
-template <int MODE>
-__device__ __forceinline__ EpAux epilogue_aux(const GemmArgs& a, int64_t row, int n) {
-  if (MODE == MODE_FWD) return {a.res ? a.res[row * a.ldr + n] : 0.f, 0.f};
-  if (MODE == MODE_DGRAD)
-    return {a.act_src ? a.act_src[row * a.ld_act + n] : 1.f, a.res ? a.res[row * a.ldr + n] : 0.f};
-  return {0.f, 0.f};
-}
-
-// Aux values gathered ahead of the stores: the whole 16-value MFMA fragment for dgrad (the
-// decoder's act_src on every layer); 4 for fwd, whose residual only the encoder has and whose
-// epilogue registers set the kernels' occupancy.
-#ifndef OF_EPG_FWD
-#define OF_EPG_FWD 4
-#endif
-#ifndef OF_EPG_DGRAD
-#define OF_EPG_DGRAD 8
-#endif
-template <int MODE>
-constexpr int EP_GATHER = MODE == MODE_DGRAD ? OF_EPG_DGRAD : OF_EPG_FWD;
-
-// Fused epilogue for one element (fwd / dgrad), v = the full K sum, aux = epilogue_aux.
-template <int MODE>
-__device__ __forceinline__ void epilogue_store(const GemmArgs& a, int64_t row, int n, float v,
-                                               float bias, float scale, float shift, EpAux aux) {
-  if (MODE == MODE_FWD) {
-    v += bias;
-    if (a.z) a.z[row * a.ldz + n] = v;
-    if (a.bn_g) v = v * scale + shift;
-    v += aux.s;
-    v = act_fwd(v, a.act, a.alpha);
-  } else if (MODE == MODE_DGRAD) {
-    v = dgrad_ep(a, v, aux.s, aux.r);
-  }
-  a.C[row * a.ldc + n] = v;
-}
-
-template <int MODE>
-__device__ __forceinline__ void column_params(const GemmArgs& a, int n, float& bias,
-                                              float& scale, float& shift);
-
-// The fused epilogue of epilogue_store for four consecutive columns n .. n + 3 of one row,
-// with 16-byte loads and stores (a.vec_ep: N and every leading dimension a multiple of 4,
-// 16-byte aligned bases).  splits > 1 writes the raw sums to this K slice's slab row.
-template <int MODE>
-__device__ __forceinline__ void epilogue_store4(const GemmArgs& a, int split, int64_t row, int n,
-                                                float4 v4) {
-  if (a.splits > 1) {
-    *reinterpret_cast<float4*>(&a.slab[(int64_t)split * a.split_stride + row * a.slab_ld + n]) = v4;
-    return;
-  }
-  float v[4] = {v4.x, v4.y, v4.z, v4.w};
-  if (MODE == MODE_FWD) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float bias, scale, shift;
-      column_params<MODE>(a, n + e, bias, scale, shift);
-      v[e] += bias;
-      (void)scale;
-      (void)shift;
-    }
-    if (a.z) *reinterpret_cast<float4*>(&a.z[row * a.ldz + n]) = make_float4(v[0], v[1], v[2], v[3]);
-    if (a.bn_g) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float bias, scale, shift;
-        column_params<MODE>(a, n + e, bias, scale, shift);
-        v[e] = v[e] * scale + shift;
-      }
-    }
-    if (a.res) {
-      const float4 r = *reinterpret_cast<const float4*>(&a.res[row * a.ldr + n]);
-      v[0] += r.x;
-      v[1] += r.y;
-      v[2] += r.z;
-      v[3] += r.w;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], a.act, a.alpha);
-  } else if (MODE == MODE_DGRAD) {
-    float4 s4 = make_float4(1.f, 1.f, 1.f, 1.f), r4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.act_src) s4 = *reinterpret_cast<const float4*>(&a.act_src[row * a.ld_act + n]);
-    if (a.res) r4 = *reinterpret_cast<const float4*>(&a.res[row * a.ldr + n]);
-    v[0] = dgrad_ep(a, v[0], s4.x, r4.x);
-    v[1] = dgrad_ep(a, v[1], s4.y, r4.y);
-    v[2] = dgrad_ep(a, v[2], s4.z, r4.z);
-    v[3] = dgrad_ep(a, v[3], s4.w, r4.w);
-  }
-  *reinterpret_cast<float4*>(&a.C[row * a.ldc + n]) = make_float4(v[0], v[1], v[2], v[3]);
-}
-
-// One wave's 32 x 32 accumulator block in the v_mfma_f32_32x32x* layout (column lane & 31,
-// rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) through a private 4 KB LDS image E, back as
-// float4 rows: f(row 0..31, column quad 0..7, value) for the 4 rows x 1 quad each lane owns.
-// Unpadded 32-float rows: the ds_write_b32 of a lane group cover one row (32 banks) and the
-// ds_read_b128 groups (rows 4 apart sharing a slot base) hit 16 distinct slots.
-template <typename F>
-__device__ __forceinline__ void transpose32(float* E, const f32x16& acc, int lane, F&& f) {
-  const int lrow = lane & 31, lk = lane >> 5;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) E[((r & 3) + 8 * (r >> 2) + 4 * lk) * 32 + lrow] = acc[r];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int c4 = lane & 7, rr = lane >> 3;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int row = 8 * q + rr;
-    f(row, c4, *reinterpret_cast<const float4*>(&E[row * 32 + 4 * c4]));
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // reads done before the next block
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <int MODE>
-__device__ __forceinline__ void column_params(const GemmArgs& a, int n, float& bias,
-                                              float& scale, float& shift) {
-  bias = 0.f;
-  scale = 1.f;
-  shift = 0.f;
-  if (MODE == MODE_FWD) {
-    if (a.bias) bias = a.bias[n];
-    if (a.bn_g) {
-      scale = a.bn_g[n] * rsqrtf(a.bn_v[n] + a.bn_eps);
-      shift = a.bn_b[n] - a.bn_m[n] * scale;
-    }
-  }
-}
-
+// (shared device helpers: conv_dev.h)
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
 __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -659,7 +443,6 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_f32(GemmArgs a) {
 //   * wave w stages k-octet w of every chunk: two channel quads, each with its own tap walk
 //     (kc need only be a multiple of 4);
 //   * packed weights are bf16 [n][k] (k contiguous, K padded to 32 per group).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int BKH = 32;                  // bf16 chunk
 constexpr int SROW16 = 5;                // LDS row stride in 16-byte units (40 bf16 = 80 B)
 
@@ -976,11 +759,6 @@ constexpr int TT_H = 8, TT_W = 16;   // wgrad halo tiles
 // 16-byte slots (5 p mod 16) are distinct in every 16-lane bank group.  An 8 x 16 tile puts
 // lanes 16-31 on the next halo row (18 px later) and collides in 2 of 16 slots per group
 // (SQ_LDS_BANK_CONFLICT was 40 % of the LDS cycles).
-#ifndef OF_TF_H
-#define OF_TF_H 4
-#define OF_TF_W 32
-#endif
-constexpr int TF_H = OF_TF_H, TF_W = OF_TF_W;
 #ifndef OF_X3_TH0
 #define OF_X3_TH0 8
 #endif
@@ -996,6 +774,13 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 // -6 %, enc.l4 -7 %; -DX3_BDMA=0 builds the register-staged form)
 #ifndef X3_BDMA
 #define X3_BDMA 1
+#endif
+// tile_x3_body's 16-byte epilogue: rows per epilogue_rows4 batch (1: one row per
+// epilogue_store4, the round-2 form)
+// (4 measured -0.3 % on the fp32 step and -1-4 % on dgrad per layer: the stores, not the aux
+// loads, bound that epilogue with one workgroup per CU)
+#ifndef X3_EPB
+#define X3_EPB 1
 #endif
 
 
@@ -1251,26 +1036,6 @@ __device__ __forceinline__ void split3x4(const float4& v, uint2& h, uint2& m, ui
 // base, and of the four such rows in a group two read octet q and two octet q ^ 1; the
 // swizzle alternates with bit 2 of the row, so the four land on q, q ^ 2, q ^ 1, q ^ 3.  (The
 // 80-byte padded rows that suit the 32 x 32 layout leave 3 of 16 slots 2-way in every group.)
-__device__ __forceinline__ int x3_sw(int p) { return ((p >> 2) & 1) << 1; }
-
-// One LDS-DMA wave-instruction (buffer_load_dwordx4 ... lds): lane L's 16 bytes at byte
-// offset voff + soff of r land at dst + 16 L (dst wave-uniform); out-of-range lanes write 0.
-__device__ __forceinline__ void dma16_to_lds(rsrc_t r, uint4* dst, uint32_t voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16,
-                                           voff, soff, 0, 0);
-}
-
-// 4 fp32 -> 4 bf16 (RNE, v_cvt_pk_bf16_f32), element 0 in the low half of .x
-__device__ __forceinline__ uint2 pack_bf16x4(const float4& v) {
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  bf16x4 r;
-  r[0] = (__bf16)v.x;
-  r[1] = (__bf16)v.y;
-  r[2] = (__bf16)v.z;
-  r[3] = (__bf16)v.w;
-  return __builtin_bit_cast(uint2, r);
-}
-
 // The halo-tiled 3x3 stride-1 body shared by the fp32 split kernel (NP = 3 planes: hi / mid /
 // lo, six MFMAs per fragment pair) and the bf16 one (NP = 1: activations rounded to bf16 RNE
 // while staged, the bf16 packed weights, one MFMA per fragment pair).
@@ -1544,14 +1309,34 @@ __device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const int n = n0 + wn0 + 16 * jp + 4 * c4;
+      if constexpr (X3_EPB > 1 && (WM / RPI) % X3_EPB == 0) {
+        // rows in batches of X3_EPB (epilogue_rows4: the aux loads ahead of the stores)
 #pragma unroll
-      for (int q = 0; q < WM / RPI; ++q) {
-        const int m = q * RPI + rr;
-        const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
-        const int mt = wm0 + m;
-        const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
-        if (oy < OH && ox < OW && n < a.N)
-          epilogue_store4<MODE>(a, split, img + (int64_t)oy * OW + ox, n, v);
+        for (int q0 = 0; q0 < WM / RPI; q0 += X3_EPB) {
+          float4 v[X3_EPB];
+          int64_t row[X3_EPB];
+          unsigned ok = 0;
+#pragma unroll
+          for (int g = 0; g < X3_EPB; ++g) {
+            const int m = (q0 + g) * RPI + rr;
+            v[g] = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
+            const int mt = wm0 + m;
+            const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
+            row[g] = img + (int64_t)oy * OW + ox;
+            ok |= (oy < OH && ox < OW && n < a.N ? 1u : 0u) << g;
+          }
+          epilogue_rows4<MODE, X3_EPB>(a, split, row, ok, n, v);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < WM / RPI; ++q) {
+          const int m = q * RPI + rr;
+          const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
+          const int mt = wm0 + m;
+          const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
+          if (oy < OH && ox < OW && n < a.N)
+            epilogue_store4<MODE>(a, split, img + (int64_t)oy * OW + ox, n, v);
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -4200,7 +3985,6 @@ static int g_wgx3_gemm = 1;
 // fwd even (564 vs 578 TFLOP/s at 8 x 32 x 128), dgrad BN 128 4 x 32 +8 %, weight gradient
 // 427 vs 449 TFLOP/s (Cout 128), 167 vs 364 (Cout 32): with one MFMA per fragment pair the
 // per-tap staging and barriers of that structure are no longer hidden.
-static int g_tile_b16 = 0;
 static int g_wgrad_b16 = 0;
 bool vec_ep_ok(const GemmArgs& a) {
   if (!g_vec_ep || a.N % 4) return false;
@@ -4288,8 +4072,16 @@ bool x3_nb1(const GemmArgs& a) {
   return a.bm != X3_TH0 * TF_W && a.splits == 1 && x3_nb1_candidate(a, false);
 }
 
+// conv_tile_ws: bf16 layers whose N tile is 128 or 96, forward and input gradient
+// (of_set_tuning key 12 = 2) or forward only (key 12 = 3).
+static int g_tile_b16 = 0;
+bool ws_ok(const of_conv_desc* d, int mode) {
+  const int N = mode == MODE_FWD ? d->cout : d->cin_p;
+  return (g_tile_b16 == 2 || (g_tile_b16 == 3 && mode == MODE_FWD)) && pick_bn(N) >= 96;
+}
+
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false,
-                   bool b16 = false) {
+                   bool b16 = false, bool ws = false) {
   GemmArgs a = base_args(d);
   const bool fwd = mode == MODE_FWD;
   a.kc = fwd ? g.cin_p : g.cout_p;
@@ -4297,8 +4089,9 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   a.nb = fwd ? d->cout : g.nd;
   a.ldb = fwd ? g.kf16 : (int)g.kd16;
   const int OH = fwd ? d->ho : d->h, OW = fwd ? d->wo : d->w;
-  // bf16: fwd only (8 x 32 tiles measured +5 % on dec3 fwd, -2 % on dgrad)
-  const bool tall = x3 || b16 ? x3_tall(d->n, OH, OW, a.N)
+  // bf16: fwd only (8 x 32 tiles measured +5 % on dec3 fwd, -2 % on dgrad); conv_tile_ws: always
+  const bool tall = ws ? true
+                  : x3 || b16 ? x3_tall(d->n, OH, OW, a.N)
                              : fwd && pick_bn(a.N) == 128 && x3_tall(d->n, OH, OW, a.N);
   const int th = tall ? X3_TH0 : TF_H;
   const int m_tiles = d->n * (int)cdiv(OH, th) * (int)cdiv(OW, TF_W);
@@ -4317,14 +4110,15 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   G.K = a.K;
   a.splits = 1;
   a.k_per_split = a.K;
-  if (x3 || b16) {
+  if (x3 || b16 || ws) {
     // One workgroup per CU (conv_tile_b16: two): choose the K split with the least modelled time, in units of one
     // chunk (9 taps): rounds of 256 workgroups x (chunks per slice + 1 for prologue and
     // epilogue), plus 0.5 per slice and tile round for the slab write and epilogue pass.
     // (Measured: enc.l3 384 tiles unsplit, dec1 192 tiles unsplit, enc.l4 96 tiles in 2.)
     // (The single-buffered BN = 128 4 x 32 configuration, used from X3_NB1_MIN tiles, runs
     // two workgroups per CU.)
-    const int slots = (b16 && !tall) || x3_nb1_candidate(a, tall) ? 2 * device_cus() : device_cus();
+    const int slots = !ws && ((b16 && !tall) || x3_nb1_candidate(a, tall)) ? 2 * device_cus()
+                                                                            : device_cus();
     int best = 1;
     double best_cost = 1e30;
     for (int sp = 1; sp <= std::min(8, a.K); ++sp) {
@@ -4411,6 +4205,17 @@ int launch_tile_b16(const GemmArgs& a, hipStream_t s, double flops) {
   else hipLaunchKernelGGL((conv_tile_b16<32, 4, 1, MODE, 4>), grid, dim3(256), 0, s, a);
   if (timing_on()) timing_end(s, 192 + MODE * 8 + cfg, flops);
   int st = check_launch("conv_tile_b16");
+  if (st || a.splits == 1) return st;
+  return launch_splitk_epilogue<MODE>(a, s);
+}
+
+// bf16 3x3 stride-1 fwd / dgrad on conv_tile_ws: timing kinds 224 + mode * 8 + cfg
+// (0: BN 128, 1: BN 96; 8 x 32 output tiles, 4 compute + 4 staging waves).
+template <int MODE>
+int launch_tile_ws(const GemmArgs& a, hipStream_t s, double flops) {
+  if (timing_on()) timing_begin(s);
+  int st = launch_tile_ws_kernel(a, MODE, s);
+  if (timing_on()) timing_end(s, 224 + MODE * 8 + (pick_bn(a.N) == 128 ? 0 : 1), flops);
   if (st || a.splits == 1) return st;
   return launch_splitk_epilogue<MODE>(a, s);
 }
@@ -4680,7 +4485,7 @@ int of_set_tuning(int key, int value) {
   if (key == 4 && value >= 0 && value <= 2) { g_wgx3b = value; return OF_OK; }
   if (key == 5 && (value == 1 || value == 2)) { g_wgx3b_mi = value; return OF_OK; }
   if (key == 6 && (value == 0 || value == 1)) { g_wgx3_gemm = value; return OF_OK; }
-  if (key == 12 && (value == 0 || value == 1)) { g_tile_b16 = value; return OF_OK; }
+  if (key == 12 && value >= 0 && value <= 3) { g_tile_b16 = value; return OF_OK; }
   if (key == 13 && (value == 0 || value == 1)) { g_wgrad_b16 = value; return OF_OK; }
   if (key == 14 && (value == 0 || value == 1)) { g_stem_wg = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
@@ -4749,13 +4554,15 @@ size_t of_conv2d_dgrad_workspace(const of_conv_desc* d) {
 
 size_t of_conv2d_fwd_bf16_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
-  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_FWD, false, g_tile_b16 != 0)
+  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_FWD, false, g_tile_b16 == 1,
+                                             ws_ok(d, MODE_FWD))
                                  : fwd_args(d, geo(d), true));
 }
 
 size_t of_conv2d_dgrad_bf16_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
-  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_DGRAD, false, g_tile_b16 != 0)
+  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_DGRAD, false, g_tile_b16 == 1,
+                                             ws_ok(d, MODE_DGRAD))
                                  : dgrad_args(d, geo(d), true));
 }
 
@@ -4792,8 +4599,9 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   }
   Geo g = geo(d);
   const bool tile = (bf16 || x3) && tile_ok(d);
-  const bool b16 = tile && bf16 && g_tile_b16;
-  GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3, b16) : fwd_args(d, g, bf16 || x3);
+  const bool ws = tile && bf16 && ws_ok(d, MODE_FWD);
+  const bool b16 = tile && bf16 && g_tile_b16 == 1;
+  GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3, b16, ws) : fwd_args(d, g, bf16 || x3);
   bool stem = x3 && !tile && g_stem_x3 && stem_x3_ok(d);
   if (stem) {                            // conv_stem_x3: one workgroup per output tile, no split
     a.splits = 1;
@@ -4846,6 +4654,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
     return check_launch("conv_stem_x3");
   }
   st = x3     ? (tile ? launch_tile_x3<MODE_FWD>(a, s, flops) : launch_gemm_x3<MODE_FWD>(a, s, flops))
+       : ws   ? launch_tile_ws<MODE_FWD>(a, s, flops)
        : b16  ? launch_tile_b16<MODE_FWD>(a, s, flops)
        : tile ? launch_tile_bf16<MODE_FWD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops)
@@ -4901,8 +4710,9 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   }
   const bool tile = (bf16 || x3) && tile_ok(d);
   const bool in_place = add && add == dx && ld_add == lddx;
-  const bool b16 = tile && bf16 && g_tile_b16;
-  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3, b16)
+  const bool ws = tile && bf16 && ws_ok(d, MODE_DGRAD);
+  const bool b16 = tile && bf16 && g_tile_b16 == 1;
+  GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3, b16, ws)
                     : dgrad_args(d, g, bf16 || x3, in_place);
   if (x3 && !tile) gemm_x3_plan(a);
   if (a.tiles_total == 0) return OF_OK;                 // every output already final
@@ -4929,6 +4739,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   a.vec_ep = vec_ep_ok(a);
   st = x3     ? (tile ? launch_tile_x3<MODE_DGRAD>(a, s, flops)
                      : launch_gemm_x3<MODE_DGRAD>(a, s, flops))
+       : ws   ? launch_tile_ws<MODE_DGRAD>(a, s, flops)
        : b16  ? launch_tile_b16<MODE_DGRAD>(a, s, flops)
        : tile ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops)

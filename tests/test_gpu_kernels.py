@@ -454,6 +454,70 @@ def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
 
 
 @pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
+    # kinds: 224 + 8 mode + cfg (cfg 0: BN 128, 1: BN 96; family tile_ws)
+    ("tall128", 8, 128, 256, 128, 128, {224, 232}),
+    ("tall96", 8, 128, 256, 128, 96, {225, 232}),
+    ("split", 2, 48, 64, 256, 256, {224, 232}),      # K split over channel chunks
+    ("ragged", 2, 41, 70, 128, 128, {224, 232}),     # partial tiles at the image border
+    ("c0", 2, 48, 64, 120, 96, {225, 232}),          # concat row: a partial channel chunk
+    ("single", 1, 8, 32, 32, 128, {224}),            # fwd one chunk: 9 steps (dgrad N 32: not ws)
+], ids=["tall128", "tall96", "split", "ragged", "c0", "single"])
+def test_conv_ws_forms(case, n, h, w, cin, cout, kinds):
+    """bf16 fwd / dgrad on the warp-specialised conv_tile_ws (of_set_tuning key 12 = 2)
+    against the round-1 conv_tile_bf16 (key 12 = 0) on the same inputs: both round x, dy and
+    the weights to bf16 RNE and accumulate in fp32, so they agree to accumulation-order noise;
+    the timing kinds name the configurations that ran.  test_conv_bf16 checks the default
+    kernels against the oracle."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_LEAKY, call
+    lib = _lib.lib()
+    x = dev(rng_tensor((n, h, w, cin), 61))
+    wt = dev(rng_tensor((3, 3, cin, cout), 62, scale=(2.0 / (9 * cin)) ** 0.5))
+    b = dev(rng_tensor((cout,), 63, scale=0.1))
+    dy = dev(rng_tensor((n, h, w, cout), 64))
+    act_src = dev(rng_tensor((n, h, w, cin), 65))
+    outs = {}
+    lib.of_timing_read(0, None, None, None)
+    try:
+        for form in (2, 0):
+            assert lib.of_set_tuning(12, form) == 0
+            lib.of_timing_enable(1 if form else 0)
+            layer = ops.ConvLayer(wt, b, stride=1, act=ACT_LEAKY, cin_p=cin, precision="bf16")
+            d = layer.desc(n, h, w)
+            assert layer.bf16(d)
+            wf, wd = layer.packed(d)
+            fent, fws = layer.fwd_entry(d)
+            dent, dws = layer.dgrad_entry(d)
+            if case == "split" and form:
+                assert fws > 0 and dws > 0, (fws, dws)
+            ws = torch.empty(max(fws, dws) // 4 + 4, device="cuda")
+            P, st = ops._ptr, ops._stream()
+            y = torch.empty(n, h, w, cout, device="cuda")
+            dx = torch.empty(n, h, w, cin, device="cuda")
+            call(fent, C.byref(d), P(x), cin, P(wf), P(b), None, None, None, None, 1e-3, None, 0,
+                 ACT_LEAKY, 0.3, None, 0, P(y), cout, P(ws), fws, st)
+            call(dent, C.byref(d), P(dy), cout, P(wd), P(act_src), cin, ACT_LEAKY, 0.3, P(dx),
+                 cin, P(ws), dws, st)
+            torch.cuda.synchronize()
+            if form:
+                lib.of_timing_enable(0)
+                cap = 64
+                k_arr, f_arr, m_arr = (C.c_int * cap)(), (C.c_double * cap)(), (C.c_float * cap)()
+                got = {k_arr[i] for i in range(lib.of_timing_read(cap, k_arr, f_arr, m_arr))}
+                assert kinds <= got, (kinds, got)
+            outs[form] = (y, dx)
+    finally:
+        lib.of_set_tuning(12, 0)                    # the default
+        lib.of_timing_enable(0)
+    for name, a1, a0 in zip(("y", "dx"), outs[2], outs[0]):
+        e = rel_l2(a1, a0)
+        print("%s %s rel_l2 %.2e rel_inf %.2e" % (case, name, e, rel_inf(a1, a0)))
+        assert e < 1e-5 and rel_inf(a1, a0) < 1e-4, name
+
+
+@pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
     # kinds: 192 + 8 mode + cfg (bench.py kind_parts, family tile_b16)
     ("tall128", 8, 128, 256, 128, 128, {192, 200, 216}),   # 8 x 32 tiles, BN 128 (1024 tiles)
     ("tall96", 8, 128, 256, 128, 96, {197, 200, 217}),     # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad

@@ -22,5 +22,5 @@ for s in optical_flow_amd/csrc/*.hip optical_flow_amd/csrc/*.cpp; do
   objs+=($o)
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/liboflow.so "${objs[@]}" -lz -lpthread
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/liboflow.so "${objs[@]}" -lz -lpthread -ldl
 echo $OUT/liboflow.so
