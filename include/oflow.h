@@ -253,6 +253,13 @@ int of_warp_fwd(const float* inp, int n, int h, int w, int c, const float* flow,
 /* dinp += scatter (atomics; caller zeroes or accumulates), dflow = d/d(flow) (written). */
 int of_warp_bwd(const float* dout, const float* inp, int n, int h, int w, int c,
                 const float* flow, float* dinp, float* dflow, void* stream);
+/* of_warp_bwd with d(flow) = dflow_add + d(warp)/d(flow): dflow_add (2 channels, row stride
+ * ld_add) is the gradient of the same flow through its other consumer -- in flow_module
+ * (model.py:93-102) flow_up feeds both warp_features and the concat, and this sums the concat
+ * slice in the store instead of a separate add pass (the same fp32 sum). */
+int of_warp_bwd_add(const float* dout, const float* inp, int n, int h, int w, int c,
+                    const float* flow, float* dinp, float* dflow, const float* dflow_add,
+                    int ld_add, void* stream);
 /* bilinear_interpolation(input, sampling_points) (transformations.py:85-129): the same sampler
  * with absolute (x, y) points instead of grid + flow. */
 int of_bilinear_fwd(const float* inp, int n, int h, int w, int c, const float* pts, float* out,
@@ -266,6 +273,9 @@ int of_upscale2x_fwd(const float* in, int n, int h, int w, int c, float scale, f
                      int ldo, void* stream);
 int of_upscale2x_bwd(const float* dout, int lddo, int n, int h, int w, int c, float scale,
                      float* din, int accumulate, void* stream);
+/* of_upscale2x_bwd into din with row stride lddi (the flow head's channel-padded gradient). */
+int of_upscale2x_bwd_ld(const float* dout, int lddo, int n, int h, int w, int c, float scale,
+                        float* din, int lddi, int accumulate, void* stream);
 
 /* Image pyramid of LossLayer (loss.py:17-18): for s=1..levels, out_s = resize(batch, H/2^s,
  * W/2^s) (half-pixel bilinear, no antialias == mean of 2x2 taps); each out_s dense 6-ch. */
@@ -285,6 +295,9 @@ int of_photo_l1_fwd(const float* img6, const float* flow, int n, int h, int w,
  * on the device, 1 if dloss == NULL); dflow written (ld 2). */
 int of_photo_l1_bwd(const float* img6, const float* flow, int n, int h, int w, float coef,
                     const float* dloss, float* dflow, void* stream);
+/* of_photo_l1_bwd writing d(flow) with row stride lddf (>= 2). */
+int of_photo_l1_bwd_ld(const float* img6, const float* flow, int n, int h, int w, float coef,
+                       const float* dloss, float* dflow, int lddf, void* stream);
 /* out[0] = sum_i coef_j * partials_j[i] over `count` groups (deterministic). */
 int of_sum_partials(const float* const* parts, const int* counts, const float* coefs,
                     int ngroups, float* out, void* stream);

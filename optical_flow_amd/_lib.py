@@ -86,15 +86,18 @@ PROTOTYPES = {
     "of_corr_concat_bwd": (I, [P, I, P, P, I, I, I, I, I, P, P, P, P]),
     "of_warp_fwd": (I, [P, I, I, I, I, P, P, P]),
     "of_warp_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
+    "of_warp_bwd_add": (I, [P, P, I, I, I, I, P, P, P, P, I, P]),
     "of_bilinear_fwd": (I, [P, I, I, I, I, P, P, P]),
     "of_bilinear_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
     "of_upscale2x_fwd": (I, [P, I, I, I, I, F, P, I, P]),
     "of_upscale2x_bwd": (I, [P, I, I, I, I, I, F, P, I, P]),
+    "of_upscale2x_bwd_ld": (I, [P, I, I, I, I, I, F, P, I, I, P]),
     "of_pyramid6": (I, [P, I, I, I, I, C.POINTER(P), P]),
     "of_split_pair": (I, [P, I, I, I, P, P]),
     "of_photo_l1_partials": (I, [I, I, I]),
     "of_photo_l1_fwd": (I, [P, P, I, I, I, P, P]),
     "of_photo_l1_bwd": (I, [P, P, I, I, I, F, P, P, P]),
+    "of_photo_l1_bwd_ld": (I, [P, P, I, I, I, F, P, P, I, P]),
     "of_sum_partials": (I, [C.POINTER(P), C.POINTER(I), C.POINTER(F), I, P, P]),
     "of_adam_keras": (I, [P, P, P, P, I64, F, F, F, F, F, P]),
     "of_adam_keras_dev": (I, [P, P, P, P, I64, P, P, F, F, F, F, P]),

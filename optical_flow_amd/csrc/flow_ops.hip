@@ -785,7 +785,8 @@ __global__ __launch_bounds__(256) void warp_bwd_wave(const float* __restrict__ d
                                                      int h, int w, int c,
                                                      const float* __restrict__ flow,
                                                      float* __restrict__ dinp,
-                                                     float* __restrict__ dflow, int absolute) {
+                                                     float* __restrict__ dflow, int absolute,
+                                                     const float* __restrict__ dfa, int ldfa) {
   const int64_t npix = (int64_t)n * h * w;
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -819,7 +820,13 @@ __global__ __launch_bounds__(256) void warp_bwd_wave(const float* __restrict__ d
       gx += __shfl_xor(gx, o, 64);
       gy += __shfl_xor(gy, o, 64);
     }
-    if (lane == 0) *reinterpret_cast<float2*>(dflow + 2 * p) = make_float2(gx, gy);
+    if (lane == 0) {
+      if (dfa) {
+        gx = dfa[p * ldfa] + gx;
+        gy = dfa[p * ldfa + 1] + gy;
+      }
+      *reinterpret_cast<float2*>(dflow + 2 * p) = make_float2(gx, gy);
+    }
   }
 }
 
@@ -842,7 +849,8 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
                                                     int w, int c,
                                                     const float* __restrict__ flow,
                                                     float* __restrict__ dinp,
-                                                    float* __restrict__ dflow) {
+                                                    float* __restrict__ dflow,
+                                                    const float* __restrict__ dfa, int ldfa) {
   __shared__ float data[WH_SLOTS * 64];
   __shared__ int tag[WH_SLOTS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -910,8 +918,12 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
       }
       if (lane == 0) {
         if (passes == 1) {
+          if (dfa) {
+            gx = dfa[p * ldfa] + gx;
+            gy = dfa[p * ldfa + 1] + gy;
+          }
           *reinterpret_cast<float2*>(dflow + 2 * p) = make_float2(gx, gy);
-        } else {                                       // dflow zeroed by the launcher
+        } else {                                       // dflow preset by the launcher
           atomicAdd(dflow + 2 * p, gx);
           atomicAdd(dflow + 2 * p + 1, gy);
         }
@@ -958,7 +970,8 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
                                                          int h, int w, int c,
                                                          const float* __restrict__ flow,
                                                          float* __restrict__ dinp,
-                                                         float* __restrict__ dflow) {
+                                                         float* __restrict__ dflow,
+                                                         const float* __restrict__ dfa, int ldfa) {
   constexpr int NP = WG_T * WG_T;                       // 64 pixels, 256 (pixel, corner) entries
   __shared__ float dtile[NP * 64];                     // dout rows of this pass
   __shared__ int2 ent[NP * 4];                         // entries sorted by destination
@@ -1123,8 +1136,12 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
     gy = row16_sum(gy);
     if (q == 0 && okg[it]) {
       if (passes == 1) {
+        if (dfa) {
+          gx = dfa[(int64_t)pixg[it] * ldfa] + gx;
+          gy = dfa[(int64_t)pixg[it] * ldfa + 1] + gy;
+        }
         *reinterpret_cast<float2*>(dflow + 2 * pixg[it]) = make_float2(gx, gy);
-      } else {                                         // dflow zeroed by the launcher
+      } else {                                         // dflow preset by the launcher
         atomicAdd(dflow + 2 * pixg[it], gx);
         atomicAdd(dflow + 2 * pixg[it] + 1, gy);
       }
@@ -1137,7 +1154,8 @@ __global__ __launch_bounds__(256) void warp_bwd_scalar(const float* __restrict__
                                                        int h, int w, int c,
                                                        const float* __restrict__ flow,
                                                        float* __restrict__ dinp,
-                                                       float* __restrict__ dflow, int absolute) {
+                                                       float* __restrict__ dflow, int absolute,
+                                                       const float* __restrict__ dfa, int ldfa) {
   const int64_t total = (int64_t)n * h * w;
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total;
        p += (int64_t)gridDim.x * blockDim.x) {
@@ -1161,8 +1179,8 @@ __global__ __launch_bounds__(256) void warp_bwd_scalar(const float* __restrict__
         atomicAdd(dinp + t.o11 * c + e, (1.f - a) * (1.f - b) * g);
       }
     }
-    dflow[2 * p] = gx;
-    dflow[2 * p + 1] = gy;
+    dflow[2 * p] = dfa ? dfa[p * ldfa] + gx : gx;
+    dflow[2 * p + 1] = dfa ? dfa[p * ldfa + 1] + gy : gy;
   }
 }
 
@@ -1226,7 +1244,8 @@ __device__ __forceinline__ int up_taps(int t, int h, int* Ys, float* ws) {
 __global__ __launch_bounds__(256) void upscale2x_bwd_kernel(const float* __restrict__ dout,
                                                             int lddo, int n, int h, int w,
                                                             int c, float scale,
-                                                            float* __restrict__ din, int accum) {
+                                                            float* __restrict__ din, int accum,
+                                                            int lddi) {
   const int H = 2 * h, W = 2 * w;
   const int64_t total = (int64_t)n * h * w * c;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
@@ -1249,7 +1268,8 @@ __global__ __launch_bounds__(256) void upscale2x_bwd_kernel(const float* __restr
       s += wy[u] * r;
     }
     s *= scale;
-    din[idx] = accum ? din[idx] + s : s;
+    const int64_t o = p * lddi + e;
+    din[o] = accum ? din[o] + s : s;
   }
 }
 
@@ -1351,7 +1371,7 @@ __global__ __launch_bounds__(256) void photo_l1_bwd_kernel(const float* __restri
                                                            const float* __restrict__ flow, int n,
                                                            int h, int w, float coef,
                                                            const float* __restrict__ dloss,
-                                                           float* __restrict__ dflow) {
+                                                           float* __restrict__ dflow, int lddf) {
   const int64_t npix = (int64_t)n * h * w;
   if (dloss) coef *= dloss[0];
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix;
@@ -1373,8 +1393,8 @@ __global__ __launch_bounds__(256) void photo_l1_bwd_kernel(const float* __restri
       gx -= g * (b * (v[0][e] - v[2][e]) + (1.f - b) * (v[1][e] - v[3][e]));
       gy -= g * (a * (v[0][e] - v[1][e]) + (1.f - a) * (v[2][e] - v[3][e]));
     }
-    dflow[2 * p] = gx;
-    dflow[2 * p + 1] = gy;
+    dflow[lddf * p] = gx;
+    dflow[lddf * p + 1] = gy;
   }
 }
 
@@ -1618,35 +1638,44 @@ int of_bilinear_fwd(const float* inp, int n, int h, int w, int c, const float* p
   return warp_fwd_impl(inp, n, h, w, c, pts, out, 1, stream);
 }
 
+// dfa (row stride ldfa, 2 channels), when given, is added to d(flow): the gradient of the flow
+// through its other consumer (the concat's flow slice), so no separate add pass runs.
 static int warp_bwd_impl(const float* dout, const float* inp, int n, int h, int w, int c,
                          const float* flow, float* dinp, float* dflow, int absolute,
-                         void* stream) {
+                         void* stream, const float* dfa = nullptr, int ldfa = 0) {
   OF_CHECK_ARG(dout && inp && flow && dflow, "warp bwd: NULL pointer");
+  OF_CHECK_ARG(!dfa || ldfa >= 2, "warp bwd: ld of the added flow gradient");
   hipStream_t s = as_stream(stream);
   const int64_t npix = (int64_t)n * h * w;
   if (!absolute && c % 64 == 0 && (int64_t)h * w < INT32_MAX) {
-    if (c > 64 && hipMemsetAsync(dflow, 0, (size_t)npix * 2 * sizeof(float), s) != hipSuccess)
-      return check_launch("warp_bwd: dflow memset");
+    if (c > 64) {     // several 64-channel passes add their d(flow) atomically: preset it
+      if (dfa) {
+        const int st = of_copy_strided(dfa, ldfa, dflow, 2, npix, 2, stream);
+        if (st) return st;
+      } else if (hipMemsetAsync(dflow, 0, (size_t)npix * 2 * sizeof(float), s) != hipSuccess) {
+        return check_launch("warp_bwd: dflow memset");
+      }
+    }
     if (g_warp_win) {
       const int64_t blocks =
           (int64_t)n * ((h + WG_T - 1) / WG_T) * ((w + WG_T - 1) / WG_T) * (c / 64);
       OF_CHECK_ARG(blocks < INT32_MAX, "warp bwd: too many tiles");
       hipLaunchKernelGGL(warp_bwd_gather, dim3((unsigned)blocks), dim3(WG_NT), 0, s, dout,
-                         inp, n, h, w, c, flow, dinp, dflow);
+                         inp, n, h, w, c, flow, dinp, dflow, c == 64 ? dfa : nullptr, ldfa);
     } else {
       const int64_t blocks =
           (int64_t)n * ((h + WH_T - 1) / WH_T) * ((w + WH_T - 1) / WH_T) * (c / 64);
       OF_CHECK_ARG(blocks < INT32_MAX, "warp bwd: too many tiles");
       hipLaunchKernelGGL(warp_bwd_agg, dim3((unsigned)blocks), dim3(64 * WH_WAVES), 0, s, dout,
-                         inp, n, h, w, c, flow, dinp, dflow);
+                         inp, n, h, w, c, flow, dinp, dflow, c == 64 ? dfa : nullptr, ldfa);
     }
   } else if (c >= 16) {
     const int g = grid_for(npix * 64, 256, 16384);
     hipLaunchKernelGGL(warp_bwd_wave, dim3(g), dim3(256), 0, s, dout, inp, n, h, w, c, flow,
-                       dinp, dflow, absolute);
+                       dinp, dflow, absolute, dfa, ldfa);
   } else {
     hipLaunchKernelGGL(warp_bwd_scalar, dim3(grid_for(npix)), dim3(256), 0, s, dout, inp, n, h,
-                       w, c, flow, dinp, dflow, absolute);
+                       w, c, flow, dinp, dflow, absolute, dfa, ldfa);
   }
   return check_launch("warp_bwd");
 }
@@ -1654,6 +1683,13 @@ static int warp_bwd_impl(const float* dout, const float* inp, int n, int h, int 
 int of_warp_bwd(const float* dout, const float* inp, int n, int h, int w, int c,
                 const float* flow, float* dinp, float* dflow, void* stream) {
   return warp_bwd_impl(dout, inp, n, h, w, c, flow, dinp, dflow, 0, stream);
+}
+
+int of_warp_bwd_add(const float* dout, const float* inp, int n, int h, int w, int c,
+                    const float* flow, float* dinp, float* dflow, const float* dflow_add,
+                    int ld_add, void* stream) {
+  OF_CHECK_ARG(dflow_add, "warp bwd add: NULL dflow_add");
+  return warp_bwd_impl(dout, inp, n, h, w, c, flow, dinp, dflow, 0, stream, dflow_add, ld_add);
 }
 
 int of_bilinear_bwd(const float* dout, const float* inp, int n, int h, int w, int c,
@@ -1670,13 +1706,18 @@ int of_upscale2x_fwd(const float* in, int n, int h, int w, int c, float scale, f
   return check_launch("upscale2x_fwd");
 }
 
-int of_upscale2x_bwd(const float* dout, int lddo, int n, int h, int w, int c, float scale,
-                     float* din, int accumulate, void* stream) {
-  OF_CHECK_ARG(dout && din && lddo >= c, "upscale bwd: args");
+int of_upscale2x_bwd_ld(const float* dout, int lddo, int n, int h, int w, int c, float scale,
+                        float* din, int lddi, int accumulate, void* stream) {
+  OF_CHECK_ARG(dout && din && lddo >= c && lddi >= c, "upscale bwd: args");
   const int64_t total = (int64_t)n * h * w * c;
   hipLaunchKernelGGL(upscale2x_bwd_kernel, dim3(grid_for(total)), dim3(256), 0,
-                     as_stream(stream), dout, lddo, n, h, w, c, scale, din, accumulate);
+                     as_stream(stream), dout, lddo, n, h, w, c, scale, din, accumulate, lddi);
   return check_launch("upscale2x_bwd");
+}
+
+int of_upscale2x_bwd(const float* dout, int lddo, int n, int h, int w, int c, float scale,
+                     float* din, int accumulate, void* stream) {
+  return of_upscale2x_bwd_ld(dout, lddo, n, h, w, c, scale, din, c, accumulate, stream);
 }
 
 int of_pyramid6(const float* batch, int n, int h, int w, int levels, float* const* outs,
@@ -1715,12 +1756,17 @@ int of_photo_l1_fwd(const float* img6, const float* flow, int n, int h, int w, f
   return check_launch("photo_l1_fwd");
 }
 
+int of_photo_l1_bwd_ld(const float* img6, const float* flow, int n, int h, int w, float coef,
+                       const float* dloss, float* dflow, int lddf, void* stream) {
+  OF_CHECK_ARG(img6 && flow && dflow && lddf >= 2, "photo l1 bwd: args");
+  hipLaunchKernelGGL(photo_l1_bwd_kernel, dim3(grid_for((int64_t)n * h * w)), dim3(256), 0,
+                     as_stream(stream), img6, flow, n, h, w, coef, dloss, dflow, lddf);
+  return check_launch("photo_l1_bwd");
+}
+
 int of_photo_l1_bwd(const float* img6, const float* flow, int n, int h, int w, float coef,
                     const float* dloss, float* dflow, void* stream) {
-  OF_CHECK_ARG(img6 && flow && dflow, "photo l1 bwd: NULL pointer");
-  hipLaunchKernelGGL(photo_l1_bwd_kernel, dim3(grid_for((int64_t)n * h * w)), dim3(256), 0,
-                     as_stream(stream), img6, flow, n, h, w, coef, dloss, dflow);
-  return check_launch("photo_l1_bwd");
+  return of_photo_l1_bwd_ld(img6, flow, n, h, w, coef, dloss, dflow, 2, stream);
 }
 
 int of_sum_partials(const float* const* parts, const int* counts, const float* coefs,

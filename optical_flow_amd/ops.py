@@ -819,7 +819,8 @@ class _ConvStackFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, *args):
-        layers = args[-1]
+        layers, ctx.fg = args[-1], args[-2]
+        args = args[:-1]
         n = len(layers)
         _check_dev(x)
         x = x.contiguous()
@@ -853,7 +854,21 @@ class _ConvStackFn(torch.autograd.Function):
         s = _stream()
         n = len(layers)
         needs = ctx.needs_input_grad
-        g = _pad_channels(dy.contiguous(), _c4(layers[-1].cout))
+        fg = ctx.fg
+        if (fg is not None and fg.filled and dy.data_ptr() == fg.buffer().data_ptr() and
+                dy.stride()[-2] == 4):
+            g = fg.buffer()                 # loss (+ upscale) gradient, already padded
+            fg.filled = fg.added = False
+        else:
+            if fg is not None and fg.added:
+                # autograd summed the loss gradient with a further consumer's before the
+                # upscale backward added its part into the buffer: that part is not in dy
+                raise RuntimeError("flow gradient routing: this flow has consumers besides the "
+                                   "photometric loss and upscale_flow; run with "
+                                   "OFLOW_FLOW_GRAD_ROUTING=0")
+            if fg is not None:
+                fg.filled = False
+            g = _pad_channels(dy.contiguous(), _c4(layers[-1].cout))
         if layers[-1].act != ACT_NONE:
             gz = torch.empty_like(g)
             y = _pad_channels(acts[-1], g.shape[-1])
@@ -901,7 +916,7 @@ class _ConvStackFn(torch.autograd.Function):
         for layer in layers:
             rets += list(layer._ret)
             layer._ret = None
-        return (dx, *rets, None)
+        return (dx, *rets, None, None)
 
 
 def wgrad_stack(layer, x, g, d, tk, tb):
@@ -916,11 +931,21 @@ def wgrad_stack(layer, x, g, d, tk, tb):
              _ptr(tb[0]), tk[1], _ptr(ws), wsb, _stream())
 
 
+FLOW_GRAD_ROUTING = os.environ.get("OFLOW_FLOW_GRAD_ROUTING", "1") == "1"
+
+
 def conv_stack(x, layers):
     flat = []
     for layer in layers:
         flat += [layer.kernel, layer.bias]
-    return _ConvStackFn.apply(x, *flat, list(layers))
+    fg = None
+    if FLOW_GRAD_ROUTING and layers[-1].cout == 2 and x.is_cuda:     # a flow head (model.py:114)
+        n, h, w, _ = x.shape
+        fg = FlowGrad((n, h, w, 2), x.device)
+    out = _ConvStackFn.apply(x, *flat, fg, list(layers))
+    if fg is not None:
+        out._of_flowgrad = fg
+    return out
 
 
 # ========================================================================= max pool ====
@@ -992,8 +1017,9 @@ class _CorrConcat(torch.autograd.Function):
     as the initial value of df1 (no copy or concat passes)."""
 
     @staticmethod
-    def forward(ctx, f1, f2w, flow_up, max_disp, cp):
+    def forward(ctx, f1, f2w, flow_up, max_disp, cp, fa):
         _check_dev(f1, f2w, flow_up)
+        ctx.fa = fa
         f1, f2w = f1.contiguous(), f2w.contiguous()
         n, h, w, c = f1.shape
         nk = (2 * max_disp + 1) ** 2
@@ -1018,7 +1044,11 @@ class _CorrConcat(torch.autograd.Function):
         df1 = new_grad(ctx.dst[0], f1)
         df2 = new_grad(ctx.dst[1], f2w) if ctx.needs_input_grad[1] else None
         dflow = None
-        if has_flow and ctx.needs_input_grad[2]:
+        defer = (has_flow and ctx.needs_input_grad[2] and ctx.fa is not None and
+                 ctx.fa.warp_flow_grad)
+        if defer:                      # the warp backward adds this slice (FlowAdd)
+            ctx.fa.addend = (dx, c + nk, cp)
+        elif has_flow and ctx.needs_input_grad[2]:
             dflow = torch.empty((n, h, w, 2), device=dx.device)
         if CORR_DF1_SIDE and dx.is_cuda and _in_slab(ctx.dst[0], df1):
             # df1 lands in the encoder output's gradient slab: its only reader is the encoder
@@ -1034,14 +1064,15 @@ class _CorrConcat(torch.autograd.Function):
             with torch.cuda.stream(corr_side_stream(dx, f1, f2w, df1)):
                 call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c,
                      max_disp, _ptr(df1), None, None, _stream())
-            return df1, df2, dflow, None, None
+            return df1, df2, dflow, None, None, None
         call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c, max_disp,
              _ptr(df1), _ptr(df2), _ptr(dflow), _stream())
-        return df1, df2, dflow, None, None
+        return df1, df2, dflow, None, None, None
 
 
 def corr_concat(f1, f2w, flow_up, max_disp, cp):
-    return _CorrConcat.apply(f1, f2w, flow_up, max_disp, cp)
+    fa = getattr(flow_up, "_of_flowadd", None) if flow_up is not None else None
+    return _CorrConcat.apply(f1, f2w, flow_up, max_disp, cp, fa)
 
 
 # ============================================================================ warp =====
@@ -1049,8 +1080,11 @@ class _Warp(torch.autograd.Function):
     """warp_features (model.py:55-73) / bilinear_interpolation (transformations.py:85-129)."""
 
     @staticmethod
-    def forward(ctx, inp, flow, absolute):
+    def forward(ctx, inp, flow, absolute, fa=None):
         _check_dev(inp, flow)
+        ctx.fa = fa
+        if fa is not None and flow.requires_grad:
+            fa.warp_flow_grad = True
         inp, flow = inp.contiguous(), flow.contiguous()
         n, h, w, c = inp.shape
         assert flow.shape == (n, h, w, 2), "flow must be (B, h, w, 2) like features"
@@ -1073,13 +1107,20 @@ class _Warp(torch.autograd.Function):
             dinp = new_grad(ctx.dst, inp)
             call("of_fill", _ptr(dinp), 0.0, dinp.numel(), s)
         dflow = torch.empty_like(flow)
-        call("of_bilinear_bwd" if ctx.absolute else "of_warp_bwd", _ptr(dout), _ptr(inp), n, h,
-             w, c, _ptr(flow), _ptr(dinp), _ptr(dflow), s)
-        return dinp, (dflow if ctx.needs_input_grad[1] else None), None
+        fa = ctx.fa
+        if fa is not None and fa.addend is not None and ctx.needs_input_grad[1]:
+            dcat, off, ld = fa.addend            # the concat's flow slice (FlowAdd)
+            call("of_warp_bwd_add", _ptr(dout), _ptr(inp), n, h, w, c, _ptr(flow), _ptr(dinp),
+                 _ptr(dflow), C.c_void_p(dcat.data_ptr() + 4 * off), ld, s)
+            fa.addend = None
+        else:
+            call("of_bilinear_bwd" if ctx.absolute else "of_warp_bwd", _ptr(dout), _ptr(inp), n,
+                 h, w, c, _ptr(flow), _ptr(dinp), _ptr(dflow), s)
+        return dinp, (dflow if ctx.needs_input_grad[1] else None), None, None
 
 
 def warp(inp, flow):
-    return _Warp.apply(inp, flow, False)
+    return _Warp.apply(inp, flow, False, getattr(flow, "_of_flowadd", None))
 
 
 def bilinear(inp, points):
@@ -1091,8 +1132,9 @@ class _Upscale2x(torch.autograd.Function):
     """upscale_flow (model.py:76-77): resize x2 (half-pixel bilinear) times 2.0."""
 
     @staticmethod
-    def forward(ctx, x, scale):
+    def forward(ctx, x, scale, fg=None):
         _check_dev(x)
+        ctx.fg = fg
         x = x.contiguous()
         n, h, w, c = x.shape
         out = torch.empty((n, 2 * h, 2 * w, c), device=x.device)
@@ -1105,13 +1147,23 @@ class _Upscale2x(torch.autograd.Function):
     def backward(ctx, dout):
         n, h, w, c = ctx.shape
         dout = dout.contiguous()
+        fg = ctx.fg
+        if fg is not None and fg.filled and c == 2:
+            # add into the loss gradient of the same flow (FlowGrad); autograd gets None
+            call("of_upscale2x_bwd_ld", _ptr(dout), c, n, h, w, c, ctx.scale, _ptr(fg.buffer()),
+                 4, 1, _stream())
+            fg.added = True
+            return None, None, None
         dx = torch.empty((n, h, w, c), device=dout.device)
         call("of_upscale2x_bwd", _ptr(dout), c, n, h, w, c, ctx.scale, _ptr(dx), 0, _stream())
-        return dx, None
+        return dx, None, None
 
 
 def upscale2x(x, scale=2.0):
-    return _Upscale2x.apply(x, scale)
+    out = _Upscale2x.apply(x, scale, getattr(x, "_of_flowgrad", None))
+    if FLOW_GRAD_ROUTING and out.requires_grad:
+        out._of_flowadd = FlowAdd()
+    return out
 
 
 # ================================================================= Siamese batching ====
@@ -1170,6 +1222,41 @@ def new_grad(dst, like):
     return torch.empty_like(like)
 
 
+class FlowGrad:
+    """Gradient routing for a flow head's output flow (B, h, w, 2) (model.py:114), whose
+    consumers are the photometric loss (loss.py:20-30) and, for the coarser levels,
+    upscale_flow (model.py:76-77).  The loss backward writes d(flow) into a channel-padded
+    (B, h, w, 4) buffer (channels 2-3 stay zero) and returns a view of it; the upscale
+    backward, which autograd runs afterwards, adds its input gradient into the same buffer
+    and returns None; the flow head's backward then reads the buffer as its padded dy.  This
+    replaces autograd's add pass and the channel-padding fill + copy per level.  The buffers
+    are cached per (device, shape): stream order protects their reuse across steps."""
+    _cache = {}
+
+    def __init__(self, shape, device):
+        self.shape, self.device = tuple(shape), device
+        self.filled = False             # the loss backward wrote the buffer this backward
+        self.added = False              # the upscale backward added into it
+
+    def buffer(self):
+        key = (str(self.device), self.shape)
+        b = FlowGrad._cache.get(key)
+        if b is None:
+            b = FlowGrad._cache[key] = torch.zeros(self.shape[:3] + (4,), device=self.device)
+        return b
+
+
+class FlowAdd:
+    """Gradient routing for an upscaled flow (flow_up, model.py:91-102) that feeds both
+    warp_features and the concat: the concat backward (autograd runs it first) leaves its
+    flow-slice gradient here instead of returning it, and the warp backward adds it in its
+    d(flow) store (of_warp_bwd_add) -- the same fp32 sum without autograd's add pass."""
+
+    def __init__(self):
+        self.warp_flow_grad = False     # a warp of this flow computes d(flow)
+        self.addend = None              # (concat gradient tensor, channel offset, row stride)
+
+
 class _Halves(torch.autograd.Function):
     """Split a (2B, ...) Siamese activation into its two (B, ...) halves; the backward returns
     the GradSlab both halves' gradients were written into (no copies when the consumers used
@@ -1224,8 +1311,9 @@ class _PhotoLoss(torch.autograd.Function):
     scale directly (the images are constants)."""
 
     @staticmethod
-    def forward(ctx, batch_imgs, *flows):
+    def forward(ctx, batch_imgs, fgs, *flows):
         _check_dev(batch_imgs, *flows)
+        ctx.fgs = fgs
         b = batch_imgs.contiguous()
         n, H, W, c = b.shape
         assert c == 6
@@ -1269,15 +1357,26 @@ class _PhotoLoss(torch.autograd.Function):
         grads = []
         for k in range(ns):
             n, h, w, _ = pyr[k].shape
-            if not ctx.needs_input_grad[1 + k]:
+            if not ctx.needs_input_grad[2 + k]:
                 grads.append(None)
+                continue
+            fg = ctx.fgs[k]
+            if fg is not None:         # into the flow head's padded gradient (FlowGrad)
+                buf = fg.buffer()
+                call("of_photo_l1_bwd_ld", _ptr(pyr[k]), _ptr(flows[k]), n, h, w, ctx.coefs[k],
+                     _ptr(dloss), _ptr(buf), 4, s)
+                fg.filled = True
+                grads.append(buf[..., :2])
                 continue
             df = torch.empty_like(flows[k])
             call("of_photo_l1_bwd", _ptr(pyr[k]), _ptr(flows[k]), n, h, w, ctx.coefs[k],
                  _ptr(dloss), _ptr(df), s)
             grads.append(df)
-        return (None, *grads)
+        return (None, None, *grads)
 
 
 def photometric_loss(batch_imgs, flows):
-    return _PhotoLoss.apply(batch_imgs, *flows)
+    fgs = [getattr(f, "_of_flowgrad", None) for f in flows]
+    if any(fg is not None and fg.shape != tuple(f.shape) for fg, f in zip(fgs, flows)):
+        fgs = [None] * len(flows)
+    return _PhotoLoss.apply(batch_imgs, fgs, *flows)

@@ -10,3 +10,4 @@ for r in 1 2; do for t in 0 3 2; do
   timeout -k 10 300 python bench.py --precision bf16 --batch 32 --steps 15 --warmup 3 --no-cpu-baseline --tune 12=$t > "$OUT/b_${t}_${r}.log" 2>&1 || { tail -3 "$OUT/b_${t}_${r}.log"; exit 1; }
   echo "round $r tune 12=$t $(grep -o '"value": [0-9.]*' $OUT/b_${t}_${r}.log)"
 done; done
+timeout -k 10 200 python tools/host_time.py --steps 10 2>&1 | grep -v amdgpu.ids | tail -5
