@@ -57,6 +57,12 @@ def kind_parts(kind):
         return 0, 0, "stem_x3"
     if kind == KIND_STEM_WG_X3:
         return 2, 0, "stem_x3"
+    if kind == KIND_STEM_B16:
+        return 0, 0, "stem_b16"
+    if kind == KIND_STEM_WG_B16:
+        return 2, 0, "stem_b16"
+    if kind >= 240:                               # conv_gemm_x3 / conv_wgrad_x3, one plane (bf16)
+        return (kind - 240) // 8, (kind - 240) % 8, "gemm_b16"
     if kind >= 224:                               # conv_tile_ws (warp-specialised bf16 3x3)
         return (kind - 224) // 8, (kind - 224) % 8, "tile_ws"
     if kind >= 216:                               # conv_wgrad_tile_b16 (x3b configs, 1 plane)
@@ -106,22 +112,26 @@ def conv_math(precision):
 
 KIND_STEM_X3 = 184   # conv_stem_x3 (the 7x7 stride-2 stem forward on the split-bf16 MFMA)
 KIND_STEM_WG_X3 = 185   # conv_wgrad_stem_x3 (its weight gradient)
+KIND_STEM_B16 = 186     # conv_stem_x3<32, 1> (the bf16 stem forward, one plane)
+KIND_STEM_WG_B16 = 187  # conv_wgrad_stem_x3<1> (its bf16 weight gradient)
 
 
 def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
     if fam == "stem_x3":
         return "wgrad_stem_x3" if mode == 2 else "fwd_stem_x3"
+    if fam == "stem_b16":
+        return "wgrad_stem_b16" if mode == 2 else "fwd_stem_b16"
     sfx = {"f32": "", "bf16": "_bf16", "tile_bf16": "_tile_bf16", "tile_f32": "_tile_f32",
            "tile_x3": "_tile_x3", "gemm_x3": "_gemm_x3", "tile_b16": "_tile_b16",
-           "wgrad_b16": "", "tile_ws": "_tile_ws"}[fam]
+           "wgrad_b16": "", "tile_ws": "_tile_ws", "gemm_b16": "_gemm_b16"}[fam]
     if fam == "tile_ws":
         return "%s%s<%s>" % (MODE_NAMES[mode], sfx, WS_BN[cfg])
     if fam == "tile_b16":
         return "%s%s<%s, %d>" % (MODE_NAMES[mode], sfx, X3_BN[cfg], X3_TH[cfg])
     if fam == "wgrad_b16":
         return "wgrad_tile_b16<%s>" % B16_WGT[cfg]
-    if fam == "gemm_x3":
+    if fam in ("gemm_x3", "gemm_b16"):
         return "%s%s<%s>" % (MODE_NAMES[mode], sfx, (GX3_WG if mode == 2 else GX3)[cfg])
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
         if fam == "tile_x3" and cfg >= 4:
@@ -138,8 +148,12 @@ def kernel_symbol(kind):
     mode, cfg, fam = kind_parts(kind)
     if fam == "stem_x3":
         if mode == 2:
-            return "oflow::conv_wgrad_stem_x3(oflow::GemmArgs)"
-        return "void oflow::conv_stem_x3<32>(oflow::GemmArgs)"   # of_set_tuning key 8 default
+            return "void oflow::conv_wgrad_stem_x3<3>(oflow::GemmArgs)"
+        return "void oflow::conv_stem_x3<32, 3>(oflow::GemmArgs)"   # of_set_tuning key 8 default
+    if fam == "stem_b16":
+        if mode == 2:
+            return "void oflow::conv_wgrad_stem_x3<1>(oflow::GemmArgs)"
+        return "void oflow::conv_stem_x3<32, 1>(oflow::GemmArgs)"
     if cfg == 7 and fam == "f32":
         return NARROW_SYMBOLS[mode]
     if fam == "tile_b16":
@@ -149,10 +163,11 @@ def kernel_symbol(kind):
         return "void oflow::conv_wgrad_tile_b16<%s>(oflow::GemmArgs)" % B16_WGT[cfg]
     if fam == "tile_ws":
         return "void oflow::conv_tile_ws<%s, %d>(oflow::GemmArgs)" % (WS_BN[cfg], mode)
-    if fam == "gemm_x3":
+    if fam in ("gemm_x3", "gemm_b16"):           # (the plane count NP: 3 split, 1 bf16)
+        np_ = 3 if fam == "gemm_x3" else 1
         if mode == 2:
-            return "void oflow::conv_wgrad_x3<%s>(oflow::GemmArgs)" % GX3_WG[cfg]
-        return "void oflow::conv_gemm_x3<%s, %d>(oflow::GemmArgs)" % (GX3[cfg], mode)
+            return "void oflow::conv_wgrad_x3<%s, %d>(oflow::GemmArgs)" % (GX3_WG[cfg], np_)
+        return "void oflow::conv_gemm_x3<%s, %d, %d>(oflow::GemmArgs)" % (GX3[cfg], mode, np_)
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
         return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (
             fam + ("b" if fam == "tile_x3" and cfg >= 4 else ""),

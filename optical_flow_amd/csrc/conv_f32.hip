@@ -1406,17 +1406,22 @@ void conv_tile_b16(GemmArgs a) {
 // CO = 64: 8 waves, 4 x 2 of 64 pixels (2 tile rows) x 32 output channels, 125 KB of LDS;
 // CO = 32: each workgroup takes half the output channels with 4 waves and 80 KB, so two share
 // a CU and one's staging / epilogue overlaps the other's MFMAs.
+// NP = 1 is the bf16 path (configs 3-5): one plane of each operand (the halo rounded to bf16
+// as conv_gemm_bf16 rounds its A, the packed bf16 weights), one MFMA per fragment pair and
+// 32 KB of LDS, so four workgroups share a CU: the stem is then bound by its HBM pass
+// (the 4-channel input read, the 64-channel output written once).
 constexpr int ST_TH = 8, ST_TW = 32;
 constexpr int ST_HH = 2 * ST_TH + 5, ST_HW = 2 * ST_TW + 6, ST_HWP = 72;
 constexpr int ST_BROW = 232;      // bf16 per B row: 7 x 32 + 8
 
-template <int CO>
-__global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : 2) void conv_stem_x3(GemmArgs a) {
-  constexpr int NP = 3, SM = 4, SN = 2, WM = 64, WN = 32, NW = CO / 8, NT = 64 * NW;
+template <int CO, int NP = 3>
+__global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : NP == 1 ? 4 : 2) void conv_stem_x3(GemmArgs a) {
+  constexpr int SM = 4, SN = 2, WM = 64, WN = 32, NW = CO / 8, NT = 64 * NW;
+  static_assert(NP == 3 || NP == 1, "three split planes (fp32) or one (bf16)");
   constexpr int B_U4 = CO * ST_BROW / 8;              // uint4 per B plane
   constexpr int H_PIX = ST_HH * ST_HWP;               // halo pixels (8 bytes each) per plane
-  constexpr int SMEM_U4 = NP * B_U4 + NP * H_PIX / 2;
-  static_assert(NW * WM * WN * 4 <= SMEM_U4 * 16, "epilogue images fit");
+  constexpr int OP_U4 = NP * B_U4 + NP * H_PIX / 2, EP_U4 = NW * WM * WN * 4 / 16;
+  constexpr int SMEM_U4 = OP_U4 > EP_U4 ? OP_U4 : EP_U4;   // operands, then epilogue images
   __shared__ uint4 smem[SMEM_U4];
   char* Bs = reinterpret_cast<char*>(smem);                          // [plane][co][k']
   char* Hs = reinterpret_cast<char*>(smem + NP * B_U4);              // [plane][hy][hx] 8 B
@@ -1452,12 +1457,16 @@ __global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : 2) void conv_stem_x3(GemmArg
     const int iy = iy0 + hy, ix = ix0 + hx;
     const bool ok = (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
     const float4 v = bload4(ra, ok ? (uint32_t)((((int64_t)b * a.h + iy) * a.w + ix) * a.lda * 4) : kOOB);
-    uint2 h, m, l;
-    split3x4(v, h, m, l);
     const int o = (hy * ST_HWP + hx) * 8;
-    *reinterpret_cast<uint2*>(Hs + o) = h;
-    *reinterpret_cast<uint2*>(Hs + H_PIX * 8 + o) = m;
-    *reinterpret_cast<uint2*>(Hs + 2 * H_PIX * 8 + o) = l;
+    if (NP == 1) {
+      *reinterpret_cast<uint2*>(Hs + o) = pack_bf16x4(v);
+    } else {
+      uint2 h, m, l;
+      split3x4(v, h, m, l);
+      *reinterpret_cast<uint2*>(Hs + o) = h;
+      *reinterpret_cast<uint2*>(Hs + H_PIX * 8 + o) = m;
+      *reinterpret_cast<uint2*>(Hs + 2 * H_PIX * 8 + o) = l;
+    }
   }
   __syncthreads();
 
@@ -1493,11 +1502,13 @@ __global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : 2) void conv_stem_x3(GemmArg
 #pragma unroll
       for (int j = 0; j < SN; ++j) {
         f32x4 x = acc4[i][j];
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
+        if (NP == 3) {
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP - 1][i], bv[0][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP - 1][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[NP / 2][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[0][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP / 2][j], x, 0, 0, 0);
+        }
         acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
       }
   }
@@ -1532,6 +1543,9 @@ __global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : 2) void conv_stem_x3(GemmArg
 // of_set_tuning key 8: the stem on conv_stem_x3 (1: two 32-channel workgroups per CU,
 // default; 2: one 64-channel workgroup) or on conv_gemm_x3 (0).
 static int g_stem_x3 = 1;
+// of_set_tuning key 15: the bf16 stem (forward and weight gradient) on the one-plane
+// conv_stem_x3<32, 1> / conv_wgrad_stem_x3<1> (1, default) or on the bf16 GEMMs (0).
+static int g_stem_bf16 = 1;
 bool stem_x3_ok(const of_conv_desc* d) {
   return d->kh == 7 && d->kw == 7 && d->stride == 2 && d->cin_p == 4 && d->cout == 64 &&
          d->pad_top >= 0 && d->pad_top <= 3 && d->pad_left >= 0 && d->pad_left <= 3;
@@ -1547,10 +1561,15 @@ bool stem_x3_ok(const of_conv_desc* d) {
 // both LDS images are double-buffered rows of four octets in the x3_sw swizzle (one barrier
 // per chunk).  Waves own WM x WN blocks of 16 x 16 tiles.  Wave w stages octet w & 3 of every
 // chunk (two channel quads with their own tap walks) for row group w >> 2.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_gemm_x3(GemmArgs a) {
+// NP = 1 is the bf16 path (configs 3-5, the stride-2 block convs and projections): one plane
+// of each operand (A rounded to bf16 as conv_gemm_bf16 rounds it, B the packed bf16 image,
+// which has the x3 hi plane's layout), one MFMA per fragment pair, and with a third of the
+// LDS two workgroups per CU.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP = 3>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NP == 1 ? 2 : 1) void conv_gemm_x3(GemmArgs a) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "x3 GEMM: fwd / dgrad");
-  constexpr int NT = 64 * WAVES_M * WAVES_N, NW = NT / 64, NP = 3;
+  static_assert(NP == 3 || NP == 1, "three split planes (fp32) or one (bf16)");
+  constexpr int NT = 64 * WAVES_M * WAVES_N, NW = NT / 64;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, SM = WM / 16, SN = WN / 16;
   static_assert(NW % 4 == 0 && SM >= 1 && SN >= 1 && WM % 16 == 0 && WN % 16 == 0, "tile");
   constexpr int RG = NW / 4;                     // row groups (4 waves each: one per octet)
@@ -1558,8 +1577,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_gemm_x3(GemmAr
   static_assert(A_SL >= 1 && BM % (64 * RG) == 0, "BM");
   constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
   constexpr int BDI = NP * BN / 16, BDW = (BDI + NW - 1) / NW;   // B DMA wave-instructions
-  static_assert(NW * WM * WN * 4 <= 2 * (A_U4 + B_U4) * 16, "epilogue images fit LDS");
-  __shared__ uint4 smem[2 * (A_U4 + B_U4)];
+  constexpr int OP_U4 = 2 * (A_U4 + B_U4), EP_U4 = NW * WM * WN * 4 / 16;
+  __shared__ uint4 smem[OP_U4 > EP_U4 ? OP_U4 : EP_U4];   // operands, then epilogue images
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1680,14 +1699,18 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_gemm_x3(GemmAr
   auto store_a = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A_SL; ++i) {
-      uint2 h0, m0v, l0, h1, m1, l1;
-      split3x4(ra[i][0], h0, m0v, l0);
-      split3x4(ra[i][1], h1, m1, l1);
       const int row = 64 * (rgrp + RG * i) + lane;
       uint4* img = smem + buf * A_U4 + row * 4 + (oct ^ x3_sw(row));
-      img[0] = make_uint4(h0.x, h0.y, h1.x, h1.y);
-      img[BM * 4] = make_uint4(m0v.x, m0v.y, m1.x, m1.y);
-      img[2 * BM * 4] = make_uint4(l0.x, l0.y, l1.x, l1.y);
+      if (NP == 1) {
+        img[0] = pack_bf16x8(ra[i][0], ra[i][1]);
+      } else {
+        uint2 h0, m0v, l0, h1, m1, l1;
+        split3x4(ra[i][0], h0, m0v, l0);
+        split3x4(ra[i][1], h1, m1, l1);
+        img[0] = make_uint4(h0.x, h0.y, h1.x, h1.y);
+        img[(NP / 2) * BM * 4] = make_uint4(m0v.x, m0v.y, m1.x, m1.y);
+        img[(NP - 1) * BM * 4] = make_uint4(l0.x, l0.y, l1.x, l1.y);
+      }
     }
   };
   // ---------------- B (x3 weight planes [plane][n][k]) by LDS DMA ----------------------------
@@ -1757,11 +1780,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_gemm_x3(GemmAr
 #pragma unroll
       for (int j = 0; j < SN; ++j) {
         f32x4 x = acc[i][j];
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
+        if (NP == 3) {
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP - 1][i], bv[0][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP - 1][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[NP / 2][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[0][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP / 2][j], x, 0, 0, 0);
+        }
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
       }
     if (more) store_a(buf ^ 1);
@@ -2295,17 +2320,21 @@ __device__ __forceinline__ void split3x8(const float* v, bf16x8& h, bf16x8& m, b
 // tiles 2w, 2w + 1 x 4 N tiles, six v_mfma_f32_16x16x32_bf16 per fragment pair (rows 147-159
 // compute discarded values).  Workgroups (three per CU) are persistent over a contiguous range
 // of a.k_per_split tiles (a.K tiles in all) and write one split-K slab each (with a.colsum the
-// bias column sums in slab row 196), reduced by wgrad_reduce_kernel.
+// bias column sums in slab row 196), reduced by wgrad_reduce_kernel.  NP = 1 is the bf16 path:
+// the halo rows and dz rounded to bf16 (round to nearest even, as conv_wgrad_bf16 rounds its
+// operands), one MFMA per fragment pair.
 constexpr int SW_TH = 4, SW_TW = 32, SW_HH = 2 * SW_TH + 5, SW_HX = 2 * SW_TW + 5, SW_HC = 36;
 constexpr int SW_HP = SW_HH * 4 * 2 * SW_HC;             // floats per halo buffer
 constexpr int SW_NW = 5, SW_NT = 64 * SW_NW;
 constexpr int SW_HQ = (SW_HH * SW_HX + SW_NT - 1) / SW_NT; // halo pixels per thread
 constexpr int SW_WGS_PER_CU = 3;
 
+template <int NP>
 __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
-  constexpr int NT = SW_NT, NP = 3;
+  constexpr int NT = SW_NT;
+  static_assert(NP == 3 || NP == 1, "three split planes (fp32) or one (bf16)");
   __shared__ float Hs[2][SW_HP];                       // 2 x 14.6 KB
-  __shared__ uint4 Ds[2][NP * 4 * 64];                 // 2 x 12 KB
+  __shared__ uint4 Ds[2][NP * 4 * 64];                 // 2 x 12 KB (4 KB for NP = 1)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int split = xcd_remap(blockIdx.x, gridDim.x);
@@ -2340,11 +2369,16 @@ __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
   };
   auto store_dz = [&](int buf, const float* v) {
     if (tid >= 256) return;
-    bf16x8 h, m, l;
-    split3x8(v, h, m, l);
-    Ds[buf][(0 * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, h);
-    Ds[buf][(1 * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, m);
-    Ds[buf][(2 * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, l);
+    if (NP == 1) {
+      Ds[buf][d_kg * 64 + d_co] = pack_bf16x8(make_float4(v[0], v[1], v[2], v[3]),
+                                             make_float4(v[4], v[5], v[6], v[7]));
+    } else {
+      bf16x8 h, m, l;
+      split3x8(v, h, m, l);
+      Ds[buf][(0 * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, h);
+      Ds[buf][((NP / 2) * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, m);
+      Ds[buf][((NP - 1) * 4 + d_kg) * 64 + d_co] = __builtin_bit_cast(uint4, l);
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum += v[e];
   };
@@ -2418,7 +2452,11 @@ __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = hrow[a_off[mt] + e];
-      split3x8(v, av[mt][0], av[mt][1], av[mt][2]);
+      if (NP == 1)
+        av[mt][0] = __builtin_bit_cast(bf16x8, pack_bf16x8(make_float4(v[0], v[1], v[2], v[3]),
+                                                           make_float4(v[4], v[5], v[6], v[7])));
+      else
+        split3x8(v, av[mt][0], av[mt][NP / 2], av[mt][NP - 1]);
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -2429,11 +2467,13 @@ __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         f32x4 x = acc[mt][nt];
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][2], bv[0], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][0], bv[2], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][1], bv[1], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][1], bv[0], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][0], bv[1], x, 0, 0, 0);
+        if (NP == 3) {
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][NP - 1], bv[0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][0], bv[NP - 1], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][NP / 2], bv[NP / 2], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][NP / 2], bv[0], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][0], bv[NP / 2], x, 0, 0, 0);
+        }
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[mt][0], bv[0], x, 0, 0, 0);
       }
     }
@@ -2980,16 +3020,19 @@ __global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_tile_b
 // one barrier per 32-pixel chunk; split-K slabs + the bias column sums, as the other wgrads.
 __device__ __forceinline__ int wx3_sw(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_wgrad_x3(GemmArgs a) {
-  constexpr int NT = 64 * WAVES_M * WAVES_N, NW = NT / 64, NP = 3;
+// NP = 1: the bf16 weight gradient of the same shapes (one plane, one MFMA per fragment pair,
+// operands rounded to bf16 as conv_wgrad_bf16 rounds them).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NP = 3>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NP == 1 ? 2 : 1) void conv_wgrad_x3(GemmArgs a) {
+  static_assert(NP == 3 || NP == 1, "three split planes (fp32) or one (bf16)");
+  constexpr int NT = 64 * WAVES_M * WAVES_N, NW = NT / 64;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, SM = WM / 16, SN = WN / 16;
   static_assert(SM >= 1 && SN >= 1 && WM % 16 == 0 && WN % 16 == 0, "tile");
   constexpr int NSLOT = BM + BN, SPT = (NSLOT + NT - 1) / NT;
   constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
-  static_assert(NW * WM * WN * 4 <= 2 * (A_U4 + B_U4) * 16 && 4 * BN * 4 <= A_U4 * 16,
-                "epilogue / column-sum images fit LDS");
-  __shared__ uint4 smem[2 * (A_U4 + B_U4)];
+  constexpr int OP_U4 = 2 * (A_U4 + B_U4), EP_U4 = NW * WM * WN * 4 / 16;
+  static_assert(4 * BN * 4 <= OP_U4 * 16, "column-sum image fits LDS");
+  __shared__ uint4 smem[OP_U4 > EP_U4 ? OP_U4 : EP_U4];   // operands, then epilogue images
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -3101,13 +3144,18 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_wgrad_x3(GemmA
         float v8[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v8[e] = (&stg[j][e].x)[c];
-        bf16x8 h, m, l;
-        split3x8(v8, h, m, l);
         const int row = s_row[j] + c;
         const int idx = row * 4 + (s_oc[j] ^ wx3_sw(row));
-        img[idx] = __builtin_bit_cast(uint4, h);
-        img[rows * 4 + idx] = __builtin_bit_cast(uint4, m);
-        img[2 * rows * 4 + idx] = __builtin_bit_cast(uint4, l);
+        if (NP == 1) {
+          img[idx] = pack_bf16x8(make_float4(v8[0], v8[1], v8[2], v8[3]),
+                                 make_float4(v8[4], v8[5], v8[6], v8[7]));
+        } else {
+          bf16x8 h, m, l;
+          split3x8(v8, h, m, l);
+          img[idx] = __builtin_bit_cast(uint4, h);
+          img[(NP / 2) * rows * 4 + idx] = __builtin_bit_cast(uint4, m);
+          img[(NP - 1) * rows * 4 + idx] = __builtin_bit_cast(uint4, l);
+        }
       }
       if (!s_isa[j] && do_colsum) {
 #pragma unroll
@@ -3157,11 +3205,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_wgrad_x3(GemmA
 #pragma unroll
       for (int j = 0; j < SN; ++j) {
         f32x4 x = acc[i][j];
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], x, 0, 0, 0);
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], x, 0, 0, 0);
+        if (NP == 3) {
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP - 1][i], bv[0][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP - 1][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[NP / 2][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[0][j], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP / 2][j], x, 0, 0, 0);
+        }
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
       }
     if (more) store(buf ^ 1);
@@ -4260,14 +4310,15 @@ void gemm_x3_plan(GemmArgs& a) {
   a.splits = (int)cdiv(kmax, a.k_per_split);
 }
 
-template <int MODE>
+// (NP = 1, the bf16 form: timing kinds 240 + mode * 8 + cfg)
+template <int MODE, int NP = 3>
 int launch_gemm_x3(const GemmArgs& a, hipStream_t s, double flops) {
   const int cfg = a.N > 64 ? 0 : 1;
   dim3 grid(a.tiles_total * a.splits), block(512);
   if (timing_on()) timing_begin(s);
-  if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3<128, 128, 4, 2, MODE>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((conv_gemm_x3<256, 64, 8, 1, MODE>), grid, block, 0, s, a);
-  if (timing_on()) timing_end(s, 160 + MODE * 8 + cfg, flops);
+  if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3<128, 128, 4, 2, MODE, NP>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((conv_gemm_x3<256, 64, 8, 1, MODE, NP>), grid, block, 0, s, a);
+  if (timing_on()) timing_end(s, (NP == 1 ? 240 : 160) + MODE * 8 + cfg, flops);
   int st = check_launch("conv_gemm_x3");
   if (st || a.splits == 1) return st;
   return launch_splitk_epilogue<MODE>(a, s);
@@ -4318,13 +4369,21 @@ int stem_wg_tiles(const of_conv_desc* d) {
 // of_set_tuning key 10: fp32 / bf16 GEMM weight-gradient split-K target workgroups per CU.
 static int g_wgrad_wgs = 4;
 
+// of_set_tuning key 16: the bf16 implicit GEMMs (stride-2 block convs, 1x1 projections; the
+// stem when key 15 = 0) on the one-plane conv_gemm_x3 / conv_wgrad_x3 forms (1, default) or
+// on conv_gemm_bf16 / conv_wgrad_bf16 (0).
+static int g_gemm_b16 = 1;
+bool gemm_b16_wg(const of_conv_desc* d) {
+  return g_gemm_b16 && !narrow_ok(d) && !tile_ok(d) && !(stem_wg_ok(d) && g_stem_bf16);
+}
+
 WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) {
   Geo g = geo(d);
   WgradPlan p;
   p.M = g.taps * g.cin_p;
   p.ldc = g.cout_p;
   p.split_stride = (int64_t)(p.M + 1) * p.ldc;   // + one row for the bias column sums
-  if (!bf16 && stem_wg_ok(d)) {
+  if (stem_wg_ok(d) && (!bf16 || g_stem_bf16)) {
     // conv_wgrad_stem_x3: K = 4 x 32 output tiles, persistent workgroups (3 per CU)
     const int T = stem_wg_tiles(d);
     int splits = std::max(1, std::min(T, SW_WGS_PER_CU * device_cus()));
@@ -4343,12 +4402,14 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
     p.splits = (int)cdiv(T, p.k_per_split);
     return p;
   }
-  if (x3 && !narrow_ok(d)) {
-    // conv_wgrad_x3: 128 x (128 | 64) tiles, one workgroup per CU; K = output pixels in
-    // 32-pixel chunks, split to fill the CUs with at least 8 chunks per slice
+  const bool g16 = bf16 && gemm_b16_wg(d);
+  if ((x3 || g16) && !narrow_ok(d)) {
+    // conv_wgrad_x3: 128 x (128 | 64) tiles, one workgroup per CU (two for the one-plane bf16
+    // form); K = output pixels in 32-pixel chunks, split to fill the CUs with at least 8
+    // chunks per slice
     const int K = d->n * d->ho * d->wo;
     const int tiles = (int)(cdiv(p.M, 128) * cdiv(d->cout, d->cout > 64 ? 128 : 64));
-    int splits = std::max(1, device_cus() / tiles);
+    int splits = std::max(1, (g16 ? 2 : 1) * device_cus() / tiles);
     splits = std::min(splits, (int)std::max<int64_t>(1, cdiv(K, 8 * BKH)));
     p.k_per_split = (int)round_up(cdiv(K, splits), BKH);
     p.splits = (int)cdiv(K, p.k_per_split);
@@ -4488,6 +4549,8 @@ int of_set_tuning(int key, int value) {
   if (key == 12 && value >= 0 && value <= 3) { g_tile_b16 = value; return OF_OK; }
   if (key == 13 && (value == 0 || value == 1)) { g_wgrad_b16 = value; return OF_OK; }
   if (key == 14 && (value == 0 || value == 1)) { g_stem_wg = value; return OF_OK; }
+  if (key == 15 && (value == 0 || value == 1)) { g_stem_bf16 = value; return OF_OK; }
+  if (key == 16 && (value == 0 || value == 1)) { g_gemm_b16 = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -4537,6 +4600,7 @@ int of_conv_pack_many(const void* dev_table, int64_t total_work, void* stream) {
 // Timing kind of the narrow (VALU) path; GEMM kinds are MODE * 8 + tile config (0..3).
 constexpr int KIND_NARROW = 7;
 constexpr int KIND_STEM_X3 = 184;   // conv_stem_x3 (bench.py kind_name)
+constexpr int KIND_STEM_B16 = 186;  // conv_stem_x3<32, 1> (bf16); 187: conv_wgrad_stem_x3<1>
 
 double conv_flops(const of_conv_desc* d) {
   return 2.0 * d->n * d->ho * d->wo * (double)d->cout * d->kh * d->kw * d->cin;
@@ -4554,16 +4618,21 @@ size_t of_conv2d_dgrad_workspace(const of_conv_desc* d) {
 
 size_t of_conv2d_fwd_bf16_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
-  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_FWD, false, g_tile_b16 == 1,
-                                             ws_ok(d, MODE_FWD))
-                                 : fwd_args(d, geo(d), true));
+  if (tile_ok(d))
+    return fd_workspace(tile_args(d, geo(d), MODE_FWD, false, g_tile_b16 == 1, ws_ok(d, MODE_FWD)));
+  GemmArgs a = fwd_args(d, geo(d), true);
+  if (g_gemm_b16) gemm_x3_plan(a);
+  return std::max(fd_workspace(a), fd_workspace(fwd_args(d, geo(d), true)));
 }
 
 size_t of_conv2d_dgrad_bf16_workspace(const of_conv_desc* d) {
   if (validate(d) != OF_OK) return 0;
-  return fd_workspace(tile_ok(d) ? tile_args(d, geo(d), MODE_DGRAD, false, g_tile_b16 == 1,
-                                             ws_ok(d, MODE_DGRAD))
-                                 : dgrad_args(d, geo(d), true));
+  if (tile_ok(d))
+    return fd_workspace(tile_args(d, geo(d), MODE_DGRAD, false, g_tile_b16 == 1,
+                                  ws_ok(d, MODE_DGRAD)));
+  GemmArgs a = dgrad_args(d, geo(d), true);
+  if (g_gemm_b16) gemm_x3_plan(a);
+  return std::max(fd_workspace(a), fd_workspace(dgrad_args(d, geo(d), true)));
 }
 
 int of_conv_path(const of_conv_desc* d) {
@@ -4602,7 +4671,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   const bool ws = tile && bf16 && ws_ok(d, MODE_FWD);
   const bool b16 = tile && bf16 && g_tile_b16 == 1;
   GemmArgs a = tile ? tile_args(d, g, MODE_FWD, x3, b16, ws) : fwd_args(d, g, bf16 || x3);
-  bool stem = x3 && !tile && g_stem_x3 && stem_x3_ok(d);
+  bool stem = (x3 || (bf16 && g_stem_bf16)) && !tile && g_stem_x3 && stem_x3_ok(d);
   if (stem) {                            // conv_stem_x3: one workgroup per output tile, no split
     a.splits = 1;
     a.k_per_split = a.K;
@@ -4615,7 +4684,8 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   a.z = z;
   a.ldz = ldz;
   stem = stem && vec_ep_ok(a);
-  if (x3 && !tile && !stem) gemm_x3_plan(a);
+  const bool g16 = bf16 && !tile && !stem && g_gemm_b16;   // conv_gemm_x3<..., 1>
+  if ((x3 || g16) && !tile && !stem) gemm_x3_plan(a);
   if (!stem) attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
   a.A = x;
   a.lda = ldx;
@@ -4646,17 +4716,20 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
     const int64_t tiles = (int64_t)d->n * cdiv(d->ho, ST_TH) * cdiv(d->wo, ST_TW);
     OF_CHECK_ARG(tiles < INT32_MAX, "conv stem: too many tiles");
     if (timing_on()) timing_begin(s);
-    if (g_stem_x3 == 2)
+    if (bf16)
+      hipLaunchKernelGGL((conv_stem_x3<32, 1>), dim3((unsigned)(2 * tiles)), dim3(256), 0, s, a);
+    else if (g_stem_x3 == 2)
       hipLaunchKernelGGL(conv_stem_x3<64>, dim3((unsigned)tiles), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL(conv_stem_x3<32>, dim3((unsigned)(2 * tiles)), dim3(256), 0, s, a);
-    if (timing_on()) timing_end(s, KIND_STEM_X3, flops);
+    if (timing_on()) timing_end(s, bf16 ? KIND_STEM_B16 : KIND_STEM_X3, flops);
     return check_launch("conv_stem_x3");
   }
   st = x3     ? (tile ? launch_tile_x3<MODE_FWD>(a, s, flops) : launch_gemm_x3<MODE_FWD>(a, s, flops))
        : ws   ? launch_tile_ws<MODE_FWD>(a, s, flops)
        : b16  ? launch_tile_b16<MODE_FWD>(a, s, flops)
        : tile ? launch_tile_bf16<MODE_FWD>(a, s, flops)
+       : g16  ? launch_gemm_x3<MODE_FWD, 1>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_FWD>(a, s, flops)
               : launch_gemm<MODE_FWD>(a, s, flops);
   return st;
@@ -4714,7 +4787,8 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   const bool b16 = tile && bf16 && g_tile_b16 == 1;
   GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3, b16, ws)
                     : dgrad_args(d, g, bf16 || x3, in_place);
-  if (x3 && !tile) gemm_x3_plan(a);
+  const bool g16 = bf16 && !tile && g_gemm_b16;             // conv_gemm_x3<..., 1>
+  if ((x3 || g16) && !tile) gemm_x3_plan(a);
   if (a.tiles_total == 0) return OF_OK;                 // every output already final
   attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
   a.A = dy;
@@ -4742,6 +4816,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
        : ws   ? launch_tile_ws<MODE_DGRAD>(a, s, flops)
        : b16  ? launch_tile_b16<MODE_DGRAD>(a, s, flops)
        : tile ? launch_tile_bf16<MODE_DGRAD>(a, s, flops)
+       : g16  ? launch_gemm_x3<MODE_DGRAD, 1>(a, s, flops)
        : bf16 ? launch_gemm_bf16<MODE_DGRAD>(a, s, flops)
               : launch_gemm<MODE_DGRAD>(a, s, flops);
   return st;
@@ -4861,6 +4936,7 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   const bool bf16 = prec == 1, x3 = prec == 2 && wgx3_ok(d);
   const bool b16 = bf16 && g_wgrad_b16 && wgx3_ok(d);   // conv_wgrad_tile_b16
   const bool x3g = prec == 2 && !x3 && g_wgx3_gemm;   // conv_wgrad_x3 (other shapes)
+  const bool g16 = bf16 && gemm_b16_wg(d);             // conv_wgrad_x3<..., 1>
   OF_CHECK_ARG(x && dy && dw && workspace, "conv wgrad: NULL pointer");
   OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "conv wgrad: ldx");
   OF_CHECK_ARG(lddy >= g.cout_p && lddy % 4 == 0, "conv wgrad: lddy");
@@ -4900,12 +4976,13 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
   a.vec_ep = vec_ep_ok(a);
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * a.K * (double)d->cout * g.taps * d->cin;
-  if (!bf16 && stem_wg_ok(d)) {
+  if (stem_wg_ok(d) && (!bf16 || g_stem_bf16)) {
     a.K = stem_wg_tiles(d);
     a.lda = ldx;
     if (timing_on()) timing_begin(s);
-    hipLaunchKernelGGL(conv_wgrad_stem_x3, dim3(a.splits), dim3(SW_NT), 0, s, a);
-    if (timing_on()) timing_end(s, 185, flops);     // bench.py KIND_STEM_WG_X3
+    if (bf16) hipLaunchKernelGGL(conv_wgrad_stem_x3<1>, dim3(a.splits), dim3(SW_NT), 0, s, a);
+    else hipLaunchKernelGGL(conv_wgrad_stem_x3<3>, dim3(a.splits), dim3(SW_NT), 0, s, a);
+    if (timing_on()) timing_end(s, bf16 ? 187 : 185, flops);     // bench.py KIND_STEM_*
     st = check_launch("conv_wgrad_stem_x3");
   } else if (b16) {
     // the x3b configurations, all 9-tap: timing kinds 216 + cfg (bench.py X3_WGT 4 + cfg)
@@ -4964,6 +5041,16 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     else hipLaunchKernelGGL((conv_wgrad_x3<128, 64, 4, 2>), grid, block, 0, s, a);
     if (timing_on()) timing_end(s, 160 + MODE_WGRAD * 8 + (bn == 128 ? 0 : 1), flops);
     st = check_launch("conv_wgrad_x3");
+  } else if (g16) {
+    const int bn = d->cout > 64 ? 128 : 64;
+    a.n_tiles = (int)cdiv(d->cout, bn);
+    a.tiles_total = (int)cdiv(a.M, 128) * a.n_tiles;
+    dim3 grid(a.tiles_total * a.splits), block(512);
+    if (timing_on()) timing_begin(s);
+    if (bn == 128) hipLaunchKernelGGL((conv_wgrad_x3<128, 128, 4, 2, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_wgrad_x3<128, 64, 4, 2, 1>), grid, block, 0, s, a);
+    if (timing_on()) timing_end(s, 240 + MODE_WGRAD * 8 + (bn == 128 ? 0 : 1), flops);
+    st = check_launch("conv_wgrad_x3_b16");
   } else if (wgt_ok(d, bf16)) {
     int cib, cob;
     wgt_blocks(d, cib, cob);

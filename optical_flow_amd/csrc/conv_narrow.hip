@@ -266,15 +266,35 @@ __device__ __forceinline__ void load_wf(const float* wf, int q, float (&w)[NK3][
     }
 }
 
-__device__ __forceinline__ void stage_halo32(float4* halo, const NarrowArgs& a, int b, int y0,
-                                             int x0) {
+// The halo staging issues all of a thread's loads before any LDS store: a loop of
+// load -> store pairs kept one 16-byte load in flight per thread (narrow kernels at 1-2 TB/s).
+constexpr int NT_HQ = NT_HH * NT_HW * NT_Q, NT_HU = (NT_HQ + 255) / 256;   // 2720 quads, 11
+__device__ __forceinline__ void load_halo32(float4 (&v)[NT_HU], const NarrowArgs& a, int b,
+                                            int y0, int x0) {
   const rsrc_t rx = make_rsrc(a.x + (int64_t)b * a.h * a.w * a.ldx, (int64_t)a.h * a.w * a.ldx * 4);
-  for (int i = threadIdx.x; i < NT_HH * NT_HW * NT_Q; i += 256) {
+#pragma unroll
+  for (int u = 0; u < NT_HU; ++u) {
+    const int i = threadIdx.x + 256 * u;
     const int qq = i & 7, pix = i >> 3, hy = pix / NT_HW, hx = pix - hy * NT_HW;
     const int iy = y0 + hy, ix = x0 + hx;
-    const bool ok = (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
-    halo[i] = bload4(rx, ok ? 4u * ((iy * a.w + ix) * a.ldx + 4 * qq) : kOOB);
+    const bool ok = i < NT_HQ && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    v[u] = bload4(rx, ok ? 4u * ((iy * a.w + ix) * a.ldx + 4 * qq) : kOOB);
   }
+}
+
+__device__ __forceinline__ void store_halo32(float4* halo, const float4 (&v)[NT_HU]) {
+#pragma unroll
+  for (int u = 0; u < NT_HU; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (NT_HQ % 256 == 0 || i < NT_HQ) halo[i] = v[u];
+  }
+}
+
+__device__ __forceinline__ void stage_halo32(float4* halo, const NarrowArgs& a, int b, int y0,
+                                             int x0) {
+  float4 v[NT_HU];
+  load_halo32(v, a, b, y0, x0);
+  store_halo32(halo, v);
 }
 
 template <int CO>
@@ -335,12 +355,19 @@ __global__ __launch_bounds__(256) void narrow_dgrad_tile(NarrowArgs a) {
   const rsrc_t rd =
       make_rsrc(a.dy + (int64_t)b * a.ho * a.wo * a.lddy, (int64_t)a.ho * a.wo * a.lddy * 4);
   const int y0 = ty0 + a.pt - 2, x0 = tx0 + a.pl - 2;       // dy halo origin
-  for (int i = threadIdx.x; i < NT_HH * NT_HW * CO; i += 256) {
+  constexpr int DQ = NT_HH * NT_HW * CO, DU = (DQ + 255) / 256;
+  float dv[DU];
+#pragma unroll
+  for (int u = 0; u < DU; ++u) {
+    const int i = threadIdx.x + 256 * u;
     const int c = i % CO, pix = i / CO, hy = pix / NT_HW, hx = pix - hy * NT_HW;
     const int oy = y0 + hy, ox = x0 + hx;
-    const bool ok = c < a.cout && (unsigned)oy < (unsigned)a.ho && (unsigned)ox < (unsigned)a.wo;
-    dyh[i] = bload1(rd, ok ? 4u * ((oy * a.wo + ox) * a.lddy + c) : kOOB);
+    const bool ok = i < DQ && c < a.cout && (unsigned)oy < (unsigned)a.ho && (unsigned)ox < (unsigned)a.wo;
+    dv[u] = bload1(rd, ok ? 4u * ((oy * a.wo + ox) * a.lddy + c) : kOOB);
   }
+#pragma unroll
+  for (int u = 0; u < DU; ++u)
+    if (threadIdx.x + 256 * u < DQ) dyh[threadIdx.x + 256 * u] = dv[u];
   __syncthreads();
   const int ix = tx0 + col;
   const float neg = a.act == OF_ACT_LEAKY ? a.alpha : 0.f;
@@ -386,20 +413,35 @@ __global__ __launch_bounds__(256) void narrow_wgrad_tile(NarrowArgs a, int tiles
 #pragma unroll
   for (int c = 0; c < CO; ++c) bacc[c] = 0.f;
   const int ntiles = tiles_x * tiles_y * a.n;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // the next tile's halo and dy are loaded into registers while this tile computes
+  constexpr int DQ = NT_H * NT_W * CO, DU = (DQ + 255) / 256;
+  float4 hv[NT_HU];
+  float dv[DU];
+  auto load = [&](int tile) {
     const int b = tile / (tiles_x * tiles_y), rem = tile - b * tiles_x * tiles_y;
     const int ty0 = (rem / tiles_x) * NT_H, tx0 = (rem % tiles_x) * NT_W;
-    __syncthreads();                                   // previous tile's LDS reads done
-    stage_halo32(halo, a, b, ty0 - a.pt, tx0 - a.pl);
+    load_halo32(hv, a, b, ty0 - a.pt, tx0 - a.pl);
     const rsrc_t rd =
         make_rsrc(a.dy + (int64_t)b * a.ho * a.wo * a.lddy, (int64_t)a.ho * a.wo * a.lddy * 4);
-    for (int i = threadIdx.x; i < NT_H * NT_W * CO; i += 256) {
+#pragma unroll
+    for (int u = 0; u < DU; ++u) {
+      const int i = threadIdx.x + 256 * u;
       const int c = i % CO, pix = i / CO, hy = pix / NT_W, hx = pix - hy * NT_W;
       const int oy = ty0 + hy, ox = tx0 + hx;
-      const bool ok = c < a.cout && oy < a.ho && ox < a.wo;
-      dyt[i] = bload1(rd, ok ? 4u * ((oy * a.wo + ox) * a.lddy + c) : kOOB);
+      const bool ok = i < DQ && c < a.cout && oy < a.ho && ox < a.wo;
+      dv[u] = bload1(rd, ok ? 4u * ((oy * a.wo + ox) * a.lddy + c) : kOOB);
     }
+  };
+  if (blockIdx.x < ntiles) load(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();                                   // previous tile's LDS reads done
+    store_halo32(halo, hv);
+#pragma unroll
+    for (int u = 0; u < DU; ++u)
+      if (threadIdx.x + 256 * u < DQ) dyt[threadIdx.x + 256 * u] = dv[u];
     __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) load(tile + gridDim.x);
+#pragma unroll 1
     for (int r = 0; r < NT_H; ++r) {
       float d[CO];
 #pragma unroll

@@ -24,6 +24,8 @@ CONV_CASES = [
     (2, 33, 70, 32, 2, 3, 1, "none", False, False),         # narrow, ragged, many slices
     (3, 40, 100, 32, 4, 3, 1, "leaky", False, False),       # narrow tiled, cout 4, ragged
     (1, 9, 33, 32, 1, 3, 1, "relu", False, False),          # narrow tiled, cout 1
+    (8, 96, 512, 32, 2, 3, 1, "leaky", False, False),       # narrow tiled: 2 tiles per wgrad block
+    (6, 128, 320, 32, 4, 3, 1, "none", False, False),       # narrow tiled: 1-2 tiles per block
     (2, 17, 65, 32, 3, 3, 1, "none", False, False),         # narrow tiled, cout 3
     (1, 10, 20, 64, 3, 3, 1, "relu", False, False),         # narrow, 16 lanes per pixel
     (2, 8, 8, 3, 2, 3, 1, "leaky", False, False),           # narrow, 1 lane per pixel
@@ -329,6 +331,164 @@ def test_conv_stem_x3(n, h, w):
     for (y, z) in outs:
         assert rel_inf(z, zref) < 5e-6 and rel_inf(y, yref) < 5e-6, (rel_inf(z, zref), rel_inf(y, yref))
     assert rel_l2(outs[0][0], yref) < 3 * rel_l2(outs[2][0], yref) + 1e-7
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout,k,s", [(4, 48, 64, 64, 128, 3, 2),    # res3_0 conv_a
+                                               (4, 24, 32, 128, 256, 3, 2),   # res4_0 conv_a
+                                               (4, 48, 64, 64, 128, 1, 2),    # projection
+                                               (3, 37, 45, 20, 40, 3, 2),     # odd, 64-col tiles
+                                               (2, 64, 96, 4, 64, 7, 2),      # stem, key 15 = 0
+                                               (64, 96, 128, 64, 128, 3, 2)])  # bench B = 32 size
+def test_conv_gemm_b16_forms(n, h, w, cin, cout, k, s):
+    """The bf16 implicit GEMMs on the one-plane split-kernel forms (conv_gemm_x3<..., 1> fwd /
+    dgrad with phase groups, conv_wgrad_x3<..., 1>; of_set_tuning key 16 = 1) against
+    conv_gemm_bf16 / conv_wgrad_bf16 (key 16 = 0): the same bf16-rounded products, fp32 sums
+    in another order; both within the bf16 tolerance of the float64 oracle on bf16-rounded
+    operands; the timing kinds say which kernels ran."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_NONE, call
+    lib = _lib.lib()
+    x = rng_tensor((n, h, w, cin), 101)
+    wt = rng_tensor((k, k, cin, cout), 102, scale=(2.0 / (k * k * cin)) ** 0.5)
+    layer = ops.ConvLayer(dev(wt), dev(torch.zeros(cout)), stride=s, act=ACT_NONE, cin_p=cin,
+                          precision="bf16")
+    d = layer.desc(n, h, w)
+    dy = rng_tensor((n, d.ho, d.wo, cout), 103)
+    wf, wd = layer.packed(d)
+    P, st = ops._ptr, ops._stream()
+    xd, dyd = dev(x), dev(dy)
+
+    def kinds():
+        kk = (C.c_int * 64)()
+        cnt = lib.of_timing_read(64, kk, None, None)
+        return {kk[i] for i in range(cnt)}
+
+    res = {}
+    try:
+        assert lib.of_set_tuning(15, 0) == 0          # the stem shape on the GEMMs as well
+        for form in (1, 0):
+            assert lib.of_set_tuning(16, form) == 0
+            fent, fws = layer.fwd_entry(d)
+            dent, dws = layer.dgrad_entry(d)
+            went, wws = layer.wgrad_entry(d)
+            ws = torch.empty(max(fws, dws, wws) // 4 + 4, device="cuda")
+            y = torch.empty(n, d.ho, d.wo, cout, device="cuda")
+            dx = torch.empty(n, h, w, cin, device="cuda")
+            dw = torch.empty(k, k, cin, cout, device="cuda")
+            lib.of_timing_enable(1)
+            call(fent, C.byref(d), P(xd), cin, P(wf), P(layer.bias), None, None, None, None,
+                 1e-3, None, 0, ACT_NONE, 0.0, None, 0, P(y), cout, P(ws), fws, st)
+            if k < 7:
+                call(dent, C.byref(d), P(dyd), cout, P(wd), None, 0, ACT_NONE, 0.0, P(dx), cin,
+                     P(ws), dws, st)
+            call(went, C.byref(d), P(xd), cin, P(dyd), cout, P(dw), None, 0, P(ws), wws, st)
+            torch.cuda.synchronize()
+            res[form] = (y, dx if k < 7 else None, dw, kinds())
+            lib.of_timing_enable(0)
+    finally:
+        lib.of_set_tuning(16, 1)
+        lib.of_set_tuning(15, 1)
+        lib.of_timing_enable(0)
+    want = {240 + (0 if cout > 64 else 1), 256 + (0 if cout > 64 else 1)}
+    if k < 7:
+        want.add(248 + (0 if cout > 64 else 1))
+    assert want <= res[1][3] and not {kk for kk in res[0][3] if kk >= 240}, (res[1][3], res[0][3])
+    # the two kernel families differ only in fp32 summation order
+    assert rel_inf(res[1][0], res[0][0]) < 1e-5
+    assert rel_l2(res[1][2], res[0][2]) < 1e-5
+    if k < 7:
+        assert rel_inf(res[1][1], res[0][1]) < 1e-5
+    if n * h * w > 300000:
+        return      # (the bench size: A/B agreement only, no float64 oracle on the host)
+    xo = f64(x).requires_grad_(True)
+    wo = f64(wt).requires_grad_(True)
+    yref = R._Bf16Conv.apply(xo, wo, None, s)
+    (yref * f64(dy)).sum().backward()
+    for form in (1, 0):
+        y, dx, dw = res[form][:3]
+        assert rel_inf(y, yref) < REL_TOL, (form, rel_inf(y, yref))
+        assert rel_l2(dw, wo.grad) < REL_TOL, (form, rel_l2(dw, wo.grad))
+        if dx is not None:
+            assert rel_inf(dx, xo.grad) < REL_TOL, (form, rel_inf(dx, xo.grad))
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (3, 38, 130), (8, 384, 512)])
+def test_conv_stem_b16(n, h, w):
+    """The bf16 stem (configs 3-5) on the one-plane stem kernels (conv_stem_x3<32, 1>,
+    conv_wgrad_stem_x3<1>; of_set_tuning key 15 = 1) against the bf16 implicit GEMMs (key 15
+    = 0) and the float64 oracle on bf16-rounded operands: forward with bias, BN and ReLU in the
+    epilogue, weight and bias gradients with accumulate, ragged tiles and the bench's B = 32
+    image size (B = 8 here); the timing kinds say which kernels
+    ran."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_RELU, call
+    lib = _lib.lib()
+    cin, cout = 4, 64
+    xc = rng_tensor((n, h, w, 3), 81)
+    x = torch.cat([xc, torch.zeros(n, h, w, 1)], -1)
+    wt = rng_tensor((7, 7, 3, cout), 82, scale=(2.0 / 147) ** 0.5)
+    b = rng_tensor((cout,), 83, scale=0.1)
+    g, be = rng_tensor((cout,), 84, scale=0.5) + 1.0, rng_tensor((cout,), 85, scale=0.1)
+    mu, var = rng_tensor((cout,), 86, scale=0.1), rng_tensor((cout,), 87).abs() + 0.5
+    layer = ops.ConvLayer(dev(wt), dev(b), stride=2, act=ACT_RELU, cin_p=cin, precision="bf16")
+    assert layer.bf16()
+    d = layer.desc(n, h, w)
+    dz = rng_tensor((n, d.ho, d.wo, cout), 88)
+    wf, _ = layer.packed(d)
+    fent, fws = layer.fwd_entry(d)
+    went, _ = layer.wgrad_entry(d)
+    ws = torch.empty(fws // 4 + 4, device="cuda")
+    P, st = ops._ptr, ops._stream()
+    xd, bd, gd, bed, mud, vard, dzd = [dev(t) for t in (x, b, g, be, mu, var, dz)]
+    prior_w, prior_b = rng_tensor((7, 7, 3, cout), 89), rng_tensor((cout,), 90)
+
+    def kinds():
+        kk = (C.c_int * 16)()
+        cnt = lib.of_timing_read(16, kk, None, None)
+        return {kk[i] for i in range(cnt)}
+
+    res = {}
+    try:
+        for form in (1, 0):
+            assert lib.of_set_tuning(15, form) == 0
+            y = torch.full((n, d.ho, d.wo, cout), 7.0, device="cuda")
+            lib.of_timing_enable(1)
+            call(fent, C.byref(d), P(xd), cin, P(wf), P(bd), P(gd), P(bed), P(mud), P(vard), 1e-3,
+                 None, 0, ACT_RELU, 0.0, None, 0, P(y), cout, P(ws), fws, st)
+            torch.cuda.synchronize()
+            kf = kinds()
+            wws = getattr(lib, went + "_workspace")(C.byref(d))
+            wsw = torch.empty(wws // 4 + 4, device="cuda")
+            dw, db = dev(prior_w.clone()), dev(prior_b.clone())
+            call(went, C.byref(d), P(xd), cin, P(dzd), cout, P(dw), P(db), 1, P(wsw), wws, st)
+            torch.cuda.synchronize()
+            kw = kinds()
+            lib.of_timing_enable(0)
+            res[form] = (y, dw.cpu().double() - f64(prior_w), db.cpu().double() - f64(prior_b),
+                         kf, kw)
+    finally:
+        lib.of_set_tuning(15, 1)
+        lib.of_timing_enable(0)
+    assert res[1][3] == {186} and 186 not in res[0][3], (res[1][3], res[0][3])
+    assert res[1][4] == {187} and 187 not in res[0][4], (res[1][4], res[0][4])
+    # oracle: bf16-rounded x and w, float64 arithmetic, BN + ReLU on the fp64 sum
+    zref = R._Bf16Conv.apply(f64(xc), f64(wt), f64(b), 2)
+    yref = torch.relu((zref - f64(mu)) / torch.sqrt(f64(var) + 1e-3) * f64(g) + f64(be))
+    wo = f64(wt).requires_grad_(True)
+    (R._Bf16Conv.apply(f64(xc), wo, None, 2) * f64(dz)).sum().backward()
+    dbref = f64(dz).sum((0, 1, 2))
+    for form in (1, 0):
+        y, dwv, dbv = res[form][:3]
+        assert rel_inf(y, yref) < REL_TOL, (form, rel_inf(y, yref))
+        assert rel_l2(dwv, wo.grad) < REL_TOL, (form, rel_l2(dwv, wo.grad))
+        assert rel_l2(dbv, dbref) < 1e-5, (form, rel_l2(dbv, dbref))
+    # the two kernel families differ only in fp32 summation order
+    assert rel_inf(res[1][0], res[0][0]) < 1e-5
+    assert rel_l2(res[1][1], res[0][1]) < 1e-5
 
 
 @pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (3, 38, 130), (8, 384, 512)])
