@@ -1546,6 +1546,10 @@ static int g_stem_x3 = 1;
 // of_set_tuning key 15: the bf16 stem (forward and weight gradient) on the one-plane
 // conv_stem_x3<32, 1> / conv_wgrad_stem_x3<1> (1, default) or on the bf16 GEMMs (0).
 static int g_stem_bf16 = 1;
+// of_set_tuning key 18: bf16 3x3 input gradients with BN = 128 on the tall (X3_TH0 x 32)
+// output tiles of conv_tile_bf16 where the grid allows (1), as the forward does, or on 4 x 32
+// tiles (0, default).
+static int g_tall16_dgrad = 0;
 bool stem_x3_ok(const of_conv_desc* d) {
   return d->kh == 7 && d->kw == 7 && d->stride == 2 && d->cin_p == 4 && d->cout == 64 &&
          d->pad_top >= 0 && d->pad_top <= 3 && d->pad_left >= 0 && d->pad_left <= 3;
@@ -4142,7 +4146,8 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   // bf16: fwd only (8 x 32 tiles measured +5 % on dec3 fwd, -2 % on dgrad); conv_tile_ws: always
   const bool tall = ws ? true
                   : x3 || b16 ? x3_tall(d->n, OH, OW, a.N)
-                             : fwd && pick_bn(a.N) == 128 && x3_tall(d->n, OH, OW, a.N);
+                             : (fwd || g_tall16_dgrad) && pick_bn(a.N) == 128 &&
+                                   x3_tall(d->n, OH, OW, a.N);
   const int th = tall ? X3_TH0 : TF_H;
   const int m_tiles = d->n * (int)cdiv(OH, th) * (int)cdiv(OW, TF_W);
   a.bm = th * TF_W;
@@ -4369,12 +4374,15 @@ int stem_wg_tiles(const of_conv_desc* d) {
 // of_set_tuning key 10: fp32 / bf16 GEMM weight-gradient split-K target workgroups per CU.
 static int g_wgrad_wgs = 4;
 
-// of_set_tuning key 16: the bf16 implicit GEMMs (stride-2 block convs, 1x1 projections; the
-// stem when key 15 = 0) on the one-plane conv_gemm_x3 / conv_wgrad_x3 forms (1, default) or
-// on conv_gemm_bf16 / conv_wgrad_bf16 (0).
-static int g_gemm_b16 = 1;
+// of_set_tuning key 16: which bf16 implicit GEMMs (stride-2 block convs, 1x1 projections; the
+// stem when key 15 = 0) run on the one-plane conv_gemm_x3 / conv_wgrad_x3 forms instead of
+// conv_gemm_bf16 / conv_wgrad_bf16: bit 0 forward, bit 1 input gradient, bit 2 weight
+// gradient.  Default 6: measured per layer at bf16 B = 32 (tools/gpu_r3n.sh), the one-plane
+// input and weight gradients are faster (0.77 -> 0.71, 0.46 -> 0.40 ms per step), the
+// forward slower (0.31 -> 0.35 ms).
+static int g_gemm_b16 = 6;
 bool gemm_b16_wg(const of_conv_desc* d) {
-  return g_gemm_b16 && !narrow_ok(d) && !tile_ok(d) && !(stem_wg_ok(d) && g_stem_bf16);
+  return (g_gemm_b16 & 4) && !narrow_ok(d) && !tile_ok(d) && !(stem_wg_ok(d) && g_stem_bf16);
 }
 
 WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) {
@@ -4550,7 +4558,8 @@ int of_set_tuning(int key, int value) {
   if (key == 13 && (value == 0 || value == 1)) { g_wgrad_b16 = value; return OF_OK; }
   if (key == 14 && (value == 0 || value == 1)) { g_stem_wg = value; return OF_OK; }
   if (key == 15 && (value == 0 || value == 1)) { g_stem_bf16 = value; return OF_OK; }
-  if (key == 16 && (value == 0 || value == 1)) { g_gemm_b16 = value; return OF_OK; }
+  if (key == 16 && value >= 0 && value <= 7) { g_gemm_b16 = value; return OF_OK; }
+  if (key == 18 && (value == 0 || value == 1)) { g_tall16_dgrad = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -4621,7 +4630,7 @@ size_t of_conv2d_fwd_bf16_workspace(const of_conv_desc* d) {
   if (tile_ok(d))
     return fd_workspace(tile_args(d, geo(d), MODE_FWD, false, g_tile_b16 == 1, ws_ok(d, MODE_FWD)));
   GemmArgs a = fwd_args(d, geo(d), true);
-  if (g_gemm_b16) gemm_x3_plan(a);
+  if (g_gemm_b16 & 1) gemm_x3_plan(a);
   return std::max(fd_workspace(a), fd_workspace(fwd_args(d, geo(d), true)));
 }
 
@@ -4631,7 +4640,7 @@ size_t of_conv2d_dgrad_bf16_workspace(const of_conv_desc* d) {
     return fd_workspace(tile_args(d, geo(d), MODE_DGRAD, false, g_tile_b16 == 1,
                                   ws_ok(d, MODE_DGRAD)));
   GemmArgs a = dgrad_args(d, geo(d), true);
-  if (g_gemm_b16) gemm_x3_plan(a);
+  if (g_gemm_b16 & 2) gemm_x3_plan(a);
   return std::max(fd_workspace(a), fd_workspace(dgrad_args(d, geo(d), true)));
 }
 
@@ -4684,7 +4693,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   a.z = z;
   a.ldz = ldz;
   stem = stem && vec_ep_ok(a);
-  const bool g16 = bf16 && !tile && !stem && g_gemm_b16;   // conv_gemm_x3<..., 1>
+  const bool g16 = bf16 && !tile && !stem && (g_gemm_b16 & 1);   // conv_gemm_x3<..., 1>
   if ((x3 || g16) && !tile && !stem) gemm_x3_plan(a);
   if (!stem) attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
   a.A = x;
@@ -4787,7 +4796,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   const bool b16 = tile && bf16 && g_tile_b16 == 1;
   GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3, b16, ws)
                     : dgrad_args(d, g, bf16 || x3, in_place);
-  const bool g16 = bf16 && !tile && g_gemm_b16;             // conv_gemm_x3<..., 1>
+  const bool g16 = bf16 && !tile && (g_gemm_b16 & 2);       // conv_gemm_x3<..., 1>
   if ((x3 || g16) && !tile) gemm_x3_plan(a);
   if (a.tiles_total == 0) return OF_OK;                 // every output already final
   attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
