@@ -1437,35 +1437,60 @@ __global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : NP == 1 ? 4 : 2) void conv_s
   const int iy0 = 2 * oy0 - a.pt, ix0 = 2 * ox0 - a.pl;
 
   // ---- B: entry (plane, co, kernel row r, octet sp) <- taps (r, 2 sp), (r, 2 sp + 1) of the
-  // x3 fwd image W16_f[co][tap * 4 + ci] (8-byte aligned pieces; tap 7 is zero)
+  // x3 fwd image W16_f[co][tap * 4 + ci] (8-byte aligned pieces; tap 7 is zero).  Every
+  // thread issues all of its B and halo loads before its first LDS store (a load -> store
+  // loop keeps one load in flight per thread: the stem is latency-bound on its staging).
+  constexpr int BE = NP * CO * 28, BQ = (BE + NT - 1) / NT;
+  constexpr int HE = ST_HH * ST_HW, HQ = (HE + NT - 1) / NT;
   const rsrc_t rb = make_rsrc(a.B, a.b_bytes);
-  for (int e = tid; e < NP * CO * 28; e += NT) {
+  const rsrc_t ra = make_rsrc(a.A, a.a_bytes);
+  uint2 blo[BQ], bhi[BQ];
+  float4 hv[HQ];
+#pragma unroll
+  for (int k = 0; k < BQ; ++k) {
+    const int e = tid + NT * k;
     const int p = e / (CO * 28), rem = e - p * (CO * 28);
     const int co = rem / 28, rs = rem - co * 28, r = rs >> 2, sp = rs & 3;
     const uint32_t src =
         (uint32_t)((p * a.b_plane + (int64_t)(co0 + co) * a.ldb + (r * 7 + 2 * sp) * 4) * 2);
-    const bool ok = co0 + co < a.nb;
-    const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok ? src : kOOB, 0, 0));
-    const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok && sp < 3 ? src + 8 : kOOB, 0, 0));
-    *reinterpret_cast<uint4*>(Bs + ((p * CO + co) * ST_BROW + r * 32 + sp * 8) * 2) =
-        make_uint4(lo.x, lo.y, hi.x, hi.y);
+    const bool ok = e < BE && co0 + co < a.nb;
+    blo[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok ? src : kOOB, 0, 0));
+    bhi[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok && sp < 3 ? src + 8 : kOOB, 0, 0));
   }
-  // ---- halo: input pixel (iy0 + hy, ix0 + hx), 4 channels, split into 3 planes
-  const rsrc_t ra = make_rsrc(a.A, a.a_bytes);
-  for (int q = tid; q < ST_HH * ST_HW; q += NT) {
+  // ---- halo: input pixel (iy0 + hy, ix0 + hx), 4 channels (split into 3 planes for fp32)
+#pragma unroll
+  for (int k = 0; k < HQ; ++k) {
+    const int q = tid + NT * k;
     const int hy = q / ST_HW, hx = q - hy * ST_HW;
     const int iy = iy0 + hy, ix = ix0 + hx;
-    const bool ok = (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
-    const float4 v = bload4(ra, ok ? (uint32_t)((((int64_t)b * a.h + iy) * a.w + ix) * a.lda * 4) : kOOB);
-    const int o = (hy * ST_HWP + hx) * 8;
-    if (NP == 1) {
-      *reinterpret_cast<uint2*>(Hs + o) = pack_bf16x4(v);
-    } else {
-      uint2 h, m, l;
-      split3x4(v, h, m, l);
-      *reinterpret_cast<uint2*>(Hs + o) = h;
-      *reinterpret_cast<uint2*>(Hs + H_PIX * 8 + o) = m;
-      *reinterpret_cast<uint2*>(Hs + 2 * H_PIX * 8 + o) = l;
+    const bool ok = q < HE && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    hv[k] = bload4(ra, ok ? (uint32_t)((((int64_t)b * a.h + iy) * a.w + ix) * a.lda * 4) : kOOB);
+  }
+#pragma unroll
+  for (int k = 0; k < BQ; ++k) {
+    const int e = tid + NT * k;
+    if (BE % NT == 0 || e < BE) {
+      const int p = e / (CO * 28), rem = e - p * (CO * 28);
+      const int co = rem / 28, rs = rem - co * 28, r = rs >> 2, sp = rs & 3;
+      *reinterpret_cast<uint4*>(Bs + ((p * CO + co) * ST_BROW + r * 32 + sp * 8) * 2) =
+          make_uint4(blo[k].x, blo[k].y, bhi[k].x, bhi[k].y);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < HQ; ++k) {
+    const int q = tid + NT * k;
+    if (HE % NT == 0 || q < HE) {
+      const int hy = q / ST_HW, hx = q - hy * ST_HW;
+      const int o = (hy * ST_HWP + hx) * 8;
+      if (NP == 1) {
+        *reinterpret_cast<uint2*>(Hs + o) = pack_bf16x4(hv[k]);
+      } else {
+        uint2 h, m, l;
+        split3x4(hv[k], h, m, l);
+        *reinterpret_cast<uint2*>(Hs + o) = h;
+        *reinterpret_cast<uint2*>(Hs + H_PIX * 8 + o) = m;
+        *reinterpret_cast<uint2*>(Hs + 2 * H_PIX * 8 + o) = l;
+      }
     }
   }
   __syncthreads();

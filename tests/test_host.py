@@ -95,11 +95,6 @@ def test_bench_kernel_symbols_match_pmc_keys():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     entries = json.load(open(os.path.join(root, "profiles", "pmc_traffic.json")))["entries"]
     keys = set().union(*(e["kernels"] for e in entries.values()))
-    # PMC passes taken before the split kernels gained their plane-count template argument
-    # (NP: 3 for fp32, 1 for bf16) name the fp32 instances without it
-    import re
-    keys = {re.sub(r"(conv_stem_x3<32|conv_gemm_x3<\d+, \d+, \d+, \d+, \d|"
-                   r"conv_wgrad_x3<\d+, \d+, \d+, \d+)>", r"\1, 3>", k) for k in keys}
     names = set()
     for mode in (0, 1):
         for cfg in bench.X3_BN:
@@ -111,7 +106,14 @@ def test_bench_kernel_symbols_match_pmc_keys():
             names.add(bench.kernel_symbol(160 + mode * 8 + cfg))
     for cfg in bench.GX3_WG:
         names.add(bench.kernel_symbol(176 + cfg))
-    names.add(bench.kernel_symbol(bench.KIND_STEM_X3))
+    for mode in (0, 1):                      # the one-plane (bf16) split GEMMs
+        for cfg in bench.GX3:
+            names.add(bench.kernel_symbol(240 + mode * 8 + cfg))
+    for cfg in bench.GX3_WG:
+        names.add(bench.kernel_symbol(256 + cfg))
+    for kind in (bench.KIND_STEM_X3, bench.KIND_STEM_WG_X3, bench.KIND_STEM_B16,
+                 bench.KIND_STEM_WG_B16):
+        names.add(bench.kernel_symbol(kind))
     x3_keys = {k for k in keys if "_x3<" in k or "_x3b<" in k}
     assert x3_keys and x3_keys <= names, sorted(x3_keys - names)
 
