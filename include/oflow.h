@@ -356,7 +356,15 @@ int of_timing_enable(int on);
  * key 13 = bf16 3x3 stride-1 weight gradient on the single-plane 9-tap kernel
  * conv_wgrad_tile_b16 (1; timing kinds 216 + cfg) or conv_wgrad_tile_bf16 (0, default);
  * key 14 = the stem's fp32 weight gradient (7x7 stride 2, 3 input channels padded to 4, 64
- * outputs) on conv_wgrad_stem_x3 (1, default; timing kind 185) or the fp32 MFMA GEMM (0). */
+ * outputs) on conv_wgrad_stem_x3 (1, default; timing kind 185) or the fp32 MFMA GEMM (0);
+ * key 15 = the bf16 stem (forward and weight gradient) on the one-plane stem kernels
+ * conv_stem_x3<32, 1> / conv_wgrad_stem_x3<1> (1, default; timing kinds 186 / 187) or on the
+ * bf16 implicit GEMMs (0);
+ * key 16 = which bf16 implicit GEMMs (stride-2 convs, 1x1 projections) run on the one-plane
+ * split-GEMM forms conv_gemm_x3<..., 1> / conv_wgrad_x3<..., 1> (timing kinds 240 + 8 mode +
+ * cfg): bit 0 forward, bit 1 input gradient, bit 2 weight gradient (default 6);
+ * key 18 = bf16 3x3 input gradients with N tiles of 128 on the tall 8 x 32 output tiles where
+ * the grid allows (1) or on 4 x 32 tiles (0, default). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 
