@@ -4571,6 +4571,7 @@ int of_set_tuning(int key, int value) {
   if (key == 8 && value >= 0 && value <= 2) { g_stem_x3 = value; return OF_OK; }
   if (key == 7 && (value == 0 || value == 1)) { g_warp_win = value; return OF_OK; }
   if (key == 9 && value >= 0 && value <= 3) { g_corr_blk = value; return OF_OK; }
+  if (key == 19 && (value == 0 || value == 1)) { g_corr_ty8 = value; return OF_OK; }
   if (key == 10 && value >= 1 && value <= 16) { g_wgrad_wgs = value; return OF_OK; }
   if (key == 11 && (value == 0 || value == 1)) { g_wgx3_c4 = value; return OF_OK; }
   if (key == 1 && value >= 1 && value <= 16) { g_split_wgs = value; return OF_OK; }

@@ -397,18 +397,22 @@ struct CorrBwdArgs {
   int tiles_x, tiles_y;
 };
 
-template <int D, int SIGN, bool VEC>
-__global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
+// TY = 4: 4 x 16-pixel tiles, 256 threads, two workgroups per CU (72.5 KB of LDS); TY = 8
+// (of_set_tuning key 19): 8 x 16 tiles with 512 threads, one workgroup per CU (108 KB): the
+// same 8 waves per CU, the src halo read 2.4x per pixel instead of 3.4x.
+template <int D, int SIGN, bool VEC, int TY = CT_Y>
+__global__ __launch_bounds__(64 * TY, TY == CT_Y ? 2 : 1) void corr_bwd_kernel(CorrBwdArgs a) {
+  constexpr int TX = CT_X, TPIX = TY * TX, NT = 4 * TPIX;
   constexpr int ND = 2 * D + 1, NK = ND * ND;
-  constexpr int HY = CT_Y + 2 * D, HX = CT_X + 2 * D, NH = HY * HX;
-  constexpr int NQ = NH * (CSLAB / 4), NU = (NQ + 255) / 256;
+  constexpr int HY = TY + 2 * D, HX = TX + 2 * D, NH = HY * HX;
+  constexpr int NQ = NH * (CSLAB / 4), NU = (NQ + NT - 1) / NT;
   // Coefficient loads: d/d(f1) reads each tile pixel's 49 contiguous g values; d/d(f2) reads,
   // per offset row i, the 7 contiguous g values of the source pixels that map into the tile.
   constexpr int GROW = HX * ND;                      // per source row, per offset row i
-  constexpr int NGQ = SIGN > 0 ? CT_PIX * NK : ND * CT_Y * GROW;
-  constexpr int NG = (NGQ + 255) / 256;
+  constexpr int NGQ = SIGN > 0 ? TPIX * NK : ND * TY * GROW;
+  constexpr int NG = (NGQ + NT - 1) / NT;
   __shared__ float4 lds4[NH * CSPS / 4];
-  __shared__ float G[NK * CT_PIX];
+  __shared__ float G[NK * TPIX];
   float* tile = reinterpret_cast<float*>(lds4);
   const int h = a.h, w = a.w;
   // 1-D grid, XCD-aware: neighbouring tiles (shared halo rows) run on one XCD's L2.
@@ -416,10 +420,10 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
   const int tl = wg % (a.tiles_x * a.tiles_y), z = wg / (a.tiles_x * a.tiles_y);
   const int b = z / a.slabs, slab = z - b * a.slabs;
   const int c_lo = slab * CSLAB, cs = min(CSLAB, a.c - c_lo);
-  const int y0 = (tl / a.tiles_x) * CT_Y, x0 = (tl % a.tiles_x) * CT_X;
+  const int y0 = (tl / a.tiles_x) * TY, x0 = (tl % a.tiles_x) * TX;
   const int tid = threadIdx.x;
   const int pix = tid >> 2, qtr = tid & 3;
-  const int ty = pix / CT_X, tx = pix % CT_X;
+  const int ty = pix / TX, tx = pix % TX;
   const int y = y0 + ty, x = x0 + tx;
   const bool valid = y < h && x < w;
   const int64_t img = (int64_t)b * h * w;
@@ -432,14 +436,14 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
   float gv[NG];
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
-    const int q = tid + 256 * u;
+    const int q = tid + NT * u;
     uint32_t off = kOOB;
     if (SIGN > 0) {
       const int p = q / NK, k = q - p * NK;
-      const int sy = y0 + p / CT_X, sx = x0 + p % CT_X;
+      const int sy = y0 + p / TX, sx = x0 + p % TX;
       if (q < NGQ && sy < h && sx < w) off = 4 * ((sy * w + sx) * a.ldg + k);
     } else {
-      const int i = q / (CT_Y * GROW), r0 = q - i * (CT_Y * GROW);
+      const int i = q / (TY * GROW), r0 = q - i * (TY * GROW);
       const int r = r0 / GROW, rem = r0 - r * GROW;
       const int hx = rem / ND, j = rem - hx * ND;
       const int sy = y0 + r + D - i, sx = x0 - D + hx;   // source of target row r
@@ -451,7 +455,7 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
   float4 hv[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    const int q = tid + 256 * u;
+    const int q = tid + NT * u;
     const int hp = q >> 4, cq = q & 15;
     const int sy = y0 - D + hp / HX, sx = x0 - D + hp % HX;
     const bool ok = q < NQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
@@ -469,21 +473,21 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
   }
 #pragma unroll
   for (int u = 0; u < NG; ++u) {
-    const int q = tid + 256 * u;
+    const int q = tid + NT * u;
     if (SIGN > 0) {
       const int p = q / NK, k = q - p * NK;
-      if (q < NGQ) G[k * CT_PIX + p] = gv[u];
+      if (q < NGQ) G[k * TPIX + p] = gv[u];
     } else {
-      const int i = q / (CT_Y * GROW), r0 = q - i * (CT_Y * GROW);
+      const int i = q / (TY * GROW), r0 = q - i * (TY * GROW);
       const int r = r0 / GROW, rem = r0 - r * GROW;
       const int hx = rem / ND, j = rem - hx * ND;
       const int tx2 = hx + j - 2 * D;                  // target column
-      if (q < NGQ && (unsigned)tx2 < (unsigned)CT_X) G[(i * ND + j) * CT_PIX + r * CT_X + tx2] = gv[u];
+      if (q < NGQ && (unsigned)tx2 < (unsigned)TX) G[(i * ND + j) * TPIX + r * TX + tx2] = gv[u];
     }
   }
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    const int q = tid + 256 * u;
+    const int q = tid + NT * u;
     if (q < NQ) *reinterpret_cast<float4*>(&tile[(q >> 4) * CSPS + 4 * (q & 15)]) = hv[u];
   }
   __syncthreads();
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(256, 2) void corr_bwd_kernel(CorrBwdArgs a) {
         const int oy = SIGN > 0 ? i : 2 * D - i;   // tile row of src[p + SIGN*d]
         const int ox = SIGN > 0 ? j : 2 * D - j;
         const float4 v = *reinterpret_cast<const float4*>(tb + (oy * HX + ox) * CSPS);
-        const float cf = G[(i * ND + j) * CT_PIX + pix];
+        const float cf = G[(i * ND + j) * TPIX + pix];
         float4& sa = s4[(i * ND + j) & 1];   // two chains: halves the FMA dependency depth
         sa.x = fmaf(cf, v.x, sa.x);
         sa.y = fmaf(cf, v.y, sa.y);
@@ -956,6 +960,7 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
 constexpr int WG_T = 8, WG_CAP = 1024, WG_NT = 256;
 int g_warp_win = 1;   // of_set_tuning key 7: warp_bwd_gather (1) or warp_bwd_agg (0)
 int g_corr_blk = 1;   // of_set_tuning key 9: bit 0 corr_fwd_blk (else corr_fwd_kernel), bit 1 corr_bwd_blk
+int g_corr_ty8 = 0;   // of_set_tuning key 19: corr_bwd_kernel on 8 x 16 tiles, 512 threads (1)
 
 __device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes of a DPP row
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
@@ -1515,9 +1520,20 @@ static int corr_bwd_launch(int sign, CorrBwdArgs a, int n, hipStream_t s) {
     return check_launch(sign > 0 ? "corr_bwd_blk_f1" : "corr_bwd_blk_f2");
   }
   a.slabs = (int)cdiv(a.c, CSLAB);
-  a.tiles_x = (int)cdiv(a.w, CT_X), a.tiles_y = (int)cdiv(a.h, CT_Y);
+  const int ty = g_corr_ty8 ? 2 * CT_Y : CT_Y;
+  a.tiles_x = (int)cdiv(a.w, CT_X), a.tiles_y = (int)cdiv(a.h, ty);
   const dim3 grid((unsigned)((int64_t)a.tiles_x * a.tiles_y * n * a.slabs));
-  if (sign > 0 && a.vec)
+  if (g_corr_ty8) {
+    const dim3 blk(4 * 2 * CT_Y * CT_X);
+    if (sign > 0 && a.vec)
+      hipLaunchKernelGGL((corr_bwd_kernel<3, 1, true, 2 * CT_Y>), grid, blk, 0, s, a);
+    else if (sign > 0)
+      hipLaunchKernelGGL((corr_bwd_kernel<3, 1, false, 2 * CT_Y>), grid, blk, 0, s, a);
+    else if (a.vec)
+      hipLaunchKernelGGL((corr_bwd_kernel<3, -1, true, 2 * CT_Y>), grid, blk, 0, s, a);
+    else
+      hipLaunchKernelGGL((corr_bwd_kernel<3, -1, false, 2 * CT_Y>), grid, blk, 0, s, a);
+  } else if (sign > 0 && a.vec)
     hipLaunchKernelGGL((corr_bwd_kernel<3, 1, true>), grid, dim3(256), 0, s, a);
   else if (sign > 0)
     hipLaunchKernelGGL((corr_bwd_kernel<3, 1, false>), grid, dim3(256), 0, s, a);

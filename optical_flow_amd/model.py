@@ -298,7 +298,8 @@ def flow_module(features1, features2, previous_flow, max_disp, head: Optional[Fl
     else:
         flow_up = None
         features2_warped = features2
-    x = ops.corr_concat(features1, features2_warped, flow_up, max_disp, head.cp)
+    x = ops.corr_concat(features1, features2_warped, flow_up, max_disp, head.cp,
+                        head.convs[0].precision)
     return ops.conv_stack(x, head.convs)
 
 

@@ -192,8 +192,16 @@ def side_stream(*tensors):
 # stream of its own beside the decoder's input-gradient chain (df2 -> warp backward -> the
 # coarser level), and the encoder backward waits for that stream (corr_side_wait).
 # Measured A/B (one box): fp32 B=8 587-589 -> 581-586 pairs/s (the main chain's convs already
-# fill the chip; the memory-bound df1 only slows them), bf16 B=32 1353 -> 1363: off by default.
-CORR_DF1_SIDE = os.environ.get("OFLOW_CORR_DF1_SIDE", "0") == "1"
+# fill the chip; the memory-bound df1 only slows them), bf16 B=32 1353 -> 1363 (round 2) and
+# 1422.7 / 1426.9 -> 1430.9 / 1435.9 (round 3, tools/gpu_r3q.sh): on for bf16 layers, off for
+# fp32.  CORR_DF1_SIDE (env OFLOW_CORR_DF1_SIDE = 0 / 1) forces it either way.
+_DF1_ENV = os.environ.get("OFLOW_CORR_DF1_SIDE")
+CORR_DF1_SIDE = None if _DF1_ENV is None else _DF1_ENV == "1"
+CORR_DF1_SIDE_DEFAULT = {"fp32": False, "bf16": True}
+
+
+def corr_df1_side(precision):
+    return CORR_DF1_SIDE if CORR_DF1_SIDE is not None else CORR_DF1_SIDE_DEFAULT[precision]
 _CORR_SIDE = {}
 
 
@@ -1017,9 +1025,10 @@ class _CorrConcat(torch.autograd.Function):
     as the initial value of df1 (no copy or concat passes)."""
 
     @staticmethod
-    def forward(ctx, f1, f2w, flow_up, max_disp, cp, fa):
+    def forward(ctx, f1, f2w, flow_up, max_disp, cp, fa, df1_side=False):
         _check_dev(f1, f2w, flow_up)
         ctx.fa = fa
+        ctx.df1_side = df1_side
         f1, f2w = f1.contiguous(), f2w.contiguous()
         n, h, w, c = f1.shape
         nk = (2 * max_disp + 1) ** 2
@@ -1050,7 +1059,7 @@ class _CorrConcat(torch.autograd.Function):
             ctx.fa.addend = (dx, c + nk, cp)
         elif has_flow and ctx.needs_input_grad[2]:
             dflow = torch.empty((n, h, w, 2), device=dx.device)
-        if CORR_DF1_SIDE and dx.is_cuda and _in_slab(ctx.dst[0], df1):
+        if ctx.df1_side and dx.is_cuda and _in_slab(ctx.dst[0], df1):
             # df1 lands in the encoder output's gradient slab: its only reader is the encoder
             # backward (corr_side_wait there and in _Halves' copy path); a df1 that autograd
             # would sum with another consumer's gradient stays on the current stream
@@ -1064,15 +1073,17 @@ class _CorrConcat(torch.autograd.Function):
             with torch.cuda.stream(corr_side_stream(dx, f1, f2w, df1)):
                 call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c,
                      max_disp, _ptr(df1), None, None, _stream())
-            return df1, df2, dflow, None, None, None
+            return df1, df2, dflow, None, None, None, None
         call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c, max_disp,
              _ptr(df1), _ptr(df2), _ptr(dflow), _stream())
-        return df1, df2, dflow, None, None, None
+        return df1, df2, dflow, None, None, None, None
 
 
-def corr_concat(f1, f2w, flow_up, max_disp, cp):
+def corr_concat(f1, f2w, flow_up, max_disp, cp, precision="fp32"):
+    """``precision``: that of the flow module's convs; it picks whether df1 runs on a stream
+    of its own (corr_df1_side)."""
     fa = getattr(flow_up, "_of_flowadd", None) if flow_up is not None else None
-    return _CorrConcat.apply(f1, f2w, flow_up, max_disp, cp, fa)
+    return _CorrConcat.apply(f1, f2w, flow_up, max_disp, cp, fa, corr_df1_side(precision))
 
 
 # ============================================================================ warp =====

@@ -1077,21 +1077,24 @@ CORR_FORM_DEFAULT = 1      # of_set_tuning key 9: bit 0 corr_fwd_blk, bit 1 corr
 
 
 class _corr_form:
-    """Select the cost-volume kernel forms (key 9) for a block, restoring the default."""
+    """Select the cost-volume kernel forms for a block, restoring the defaults: bits 0-1 are
+    of_set_tuning key 9, bit 2 key 19 (the gather backward on 8 x 16 tiles)."""
 
     def __init__(self, form):
         self.form = form
 
     def __enter__(self):
         from optical_flow_amd import _lib
-        assert _lib.lib().of_set_tuning(9, self.form) == 0
+        assert _lib.lib().of_set_tuning(9, self.form & 3) == 0
+        assert _lib.lib().of_set_tuning(19, (self.form >> 2) & 1) == 0
 
     def __exit__(self, *exc):
         from optical_flow_amd import _lib
         _lib.lib().of_set_tuning(9, CORR_FORM_DEFAULT)
+        _lib.lib().of_set_tuning(19, 0)
 
 
-@pytest.mark.parametrize("form", [1, 3, 0])
+@pytest.mark.parametrize("form", [1, 3, 0, 5])
 @pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6), (1, 19, 70, 32),
                                    (3, 40, 56, 64), (1, 17, 35, 100)])
 def test_cost_volume(form, shape):
@@ -1126,7 +1129,7 @@ def test_cost_volume(form, shape):
                                                   (1, 4, 8, 128, 180, True),
                                                   (1, 2, 4, 256, 308, False),
                                                   (8, 48, 64, 128, 180, True)])
-@pytest.mark.parametrize("form", [1, 3, 0])
+@pytest.mark.parametrize("form", [1, 3, 0, 5])
 def test_corr_concat(form, n, h, w, c, cp, has_flow):
     """The fused concat([f1, cost volume, flow]) kernel and its gradient, for both kernel
     forms (key 9): multi-tile and ragged shapes, 1 to 8 channel slabs (and slab groups with
