@@ -784,8 +784,10 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #endif
 
 
-template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH = OF_TF_H>
+// PF (of_set_tuning key 20, default 1): the MFMA loop's fragments read one sub-step ahead.
+template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH = OF_TF_H, int PF = 1>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES_N)) void conv_tile_bf16(GemmArgs a) {
+  constexpr bool g_tile16_pf_dev = PF != 0;
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int BM = TH * TF_W, KS = 3;
   constexpr int HH = TH + KS - 1, HW = TF_W + KS - 1, HP = HH * HW;
@@ -924,19 +926,41 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES
     const int nc = c_begin + nq / KS, nr = nq % KS;
     if (more) load_b(nc, nr);
     if (r == 0 && q + KS < steps) load_halo(c_begin + q / KS + 1);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
+    // sub-step k = (tap s, K half st): its TM A and TN B fragments
+    auto frags = [&](int k, bf16x8 (&av)[TM], bf16x8 (&bv)[TN]) {
+      const int s = k >> 1, st = k & 1;
       const int dh = MODE == MODE_FWD ? r * HW + s : -(r * HW + s);
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8 av[TM], bv[TN];
+      for (int i = 0; i < TM; ++i)
+        av[i] = __builtin_bit_cast(bf16x8, Ah[(a_hp[i] + dh) * SROW16 + 2 * st + lk]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bv[j] = __builtin_bit_cast(
+            bf16x8, Bs[buf][(s * BN + wn0 + 32 * j + lrow) * SROW16 + 2 * st + lk]);
+    };
+    if (g_tile16_pf_dev) {
+      // fragments one sub-step ahead of their MFMAs (the scheduler otherwise sinks each read
+      // to its first MFMA, a ds_read latency exposed per TM x TN MFMAs); sched_barrier fences
+      bf16x8 av[2][TM], bv[2][TN];
+      frags(0, av[0], bv[0]);
+#pragma unroll
+      for (int k = 0; k < 2 * KS; ++k) {
+        const int cur = k & 1;
+        if (k + 1 < 2 * KS) frags(k + 1, av[cur ^ 1], bv[cur ^ 1]);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          av[i] = __builtin_bit_cast(bf16x8, Ah[(a_hp[i] + dh) * SROW16 + 2 * st + lk]);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          bv[j] = __builtin_bit_cast(
-              bf16x8, Bs[buf][(s * BN + wn0 + 32 * j + lrow) * SROW16 + 2 * st + lk]);
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[cur][i], bv[cur][j], acc[i][j],
+                                                                0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2 * KS; ++k) {
+        bf16x8 av[TM], bv[TN];
+        frags(k, av, bv);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1575,6 +1599,9 @@ static int g_stem_bf16 = 1;
 // output tiles of conv_tile_bf16 where the grid allows (1), as the forward does, or on 4 x 32
 // tiles (0, default).
 static int g_tall16_dgrad = 0;
+// of_set_tuning key 20: conv_tile_bf16 with its fragments read one sub-step ahead (1, default)
+// or right before their MFMAs (0, the round-1 schedule).
+static int g_tile16_pf = 1;
 bool stem_x3_ok(const of_conv_desc* d) {
   return d->kh == 7 && d->kw == 7 && d->stride == 2 && d->cin_p == 4 && d->cout == 64 &&
          d->pad_top >= 0 && d->pad_top <= 3 && d->pad_left >= 0 && d->pad_left <= 3;
@@ -2113,7 +2140,12 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_bf16(GemmArgs a) {
 // conflict-free: x rows (s, hy, ci) of 2 octets swap the octets of ci & 8; dy rows of 16
 // octets XOR the octet with co & 15.  K slice = a range of pixel tiles (a.K tiles in all).
 // Output: the same split-K slabs as conv_wgrad_bf16 (rows tap * kc + ci, bias row M).
-template <int WAVES_CI, int WAVES_CO>
+// PF = 1 (of_set_tuning key 17, default): the fragments are software-pipelined.  A tap row's
+// fragment (x row kk + r, shift s) serves the three output rows kk = row - r, so a tile needs
+// 10 x 3 distinct A reads, not 8 x 9: rows are read two output rows ahead of their first use,
+// and the tile's 8 B fragments at its start (PF = 0 read 9 A and 1 B fragment per output row
+// right before their MFMAs, the B one behind a full lgkmcnt(0) wait).
+template <int WAVES_CI, int WAVES_CO, int PF = 1>
 __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
   constexpr int CIB = 32 * WAVES_CI, COB = 32 * WAVES_CO, KS = 3, HH = TT_H + KS - 1;
   static_assert(WAVES_CI * WAVES_CO == 4 && COB >= 64, "4 waves, COB >= 64");
@@ -2263,17 +2295,51 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_tile_bf16(GemmArgs a) {
     const int buf = i & 1;
     const bool more = i + 1 < steps;
     if (more) load(t_begin + i + 1);
+    if (PF) {
+      auto afrag = [&](int row, int s) {
+        return __builtin_bit_cast(bf16x8, Xs[buf][(s * HH + row) * CIB * 2 + a_base]);
+      };
+      auto bfrag = [&](int kk) {
+        return __builtin_bit_cast(bf16x8, Ds[buf][b_base + ((2 * kk + lk) ^ b_sw)]);
+      };
+      bf16x8 bvs[TT_H], af[HH][KS];
+      bvs[0] = bfrag(0);
 #pragma unroll
-    for (int kk = 0; kk < TT_H; ++kk) {
-      const bf16x8 bv = __builtin_bit_cast(bf16x8, Ds[buf][b_base + ((2 * kk + lk) ^ b_sw)]);
+      for (int row = 0; row < KS + 1; ++row)
 #pragma unroll
-      for (int r = 0; r < KS; ++r)
+        for (int s = 0; s < KS; ++s) af[row][s] = afrag(row, s);
+      // the scheduler would otherwise sink every read to its first MFMA (one B read behind a
+      // full lgkmcnt(0) wait per output row): sched_barrier fences keep the reads of output
+      // row kk + 1's B and of x row kk + 4 ahead of row kk's 9 MFMAs
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const bf16x8 av = __builtin_bit_cast(
-              bf16x8, Xs[buf][(s * HH + kk + r) * CIB * 2 + a_base]);
-          acc[r * KS + s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[r * KS + s], 0, 0, 0);
+      for (int kk = 0; kk < TT_H; ++kk) {
+        if (kk + 1 < TT_H) bvs[kk + 1] = bfrag(kk + 1);
+        if (kk + KS + 1 < HH) {                   // x row kk + 4: first used at kk + 2
+#pragma unroll
+          for (int s = 0; s < KS; ++s) af[kk + KS + 1][s] = afrag(kk + KS + 1, s);
         }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = 0; r < KS; ++r)
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+            acc[r * KS + s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk + r][s], bvs[kk],
+                                                                      acc[r * KS + s], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < TT_H; ++kk) {
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, Ds[buf][b_base + ((2 * kk + lk) ^ b_sw)]);
+#pragma unroll
+        for (int r = 0; r < KS; ++r)
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const bf16x8 av = __builtin_bit_cast(
+                bf16x8, Xs[buf][(s * HH + kk + r) * CIB * 2 + a_base]);
+            acc[r * KS + s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[r * KS + s], 0, 0, 0);
+          }
+      }
     }
     if (more) store(buf ^ 1);
     __syncthreads();
@@ -4230,7 +4296,13 @@ int launch_tile_bf16(const GemmArgs& a, hipStream_t s, double flops) {
   const bool tall = a.bm == X3_TH0 * TF_W;
   const int cfg = bn == 128 ? (tall ? 4 : 0) : bn == 96 ? 1 : bn == 64 ? 2 : 3;
   if (timing_on()) timing_begin(s);
-  if (cfg == 4) hipLaunchKernelGGL((conv_tile_bf16<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);
+  if (!g_tile16_pf) {
+    if (cfg == 4) hipLaunchKernelGGL((conv_tile_bf16<128, 4, 2, MODE, X3_TH0, 0>), grid, dim3(512), 0, s, a);
+    else if (cfg == 0) hipLaunchKernelGGL((conv_tile_bf16<128, 2, 2, MODE, OF_TF_H, 0>), grid, block, 0, s, a);
+    else if (cfg == 1) hipLaunchKernelGGL((conv_tile_bf16<96, 4, 1, MODE, OF_TF_H, 0>), grid, block, 0, s, a);
+    else if (cfg == 2) hipLaunchKernelGGL((conv_tile_bf16<64, 2, 2, MODE, OF_TF_H, 0>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_tile_bf16<32, 4, 1, MODE, OF_TF_H, 0>), grid, block, 0, s, a);
+  } else if (cfg == 4) hipLaunchKernelGGL((conv_tile_bf16<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);
   else if (cfg == 0) hipLaunchKernelGGL((conv_tile_bf16<128, 2, 2, MODE>), grid, block, 0, s, a);
   else if (cfg == 1) hipLaunchKernelGGL((conv_tile_bf16<96, 4, 1, MODE>), grid, block, 0, s, a);
   else if (cfg == 2) hipLaunchKernelGGL((conv_tile_bf16<64, 2, 2, MODE>), grid, block, 0, s, a);
@@ -4406,6 +4478,9 @@ static int g_wgrad_wgs = 4;
 // input and weight gradients are faster (0.77 -> 0.71, 0.46 -> 0.40 ms per step), the
 // forward slower (0.31 -> 0.35 ms).
 static int g_gemm_b16 = 6;
+// of_set_tuning key 17: conv_wgrad_tile_bf16 with software-pipelined fragments (1, default)
+// or the round-1 per-row reads (0).
+static int g_wgt_pf = 1;
 bool gemm_b16_wg(const of_conv_desc* d) {
   return (g_gemm_b16 & 4) && !narrow_ok(d) && !tile_ok(d) && !(stem_wg_ok(d) && g_stem_bf16);
 }
@@ -4586,6 +4661,8 @@ int of_set_tuning(int key, int value) {
   if (key == 15 && (value == 0 || value == 1)) { g_stem_bf16 = value; return OF_OK; }
   if (key == 16 && value >= 0 && value <= 7) { g_gemm_b16 = value; return OF_OK; }
   if (key == 18 && (value == 0 || value == 1)) { g_tall16_dgrad = value; return OF_OK; }
+  if (key == 17 && (value == 0 || value == 1)) { g_wgt_pf = value; return OF_OK; }
+  if (key == 20 && (value == 0 || value == 1)) { g_tile16_pf = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -5095,7 +5172,10 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     const int cfg = wgt_cfg(d);
     dim3 grid(a.tiles_total * a.splits), block(256);
     if (timing_on()) timing_begin(s);
-    if (bf16) {
+    if (bf16 && !g_wgt_pf) {
+      if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_bf16<1, 4, 0>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((conv_wgrad_tile_bf16<2, 2, 0>), grid, block, 0, s, a);
+    } else if (bf16) {
       if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_tile_bf16<1, 4>), grid, block, 0, s, a);
       else hipLaunchKernelGGL((conv_wgrad_tile_bf16<2, 2>), grid, block, 0, s, a);
     } else {

@@ -414,6 +414,58 @@ def test_conv_gemm_b16_forms(n, h, w, cin, cout, k, s):
             assert rel_inf(dx, xo.grad) < REL_TOL, (form, rel_inf(dx, xo.grad))
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 40, 70, 64, 64), (1, 24, 48, 128, 96),
+                                             (8, 96, 128, 128, 128), (2, 17, 20, 64, 32),
+                                             (4, 64, 96, 115, 128), (8, 128, 256, 128, 128)])
+def test_conv_bf16_prefetch_forms(n, h, w, cin, cout):
+    """The bf16 3x3 kernels with their MFMA fragments read ahead (conv_tile_bf16 PF = 1,
+    of_set_tuning key 20; conv_wgrad_tile_bf16 PF = 1, key 17; the defaults) do the same MFMAs
+    in the same order as the round-1 schedules (keys = 0): forward, input and weight gradients
+    bitwise equal, on every channel-tile form, ragged tiles and the tall forward tiles."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_LEAKY, call
+    lib = _lib.lib()
+    cin_p = (cin + 3) // 4 * 4
+    x = torch.zeros(n, h, w, cin_p)
+    x[..., :cin] = rng_tensor((n, h, w, cin), 121)
+    wt = rng_tensor((3, 3, cin, cout), 122, scale=(2.0 / (9 * cin)) ** 0.5)
+    layer = ops.ConvLayer(dev(wt), dev(rng_tensor((cout,), 123, scale=0.1)), stride=1,
+                          act=ACT_LEAKY, cin_p=cin_p, precision="bf16")
+    d = layer.desc(n, h, w)
+    cout_p = (cout + 3) // 4 * 4
+    dy = torch.zeros(n, h, w, cout_p)
+    dy[..., :cout] = rng_tensor((n, h, w, cout), 124)
+    xd, dyd = dev(x), dev(dy)
+    wf, wd = layer.packed(d)
+    P, st = ops._ptr, ops._stream()
+    res = {}
+    try:
+        for form in (1, 0):
+            assert lib.of_set_tuning(17, form) == 0 and lib.of_set_tuning(20, form) == 0
+            fent, fws = layer.fwd_entry(d)
+            dent, dws = layer.dgrad_entry(d)
+            went, wws = layer.wgrad_entry(d)
+            ws = torch.empty(max(fws, dws, wws) // 4 + 4, device="cuda")
+            y = torch.empty(n, h, w, cout, device="cuda")
+            dx = torch.empty(n, h, w, cin_p, device="cuda")
+            dw = torch.empty(3, 3, cin, cout, device="cuda")
+            db = torch.empty(cout, device="cuda")
+            call(fent, C.byref(d), P(xd), cin_p, P(wf), P(layer.bias), None, None, None, None,
+                 1e-3, None, 0, ACT_LEAKY, 0.3, None, 0, P(y), cout, P(ws), fws, st)
+            call(dent, C.byref(d), P(dyd), cout_p, P(wd), P(xd), cin_p, ACT_LEAKY, 0.3, P(dx),
+                 cin_p, P(ws), dws, st)
+            call(went, C.byref(d), P(xd), cin_p, P(dyd), cout_p, P(dw), P(db), 0, P(ws), wws, st)
+            torch.cuda.synchronize()
+            res[form] = [t.cpu() for t in (y, dx, dw, db)]
+    finally:
+        lib.of_set_tuning(17, 1)
+        lib.of_set_tuning(20, 1)
+    for a_, b_, what in zip(res[1], res[0], ("fwd", "dgrad", "wgrad", "bias grad")):
+        assert torch.equal(a_, b_), what
+
+
 @pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (3, 38, 130), (8, 384, 512)])
 def test_conv_stem_b16(n, h, w):
     """The bf16 stem (configs 3-5) on the one-plane stem kernels (conv_stem_x3<32, 1>,
