@@ -169,16 +169,19 @@ def kernel_symbol(kind):
             return "void oflow::conv_wgrad_x3<%s, %d>(oflow::GemmArgs)" % (GX3_WG[cfg], np_)
         return "void oflow::conv_gemm_x3<%s, %d, %d>(oflow::GemmArgs)" % (GX3[cfg], mode, np_)
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
-        return "void oflow::conv_wgrad_%s<%s>(oflow::GemmArgs)" % (
+        # the bf16 form prints its defaulted fragment-prefetch flag too (PF = 1, key 17)
+        return "void oflow::conv_wgrad_%s<%s%s>(oflow::GemmArgs)" % (
             fam + ("b" if fam == "tile_x3" and cfg >= 4 else ""),
-            X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg])
+            X3_WGT[cfg] if fam == "tile_x3" else WGT_WAVES[cfg],
+            ", 1" if fam == "tile_bf16" else "")
     if fam in ("tile_bf16", "tile_x3"):
         if fam == "tile_x3":
             # the demangled name prints the defaulted NB too (conv_tile_x3<..., TH, NB>)
             return "void oflow::conv_tile_x3<%s, %d, %d, %d>(oflow::GemmArgs)" % (
                 X3_BN[cfg], mode, X3_TH[cfg], X3_NB.get(cfg, 2))
-        return "void oflow::conv_tile_bf16<%s, %d, %d>(oflow::GemmArgs)" % (TILE_BN[cfg], mode,
-                                                                            TILE_TH[cfg])
+        # (with its defaulted fragment-prefetch flag, PF = 1, of_set_tuning key 20)
+        return "void oflow::conv_tile_bf16<%s, %d, %d, 1>(oflow::GemmArgs)" % (TILE_BN[cfg], mode,
+                                                                               TILE_TH[cfg])
     if fam == "bf16" and mode == 2:
         return "void oflow::conv_wgrad_bf16<%s>(oflow::GemmArgs)" % TILE_TEMPLATE[cfg]
     return "void oflow::conv_gemm_%s<%s, %d>(oflow::GemmArgs)" % (fam, TILE_TEMPLATE[cfg], mode)
