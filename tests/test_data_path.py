@@ -249,9 +249,13 @@ def test_read_kitti_listing(lib, tmp_path):
     assert all("image_03" in b for _, b in first[3:])
 
 
-def _reader(tmp_path, batch=4, seed=7, nworkers=3, nslots=2):
+def _reader(tmp_path, batch=4, seed=7, nworkers=3, nslots=2, content=None):
+    """An AsyncReader over tmp_path's KITTI tree, written first unless ``content`` (the tree's
+    frames, already on disk) is given: a reader's worker threads start decoding at once, so a
+    second reader must not rewrite the files under the first one."""
     from optical_flow_amd.data_reader import AsyncReader, ReaderOpts
-    content = make_kitti(str(tmp_path))
+    if content is None:
+        content = make_kitti(str(tmp_path))
     opts = ReaderOpts(str(tmp_path), batch, 16, 24, nworkers, seed=seed, nslots=nslots)
     return AsyncReader(opts, pinned=False), content
 
@@ -282,9 +286,9 @@ def test_async_reader_epochs_and_swaps(lib, tmp_path):
 
 
 def test_async_reader_is_deterministic(lib, tmp_path):
-    a, _ = _reader(tmp_path, seed=11)
-    b, _ = _reader(tmp_path, seed=11)
-    c, _ = _reader(tmp_path, seed=12)
+    a, content = _reader(tmp_path, seed=11)
+    b, _ = _reader(tmp_path, seed=11, content=content)
+    c, _ = _reader(tmp_path, seed=12, content=content)
     order = {}
     for name, r in (("a", a), ("b", b), ("c", c)):
         with r:
