@@ -15,6 +15,9 @@ namespace oflow {
 #ifndef BNP_UNROLL
 #define BNP_UNROLL 4   // 4 pixel rows of 3 float4 loads in flight per thread (2: -8 % on the step's BN backward)
 #endif
+#ifndef MPB_UNROLL
+#define MPB_UNROLL 2   // the stem's max-pool + BN backward: 2 pooled pixels (18 float4 loads) in flight
+#endif
 constexpr int RED_TARGET_BLOCKS = RED_BLOCKS;
 
 struct RedGeo {
@@ -239,6 +242,7 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
       bt = *reinterpret_cast<const float4*>(beta + ch);
       ig = make_float4(1.f / gm.x, 1.f / gm.y, 1.f / gm.z, 1.f / gm.w);
     }
+#pragma unroll MPB_UNROLL
     for (int64_t p = p0 + r; p < p1; p += rows) {
       const int ox = (int)(p % wo);
       const int64_t t2 = p / wo;
