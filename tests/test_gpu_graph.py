@@ -89,7 +89,10 @@ def test_graph_matches_eager(precision, comm):
         print("%s %s replay %d: loss %.7e vs eager %.7e, grads rel_l2 %.2e, weights %.2e" % (
             precision, comm, k, float(lg), float(le), eg, ew))
         assert abs(float(lg) - float(le)) <= 1e-6 * abs(float(le))
-        assert eg < 1e-4, eg
+        # bf16: the warp backward's atomic-order noise (one fp32 ulp) can flip the bf16
+        # rounding of a gradient element the next conv reads (a 2^-8 relative step), so the
+        # gradients of two identical steps differ by up to ~2e-4 rel_l2 (measured 1.6e-4)
+        assert eg < (1e-4 if precision == "fp32" else 1e-3), eg
         assert ew < 1e-5, ew
     assert gt.optimizer.iterations == 5
     if c is not None:
