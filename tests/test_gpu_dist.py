@@ -145,5 +145,6 @@ def test_rccl_dp_step_world1(precision, H, W, B):
     assert loss == loss_ref
     err = ((got - ref).norm() / ref.norm()).item()
     print("%s RCCL world-1 step vs plain step: grad rel_l2 %.2e, %d buckets" % (precision, err, nb))
-    assert err < 1e-5, err
+    # (bf16: the atomic-order noise can flip bf16 roundings downstream, test_gpu_graph.py)
+    assert err < (1e-5 if precision == "fp32" else 1e-4), err
     comm.close()
