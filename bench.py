@@ -270,6 +270,27 @@ def cpu_baseline(batch_np, vals, steps=3, precision="fp32", levels=4, max_s=60.0
     return n * x.shape[0] / dt, threads, total, n, flows0, float(loss0)
 
 
+def final_parity(pair_np, params, flows_hip, precision="fp32", levels=4):
+    """EPE / relative error of the HIP forward against the oracle's forward (float64; for bf16
+    with the build's bf16 operand rounding) on one pair at the weights the timed steps ended
+    with -- the parity probe above checks only the initial weights."""
+    from oracle import ref_flow as R
+    from optical_flow_amd.params import encoder_blocks
+    p = {k: v.double() for k, v in params.items()}
+    R.set_conv_precision(precision)
+    try:
+        with torch.no_grad():
+            fo = R.flow_net(torch.tensor(pair_np, dtype=torch.float64), p,
+                            list(encoder_blocks(levels)))
+    finally:
+        R.set_conv_precision("fp32")
+    epe = [float((a.double() - b).norm(dim=-1).mean()) for a, b in zip(flows_hip, fo)]
+    rel = [float((a.double() - b).abs().max() / b.abs().max()) for a, b in zip(flows_hip, fo)]
+    return {"epe": [round(e, 6) for e in epe], "flow_rel_inf": [float("%.3e" % r) for r in rel],
+            "note": "HIP forward vs the oracle's, pair 0 of the bench batch, the weights after "
+                    "the last timed step"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -298,10 +319,14 @@ def main():
                          "launches through the Python glue")
     ap.add_argument("--side-stream", type=int, choices=[0, 1], default=1,
                     help="1: weight-gradient kernels on a second HIP stream (ops.side_stream)")
+    ap.add_argument("--deterministic", type=int, choices=[0, 1], default=0,
+                    help="1: the deterministic (sort + fixed-order gather) warp backward "
+                         "(ops.DETERMINISTIC)")
     args = ap.parse_args()
 
     from optical_flow_amd import _lib, ops
     ops.SIDE_STREAM_WGRAD = bool(args.side_stream)
+    ops.set_deterministic(bool(args.deterministic))
     if args.tune:
         for kv in args.tune.split(","):
             k, v = kv.split("=")
@@ -373,10 +398,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     timed_from = max(0, args.steps - args.timing_steps)      # the last timing_steps steps
+    first = None                    # (loss, flows) of the first timed step, read afterwards
     t0 = time.perf_counter()
     for i in range(args.steps):
         if graphed is not None:
             loss, flows = graphed()
+            if i == 0:
+                first = (loss.clone(), [f.clone() for f in flows])
             continue
         if live and i == timed_from:
             ops.TIMING_TAGS = []
@@ -385,6 +413,8 @@ def main():
             else:                                   # fallback: every conv launch
                 lib.of_timing_enable(1)
         loss, flows = trainer.train_step(batch, args.warmup + i)
+        if i == 0:
+            first = (loss, flows)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if live:
@@ -399,8 +429,17 @@ def main():
     pairs = world * B * args.steps
     value = pairs / elapsed
     final_loss = float(loss)
-    # the warp backward's atomics depend on where the flows send samples (clipped borders)
+    # The training state the timed steps ran in (the warp backward's work depends on where
+    # the flows send samples: clipped borders): loss and mean / max |flow| per level at the
+    # first and the last timed step.  From this start the reference semantics themselves
+    # diverge at the coarse levels within ~20 steps (profiles/r4_oracle_traj_f32.jsonl).
     flow_abs = [[round(float(f.abs().mean()), 4), round(float(f.abs().max()), 3)] for f in flows]
+    timed_state = {"first": {"loss": float(first[0]),
+                             "flow_abs_mean": [round(float(f.abs().mean()), 4) for f in first[1]]},
+                   "last": {"loss": final_loss,
+                            "flow_abs_mean": [round(float(f.abs().mean()), 4) for f in flows]},
+                   "train_steps_before_first": args.warmup + (1 if live else 0) +
+                                               (3 if graphed is not None else 0)}
 
     # ---- dominant-kernel roofline ------------------------------------------------------------
     nsteps = args.steps - timed_from
@@ -475,6 +514,12 @@ def main():
                                 "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
                                for k, v in sorted(table.items())}}
 
+    # ---- parity probe at the final weights: HIP forward of one pair (the oracle runs after
+    # the timed region, below) -------------------------------------------------------------
+    with torch.no_grad():
+        flows_fin = [f.cpu() for f in net(batch[:1])]
+    params_fin = {k: v.detach().cpu() for k, v in net.store.params.items()}
+
     # ---- CPU baseline + EPE vs the oracle (rank 0 only) ----------------------------------
     cpu = None
     parity = None
@@ -495,6 +540,8 @@ def main():
                   "note": "HIP %s vs CPU oracle (%s operand rounding), the bench batch (B=%d) "
                           "and initial weights, flows [H/2 ... H/%d]" % (
                               args.precision, args.precision, B, 2 ** args.levels)}
+        parity["final_weights"] = final_parity(batch[:1].cpu().numpy(), params_fin, flows_fin,
+                                               args.precision, args.levels)
 
     gfp = gflop_per_pair(H, W, levels=args.levels)
     if rank == 0:
@@ -519,12 +566,14 @@ def main():
                        "conv_math": conv_math(args.precision),
                        "execution": ("HIP graph: the train step captured once, replayed per step"
                                      if graphed is not None else "eager launches"),
+                       "warp_backward": "deterministic" if ops.DETERMINISTIC else "atomic",
                        **({"levels": args.levels} if args.levels != 4 else {})},
             "algorithmic_gflop_per_pair": round(gfp, 2),
             "model_tflops": round(gfp * value / 1e3, 2),
             "conv_ms_per_step": round(conv_ms_step, 3),
             "final_loss": final_loss,
             "flow_abs_mean_max": flow_abs,
+            "timed_state": timed_state,
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,

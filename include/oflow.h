@@ -194,8 +194,10 @@ int of_colsum(const float* x, int64_t npix, int c, int ld, float* out, int accum
 
 /* Inference BatchNorm + (residual) + activation backward (model.py:14-15, resnet blocks):
  * dt = dy * act'(y) (act: OF_ACT_NONE or OF_ACT_RELU); dres = dt (if dres);
- * dz = dt * gamma*invstd; dgamma = sum dt*(z-mean)*invstd; dbeta = sum dt; dbias = sum dz
- * (each of the three [c] vectors optional; accumulate != 0 adds into them).
+ * dz = dt * gamma*invstd (if dz); dgamma = sum dt*(z-mean)*invstd; dbeta = sum dt;
+ * dbias = sum dt * gamma*invstd (each of the three [c] vectors optional; accumulate != 0 adds
+ * into them).  With dz == NULL and dres this is of_bn_bwd_reduce from the stored z: the
+ * layers whose gamma came near 0 (ops.BNZGuard), where zhat cannot be recovered from y.
  * y, z, dy, dz, dres dense [npix][c]; workspace: of_bn_act_bwd_workspace(npix, c) bytes. */
 size_t of_bn_act_bwd_workspace(int64_t npix, int c);
 int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
@@ -266,6 +268,18 @@ int of_bilinear_fwd(const float* inp, int n, int h, int w, int c, const float* p
                     void* stream);
 int of_bilinear_bwd(const float* dout, const float* inp, int n, int h, int w, int c,
                     const float* pts, float* dinp, float* dpts, void* stream);
+/* Deterministic mode of the three backward entry points above (no atomics in the
+ * warp backward; the gradient of the gathers of transformations.py:110-113,128): the scatter
+ * into dinp becomes a stable sort of the (source pixel, corner) entries by destination and a
+ * fixed-order gather, so the result is bitwise reproducible.  dinp is WRITTEN (not accumulated;
+ * NULL skips it), dflow = d/d(flow) (+ dflow_add with row stride ld_add if non-NULL);
+ * absolute != 0: flow holds absolute (x, y) sampling points (of_bilinear_bwd).  Workspace:
+ * of_warp_bwd_det_workspace(n, h, w, c) bytes. */
+size_t of_warp_bwd_det_workspace(int n, int h, int w, int c);
+int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, int c,
+                    const float* flow, int absolute, float* dinp, float* dflow,
+                    const float* dflow_add, int ld_add, void* workspace, size_t ws_bytes,
+                    void* stream);
 
 /* upscale_flow (model.py:76-77; P6, P7): out = resize_bilinear_x2(in) * scale, half-pixel
  * centres.  in: [n][h][w][c] dense, out: [n][2h][2w] pixels of ldo (channel slice). */
@@ -467,6 +481,12 @@ int of_bn_bwd_reduce(int64_t npix, int c, int act, const float* dy, const float*
                      const float* res, const float* gamma, const float* beta, const float* var,
                      float eps, float* t_out, float* dgamma, float* dbeta, float* dbias,
                      int accumulate, void* workspace, void* stream);
+/* Recovering zhat = (y - res - beta) / gamma from y loses precision as |gamma| -> 0 (and is
+ * undefined at 0); the host keeps z for a BN layer once any of its gammas falls below a
+ * threshold (ops.BNZGuard).  This gives min |gamma| per layer in one launch: out[i] =
+ * min |dev_ptrs[i][0 .. dev_lens[i])| (both arrays in device memory). */
+int of_min_abs_segments(const float* const* dev_ptrs, const int* dev_lens, int nseg, float* out,
+                        void* stream);
 /* of_maxpool_bn_act_bwd without z (zhat from y) for the stem: conv1 -> BN -> ReLU -> max-pool. */
 int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const float* g,
                            const float* y, const float* gamma, const float* beta,

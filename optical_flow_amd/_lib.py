@@ -75,6 +75,7 @@ PROTOTYPES = {
     "of_colsum": (I, [P, I64, I, I, P, I, P, P]),
     "of_bn_act_bwd_workspace": (SZ, [I64, I]),
     "of_bn_act_bwd": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, P, I, P, P]),
+    "of_min_abs_segments": (I, [P, P, I, P, P]),
     "of_maxpool_bn_act_bwd_workspace": (SZ, [I, I, I, I]),
     "of_maxpool_bn_act_bwd": (I, [I, I, I, I, P, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     "of_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
@@ -89,6 +90,8 @@ PROTOTYPES = {
     "of_warp_bwd_add": (I, [P, P, I, I, I, I, P, P, P, P, I, P]),
     "of_bilinear_fwd": (I, [P, I, I, I, I, P, P, P]),
     "of_bilinear_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
+    "of_warp_bwd_det_workspace": (SZ, [I, I, I, I]),
+    "of_warp_bwd_det": (I, [P, P, I, I, I, I, P, I, P, P, P, I, P, SZ, P]),
     "of_upscale2x_fwd": (I, [P, I, I, I, I, F, P, I, P]),
     "of_upscale2x_bwd": (I, [P, I, I, I, I, I, F, P, I, P]),
     "of_upscale2x_bwd_ld": (I, [P, I, I, I, I, I, F, P, I, I, P]),

@@ -592,7 +592,7 @@ int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
                   const float* z, const float* gamma, const float* mean, const float* var,
                   float eps, float* dz, float* dres, float* dgamma, float* dbeta, float* dbias,
                   int accumulate, void* workspace, void* stream) {
-  OF_CHECK_ARG(dy && y && z && gamma && mean && var && dz && workspace, "bn_act_bwd: args");
+  OF_CHECK_ARG(dy && y && z && gamma && mean && var && workspace, "bn_act_bwd: args");
   OF_CHECK_ARG(act == OF_ACT_NONE || act == OF_ACT_RELU, "bn_act_bwd: act must be none/relu");
   OF_CHECK_ARG(c % 4 == 0 && npix > 0, "bn_act_bwd: c must be a multiple of 4");
   OF_CHECK_ARG((((uintptr_t)dy | (uintptr_t)y | (uintptr_t)z | (uintptr_t)dz |
@@ -611,6 +611,33 @@ int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
   return check_launch("bn_act_bwd_final");
 }
 
+
+// min |x| over each of nseg segments (the BN gammas of a network, ptrs / lens in device
+// memory): one workgroup per segment, a fixed-order reduction.
+__global__ __launch_bounds__(256) void min_abs_segments_kernel(const float* const* ptrs,
+                                                               const int* lens,
+                                                               float* __restrict__ out) {
+  __shared__ float red[256];
+  const float* p = ptrs[blockIdx.x];
+  const int n = lens[blockIdx.x];
+  float m = INFINITY;
+  for (int i = threadIdx.x; i < n; i += 256) m = fminf(m, fabsf(p[i]));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fminf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+int of_min_abs_segments(const float* const* dev_ptrs, const int* dev_lens, int nseg, float* out,
+                        void* stream) {
+  OF_CHECK_ARG(dev_ptrs && dev_lens && out && nseg > 0, "min_abs_segments: args");
+  hipLaunchKernelGGL(min_abs_segments_kernel, dim3(nseg), dim3(256), 0, as_stream(stream),
+                     dev_ptrs, dev_lens, out);
+  return check_launch("min_abs_segments");
+}
 
 size_t of_maxpool_bn_act_bwd_workspace(int n, int h, int w, int c) {
   return of_bn_act_bwd_workspace((int64_t)n * (h / 2) * (w / 2), c);

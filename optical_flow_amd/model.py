@@ -81,6 +81,7 @@ class ParamStore:
                 v = self.buffers[o:o + p.size].view(p.shape)
             self.params[p.name] = v
         self.version = 0
+        self.bn_guard = None        # ops.BNZGuard, made by the model on its first forward
         self.load(values)
 
     def __getitem__(self, name) -> torch.Tensor:
@@ -103,6 +104,8 @@ class ParamStore:
             assert tuple(t.shape) == tuple(self.spec[n].shape), (n, t.shape, self.spec[n].shape)
             self.params[n].copy_(t.to(self.params[n].device))
         self.version += 1
+        if self.bn_guard is not None:        # new gammas: check them before the next step
+            self.bn_guard.check_now()
 
     def state(self) -> "OrderedDict[str, np.ndarray]":
         return OrderedDict((n, self.params[n].detach().cpu().numpy()) for n in self.spec)
@@ -360,6 +363,9 @@ class FlowNet:
         assert batch_imgs.shape[3] == 6
         if self._packer is None:
             self._packer = ops.ConvPacker(self.conv_layers(), lambda: self.store.version)
+        if self.store.bn_guard is None:              # z kept for BN layers with gamma ~ 0
+            self.store.bn_guard = ops.BNZGuard(self.conv_layers())
+        self.store.bn_guard.poll()
         self._packer.ensure()                        # all conv weights packed in one launch
         imgs = ops.split_pair(batch_imgs)            # image1s then image2s (model.py:122-123)
         feats = self.encoder.forward4(imgs)          # shared encoder, both images (P12)

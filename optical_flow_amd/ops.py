@@ -45,6 +45,31 @@ def _tag(layer, kind):
         TIMING_TAGS.append((layer.name, kind))
 
 
+# Deterministic mode: the feature-warp backward -- the only kernel of the step
+# that adds with float atomics (the scatter-add gradient of the gathers of
+# transformations.py:110-113,128) -- runs as a stable sort + fixed-order gather
+# (of_warp_bwd_det), so a train step is bitwise reproducible run to run, eager or replayed
+# from a graph.  Every other reduction of the step is fixed-order already.  Off by default
+# (DESIGN.md §3 gives its cost); OFLOW_DETERMINISTIC=1 or set_deterministic(True) turns it on.
+DETERMINISTIC = os.environ.get("OFLOW_DETERMINISTIC", "0") == "1"
+
+
+def set_deterministic(on: bool = True) -> bool:
+    """Select the deterministic warp backward; returns the previous setting."""
+    global DETERMINISTIC
+    prev, DETERMINISTIC = DETERMINISTIC, bool(on)
+    return prev
+
+
+@contextlib.contextmanager
+def deterministic(on: bool = True):
+    prev = set_deterministic(on)
+    try:
+        yield
+    finally:
+        set_deterministic(prev)
+
+
 def _workspace(nbytes: int, device):
     """Scratch for one launch: (tensor keeping it alive, pointer, bytes).  The caching
     allocator is stream-ordered, so the block is only reused after this stream's kernel."""
@@ -287,6 +312,7 @@ class ConvLayer:
         self._bf16 = None
         self._mode = None
         self.f32_split = F32_SPLIT if f32_split is None else bool(f32_split)
+        self.store_z = False              # BN layers: keep z for the backward (BNZGuard)
 
     def desc(self, n, h, w) -> ConvDesc:
         key = (n, h, w)
@@ -432,6 +458,86 @@ class ConvPacker:
         self._version = v
 
 
+class BNZGuard:
+    """Keeps z (the pre-BN conv output) for the BN layers whose gamma came near 0.
+
+    The inference-BN backward recovers the normalised value from the layer output,
+    zhat = (y - res - beta) / gamma (of_bn_bwd_reduce): exact while |gamma| is not small, but
+    its error grows like eps (|beta| + |res|) / |gamma zhat| and it is undefined at gamma = 0,
+    where the reference's FusedBatchNormGrad (model.py:14, trained by train.py:55-56) still
+    reads the stored z.  This guard watches min |gamma| of every BN layer on the device (one
+    launch, of_min_abs_segments, every EVERY optimizer steps, read back through pinned memory
+    without a sync) and switches a layer to storing z -- for good -- once it falls below the
+    threshold; its backward then reads z (of_bn_act_bwd / of_maxpool_bn_act_bwd).  The
+    threshold covers the lag: Keras Adam moves a weight by at most a few lr per step, and a
+    check older than LAG_MAX steps is waited for.  Not active inside a HIP-graph capture (the
+    mode is the one in force when the graph was captured)."""
+    GAMMA_MIN = 1e-2
+    EVERY = 4
+    LAG_MAX = 8
+
+    def __init__(self, layers):
+        self.layers = [L for L in layers if L.bn is not None]
+        self.pending = []
+        self.steps = 0
+        if not self.layers:
+            return
+        dev = self.layers[0].kernel.device
+        self.ptrs = torch.tensor([L.bn[0].data_ptr() for L in self.layers], dtype=torch.int64,
+                                 device=dev)
+        self.lens = torch.tensor([L.bn[0].numel() for L in self.layers], dtype=torch.int32,
+                                 device=dev)
+        self.out = torch.empty(len(self.layers), device=dev)
+        self.check_now()
+
+    def threshold(self, lr):
+        return max(self.GAMMA_MIN, 4.0 * lr * (self.EVERY + self.LAG_MAX))
+
+    def _launch(self):
+        call("of_min_abs_segments", _ptr(self.ptrs), _ptr(self.lens), len(self.layers),
+             _ptr(self.out), _stream())
+
+    def _apply(self, mins, thr):
+        for L, m in zip(self.layers, mins):
+            if m < thr and not L.store_z:
+                L.store_z = True
+
+    def check_now(self, lr=1e-4):
+        """Synchronous check (construction, weight loading)."""
+        if not self.layers:
+            return
+        self._launch()
+        self._apply(self.out.cpu().tolist(), self.threshold(lr))
+
+    def after_update(self, lr):
+        if not self.layers or torch.cuda.is_current_stream_capturing():
+            return
+        self.steps += 1
+        if self.steps % self.EVERY:
+            return
+        self._launch()
+        host = torch.empty(len(self.layers), pin_memory=True)
+        host.copy_(self.out, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((self.steps, ev, host, lr))
+
+    def poll(self):
+        if torch.cuda.is_current_stream_capturing():
+            return
+        while self.pending:
+            st, ev, host, lr = self.pending[0]
+            if not ev.query():
+                if self.steps - st < self.LAG_MAX:
+                    return
+                ev.synchronize()
+            self.pending.pop(0)
+            self._apply(host.tolist(), self.threshold(lr))
+
+    def stored(self):
+        return [L.name for L in self.layers if L.store_z]
+
+
 def _pad_channels(t: torch.Tensor, cp: int) -> torch.Tensor:
     """Copy an NHWC tensor into a zero-padded one with cp channels (the conv ABI reads
     round_up(C,4) channels)."""
@@ -456,8 +562,10 @@ def _conv_forward(layer: "ConvLayer", x, residual=None):
     d = layer.desc(n, h, w)
     wf, _ = layer.packed(d)
     y = torch.empty((n, d.ho, d.wo, layer.cout), device=x.device)
-    z = None      # BN layers: z is not stored, the backward recovers zhat from y (_conv_backward)
     bn = layer.bn
+    # BN layers: z is not stored, the backward recovers zhat from y (_conv_backward) -- unless
+    # a gamma of the layer came near 0 (BNZGuard), where that recovery loses its precision
+    z = torch.empty_like(y) if (bn is not None and layer.store_z) else None
     if residual is not None:
         residual = residual.contiguous()
         assert residual.shape == y.shape
@@ -520,16 +628,26 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
             dz = dy                     # already t
             # only parameter gradients come out: off the critical path (BN_REDUCE_SIDE)
             side = BN_REDUCE_SIDE and SIDE_STREAM_WGRAD and acc == 1
-            with torch.cuda.stream(side_stream(dz, y, res_src, ws)) if side else \
+            with torch.cuda.stream(side_stream(dz, y, res_src, ws, z)) if side else \
                     contextlib.nullcontext():
-                call("of_bn_bwd_reduce", npix, layer.cout, ACT_NONE, _ptr(dz), _ptr(y),
-                     _ptr(res_src), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, None,
-                     _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
+                if z is not None:       # zhat from the stored z (BNZGuard)
+                    call("of_bn_act_bwd", npix, layer.cout, ACT_NONE, _ptr(dz), _ptr(y), _ptr(z),
+                         _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, None, None, _ptr(tg[0]),
+                         _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
+                else:
+                    call("of_bn_bwd_reduce", npix, layer.cout, ACT_NONE, _ptr(dz), _ptr(y),
+                         _ptr(res_src), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, None,
+                         _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
         else:
             dz = torch.empty_like(dy)    # t = dy * act'(y)
-            call("of_bn_bwd_reduce", npix, layer.cout, layer.act, _ptr(dy), _ptr(y),
-                 _ptr(res_src), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, _ptr(dz),
-                 _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
+            if z is not None:
+                call("of_bn_act_bwd", npix, layer.cout, layer.act, _ptr(dy), _ptr(y), _ptr(z),
+                     _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, None, _ptr(dz), _ptr(tg[0]),
+                     _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
+            else:
+                call("of_bn_bwd_reduce", npix, layer.cout, layer.act, _ptr(dy), _ptr(y),
+                     _ptr(res_src), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, _ptr(dz),
+                     _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), s)
         if has_res and need_res:
             dres = dz                   # the residual branch's gradient is t itself
         bias_done = True
@@ -794,9 +912,14 @@ class _EncoderFn(torch.autograd.Function):
         dz0 = torch.empty_like(y0)
         ws = torch.empty(_lib.lib().of_maxpool_bn_act_bwd_workspace(n, h, w, c) // 4 + 1,
                          device=y0.device)
-        call("of_maxpool_bn_relu_bwd", n, h, w, c, _ptr(dy.contiguous()), _ptr(gouts[0]),
-             _ptr(y0), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, _ptr(dz0), _ptr(tg[0]),
-             _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
+        if z0 is not None:              # zhat from the stored z (BNZGuard)
+            call("of_maxpool_bn_act_bwd", n, h, w, c, _ptr(dy.contiguous()), _ptr(gouts[0]),
+                 _ptr(y0), _ptr(z0), _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, _ptr(dz0),
+                 _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
+        else:
+            call("of_maxpool_bn_relu_bwd", n, h, w, c, _ptr(dy.contiguous()), _ptr(gouts[0]),
+                 _ptr(y0), _ptr(gamma), _ptr(beta), _ptr(var), BN_EPS, _ptr(dz0), _ptr(tg[0]),
+                 _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
         _, gk, _, _, _, _ = _conv_backward(conv1, x4, y0, z0, None, False,
                                            (False, nk, nbias, ng, nbe, False), dz_given=dz0)
         stem = [gk, tbias[2], tg[2], tb[2]]
@@ -1116,9 +1239,22 @@ class _Warp(torch.autograd.Function):
         dinp = None
         if ctx.needs_input_grad[0]:
             dinp = new_grad(ctx.dst, inp)
-            call("of_fill", _ptr(dinp), 0.0, dinp.numel(), s)
         dflow = torch.empty_like(flow)
         fa = ctx.fa
+        if DETERMINISTIC:       # sort-based fixed-order gather: dinp written, no fill
+            add, ld = None, 0
+            if fa is not None and fa.addend is not None and ctx.needs_input_grad[1]:
+                dcat, off, ld = fa.addend
+                add = C.c_void_p(dcat.data_ptr() + 4 * off)
+                fa.addend = None
+            wsk, wsp, wsb = _workspace(
+                _lib.lib().of_warp_bwd_det_workspace(n, h, w, c) if dinp is not None else 0,
+                dout.device)
+            call("of_warp_bwd_det", _ptr(dout), _ptr(inp), n, h, w, c, _ptr(flow),
+                 int(ctx.absolute), _ptr(dinp), _ptr(dflow), add, ld, wsp, wsb, s)
+            return dinp, (dflow if ctx.needs_input_grad[1] else None), None, None
+        if dinp is not None:
+            call("of_fill", _ptr(dinp), 0.0, dinp.numel(), s)
         if fa is not None and fa.addend is not None and ctx.needs_input_grad[1]:
             dcat, off, ld = fa.addend            # the concat's flow slice (FlowAdd)
             call("of_warp_bwd_add", _ptr(dout), _ptr(inp), n, h, w, c, _ptr(flow), _ptr(dinp),

@@ -74,6 +74,8 @@ class KerasAdam:
              C.c_void_p(self._iter.data_ptr()), self.beta_1, self.beta_2, self.epsilon,
              grad_scale, ops._stream())
         s.version += 1       # packed conv weights are refreshed lazily on next use
+        if getattr(s, "bn_guard", None) is not None:
+            s.bn_guard.after_update(self._lr)
 
 
 class Trainer:

@@ -126,18 +126,22 @@ def _grads(precision, H, W, B, comm=None, seed=0):
     return net.store.grad_arena.clone(), float(loss), launched_mid, trainer
 
 
+@pytest.mark.parametrize("det", [False, True], ids=["atomic", "det"])
 @pytest.mark.parametrize("precision,H,W,B", [("fp32", 64, 128, 2), ("bf16", 384, 512, 32)],
                          ids=["fp32_64x128_b2", "bf16_384x512_b32"])
-def test_rccl_dp_step_world1(precision, H, W, B):
+def test_rccl_dp_step_world1(precision, H, W, B, det):
     """A train step whose gradient buckets are all-reduced over a one-rank RCCL communicator
     during the backward (the bench's --gpus N path at N=1): the buckets launch progressively
     on the weight-gradient side stream, the gradients equal the step without data parallelism
     (scale 1, up to the feature-warp backward's atomic-order noise), for the fp32 config and
-    the bf16 B=32 config 3."""
+    the bf16 B=32 config 3.  det: with the deterministic warp backward the two steps must
+    agree BITWISE."""
+    from optical_flow_amd import ops
     from optical_flow_amd.comm import RcclComm
-    ref, loss_ref, _, _ = _grads(precision, H, W, B)
-    comm = RcclComm(0, 1)
-    got, loss, mid, trainer = _grads(precision, H, W, B, comm=comm)
+    with ops.deterministic(det):
+        ref, loss_ref, _, _ = _grads(precision, H, W, B)
+        comm = RcclComm(0, 1)
+        got, loss, mid, trainer = _grads(precision, H, W, B, comm=comm)
     nb = len(trainer.reducer.buckets)
     assert trainer.reducer.comm is comm and trainer.reducer.world == 1
     assert nb >= 3 and 0 < mid[len(mid) // 2] < nb, (nb, mid[len(mid) // 2])
@@ -145,6 +149,8 @@ def test_rccl_dp_step_world1(precision, H, W, B):
     assert loss == loss_ref
     err = ((got - ref).norm() / ref.norm()).item()
     print("%s RCCL world-1 step vs plain step: grad rel_l2 %.2e, %d buckets" % (precision, err, nb))
-    # (bf16: the atomic-order noise can flip bf16 roundings downstream, test_gpu_graph.py)
-    assert err < (1e-5 if precision == "fp32" else 1e-4), err
+    if det:
+        assert torch.equal(got, ref), err
+    else:
+        assert err < 1e-5, err
     comm.close()

@@ -59,9 +59,10 @@ def _sync_state(dst, src):
         getattr(dst.optimizer, name).copy_(getattr(src.optimizer, name))
 
 
+@pytest.mark.parametrize("det", [False, True], ids=["atomic", "det"])
 @pytest.mark.parametrize("precision,comm", [("fp32", None), ("bf16", None), ("fp32", "rccl")],
                          ids=["fp32", "bf16", "fp32_rccl_world1"])
-def test_graph_matches_eager(precision, comm):
+def test_graph_matches_eager(precision, comm, det):
     """Each replay of the captured step (a new batch loaded into the static input first) does
     what one eager step does from the same state: before every replay an eager trainer takes
     the graphed trainer's weights, Adam moments and step counter and runs train_step on the
@@ -69,7 +70,15 @@ def test_graph_matches_eager(precision, comm):
     backward's atomic-order noise.  (Comparing whole trajectories instead would measure
     Adam's amplification of that noise: a gradient near 0 whose sign flips moves its weight
     by 2 lr.)  With comm="rccl" the bucket all-reduces of a one-rank RCCL communicator are
-    inside the captured graph."""
+    inside the captured graph.  det: the deterministic warp backward (ops.deterministic(),
+    of_warp_bwd_det) -- then every reduction of the step has a fixed order and replay and
+    eager step must agree BITWISE (loss, every gradient, the updated weights)."""
+    from optical_flow_amd import ops
+    with ops.deterministic(det):
+        _graph_vs_eager(precision, comm, det)
+
+
+def _graph_vs_eager(precision, comm, det):
     from optical_flow_amd.comm import RcclComm
     from optical_flow_amd.data import synthetic_batch
     H, W, B = 128, 256, 2
@@ -88,11 +97,17 @@ def test_graph_matches_eager(precision, comm):
         ew = rel_l2(gt.flow_net.store.arena, eager.flow_net.store.arena)
         print("%s %s replay %d: loss %.7e vs eager %.7e, grads rel_l2 %.2e, weights %.2e" % (
             precision, comm, k, float(lg), float(le), eg, ew))
+        if det:
+            assert float(lg) == float(le)
+            assert torch.equal(gg, ge), eg
+            assert torch.equal(gt.flow_net.store.arena, eager.flow_net.store.arena), ew
+            continue
         assert abs(float(lg) - float(le)) <= 1e-6 * abs(float(le))
-        # bf16: the warp backward's atomic-order noise (one fp32 ulp) can flip the bf16
+        # bf16: the atomic warp backward's add-order noise (one fp32 ulp) can flip the bf16
         # rounding of a gradient element the next conv reads (a 2^-8 relative step), so the
-        # gradients of two identical steps differ by up to ~2e-4 rel_l2 (measured 1.6e-4)
-        assert eg < (1e-4 if precision == "fp32" else 1e-3), eg
+        # gradients of two identical steps differ by up to ~2e-4 rel_l2 (measured 1.63e-4 in
+        # round 3; the det case above is the exact check)
+        assert eg < (1e-4 if precision == "fp32" else 3e-4), eg
         assert ew < 1e-5, ew
     assert gt.optimizer.iterations == 5
     if c is not None:

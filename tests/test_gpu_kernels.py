@@ -1280,6 +1280,53 @@ def test_bilinear_interpolation_absolute():
     assert rel_inf(pd.grad, po.grad) < REL_TOL
 
 
+@pytest.mark.parametrize("absolute", [False, True], ids=["grid", "absolute"])
+@pytest.mark.parametrize("shape,flow_scale,offset", [((2, 40, 56, 64), 0.3, 0.0),
+                                                     ((2, 24, 40, 128), 0.8, 0.0),
+                                                     ((1, 33, 45, 64), 0.3, 30.0),
+                                                     ((1, 20, 24, 64), 0.3, -30.0),
+                                                     ((2, 20, 28, 64), 5.0, 0.0),
+                                                     ((2, 10, 14, 3), 4.0, 0.0),
+                                                     ((1, 17, 23, 32), 2.0, 0.0),
+                                                     ((1, 9, 11, 6), 1.0, 0.0),
+                                                     ((8, 96, 128, 64), 1.5, 0.0)])
+def test_warp_bwd_deterministic(shape, flow_scale, offset, absolute):
+    """The deterministic warp backward (of_warp_bwd_det, ops.deterministic()): against fp64
+    autograd of the reference sampler (transformations.py:85-129) for sub-pixel, spread and
+    border-clipped flows (20 x 24 at offset -30: every sample clamps onto one corner pixel, the
+    longest possible run), any channel count, grid + flow and absolute points; BITWISE equal
+    over repeated launches; the atomic default agrees up to its add order."""
+    from optical_flow_amd.transformations import bilinear_interpolation
+    ops = _ops()
+    n, h, w, c = shape
+    f2 = rng_tensor(shape, 41)
+    fl = rng_tensor((n, h, w, 2), 42, scale=flow_scale) + offset
+    if absolute:
+        fl = fl + torch.stack(torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij"),
+                              -1).float()
+    fwd_ref = R.bilinear_interpolation if absolute else R.warp_features
+    a, fo = f64(f2).requires_grad_(True), f64(fl).requires_grad_(True)
+    out = fwd_ref(a, fo) if absolute else fwd_ref(fo, a)
+    g = rng_tensor(tuple(out.shape), 43)
+    (out * f64(g)).sum().backward()
+    fwd = (lambda x, f: bilinear_interpolation(x, f)) if absolute else (lambda x, f: ops.warp(x, f))
+    runs = []
+    with ops.deterministic():
+        for _ in range(3):
+            ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
+            (fwd(ad, fd) * dev(g)).sum().backward()
+            torch.cuda.synchronize()
+            runs.append((ad.grad.clone(), fd.grad.clone()))
+    assert rel_inf(runs[0][0], a.grad) < REL_TOL
+    assert rel_inf(runs[0][1], fo.grad) < REL_TOL
+    for gi, gf in runs[1:]:
+        assert torch.equal(gi, runs[0][0]) and torch.equal(gf, runs[0][1])
+    ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
+    (fwd(ad, fd) * dev(g)).sum().backward()                 # the atomic default
+    assert rel_inf(ad.grad, runs[0][0]) < REL_TOL
+    assert rel_inf(fd.grad, runs[0][1]) < REL_TOL
+
+
 # -------------------------------------------------------------------------- upscale -----
 @pytest.mark.parametrize("shape", [(2, 6, 8, 2), (1, 24, 32, 2), (2, 5, 7, 3), (1, 2, 4, 2)])
 def test_upscale(shape):

@@ -245,3 +245,48 @@ def test_resnet_layer_simple_fresh_layers():
     assert set(y1._resnet_store.params) >= {"ResNet18/res3_0/proj/kernel",
                                             "ResNet18/res3_1/conv_b/kernel"}
     assert torch.equal(y1, y2)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_bn_gamma_near_zero(precision):
+    """Inference BN (model.py:14, the resnet blocks) with gammas at 0 and 1e-4 and a large
+    beta / residual: the backward's zhat = (y - res - beta) / gamma is undefined or
+    imprecise there, so ops.BNZGuard keeps z for those layers and the BN backward reads it.
+    Every gradient against the oracle (float64; bf16: the bf16-rounded oracle at the module
+    test's 1e-2), no NaN, and the guard picked exactly the layers with small gammas."""
+    from optical_flow_amd.loss import LossLayer
+    from optical_flow_amd.data import synthetic_batch
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params, perturb_params
+    H, W, B = 64, 128, 2
+    vals = perturb_params(init_params(flow_net_spec(), 7), 8)
+    g = vals["ResNet18/layer1_bn/gamma"].copy()
+    g[::2] = 0.0                                   # stem: half the channels exactly 0
+    vals["ResNet18/layer1_bn/gamma"] = g
+    vals["ResNet18/res2_0/bn_a/gamma"] = np.full(64, 1e-4, np.float32)
+    vals["ResNet18/res3_0/bn_b/gamma"][:] = 0.0    # conv_b: residual added after BN
+    vals["ResNet18/res3_0/bn_proj/beta"][:] = 30.0   # large residual into res3_0's add
+    vals["ResNet18/res4_0/bn_proj/gamma"][:5] = 1e-4
+    net = FlowNet(H, W, values=vals, precision=precision)
+    batch = synthetic_batch(B, H, W, seed=77)
+    p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+    R.set_conv_precision(precision)
+    try:
+        loss_o, flows_o, grads_o = R.train_step(torch.tensor(batch, dtype=torch.float64), p,
+                                                list(encoder_blocks()), None)
+    finally:
+        R.set_conv_precision("fp32")
+    net.store.zero_grad()
+    bd = dev(torch.from_numpy(batch))
+    flows = net(bd)
+    LossLayer()(bd, flows).backward()
+    torch.cuda.synchronize()
+    assert sorted(net.store.bn_guard.stored()) == sorted(
+        ["conv1", "ResNet18/res2_0/conv_a", "ResNet18/res3_0/conv_b",
+         "ResNet18/res4_0/proj"]), net.store.bn_guard.stored()
+    tol = REL_TOL if precision == "fp32" else 1e-2
+    for name, gr in net.store.grads().items():
+        assert torch.isfinite(gr).all(), name
+        if name.startswith("ResNet18"):
+            e = rel_l2(gr, grads_o[name])
+            assert e < tol, "grad %s rel_l2 %.3e" % (name, e)

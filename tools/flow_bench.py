@@ -84,6 +84,11 @@ def main():
                 call("of_fill", P(dw), 0.0, dw.numel(), st)
                 call("of_warp_bwd", P(g), P(f2), n, h, w, c, P(fl), P(dw), P(dfl2), st)
             res["warp_bwd"] = (timeit(wb2, args.reps), 4 * npx * (4 * c + 4))
+            dwsb = _lib.lib().of_warp_bwd_det_workspace(n, h, w, c)
+            dws = torch.empty(dwsb // 4 + 4, device="cuda")
+            res["warp_bwd_det"] = (timeit(lambda: call(
+                "of_warp_bwd_det", P(g), P(f2), n, h, w, c, P(fl), 0, P(dw), P(dfl2), None, 0,
+                P(dws), dwsb, st), args.reps), 4 * npx * (4 * c + 4))
         line = "level %d %3dx%3d c=%3d |" % (lvl, h, w, c)
         for k, (ms, by) in res.items():
             line += " %s %7.1f us %6.0f GB/s |" % (k, ms * 1e3, by / (ms * 1e-3) / 1e9)
