@@ -382,6 +382,24 @@ int of_timing_enable(int on);
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 
+/* ==== bf16 activation images (configs 3-5, round 4) ====================================== */
+/* x (npix pixels of ldx fp32, c used) -> y16: npix pixels of ldo bf16 (RNE), channels [c, ldo)
+ * zero; ldo % 8 == 0. */
+int of_to_bf16_image(const float* x, int64_t npix, int c, int ldx, void* y16, int ldo,
+                     void* stream);
+/* 3x3 stride-1 forward (mode 0) / input gradient (mode 1) whose GEMM A source -- fwd: x,
+ * dgrad: dy -- is a bf16 image a16 (lda16 channels per pixel, a multiple of 32 and >=
+ * round_up(kc, 32), kc = cin_p (fwd) / round_up(cout, 4) (dgrad); channels past kc zero), with
+ * the packed bf16 weights of of_conv_pack_weights_bf16 and the fp32 epilogues of
+ * of_conv2d_fwd (bias, BN, aux = residual, act) / of_conv2d_dgrad (act_src, act, aux = added
+ * gradient); output y fp32 (ldy).  The same convs as of_conv2d_{fwd,dgrad}_bf16 (model.py:104-114
+ * and the resnet blocks' 3x3 convs), on the DMA-fed large-tile kernel conv_halo_b16. */
+int of_conv2d_b16i(int mode, const of_conv_desc* d, const void* a16, int lda16, const void* w16,
+                   const float* bias, const float* bn_gamma, const float* bn_beta,
+                   const float* bn_mean, const float* bn_var, float bn_eps, const float* aux,
+                   int ldr, const float* act_src, int ld_act, int act, float alpha, float* y,
+                   int ldy, void* stream);
+
 /* ==== SURVEY.md §8 f row 1: the KITTI data path (data_reader.py) ========================== */
 
 /* One decoded frame inside a raw batch buffer: 8-bit BGR, h x w x 3, at byte `offset` from the

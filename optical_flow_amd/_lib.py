@@ -90,6 +90,8 @@ PROTOTYPES = {
     "of_warp_bwd_add": (I, [P, P, I, I, I, I, P, P, P, P, I, P]),
     "of_bilinear_fwd": (I, [P, I, I, I, I, P, P, P]),
     "of_bilinear_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
+    "of_to_bf16_image": (I, [P, I64, I, I, P, I, P]),
+    "of_conv2d_b16i": (I, [I, PD, P, I, P, P, P, P, P, P, F, P, I, P, I, I, F, P, I, P]),
     "of_warp_bwd_det_workspace": (SZ, [I, I, I, I]),
     "of_warp_bwd_det": (I, [P, P, I, I, I, I, P, I, P, P, P, I, P, SZ, P]),
     "of_upscale2x_fwd": (I, [P, I, I, I, I, F, P, I, P]),

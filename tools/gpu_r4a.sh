@@ -7,6 +7,8 @@ export TMPDIR=/tmp
 OUT=${1:-gpurun_out/r4a}
 mkdir -p "$OUT"
 run() { local t=$1; shift; timeout -k 10 "$t" "$@"; }
+run 300 python tools/b16i_bench.py --batch 8 > "$OUT/b16i_b8.txt" 2>&1; echo "b16i b8 rc $?"; cat "$OUT/b16i_b8.txt"
+run 300 python tools/b16i_bench.py --batch 32 > "$OUT/b16i_b32.txt" 2>&1; echo "b16i b32 rc $?"; cat "$OUT/b16i_b32.txt"
 run 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   "tests/test_gpu_kernels.py::test_warp_bwd_deterministic" \
   "tests/test_gpu_kernels.py::test_warp" "tests/test_gpu_kernels.py::test_warp_bwd_forms" \
