@@ -387,18 +387,44 @@ int of_timing_read(int max, int* kinds, double* flops, float* ms);
  * zero; ldo % 8 == 0. */
 int of_to_bf16_image(const float* x, int64_t npix, int c, int ldx, void* y16, int ldo,
                      void* stream);
-/* 3x3 stride-1 forward (mode 0) / input gradient (mode 1) whose GEMM A source -- fwd: x,
- * dgrad: dy -- is a bf16 image a16 (lda16 channels per pixel, a multiple of 32 and >=
- * round_up(kc, 32), kc = cin_p (fwd) / round_up(cout, 4) (dgrad); channels past kc zero), with
- * the packed bf16 weights of of_conv_pack_weights_bf16 and the fp32 epilogues of
- * of_conv2d_fwd (bias, BN, aux = residual, act) / of_conv2d_dgrad (act_src, act, aux = added
- * gradient); output y fp32 (ldy).  The same convs as of_conv2d_{fwd,dgrad}_bf16 (model.py:104-114
- * and the resnet blocks' 3x3 convs), on the DMA-fed large-tile kernel conv_halo_b16. */
-int of_conv2d_b16i(int mode, const of_conv_desc* d, const void* a16, int lda16, const void* w16,
+/* 3x3 stride-1 forward (mode 0) / input gradient (mode 1) of the convs of model.py:104-114 and
+ * the resnet blocks, on the DMA-fed large-tile kernel conv_halo_b16, with bf16 activation
+ * images at both ends: the GEMM A source (fwd: x, dgrad: dy) is the bf16 image a16 (lda16
+ * channels per pixel, a multiple of 32 and >= round_up(kc, 32), kc = cin_p (fwd) /
+ * round_up(cout, 4) (dgrad); channels past kc zero), the weights the packed bf16 images of
+ * of_conv_pack_weights_bf16.  Epilogue as of_conv2d_fwd (bias, BN, aux = residual, act) /
+ * of_conv2d_dgrad (the producer's act' from act_src (fp32) or act16 (bf16 image), aux = an
+ * added gradient); the result goes to y (fp32) and / or y16 (bf16 image, RNE).  col_part
+ * (dgrad, optional): per output tile the column sums of the fp32 result, [tiles][N] with tiles =
+ * of_conv2d_b16i_tiles(1, d) -- the bias gradient of the layer that produced dy, reduced by
+ * of_col_part_reduce.  No workspace (one K slice). */
+typedef struct of_b16i_io {
+  const void* a16; int lda16;
+  float* y; int ldy;
+  void* y16; int ldy16;
+  const float* aux; int ldr;
+  const float* act_src; int ld_act;
+  const void* act16; int ld_act16;
+  float* col_part;
+} of_b16i_io;
+int of_conv2d_b16i_tiles(int mode, const of_conv_desc* d);
+int of_conv2d_b16i(int mode, const of_conv_desc* d, const of_b16i_io* io, const void* w16,
                    const float* bias, const float* bn_gamma, const float* bn_beta,
-                   const float* bn_mean, const float* bn_var, float bn_eps, const float* aux,
-                   int ldr, const float* act_src, int ld_act, int act, float alpha, float* y,
-                   int ldy, void* stream);
+                   const float* bn_mean, const float* bn_var, float bn_eps, int act, float alpha,
+                   void* stream);
+/* Weight gradient of the same convs from bf16 images (x16: ldx16 bf16 per pixel, >= cin_p;
+ * dy16: lddy16 >= cout), dw HWIO [3][3][cin][cout] (accumulate != 0 adds), scaled per output
+ * channel by gamma / sqrt(var + eps) when bn_gamma (the folded inference BN); no bias gradient
+ * (of_col_part_reduce gives it).  Deterministic: per-slice fp32 slabs in workspace
+ * (of_conv2d_wgrad_b16i_workspace(d) bytes), reduced in a fixed order. */
+size_t of_conv2d_wgrad_b16i_workspace(const of_conv_desc* d);
+int of_conv2d_wgrad_b16i(const of_conv_desc* d, const void* x16, int ldx16, const void* dy16,
+                         int lddy16, float* dw, int accumulate, const float* bn_gamma,
+                         const float* bn_var, float bn_eps, void* workspace, size_t ws_bytes,
+                         void* stream);
+/* out[c] (+)= sum_r part[r][c], fixed order (deterministic). */
+int of_col_part_reduce(const float* part, int rows, int n, float* out, int accumulate,
+                       void* stream);
 
 /* ==== SURVEY.md §8 f row 1: the KITTI data path (data_reader.py) ========================== */
 

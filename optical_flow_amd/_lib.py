@@ -18,6 +18,14 @@ OF_OK, OF_EINVAL, OF_EHIP, OF_EUNSUPPORTED = 0, 1, 2, 3
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
 
 
+class B16iIO(C.Structure):
+    """of_b16i_io (include/oflow.h): the ends of one conv_halo_b16 launch."""
+    _fields_ = [("a16", C.c_void_p), ("lda16", C.c_int), ("y", C.c_void_p), ("ldy", C.c_int),
+                ("y16", C.c_void_p), ("ldy16", C.c_int), ("aux", C.c_void_p), ("ldr", C.c_int),
+                ("act_src", C.c_void_p), ("ld_act", C.c_int), ("act16", C.c_void_p),
+                ("ld_act16", C.c_int), ("col_part", C.c_void_p)]
+
+
 class ConvDesc(C.Structure):
     _fields_ = [(n, C.c_int32) for n in
                 ("n", "h", "w", "cin", "cin_p", "cout", "kh", "kw", "stride", "pad_top",
@@ -91,7 +99,11 @@ PROTOTYPES = {
     "of_bilinear_fwd": (I, [P, I, I, I, I, P, P, P]),
     "of_bilinear_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
     "of_to_bf16_image": (I, [P, I64, I, I, P, I, P]),
-    "of_conv2d_b16i": (I, [I, PD, P, I, P, P, P, P, P, P, F, P, I, P, I, I, F, P, I, P]),
+    "of_conv2d_b16i_tiles": (I, [I, PD]),
+    "of_conv2d_b16i": (I, [I, PD, P, P, P, P, P, P, P, F, I, F, P]),
+    "of_col_part_reduce": (I, [P, I, I, P, I, P]),
+    "of_conv2d_wgrad_b16i_workspace": (SZ, [PD]),
+    "of_conv2d_wgrad_b16i": (I, [PD, P, I, P, I, P, I, P, P, F, P, SZ, P]),
     "of_warp_bwd_det_workspace": (SZ, [I, I, I, I]),
     "of_warp_bwd_det": (I, [P, P, I, I, I, I, P, I, P, P, P, I, P, SZ, P]),
     "of_upscale2x_fwd": (I, [P, I, I, I, I, F, P, I, P]),

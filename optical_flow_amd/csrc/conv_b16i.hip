@@ -19,6 +19,8 @@
 //     pre-swizzling each lane's source octet (guide rule 21).
 //   * epilogue: the fp32 epilogues of conv_dev.h (bias, BN, residual, activation / the
 //     producer's activation derivative) through a per-wave LDS transpose as 16-byte rows.
+#include <algorithm>
+
 #include "conv_dev.h"
 
 namespace oflow {
@@ -26,6 +28,77 @@ namespace oflow {
 namespace {
 
 constexpr int BI_TH = 16, BI_TW = 32;
+
+__device__ __forceinline__ float4 bf16x4_to_f4(uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+
+// The fused epilogue of R rows of one lane's column quad n .. n + 3 (row[r] valid where bit r
+// of ok is set), as epilogue_rows4 (conv_dev.h) but with the bf16-image ends: fwd bias / BN /
+// residual / activation, dgrad the producer's activation derivative from an fp32 source or a
+// bf16 image (act16: only the sign matters, and RNE keeps it) plus an added gradient; the
+// result goes to the fp32 output C and / or the bf16 image C16; dgrad also sums each column
+// (cs, for the bias-gradient partials; the fp32 values, before any rounding).
+template <int MODE, int R>
+__device__ __forceinline__ void halo_epilogue(const GemmArgs& a, const int64_t* row, unsigned ok,
+                                              int n, const float4* v, float4& cs) {
+  float x[R][4];
+  if (MODE == MODE_FWD) {
+    float bias[4], scale[4], shift[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) column_params<MODE>(a, n + e, bias[e], scale[e], shift[e]);
+    float4 r4[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      r4[r] = a.res && ((ok >> r) & 1) ? *reinterpret_cast<const float4*>(&a.res[row[r] * a.ldr + n])
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float vv[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+      const float rr[4] = {r4[r].x, r4[r].y, r4[r].z, r4[r].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = vv[e] + bias[e];
+        if (a.bn_g) t = t * scale[e] + shift[e];
+        x[r][e] = act_fwd(t + rr[e], a.act, a.alpha);
+      }
+    }
+  } else {
+    float4 s4[R], r4[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool k = (ok >> r) & 1;
+      s4[r] = a.act16 && k ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(&a.act16[row[r] * a.ld_act16 + n]))
+              : a.act_src && k ? *reinterpret_cast<const float4*>(&a.act_src[row[r] * a.ld_act + n])
+                               : make_float4(1.f, 1.f, 1.f, 1.f);
+      r4[r] = a.res && k ? *reinterpret_cast<const float4*>(&a.res[row[r] * a.ldr + n])
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      x[r][0] = dgrad_ep(a, v[r].x, s4[r].x, r4[r].x);
+      x[r][1] = dgrad_ep(a, v[r].y, s4[r].y, r4[r].y);
+      x[r][2] = dgrad_ep(a, v[r].z, s4[r].z, r4[r].z);
+      x[r][3] = dgrad_ep(a, v[r].w, s4[r].w, r4[r].w);
+      if ((ok >> r) & 1) {
+        cs.x += x[r][0];
+        cs.y += x[r][1];
+        cs.z += x[r][2];
+        cs.w += x[r][3];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (!((ok >> r) & 1)) continue;
+    if (a.C)
+      *reinterpret_cast<float4*>(&a.C[row[r] * a.ldc + n]) = make_float4(x[r][0], x[r][1], x[r][2], x[r][3]);
+    if (a.C16)
+      *reinterpret_cast<uint2*>(&a.C16[row[r] * a.ldc16 + n]) =
+          pack_bf16x4(make_float4(x[r][0], x[r][1], x[r][2], x[r][3]));
+  }
+}
 
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int TW>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmArgs a) {
@@ -41,10 +114,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   constexpr int BDI = KS * BN / 16, BDW = (BDI + NW - 1) / NW;   // B DMA instructions per step
   constexpr int H_U4 = HPD * 4, B_U4 = KS * BN * 4;               // uint4 per buffer
   constexpr int LOOP_U4 = 2 * H_U4 + 2 * B_U4;
-  constexpr int EJ = NW * WM * 16 * SN * 4 <= LOOP_U4 * 16 ? SN
-                     : NW * WM * 16 * 2 * 4 <= LOOP_U4 * 16 && SN % 2 == 0 ? 2 : 1;
+  constexpr int EJ = NW * WM * 16 * SN * 4 + WAVES_M * BN * 4 <= LOOP_U4 * 16 ? SN
+                     : NW * WM * 16 * 2 * 4 + WAVES_M * BN * 4 <= LOOP_U4 * 16 && SN % 2 == 0 ? 2
+                                                                                     : 1;
   constexpr int EPW = 16 * EJ;
-  constexpr int EP_U4 = NW * WM * EPW / 4;
+  constexpr int EP_U4 = NW * WM * EPW / 4 + WAVES_M * BN / 4;     // + the column-sum buffer
   constexpr int SM_U4 = LOOP_U4 > EP_U4 ? LOOP_U4 : EP_U4;
   static_assert(SM_U4 * 16 <= 160 * 1024, "LDS");
   __shared__ uint4 smem[SM_U4];
@@ -181,8 +255,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   // per pass), back as float4 rows (16-byte loads / stores, 4 EJ lanes per pixel row)
   const int64_t img = (int64_t)b * OH * OW;
   float* E = reinterpret_cast<float*>(smem) + wave * WM * EPW;
+  float* colbuf = reinterpret_cast<float*>(smem) + NW * WM * EPW;   // [WAVES_M][BN]
   constexpr int LPR = 4 * EJ, RPI = 64 / LPR;
   const int c4 = lane % LPR, rr = lane / LPR;
+  const bool colsums = MODE == MODE_DGRAD && a.col_part != nullptr;
 #pragma unroll
   for (int jp = 0; jp < SN; jp += EJ) {
 #pragma unroll
@@ -195,6 +271,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int n = n0 + wn0 + 16 * jp + 4 * c4;
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
     constexpr int EB = (WM / RPI) % 4 == 0 ? 4 : 1;
 #pragma unroll
     for (int q0 = 0; q0 < WM / RPI; q0 += EB) {
@@ -210,11 +287,238 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
         row[g] = img + (int64_t)oy * OW + ox;
         ok |= (oy < OH && ox < OW && n < a.N ? 1u : 0u) << g;
       }
-      epilogue_rows4<MODE, EB>(a, split, row, ok, n, v);
+      halo_epilogue<MODE, EB>(a, row, ok, n, v, cs);
+    }
+    if (colsums) {
+      // sum over the RPI row groups of lanes with the same column quad, fixed order
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        cs.x += __shfl_xor(cs.x, o, 64);
+        cs.y += __shfl_xor(cs.y, o, 64);
+        cs.z += __shfl_xor(cs.z, o, 64);
+        cs.w += __shfl_xor(cs.w, o, 64);
+      }
+      if (rr == 0)
+        *reinterpret_cast<float4*>(&colbuf[(wave / WAVES_N) * BN + wn0 + 16 * jp + 4 * c4]) = cs;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (colsums) {          // this tile's column sums: the WAVES_M row blocks in a fixed order
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES_M; ++w) v += colbuf[w * BN + tid];
+      a.col_part[(int64_t)tile_m * a.N + n0 + tid] = v;
+    }
+  }
+}
+
+// ---- weight gradient from bf16 images: dW[r][s][ci][co] = sum_p x(p + (r, s) - pad)[ci] .
+// dy(p)[co] (Conv2DBackpropFilter of the same convs).  A workgroup owns CIB input x COB output
+// channels for all 9 taps and walks a contiguous range of 8 x 16 output-pixel tiles (its K
+// slice).  Per tile the x halo (10 x 18 px x CIB) and the dy tile (128 px x COB) go global ->
+// LDS by DMA, in the images' own [pixel][channel] layout, double-buffered one tile ahead; the
+// MFMA operands want pixels along K, so they are read with ds_read_b64_tr_b16 (the hardware
+// transposing read: a 16-lane group reads 4 pixel rows x 16 channels, lane i receives channel
+// i's 4 pixels).  Each wave owns 32 ci x 32 co x 9 taps (v_mfma_f32_32x32x16_bf16, 9
+// accumulators); per output row kk the B fragment (dy row kk) serves the 9 taps and an x-row
+// fragment (halo row j, shift s) serves the output rows j - r, so a tile needs 10 x 3 + 8
+// fragment reads for 72 MFMAs.  LDS chunk swizzles (16-byte chunks of a pixel row) make the
+// transposing reads conflict-free: 256-byte rows XOR the chunk with (px & 3) << 2, 128-byte
+// rows with ((px >> 1) & 1) << 2.  Output: fp32 slabs [slice][tap][kc][ldc] reduced in a fixed
+// order by b16i_wgrad_reduce.
+constexpr int WB_TH = 8, WB_TW = 16, WB_HH = WB_TH + 2, WB_HW = WB_TW + 2;
+constexpr int WB_HP = WB_HH * WB_HW;          // 180 halo pixels
+
+__device__ __forceinline__ int wb_sw(int px, int row_chunks) {
+  return row_chunks >= 16 ? (px & 3) << 2 : ((px >> 1) & 1) << 2;
+}
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+// 8 bf16 (two transposing reads of 4 pixel rows each) of one MFMA operand fragment
+__device__ __forceinline__ bf16x8 tr_frag(const char* base, int off0, int off1) {
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16*)(base + off0));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16*)(base + off1));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int WAVES_CI, int WAVES_CO>
+__global__ __launch_bounds__(64 * WAVES_CI * WAVES_CO, 1) void conv_wgrad_b16i(GemmArgs a) {
+  constexpr int NW = WAVES_CI * WAVES_CO, NT = 64 * NW;
+  constexpr int CIB = 32 * WAVES_CI, COB = 32 * WAVES_CO;
+  constexpr int XC = CIB / 8, DC = COB / 8;                 // 16-byte chunks per pixel row
+  constexpr int XPI = 64 / XC, DPI = 64 / DC;               // pixels per DMA instruction
+  constexpr int XDI = (WB_HP + XPI - 1) / XPI, DDI = WB_TH * WB_TW / DPI;
+  constexpr int XDW = (XDI + NW - 1) / NW, DDW = (DDI + NW - 1) / NW;
+  constexpr int X_B = XDI * 1024, D_B = DDI * 1024;         // bytes per buffer (whole instrs)
+  constexpr int LDS_B = 2 * (X_B + D_B);
+  static_assert(LDS_B <= 160 * 1024, "LDS");
+  __shared__ uint4 smem[LDS_B / 16];
+  char* lds = reinterpret_cast<char*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wgid / a.tiles_total;
+  const int tile = wgid - split * a.tiles_total;
+  const int tile_co = tile % a.n_tiles, tile_ci = tile / a.n_tiles;
+  const int ci0 = tile_ci * CIB, co0 = tile_co * COB;
+  const int t_begin = split * a.k_per_split;
+  const int t_end = min(a.K, t_begin + a.k_per_split);
+  const int ntiles = max(0, t_end - t_begin);
+  const int tiles_x = (a.wo + WB_TW - 1) / WB_TW, tiles_y = (a.ho + WB_TH - 1) / WB_TH;
+  const rsrc_t rx = make_rsrc(a.A, a.a_bytes);   // x image: a.lda bf16 per pixel
+  const rsrc_t rd = make_rsrc(a.B, a.b_bytes);   // dy image: a.ldb bf16 per pixel
+
+  // DMA slots: instruction g covers XPI halo pixels (DPI dy pixels); lane -> (pixel, chunk),
+  // the chunk pre-swizzled so the image lands swizzled (recomputed per tile: registers)
+  auto dma = [&](int t, int buf) {
+    const int b = t / (tiles_x * tiles_y);
+    const int trem = t - b * tiles_x * tiles_y;
+    const int oy0 = (trem / tiles_x) * WB_TH, ox0 = (trem % tiles_x) * WB_TW;
+    char* xb = lds + buf * (X_B + D_B);
+    char* db = xb + X_B;
+#pragma unroll
+    for (int k = 0; k < XDW; ++k) {
+      const int g = wave + NW * k;
+      if (XDI % NW != 0 && g >= XDI) continue;
+      const int hp = g * XPI + lane / XC;
+      const int xch = (lane % XC) ^ wb_sw(hp, XC);
+      const int iy = oy0 - a.pt + hp / WB_HW, ix = ox0 - a.pl + hp % WB_HW;
+      const bool ok = hp < WB_HP && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w &&
+                      ci0 + 8 * xch < a.kc;
+      const uint32_t off = ok ? (uint32_t)((((int64_t)(b * a.h + iy) * a.w + ix) * a.lda + ci0 +
+                                            8 * xch) * 2) : kOOB;
+      dma16_to_lds(rx, reinterpret_cast<uint4*>(xb + 1024 * g), off, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < DDW; ++k) {
+      const int g = wave + NW * k;
+      if (DDI % NW != 0 && g >= DDI) continue;
+      const int p = g * DPI + lane / DC;
+      const int dch = (lane % DC) ^ wb_sw(p, DC);
+      const int oy = oy0 + p / WB_TW, ox = ox0 + p % WB_TW;
+      const bool ok = oy < a.ho && ox < a.wo && co0 + 8 * dch < a.nb;
+      const uint32_t off = ok ? (uint32_t)((((int64_t)(b * a.ho + oy) * a.wo + ox) * a.ldb + co0 +
+                                            8 * dch) * 2) : kOOB;
+      dma16_to_lds(rd, reinterpret_cast<uint4*>(db + 1024 * g), off, 0);
+    }
+  };
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const int wci = (wave / WAVES_CO) * 32, wco = (wave % WAVES_CO) * 32;
+  // transposing-read addresses: lane 4q + p of 16-lane group g reads row q, columns 4p..4p+3
+  // of the group's 16 channels (16 (g & 1) within the wave's 32), pixels 8 (g >> 1) + q (+4)
+  const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int colx = wci + 16 * (grp & 1) + 4 * pp;          // x channel (within CIB)
+  const int cold = wco + 16 * (grp & 1) + 4 * pp;          // dy channel (within COB)
+  auto xoff = [&](int px) {                                // byte offset of (px, colx) in a row
+    const int ch = colx >> 3;
+    return px * (XC * 16) + ((ch ^ wb_sw(px, XC)) << 4) + 2 * (colx & 7);
+  };
+  auto doff = [&](int px) {
+    const int ch = cold >> 3;
+    return px * (DC * 16) + ((ch ^ wb_sw(px, DC)) << 4) + 2 * (cold & 7);
+  };
+  const int kofs = 8 * (grp >> 1) + q;                      // this lane's pixel within K16
+
+  if (ntiles > 0) dma(t_begin, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int i = 0; i < ntiles; ++i) {
+    const int buf = i & 1;
+    if (i + 1 < ntiles) dma(t_begin + i + 1, buf ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const char* xb = lds + buf * (X_B + D_B);
+    const char* db = xb + X_B;
+    auto afrag = [&](int row, int s) {      // x halo row `row`, shift s: pixels row*18 + s + k
+      const int px = row * WB_HW + s + kofs;
+      return tr_frag(xb, xoff(px), xoff(px + 4));
+    };
+    auto bfrag = [&](int kk) {
+      const int px = kk * WB_TW + kofs;
+      return tr_frag(db, doff(px), doff(px + 4));
+    };
+    bf16x8 af[WB_HH][3];
+#pragma unroll
+    for (int row = 0; row < 3; ++row)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) af[row][s] = afrag(row, s);
+#pragma unroll
+    for (int kk = 0; kk < WB_TH; ++kk) {
+      const bf16x8 bv = bfrag(kk);
+      if (kk + 3 < WB_HH) {          // x row kk + 3, first used by output row kk + 1
+#pragma unroll
+        for (int s = 0; s < 3; ++s) af[kk + 3][s] = afrag(kk + 3, s);
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+          acc[r * 3 + s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk + r][s], bv,
+                                                                  acc[r * 3 + s], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- this slice's partial dW: slab [split][tap][kc rows][slab_ld] (32 x 32 layout: column
+  // lane & 31, rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
+  float* S = a.slab + (int64_t)split * a.split_stride;
+  const int n = co0 + wco + (lane & 31);
+  if (n < a.N) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = ci0 + wci + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (ci < a.M) S[((int64_t)t * a.M + ci) * a.slab_ld + n] = acc[t][r];
+      }
+  }
+}
+
+// dw[tap][ci][co] (+)= sum over slices of slab[slice][tap][ci][co] (fixed order), ci < cin,
+// co < cout; one thread per (row, column quad).
+__global__ __launch_bounds__(256) void b16i_wgrad_reduce(const float* __restrict__ slab, int slices,
+                                                         int64_t stride, int rows, int ld,
+                                                         int cout, float* __restrict__ dw, int acc,
+                                                         const float* __restrict__ bn_g,
+                                                         const float* __restrict__ bn_v,
+                                                         float bn_eps) {
+  const int cq = (cout + 3) / 4;
+  const int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (item >= (int64_t)rows * cq) return;
+  const int row = (int)(item / cq), q = (int)(item - (int64_t)row * cq);
+  const float* src = slab + (int64_t)row * ld + 4 * q;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  int z = 0;
+  for (; z + 3 < slices; z += 4) {
+    float4 u[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = *reinterpret_cast<const float4*>(src + (int64_t)(z + k) * stride);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) add4(v, u[k]);
+  }
+  for (; z < slices; ++z) add4(v, *reinterpret_cast<const float4*>(src + (int64_t)z * stride));
+  float x[4] = {v.x, v.y, v.z, v.w};
+  const int nv = min(4, cout - 4 * q);
+  float* dst = dw + (int64_t)row * cout + 4 * q;
+  for (int e = 0; e < nv; ++e) {
+    float t = x[e];
+    if (bn_g) t *= bn_g[4 * q + e] * rsqrtf(bn_v[4 * q + e] + bn_eps);
+    dst[e] = acc ? dst[e] + t : t;
   }
 }
 
@@ -254,69 +558,211 @@ int of_to_bf16_image(const float* x, int64_t npix, int c, int ldx, void* y16, in
   return check_launch("to_bf16_image");
 }
 
-// Experimental entry (round 4): mode 0 fwd / 1 input gradient of a 3x3 stride-1 conv whose
-// A source (fwd: x, dgrad: dy) is a bf16 image a16 with lda16 channels per pixel (a multiple
-// of 32, >= round_up(kc, 32), the channels past kc zero); w16: the packed bf16 fwd / bwd image
-// of of_conv_pack_weights_bf16.  aux: fwd residual / dgrad added gradient (ldr); act_src:
-// dgrad activation source.  Unsplit (one K slice).
-int of_conv2d_b16i(int mode, const of_conv_desc* d, const void* a16, int lda16, const void* w16,
-                   const float* bias, const float* bn_gamma, const float* bn_beta,
-                   const float* bn_mean, const float* bn_var, float bn_eps, const float* aux,
-                   int ldr, const float* act_src, int ld_act, int act, float alpha, float* y,
-                   int ldy, void* stream) {
-  OF_CHECK_ARG(d && a16 && w16 && y, "conv b16i: NULL pointer");
-  OF_CHECK_ARG(d->kh == 3 && d->kw == 3 && d->stride == 1, "conv b16i: 3x3 stride 1 only");
-  OF_CHECK_ARG(mode == 0 || mode == 1, "conv b16i: mode");
+// Tile configurations by N tile: (BN, waves M x N, TH x TW) -- all 8 waves, 512-pixel tiles.
+static int b16i_bn(int N) { return N > 96 ? 128 : N > 64 ? 96 : N > 32 ? 64 : 32; }
+
+static int b16i_plan(int mode, const of_conv_desc* d, GemmArgs& a) {
   const int cout_p = (int)round_up(d->cout, 4);
   const int kc = mode == 0 ? d->cin_p : cout_p;
   const int N = mode == 0 ? d->cout : d->cin_p;
-  OF_CHECK_ARG(lda16 % 32 == 0 && lda16 >= round_up(kc, 32), "conv b16i: lda16");
-  OF_CHECK_ARG(N % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)y & 15) == 0, "conv b16i: output");
-  GemmArgs a{};
+  a = GemmArgs{};
   a.n = d->n, a.h = d->h, a.w = d->w, a.ho = d->ho, a.wo = d->wo;
   a.kh = 3, a.kw = 3, a.stride = 1, a.pt = d->pad_top, a.pl = d->pad_left, a.dt = 1;
   a.kc = kc;
   a.N = N;
   a.nb = mode == 0 ? d->cout : d->cin_p;
-  const int kf16 = (int)round_up((int64_t)9 * d->cin_p, 32);
-  const int kd16 = (int)round_up((int64_t)9 * cout_p, 32);
-  a.ldb = mode == 0 ? kf16 : kd16;
+  a.ldb = mode == 0 ? (int)round_up((int64_t)9 * d->cin_p, 32) : (int)round_up((int64_t)9 * cout_p, 32);
   const int OH = mode == 0 ? d->ho : d->h, OW = mode == 0 ? d->wo : d->w;
-  const int SH = mode == 0 ? d->h : d->ho, SW = mode == 0 ? d->w : d->wo;
-  constexpr int BN = 128;
-  OF_CHECK_ARG(N <= BN, "conv b16i: N <= 128 (experimental)");
-  a.n_tiles = (int)cdiv(N, BN);
+  const int bn = b16i_bn(N);
+  a.n_tiles = (int)cdiv(N, bn);
   const int64_t mt = (int64_t)d->n * cdiv(OH, BI_TH) * cdiv(OW, BI_TW);
+  if (mt * a.n_tiles >= INT32_MAX) return fail(OF_EINVAL, "conv b16i: too many tiles");
   a.tiles_total = (int)(mt * a.n_tiles);
+  a.bm = BI_TH * BI_TW;
   a.K = (int)cdiv(kc, 32);
   a.k_per_split = a.K;
   a.splits = 1;
-  a.A = static_cast<const float*>(a16);
-  a.lda = lda16;
-  a.a_bytes = (int64_t)d->n * SH * SW * lda16 * 2;
+  a.M = (int)mt;                 // M tiles: rows of the column-sum partials
+  return OF_OK;
+}
+
+int of_conv2d_b16i_tiles(int mode, const of_conv_desc* d) {
+  GemmArgs a;
+  if (!d || b16i_plan(mode, d, a)) return -1;
+  return a.M;
+}
+
+int of_conv2d_b16i(int mode, const of_conv_desc* d, const of_b16i_io* io, const void* w16,
+                   const float* bias, const float* bn_gamma, const float* bn_beta,
+                   const float* bn_mean, const float* bn_var, float bn_eps, int act, float alpha,
+                   void* stream) {
+  OF_CHECK_ARG(d && io && io->a16 && w16, "conv b16i: NULL pointer");
+  OF_CHECK_ARG(io->y || io->y16, "conv b16i: no output");
+  OF_CHECK_ARG(d->kh == 3 && d->kw == 3 && d->stride == 1, "conv b16i: 3x3 stride 1 only");
+  OF_CHECK_ARG(mode == 0 || mode == 1, "conv b16i: mode");
+  GemmArgs a;
+  if (int st = b16i_plan(mode, d, a)) return st;
+  OF_CHECK_ARG(io->lda16 % 32 == 0 && io->lda16 >= round_up(a.kc, 32), "conv b16i: lda16");
+  OF_CHECK_ARG(a.N % 4 == 0, "conv b16i: N % 4");
+  OF_CHECK_ARG(!io->y || (io->ldy >= a.N && io->ldy % 4 == 0 && ((uintptr_t)io->y & 15) == 0),
+               "conv b16i: fp32 output");
+  OF_CHECK_ARG(!io->y16 || (io->ldy16 >= a.N && io->ldy16 % 4 == 0 && ((uintptr_t)io->y16 & 7) == 0),
+               "conv b16i: bf16 output");
+  OF_CHECK_ARG(!io->aux || (io->ldr >= a.N && io->ldr % 4 == 0 && ((uintptr_t)io->aux & 15) == 0),
+               "conv b16i: aux");
+  OF_CHECK_ARG(!io->act_src || (io->ld_act >= a.N && io->ld_act % 4 == 0 &&
+                                ((uintptr_t)io->act_src & 15) == 0), "conv b16i: act_src");
+  OF_CHECK_ARG(!io->act16 || (io->ld_act16 >= a.N && io->ld_act16 % 4 == 0 &&
+                              ((uintptr_t)io->act16 & 7) == 0), "conv b16i: act16");
+  OF_CHECK_ARG(mode == 1 || !io->col_part, "conv b16i: column sums are a dgrad output");
+  const int SH = mode == 0 ? d->h : d->ho, SW = mode == 0 ? d->w : d->wo;
+  a.A = static_cast<const float*>(io->a16);
+  a.lda = io->lda16;
+  a.a_bytes = (int64_t)d->n * SH * SW * io->lda16 * 2;
   a.B = static_cast<const float*>(w16);
   a.b_bytes = (int64_t)a.nb * a.ldb * 2;
   OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX, "conv b16i: < 2 GiB tensors");
-  a.C = y, a.ldc = ldy;
+  a.C = io->y, a.ldc = io->ldy;
+  a.C16 = static_cast<uint16_t*>(io->y16), a.ldc16 = io->ldy16;
   a.bias = mode == 0 ? bias : nullptr;
   a.bn_g = mode == 0 ? bn_gamma : nullptr;
   a.bn_b = bn_beta, a.bn_m = bn_mean, a.bn_v = bn_var, a.bn_eps = bn_eps;
-  a.res = aux, a.ldr = ldr;
-  a.act_src = mode == 1 ? act_src : nullptr;
-  a.ld_act = ld_act;
+  a.res = io->aux, a.ldr = io->ldr;
+  a.act_src = mode == 1 ? io->act_src : nullptr;
+  a.ld_act = io->ld_act;
+  a.act16 = mode == 1 ? static_cast<const uint16_t*>(io->act16) : nullptr;
+  a.ld_act16 = io->ld_act16;
+  a.col_part = mode == 1 ? io->col_part : nullptr;
   a.act = act, a.alpha = alpha;
   a.vec_ep = 1;
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * 9 * d->cin;
+  const int bn = b16i_bn(a.N);
+  const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
+  const dim3 grid(a.tiles_total), block(512);
   if (timing_on()) timing_begin(s);
-  if (mode == 0)
-    hipLaunchKernelGGL((conv_halo_b16<128, 4, 2, MODE_FWD, BI_TH, BI_TW>), dim3(a.tiles_total),
-                       dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_halo_b16<128, 4, 2, MODE_DGRAD, BI_TH, BI_TW>), dim3(a.tiles_total),
-                       dim3(512), 0, s, a);
-  if (timing_on()) timing_end(s, 256 + 8 * mode, flops);
+#define B16I_LAUNCH(MODE)                                                                        \
+  if (cfg == 0) hipLaunchKernelGGL((conv_halo_b16<128, 4, 2, MODE, BI_TH, BI_TW>), grid, block, 0, s, a); \
+  else if (cfg == 1) hipLaunchKernelGGL((conv_halo_b16<96, 4, 2, MODE, BI_TH, BI_TW>), grid, block, 0, s, a); \
+  else if (cfg == 2) hipLaunchKernelGGL((conv_halo_b16<64, 8, 1, MODE, BI_TH, BI_TW>), grid, block, 0, s, a); \
+  else hipLaunchKernelGGL((conv_halo_b16<32, 8, 1, MODE, BI_TH, BI_TW>), grid, block, 0, s, a);
+  if (mode == 0) {
+    B16I_LAUNCH(MODE_FWD)
+  } else {
+    B16I_LAUNCH(MODE_DGRAD)
+  }
+#undef B16I_LAUNCH
+  if (timing_on()) timing_end(s, 256 + 8 * mode + cfg, flops);
   return check_launch("conv_halo_b16");
+}
+
+// ---- weight gradient from bf16 images (conv_wgrad_b16i) ------------------------------------
+struct WgB16iPlan {
+  int wci, wco;          // waves
+  GemmArgs a;
+};
+
+static void wgrad_b16i_plan(const of_conv_desc* d, WgB16iPlan& P) {
+  GemmArgs& a = P.a;
+  a = GemmArgs{};
+  if (d->cout > 64) P.wci = 2, P.wco = 4;
+  else if (d->cout > 32) P.wci = 4, P.wco = 2;
+  else P.wci = 4, P.wco = 1;
+  const int cib = 32 * P.wci, cob = 32 * P.wco;
+  a.n = d->n, a.h = d->h, a.w = d->w, a.ho = d->ho, a.wo = d->wo;
+  a.kh = 3, a.kw = 3, a.stride = 1, a.pt = d->pad_top, a.pl = d->pad_left, a.dt = 1;
+  a.kc = d->cin_p;
+  a.M = d->cin;                           // slab rows per tap
+  a.N = d->cout;
+  a.nb = d->cout;
+  a.n_tiles = (int)cdiv(d->cout, cob);
+  a.tiles_total = (int)cdiv(d->cin_p, cib) * a.n_tiles;
+  const int64_t T = (int64_t)d->n * cdiv(d->ho, WB_TH) * cdiv(d->wo, WB_TW);
+  a.K = (int)T;
+  int S = std::max(1, (int)(device_cus() / a.tiles_total));
+  S = (int)std::min<int64_t>(S, std::max<int64_t>(1, T / 4));
+  a.k_per_split = (int)cdiv(T, S);
+  a.splits = (int)cdiv(T, a.k_per_split);
+  a.slab_ld = (int)round_up(d->cout, 4);
+  a.split_stride = (int64_t)9 * d->cin * a.slab_ld;
+}
+
+size_t of_conv2d_wgrad_b16i_workspace(const of_conv_desc* d) {
+  if (!d || d->kh != 3 || d->kw != 3 || d->stride != 1) return 0;
+  WgB16iPlan P;
+  wgrad_b16i_plan(d, P);
+  return (size_t)P.a.splits * P.a.split_stride * sizeof(float);
+}
+
+int of_conv2d_wgrad_b16i(const of_conv_desc* d, const void* x16, int ldx16, const void* dy16,
+                         int lddy16, float* dw, int accumulate, const float* bn_gamma,
+                         const float* bn_var, float bn_eps, void* workspace, size_t ws_bytes,
+                         void* stream) {
+  OF_CHECK_ARG(d && x16 && dy16 && dw && workspace, "conv wgrad b16i: NULL pointer");
+  OF_CHECK_ARG(d->kh == 3 && d->kw == 3 && d->stride == 1, "conv wgrad b16i: 3x3 stride 1 only");
+  OF_CHECK_ARG(ldx16 % 8 == 0 && ldx16 >= d->cin_p && lddy16 % 8 == 0 && lddy16 >= d->cout,
+               "conv wgrad b16i: image strides");
+  OF_CHECK_ARG(!bn_gamma || bn_var, "conv wgrad b16i: BN scale needs gamma and var");
+  WgB16iPlan P;
+  wgrad_b16i_plan(d, P);
+  GemmArgs& a = P.a;
+  OF_CHECK_ARG(ws_bytes >= (size_t)a.splits * a.split_stride * sizeof(float),
+               "conv wgrad b16i: workspace too small");
+  a.A = static_cast<const float*>(x16);
+  a.lda = ldx16;
+  a.a_bytes = (int64_t)d->n * d->h * d->w * ldx16 * 2;
+  a.B = static_cast<const float*>(dy16);
+  a.ldb = lddy16;
+  a.b_bytes = (int64_t)d->n * d->ho * d->wo * lddy16 * 2;
+  OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX, "conv wgrad b16i: < 2 GiB images");
+  a.slab = static_cast<float*>(workspace);
+  hipStream_t s = as_stream(stream);
+  const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * 9 * d->cin;
+  const int cfg = P.wco == 4 ? 0 : P.wco == 2 ? 1 : 2;
+  if (timing_on()) timing_begin(s);
+  const dim3 grid(a.tiles_total * a.splits);
+  if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_b16i<2, 4>), grid, dim3(512), 0, s, a);
+  else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_b16i<4, 2>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((conv_wgrad_b16i<4, 1>), grid, dim3(256), 0, s, a);
+  int st = check_launch("conv_wgrad_b16i");
+  if (st) return st;
+  const int rows = 9 * d->cin;
+  const int64_t items = (int64_t)rows * cdiv(d->cout, 4);
+  hipLaunchKernelGGL(b16i_wgrad_reduce, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, s, a.slab,
+                     a.splits, a.split_stride, rows, a.slab_ld, d->cout, dw, accumulate, bn_gamma,
+                     bn_var, bn_eps);
+  if (timing_on()) timing_end(s, 256 + 16 + cfg, flops);
+  return check_launch("b16i_wgrad_reduce");
+}
+
+// out[n] (+)= sum over rows of part[rows][n] in a fixed order (the bias gradient from the dgrad
+// kernels' per-tile column sums): 8 row groups x 32 columns per workgroup, rows strided by 8,
+// the 8 group sums added in order.
+__global__ __launch_bounds__(256) void col_part_reduce_kernel(const float* __restrict__ part,
+                                                              int rows, int n,
+                                                              float* __restrict__ out, int acc) {
+  __shared__ float red[8][32];
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + cl;
+  float s = 0.f;
+  if (col < n)
+    for (int r = g; r < rows; r += 8) s += part[(int64_t)r * n + col];
+  red[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && col < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][cl];
+    out[col] = acc ? out[col] + t : t;
+  }
+}
+
+int of_col_part_reduce(const float* part, int rows, int n, float* out, int accumulate,
+                       void* stream) {
+  OF_CHECK_ARG(part && out && rows > 0 && n > 0, "col_part_reduce: args");
+  hipLaunchKernelGGL(col_part_reduce_kernel, dim3((unsigned)cdiv(n, 32)), dim3(256), 0,
+                     as_stream(stream), part, rows, n, out, accumulate);
+  return check_launch("col_part_reduce");
 }
 
 }  // extern "C"

@@ -55,6 +55,12 @@ struct GemmArgs {
   int vec_ep;             // tile kernels: 4-column epilogue (N, every ld a multiple of 4,
                           // every row pointer 16-byte aligned)
   int act_post;           // dgrad: dx = act'(act_src) * (sum + res) instead of act' * sum + res
+  // bf16 activation images (conv_b16i.hip): output image (C16, ldc16 bf16 per pixel; C may then
+  // be NULL), the dgrad activation source as an image (act16; its sign is all act' needs), and
+  // per-M-tile column sums of the dgrad output (col_part [m tile][N]: bias-gradient partials)
+  uint16_t* C16; int ldc16;
+  const uint16_t* act16; int ld_act16;
+  float* col_part;
   Group grp[MAX_GROUPS];
 };
 

@@ -213,7 +213,13 @@ def resnet_layer_simple(x, nblocks, downsample, idx, store: Optional[ParamStore]
     blocks = stage_blocks(idx, x.shape[-1], nblocks, downsample)
     if store is None:
         store = ParamStore(blocks_spec(blocks), seed=seed, device=x.device)
-    for a, b, p in block_layers(store, blocks):
+    layers = block_layers(store, blocks)
+    flat = [L for blk in layers for L in blk if L is not None]
+    if store.bn_guard is None:          # z kept for BN layers with gamma ~ 0 (ops.BNZGuard)
+        store.bn_guard = ops.BNZGuard(flat)
+    store.bn_guard.poll()
+    store.bn_guard.mark(flat)
+    for a, b, p in layers:
         x = ops.res_block(x, a, b, p)
     x._resnet_store = store
     return x

@@ -480,6 +480,7 @@ class BNZGuard:
         self.layers = [L for L in layers if L.bn is not None]
         self.pending = []
         self.steps = 0
+        self.flagged = set()     # names of the layers that keep z
         if not self.layers:
             return
         dev = self.layers[0].kernel.device
@@ -499,7 +500,14 @@ class BNZGuard:
 
     def _apply(self, mins, thr):
         for L, m in zip(self.layers, mins):
-            if m < thr and not L.store_z:
+            if m < thr:
+                L.store_z = True
+                self.flagged.add(L.name)
+
+    def mark(self, layers):
+        """Apply the flags to other ConvLayer objects over the same weights (by name)."""
+        for L in layers:
+            if L.bn is not None and L.name in self.flagged:
                 L.store_z = True
 
     def check_now(self, lr=1e-4):

@@ -235,6 +235,52 @@ def test_resnet_layer_simple(idx, nblocks, down, cin):
         assert e < REL_TOL, "grad %s rel_l2 %.3e" % (name, e)
 
 
+@pytest.mark.parametrize("case", ["gamma0", "gamma1e-4", "large_residual"])
+def test_resnet_block_bn_guard(case):
+    """One projected residual block (resnet_layer_simple, model.py:20) whose BN gammas are 0 or
+    1e-4, or whose conv_b output is added to a large residual (beta 40 on the projection's BN,
+    |res + beta| >> |gamma zhat|): where recovering zhat from y would divide by ~0 or cancel
+    (ADVICE r3), ops.BNZGuard keeps z for the layer; output, input gradient and every weight
+    gradient against the float64 oracle at 1e-3."""
+    from optical_flow_amd.model import ParamStore, resnet_layer_simple
+    from optical_flow_amd.params import blocks_spec, init_params, perturb_params, stage_blocks
+    blocks = stage_blocks(3, 64, 1, True)
+    spec = blocks_spec(blocks)
+    vals = perturb_params(init_params(spec, 15), 16)
+    pre = blocks[0][0]
+    if case == "gamma0":
+        vals[pre + "/bn_a/gamma"][::3] = 0.0
+        vals[pre + "/bn_b/gamma"][:] = 0.0
+    elif case == "gamma1e-4":
+        vals[pre + "/bn_a/gamma"][:] = 1e-4
+        vals[pre + "/bn_proj/gamma"][:7] = -1e-4
+    else:
+        vals[pre + "/bn_proj/beta"][:] = 40.0
+        vals[pre + "/bn_b/gamma"][:] = 2e-3
+    store = ParamStore(spec, values=vals, device="cuda")
+    g = torch.Generator().manual_seed(3)
+    x0 = torch.randn(2, 32, 48, 64, generator=g, dtype=torch.float64)
+    x = dev(x0.float()).requires_grad_(True)
+    store.zero_grad()
+    y = resnet_layer_simple(x, 1, True, 3, store=store)
+    dy0 = torch.randn(tuple(y.shape), generator=g, dtype=torch.float64)
+    y.backward(dev(dy0.float()))
+    torch.cuda.synchronize()
+    want = {"gamma0": {pre + "/conv_a", pre + "/conv_b"}, "gamma1e-4": {pre + "/conv_a", pre + "/proj"},
+            "large_residual": {pre + "/conv_b"}}[case]
+    assert store.bn_guard.flagged == want, store.bn_guard.flagged
+    p = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in vals.items()}
+    xo = x0.clone().requires_grad_(True)
+    yo = R.resnet_block(xo, p, pre, 2, True)
+    yo.backward(dy0)
+    assert rel_inf(y, yo) < REL_TOL
+    assert rel_l2(x.grad, xo.grad) < REL_TOL
+    for name, gr in store.grads().items():
+        assert torch.isfinite(gr).all(), name
+        e = rel_l2(gr, p[name].grad)
+        assert e < REL_TOL, "grad %s rel_l2 %.3e" % (name, e)
+
+
 def test_resnet_layer_simple_fresh_layers():
     """Without a store the call creates fresh layers (Keras functional semantics), seeded."""
     from optical_flow_amd.model import resnet_layer_simple
@@ -265,7 +311,6 @@ def test_bn_gamma_near_zero(precision):
     vals["ResNet18/layer1_bn/gamma"] = g
     vals["ResNet18/res2_0/bn_a/gamma"] = np.full(64, 1e-4, np.float32)
     vals["ResNet18/res3_0/bn_b/gamma"][:] = 0.0    # conv_b: residual added after BN
-    vals["ResNet18/res3_0/bn_proj/beta"][:] = 30.0   # large residual into res3_0's add
     vals["ResNet18/res4_0/bn_proj/gamma"][:5] = 1e-4
     net = FlowNet(H, W, values=vals, precision=precision)
     batch = synthetic_batch(B, H, W, seed=77)
@@ -285,8 +330,11 @@ def test_bn_gamma_near_zero(precision):
         ["conv1", "ResNet18/res2_0/conv_a", "ResNet18/res3_0/conv_b",
          "ResNet18/res4_0/proj"]), net.store.bn_guard.stored()
     tol = REL_TOL if precision == "fp32" else 1e-2
+    bad = []
     for name, gr in net.store.grads().items():
         assert torch.isfinite(gr).all(), name
-        if name.startswith("ResNet18"):
-            e = rel_l2(gr, grads_o[name])
-            assert e < tol, "grad %s rel_l2 %.3e" % (name, e)
+        e = rel_l2(gr, grads_o[name])
+        print("%-40s rel_l2 %.3e" % (name, e))
+        if name.startswith("ResNet18") and e >= tol:
+            bad.append((name, e))
+    assert not bad, bad
