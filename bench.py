@@ -53,6 +53,10 @@ def kind_parts(kind):
     bf16 implicit GEMMs 64 + mode*8 + cfg, bf16 halo-tiled 3x3 96 + mode*8 + cfg,
     fp32 on the split-bf16 halo-tiled 3x3 kernels 128 + mode*8 + cfg, on the split-bf16
     implicit GEMM (other shapes) 160 + mode*8 + cfg (optical_flow_amd/csrc/conv_f32.hip)."""
+    if kind >= 304:                               # conv_wgrad_b16i (bf16 images)
+        return 2, kind - 304, "wgrad_b16i"
+    if kind >= 288:                               # conv_halo_b16 (bf16 images) fwd / dgrad
+        return (kind - 288) // 8, (kind - 288) % 8, "halo_b16"
     if kind == KIND_STEM_X3:
         return 0, 0, "stem_x3"
     if kind == KIND_STEM_WG_X3:
@@ -116,8 +120,16 @@ KIND_STEM_B16 = 186     # conv_stem_x3<32, 1> (the bf16 stem forward, one plane)
 KIND_STEM_WG_B16 = 187  # conv_wgrad_stem_x3<1> (its bf16 weight gradient)
 
 
+HALO_B16 = {0: "128, 4, 2", 1: "96, 4, 2", 2: "64, 8, 1", 3: "32, 8, 1"}  # conv_halo_b16<BN, waves>
+WGRAD_B16I = {0: "2, 4", 1: "4, 2", 2: "4, 1"}                          # conv_wgrad_b16i<waves>
+
+
 def kind_name(kind):
     mode, cfg, fam = kind_parts(kind)
+    if fam == "halo_b16":
+        return "%s_halo_b16<%s>" % (MODE_NAMES[mode], HALO_B16[cfg])
+    if fam == "wgrad_b16i":
+        return "wgrad_b16i<%s>" % WGRAD_B16I[cfg]
     if fam == "stem_x3":
         return "wgrad_stem_x3" if mode == 2 else "fwd_stem_x3"
     if fam == "stem_b16":
@@ -146,6 +158,11 @@ def kind_name(kind):
 def kernel_symbol(kind):
     """rocprofv3 name of the conv kernel instance behind a timing kind."""
     mode, cfg, fam = kind_parts(kind)
+    if fam == "halo_b16":
+        return "void oflow::(anonymous namespace)::conv_halo_b16<%s, %d, 16, 32>(oflow::GemmArgs)" % (
+            HALO_B16[cfg], mode)
+    if fam == "wgrad_b16i":
+        return "void oflow::(anonymous namespace)::conv_wgrad_b16i<%s>(oflow::GemmArgs)" % WGRAD_B16I[cfg]
     if fam == "stem_x3":
         if mode == 2:
             return "void oflow::conv_wgrad_stem_x3<3>(oflow::GemmArgs)"

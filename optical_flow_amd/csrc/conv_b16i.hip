@@ -652,7 +652,7 @@ int of_conv2d_b16i(int mode, const of_conv_desc* d, const of_b16i_io* io, const 
     B16I_LAUNCH(MODE_DGRAD)
   }
 #undef B16I_LAUNCH
-  if (timing_on()) timing_end(s, 256 + 8 * mode + cfg, flops);
+  if (timing_on()) timing_end(s, 288 + 8 * mode + cfg, flops);   // bench.py kind_parts
   return check_launch("conv_halo_b16");
 }
 
@@ -724,6 +724,7 @@ int of_conv2d_wgrad_b16i(const of_conv_desc* d, const void* x16, int ldx16, cons
   if (cfg == 0) hipLaunchKernelGGL((conv_wgrad_b16i<2, 4>), grid, dim3(512), 0, s, a);
   else if (cfg == 1) hipLaunchKernelGGL((conv_wgrad_b16i<4, 2>), grid, dim3(512), 0, s, a);
   else hipLaunchKernelGGL((conv_wgrad_b16i<4, 1>), grid, dim3(256), 0, s, a);
+  if (timing_on()) timing_end(s, 304 + cfg, flops);     // (the kernel, not the reduce)
   int st = check_launch("conv_wgrad_b16i");
   if (st) return st;
   const int rows = 9 * d->cin;
@@ -731,7 +732,6 @@ int of_conv2d_wgrad_b16i(const of_conv_desc* d, const void* x16, int ldx16, cons
   hipLaunchKernelGGL(b16i_wgrad_reduce, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, s, a.slab,
                      a.splits, a.split_stride, rows, a.slab_ld, d->cout, dw, accumulate, bn_gamma,
                      bn_var, bn_eps);
-  if (timing_on()) timing_end(s, 256 + 16 + cfg, flops);
   return check_launch("b16i_wgrad_reduce");
 }
 

@@ -950,11 +950,179 @@ def res_block(x, a: ConvLayer, b: ConvLayer, p: Optional[ConvLayer] = None):
     return _ResBlockFn.apply(x, *params, (a, b, p))
 
 
+# bf16 activation images for the bf16 flow heads (configs 3-5; conv_b16i.hip).  In bf16 mode
+# every consumer of a head conv's output rounds it to bf16 anyway (the next conv's forward and
+# weight gradient) or needs only its sign (the LeakyReLU derivative), so the outputs of c0..c3
+# are stored as bf16 NHWC images only, the input gradients between them likewise, and the
+# convs run on the DMA-fed large-tile kernels (of_conv2d_b16i, of_conv2d_wgrad_b16i); the bias
+# gradients come from the input-gradient kernels' column sums of the fp32 values (exact sums,
+# as the oracle's).  The rounding points are those of the fp32-image path, so the results
+# agree with it up to fp32 summation order.  Used for levels whose forward grid has at least
+# B16I_MIN_TILES 16 x 32 tiles (the kernels take one K slice: smaller grids keep the halo
+# kernels with K splits); OFLOW_B16I=0 turns it off, OFLOW_B16I_MIN_TILES overrides the size.
+B16I = os.environ.get("OFLOW_B16I", "1") == "1"
+B16I_MIN_TILES = int(os.environ.get("OFLOW_B16I_MIN_TILES", "256"))
+
+
+def _img16_ok(layers, x) -> bool:
+    if not B16I or len(layers) < 3:
+        return False
+    n, h, w, _ = x.shape
+    if (n * ((h + 15) // 16) * ((w + 31) // 32)) < B16I_MIN_TILES:
+        return False
+    for L in layers[:-1]:
+        if not (L.precision == "bf16" and L.kh == 3 and L.kw == 3 and L.stride == 1 and
+                L.bn is None and L.cout % 32 == 0 and L.act == ACT_LEAKY):
+            return False
+    last = layers[-1]
+    return last.kh == 3 and last.stride == 1 and last.cout <= 4 and last.cin_p == layers[-2].cout
+
+
+def _img(shape, device):
+    return torch.empty(shape, device=device, dtype=torch.bfloat16)
+
+
+def _to_img16(t, ld):
+    """fp32 NHWC -> bf16 image with ld channels (zero-padded)."""
+    n, h, w, c = t.shape
+    out = _img((n, h, w, ld), t.device)
+    call("of_to_bf16_image", _ptr(t), n * h * w, c, c, _ptr(out), ld, _stream())
+    return out
+
+
+def _b16i_io(**kw):
+    r = _lib.B16iIO()
+    for k, v in kw.items():
+        setattr(r, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
+    return r
+
+
+def _stack_fwd_img16(layers, x):
+    """Forward of a bf16 flow head on images: returns (saved tensors, output)."""
+    nb, h, w, cx = x.shape
+    s = _stream()
+    x16 = _to_img16(x, (cx + 31) // 32 * 32)
+    imgs = [x16]
+    cur = x16
+    for i, layer in enumerate(layers[:-2]):
+        d = layer.desc(nb, h, w)
+        wf, _ = layer.packed(d)
+        y16 = _img((nb, h, w, layer.cout), x.device)
+        _tag(layer, 0)
+        io = _b16i_io(a16=cur, lda16=cur.shape[-1], y16=y16, ldy16=layer.cout)
+        call("of_conv2d_b16i", 0, C.byref(d), C.byref(io), _ptr(wf), _ptr(layer.bias), None, None,
+             None, None, BN_EPS, layer.act, layer.alpha, s)
+        imgs.append(y16)
+        cur = y16
+    l4 = layers[-2]                      # fp32 output: the narrow flow conv reads it
+    d = l4.desc(nb, h, w)
+    wf, _ = l4.packed(d)
+    y4 = torch.empty((nb, h, w, l4.cout), device=x.device)
+    _tag(l4, 0)
+    io = _b16i_io(a16=cur, lda16=cur.shape[-1], y=y4, ldy=l4.cout)
+    call("of_conv2d_b16i", 0, C.byref(d), C.byref(io), _ptr(wf), _ptr(l4.bias), None, None, None,
+         None, BN_EPS, l4.act, l4.alpha, s)
+    l5 = layers[-1]
+    d = l5.desc(nb, h, w)
+    wf, _ = l5.packed(d)
+    y5 = torch.empty((nb, h, w, l5.cout), device=x.device)
+    _tag(l5, 0)
+    entry, wsz = l5.fwd_entry(d)
+    wsk, wsp, wsb = _workspace(wsz, x.device)
+    call(entry, C.byref(d), _ptr(y4), l4.cout, _ptr(wf), _ptr(l5.bias), None, None, None, None,
+         BN_EPS, None, 0, l5.act, l5.alpha, None, 0, _ptr(y5), l5.cout, wsp, wsb, s)
+    return imgs + [y4, y5], y5
+
+
+def _wgrad_img16(layer, d, x16, dy16, tk, part=None, dy32=None):
+    """Weight gradient of one head conv from images + its bias gradient (from the column
+    sums the input-gradient kernel left in ``part``, or from the fp32 dy32)."""
+    tb = grad_target(layer.bias)
+    if tk[1] != tb[1]:
+        raise RuntimeError("kernel and bias gradients must both use the arena or not")
+    side = SIDE_STREAM_WGRAD and tk[1] == 1 and d.n * d.ho * d.wo <= _side_max_pix(layer)
+    with torch.cuda.stream(side_stream(x16, dy16, part, dy32)) if side else \
+            contextlib.nullcontext():
+        ss = _stream()
+        wsb = _lib.lib().of_conv2d_wgrad_b16i_workspace(C.byref(d))
+        ws = torch.empty(wsb // 4 + 1, device=x16.device)
+        _tag(layer, 2)
+        call("of_conv2d_wgrad_b16i", C.byref(d), _ptr(x16), x16.shape[-1], _ptr(dy16),
+             dy16.shape[-1], _ptr(tk[0]), tk[1], None, None, 0.0, _ptr(ws), wsb, ss)
+        if part is not None:
+            call("of_col_part_reduce", _ptr(part), part.shape[0], layer.cout, _ptr(tb[0]), tb[1],
+                 ss)
+        else:
+            npix = dy32.numel() // dy32.shape[-1]
+            cws = torch.empty(_lib.lib().of_colsum_workspace(npix, layer.cout) // 4 + 1,
+                              device=dy32.device)
+            call("of_colsum", _ptr(dy32), npix, layer.cout, dy32.shape[-1], _ptr(tb[0]), tb[1],
+                 _ptr(cws), ss)
+    return tb
+
+
+def _stack_bwd_img16(layers, saved, g, need_x):
+    """Backward of _stack_fwd_img16 (g: the padded flow gradient of the last conv)."""
+    imgs, y4, y5 = saved[:-2], saved[-2], saved[-1]
+    nb, h, w, _ = y4.shape
+    s = _stream()
+    rets = {}
+    l5, l4 = layers[-1], layers[-2]
+    # c5 (narrow, fp32): weight gradient and input gradient (with c4's LeakyReLU derivative)
+    d5 = l5.desc(nb, h, w)
+    _, wd5 = l5.packed(d5)
+    tk5, tb5 = grad_target(l5.kernel), grad_target(l5.bias)
+    wgrad_stack(l5, y4, g, d5, tk5, tb5)
+    _grad_ready(l5.kernel, l5.bias)
+    gy4 = torch.empty_like(y4)
+    _tag(l5, 1)
+    entry, wsz = l5.dgrad_entry(d5)
+    wsk, wsp, wsb = _workspace(wsz, y4.device)
+    call(entry, C.byref(d5), _ptr(g), g.shape[-1], _ptr(wd5), _ptr(y4), l4.cout, l4.act, l4.alpha,
+         _ptr(gy4), l4.cout, wsp, wsb, s)
+    rets[l5.name] = (tk5[2], tb5[2])
+    dy16 = _to_img16(gy4, l4.cout)
+    dy32 = gy4
+    part = None
+    dx = None
+    for i in range(len(layers) - 2, -1, -1):
+        layer = layers[i]
+        x16 = imgs[i]
+        d = layer.desc(nb, h, w)
+        _, wd = layer.packed(d)
+        tk = grad_target(layer.kernel)
+        tb = _wgrad_img16(layer, d, x16, dy16, tk, part=part, dy32=dy32 if part is None else None)
+        _grad_ready(layer.kernel, layer.bias)
+        rets[layer.name] = (tk[2], tb[2])
+        if i > 0:
+            prev = layers[i - 1]
+            tiles = _lib.lib().of_conv2d_b16i_tiles(1, C.byref(d))
+            part = torch.empty((tiles, layer.cin_p), device=y4.device)
+            gx16 = _img((nb, h, w, layer.cin_p), y4.device)
+            _tag(layer, 1)
+            io = _b16i_io(a16=dy16, lda16=dy16.shape[-1], y16=gx16, ldy16=layer.cin_p,
+                          act16=x16, ld_act16=x16.shape[-1], col_part=part)
+            call("of_conv2d_b16i", 1, C.byref(d), C.byref(io), _ptr(wd), None, None, None, None,
+                 None, 0.0, prev.act, prev.alpha, s)
+            dy16, dy32 = gx16, None
+        elif need_x:
+            dx = torch.empty((nb, h, w, layer.cin_p), device=y4.device)
+            _tag(layer, 1)
+            io = _b16i_io(a16=dy16, lda16=dy16.shape[-1], y=dx, ldy=layer.cin_p)
+            call("of_conv2d_b16i", 1, C.byref(d), C.byref(io), _ptr(wd), None, None, None, None,
+                 None, 0.0, ACT_NONE, 0.0, s)
+    out = []
+    for layer in layers:
+        out += list(rets[layer.name])
+    return dx, out
+
+
 class _ConvStackFn(torch.autograd.Function):
     """A chain of plain convs (bias + activation, no BN / residual): the six-conv flow head
     of ``flow_module`` (model.py:104-114).  The backward is fused across layers: each input
     gradient kernel multiplies by the producer layer's LeakyReLU derivative in its epilogue
-    (act_src = that layer's saved output), so no separate activation-backward pass runs."""
+    (act_src = that layer's saved output), so no separate activation-backward pass runs.
+    bf16 heads on large grids keep their activations as bf16 images (_img16_ok)."""
 
     @staticmethod
     def forward(ctx, x, *args):
@@ -963,6 +1131,12 @@ class _ConvStackFn(torch.autograd.Function):
         n = len(layers)
         _check_dev(x)
         x = x.contiguous()
+        ctx.img16 = _img16_ok(layers, x)
+        if ctx.img16:
+            saved, out = _stack_fwd_img16(layers, x)
+            ctx.layers = layers
+            ctx.save_for_backward(*saved)
+            return out
         s = _stream()
         acts = [x]
         for i, layer in enumerate(layers):
@@ -1008,6 +1182,10 @@ class _ConvStackFn(torch.autograd.Function):
             if fg is not None:
                 fg.filled = False
             g = _pad_channels(dy.contiguous(), _c4(layers[-1].cout))
+        if ctx.img16:
+            assert layers[-1].act == ACT_NONE
+            dx, rets = _stack_bwd_img16(layers, acts, g, needs[0])
+            return (dx, *rets, None, None)
         if layers[-1].act != ACT_NONE:
             gz = torch.empty_like(g)
             y = _pad_channels(acts[-1], g.shape[-1])

@@ -93,8 +93,14 @@ def _rand_like(t, seed):
     return torch.tensor(r.standard_normal(tuple(t.shape)), dtype=torch.float64)
 
 
+@pytest.mark.parametrize("img16", [False, True], ids=["f32img", "bf16img"])
 @pytest.mark.parametrize("level", [0, 1, 2, 3])
-def test_flow_module_bf16_teacher_forced(setup, level):
+def test_flow_module_bf16_teacher_forced(setup, level, img16, monkeypatch):
+    """img16: the head runs on bf16 activation images and the conv_halo_b16 / conv_wgrad_b16i
+    kernels (ops._img16_ok, forced here for every level by B16I_MIN_TILES = 0); otherwise
+    (threshold above the grid) on the fp32-activation halo kernels."""
+    from optical_flow_amd import ops
+    monkeypatch.setattr(ops, "B16I_MIN_TILES", 0 if img16 else 1 << 30)
     net, p, blocks, stage_in, feats, flows = setup
     f = feats[3 - level]
     n = f.shape[0] // 2
@@ -110,6 +116,7 @@ def test_flow_module_bf16_teacher_forced(setup, level):
     # the slopes the HIP head took: its saved LeakyReLU outputs (the conv stack's autograd
     # node keeps them for the fused activation-derivative epilogues)
     acts = out.grad_fn.saved_tensors
+    assert (acts[1].dtype == torch.bfloat16) == img16          # the path the test asked for
     masks = [(a > 0).cpu() for a in acts[1:6]]
     (out * dev(g.float())).sum().backward()
     torch.cuda.synchronize()
