@@ -584,6 +584,11 @@ def main():
                        "execution": ("HIP graph: the train step captured once, replayed per step"
                                      if graphed is not None else "eager launches"),
                        "warp_backward": "deterministic" if ops.DETERMINISTIC else "atomic",
+                       **({"grad_allreduce": (
+                           "C-ABI RCCL communicator (of_comm_*), self-tested at init"
+                           if trainer.reducer.comm.kind == "rccl" else
+                           "torch.distributed %s" % dist.get_backend(trainer.reducer.comm.group))}
+                          if trainer.reducer is not None else {}),
                        **({"levels": args.levels} if args.levels != 4 else {})},
             "algorithmic_gflop_per_pair": round(gfp, 2),
             "model_tflops": round(gfp * value / 1e3, 2),

@@ -113,11 +113,49 @@ class TorchComm:
         self._works = []
 
 
+def selftest(comm, rank: int, world: int, n: int = 4096) -> bool:
+    """One small all-reduce checked on the host: every rank contributes rank + 1 (plus a
+    position ramp), the sum is known in closed form.  Run once when a data-parallel trainer
+    makes its communicator, so an N > 1 RCCL path that cannot sum correctly is caught before
+    the first step (it has only ever run at N = 1 on the development boxes)."""
+    t = (torch.arange(n, dtype=torch.float32, device="cuda") + (rank + 1)).contiguous()
+    comm.allreduce_(t)
+    torch.cuda.current_stream().synchronize()
+    comm.wait()
+    want = torch.arange(n, dtype=torch.float32, device="cuda") * world + world * (world + 1) / 2
+    return bool(torch.equal(t, want))
+
+
 def make_comm(kind: str, rank: int = 0, world: int = 1):
-    """"rccl" -> RcclComm(rank, world) on the current device; "torch" -> TorchComm over the
-    default process group."""
+    """"rccl" -> RcclComm(rank, world) on the current device, self-tested (``selftest``) when
+    world > 1; if that fails on any rank (the decision is taken jointly over the default
+    process group), every rank falls back to torch.distributed's own RCCL (a "nccl" process
+    group) with a warning.  "torch" -> TorchComm over the default process group;
+    "torch-nccl" -> TorchComm over a new "nccl" group (RCCL through torch)."""
     if kind == "rccl":
-        return RcclComm(rank, world)
+        if world <= 1:
+            return RcclComm(rank, world)
+        import torch.distributed as dist
+        comm, ok = None, False
+        try:
+            comm = RcclComm(rank, world)
+            ok = selftest(comm, rank, world)
+        except Exception as e:  # noqa: BLE001 -- any failure means: fall back
+            import warnings
+            warnings.warn("C-ABI RCCL communicator failed on rank %d: %r" % (rank, e))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)        # control plane (gloo)
+        if int(flag) == 1:
+            return comm
+        import warnings
+        warnings.warn("C-ABI RCCL communicator self-test failed: gradients go over "
+                      "torch.distributed's nccl (RCCL) backend instead")
+        if comm is not None:
+            comm.close(abort=True)
+        kind = "torch-nccl"
     if kind == "torch":
         return TorchComm()
-    raise ValueError("comm kind %r (rccl | torch)" % kind)
+    if kind == "torch-nccl":
+        import torch.distributed as dist
+        return TorchComm(dist.new_group(backend="nccl"))
+    raise ValueError("comm kind %r (rccl | torch | torch-nccl)" % kind)

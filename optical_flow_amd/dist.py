@@ -4,10 +4,11 @@ communicator of comm.py, over xGMI inside an MI355X node).
 The reference is single-process; this is the build-added K14.  Buckets are
 contiguous slices of the gradient arena (ordered by backward completion, model.backward_order)
 and each is all-reduced (SUM) as soon as every parameter in it has been written by its
-backward kernels: the reduction is enqueued on the weight-gradient side stream once that has
-waited for the compute stream, so RCCL runs after the producing kernels and the reduction of
-the finest flow head overlaps the backward of the coarser levels and the encoder.  The
-compute stream joins the side stream at the end of the backward (ops._side_join), before Adam.
+backward kernels: the reduction is enqueued on a stream of its own (ops.comm_stream) once that
+has waited for the compute stream and the weight-gradient side stream, so RCCL runs after the
+producing kernels, the reduction of the finest flow head overlaps the backward of the coarser
+levels and the encoder, and a slow peer stalls neither stream.  The compute stream joins the
+collective stream at the end of the backward (ops._side_join), before Adam.
 The 1/world average is folded into the Adam launch (grad_scale).
 """
 from __future__ import annotations
@@ -55,6 +56,7 @@ class GradBucketReducer:
                 self.bucket_of[id(store.params[n])] = bi
         self._pending: List[int] = []
         self._launched: List[bool] = []
+        self.launch_log: List[tuple] = []      # (bucket, on the collective stream) per launch
 
     # -- called by ops after a parameter's gradient kernels are enqueued -----------------
     def _on_grad(self, param):
@@ -70,17 +72,20 @@ class GradBucketReducer:
         view = self.store.grad_arena[lo:hi]
         # A bucket's gradients are written on the current stream (BN / bias reductions) and on
         # the wgrad side stream (ops.side_stream): during the backward the all-reduce is
-        # enqueued on the side stream once it has waited for the current one, so RCCL is
-        # ordered after both without stalling the input-gradient chain.
-        side = in_backward and view.is_cuda and ops.SIDE_STREAM_WGRAD
-        with torch.cuda.stream(ops.side_stream()) if side else contextlib.nullcontext():
+        # enqueued on the collective stream once that has waited for both.
+        own = in_backward and _device_tensor(view)
+        with torch.cuda.stream(ops.comm_stream(view)) if own else contextlib.nullcontext():
             self.comm.allreduce_(view)
         self._launched[bi] = True
+        self.launch_log.append((bi, own))
 
     def begin(self):
         """Arm for one backward pass."""
         self._pending = [len(b) for b in self.buckets]
         self._launched = [False] * len(self.buckets)
+        self.launch_log = []
+        if self.world == 1 and getattr(self.comm, "kind", "") == "torch":
+            return            # nothing to reduce, and maybe no process group to reduce over
         ops.set_grad_ready_hook(self._on_grad)
 
     def finish(self) -> float:
@@ -89,12 +94,20 @@ class GradBucketReducer:
         already joined the side stream at the end of the backward, so only an asynchronous
         communicator failure is checked); returns the grad scale (1/world) for the optimizer."""
         ops.set_grad_ready_hook(None)
+        if self.world == 1 and getattr(self.comm, "kind", "") == "torch":
+            return 1.0
         for bi in range(len(self.buckets)):
             if not self._launched[bi]:
                 self._launch(bi, in_backward=False)
-        ops.side_join_now()
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            ops.side_join_now()
         self.comm.wait()
         return 1.0 / self.world
+
+
+def _device_tensor(t) -> bool:
+    """Whether a bucket lives in GPU memory (its all-reduce then gets the collective stream)."""
+    return t.is_cuda
 
 
 def init_from_env(backend: Optional[str] = None):

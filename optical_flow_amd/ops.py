@@ -189,8 +189,35 @@ def _side_join():
 def side_join_now():
     """Order each device's current stream after everything enqueued so far on its side
     streams (the end-of-backward join, also used after work launched outside a backward)."""
-    for dev, s in list(_SIDE.items()) + list(_CORR_SIDE.items()):
+    for dev, s in list(_SIDE.items()) + list(_CORR_SIDE.items()) + list(_COMM.items()):
         stream_wait(torch.cuda.current_stream(dev), s)
+
+
+# The data-parallel collectives' own stream (dist.GradBucketReducer): a bucket's all-reduce
+# waits for the work enqueued so far on the current stream and on the wgrad side stream (the
+# kernels that wrote the bucket), and nothing but the end-of-backward join waits for it -- a
+# slow peer's collective then holds back neither this rank's remaining weight gradients (side
+# stream) nor its input-gradient chain (current stream).
+_COMM = {}
+
+
+def comm_stream(*tensors):
+    global _side_armed
+    cur = torch.cuda.current_stream()
+    s = _COMM.get(cur.device)
+    if s is None:
+        s = _COMM[cur.device] = torch.cuda.Stream(cur.device)
+    stream_wait(s, cur)
+    side = _SIDE.get(cur.device)
+    if side is not None:
+        stream_wait(s, side)
+    for t in tensors:
+        if t is not None:
+            t.record_stream(s)
+    if not _side_armed:
+        _side_armed = True
+        torch.autograd.Variable._execution_engine.queue_callback(_side_join)
+    return s
 
 
 def side_stream(*tensors):
@@ -1172,6 +1199,7 @@ class _ConvStackFn(torch.autograd.Function):
                 dy.stride()[-2] == 4):
             g = fg.buffer()                 # loss (+ upscale) gradient, already padded
             fg.filled = fg.added = False
+            ctx.fg_release = fg             # back to the pool once its readers are enqueued
         else:
             if fg is not None and fg.added:
                 # autograd summed the loss gradient with a further consumer's before the
@@ -1185,6 +1213,8 @@ class _ConvStackFn(torch.autograd.Function):
         if ctx.img16:
             assert layers[-1].act == ACT_NONE
             dx, rets = _stack_bwd_img16(layers, acts, g, needs[0])
+            if getattr(ctx, "fg_release", None) is not None:
+                ctx.fg_release.release()
             return (dx, *rets, None, None)
         if layers[-1].act != ACT_NONE:
             gz = torch.empty_like(g)
@@ -1233,6 +1263,8 @@ class _ConvStackFn(torch.autograd.Function):
         for layer in layers:
             rets += list(layer._ret)
             layer._ret = None
+        if getattr(ctx, "fg_release", None) is not None:
+            ctx.fg_release.release()
         return (dx, *rets, None, None)
 
 
@@ -1562,21 +1594,40 @@ class FlowGrad:
     (B, h, w, 4) buffer (channels 2-3 stay zero) and returns a view of it; the upscale
     backward, which autograd runs afterwards, adds its input gradient into the same buffer
     and returns None; the flow head's backward then reads the buffer as its padded dy.  This
-    replaces autograd's add pass and the channel-padding fill + copy per level.  The buffers
-    are cached per (device, shape): stream order protects their reuse across steps."""
-    _cache = {}
+    replaces autograd's add pass and the channel-padding fill + copy per level.  Each FlowGrad
+    (one per forward of a flow head) owns its buffer from first use until the head's backward
+    has consumed it (or the FlowGrad is dropped): two forwards before one backward (micro-batch
+    accumulation, two same-shape models) get distinct buffers.  Released buffers are pooled per
+    (device, shape) for the next steps; stream order protects their reuse."""
+    _pool = {}
 
     def __init__(self, shape, device):
         self.shape, self.device = tuple(shape), device
         self.filled = False             # the loss backward wrote the buffer this backward
         self.added = False              # the upscale backward added into it
+        self._buf = None
+
+    def _key(self):
+        return (str(self.device), self.shape)
 
     def buffer(self):
-        key = (str(self.device), self.shape)
-        b = FlowGrad._cache.get(key)
-        if b is None:
-            b = FlowGrad._cache[key] = torch.zeros(self.shape[:3] + (4,), device=self.device)
-        return b
+        if self._buf is None:
+            free = FlowGrad._pool.setdefault(self._key(), [])
+            self._buf = free.pop() if free else torch.zeros(self.shape[:3] + (4,),
+                                                            device=self.device)
+        return self._buf
+
+    def release(self):
+        """Return the buffer to the pool (its consumers are enqueued; channels 2-3 stay 0)."""
+        if self._buf is not None:
+            FlowGrad._pool.setdefault(self._key(), []).append(self._buf)
+            self._buf = None
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:       # interpreter shutdown
+            pass
 
 
 class FlowAdd:

@@ -101,7 +101,8 @@ class Trainer:
                 dist = torch.distributed
                 rank, world = ((dist.get_rank(), dist.get_world_size())
                                if dist.is_initialized() else (0, 1))
-                kind = comm or ("rccl" if flow_net.store.arena.is_cuda else "torch")
+                kind = comm or os.environ.get("OFLOW_DP_COMM") or (
+                    "rccl" if flow_net.store.arena.is_cuda else "torch")
                 comm = make_comm(kind, rank, world)
             self.reducer = GradBucketReducer(flow_net.store, comm=comm)
 

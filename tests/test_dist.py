@@ -109,3 +109,51 @@ def test_data_parallel_average_equals_global_batch():
     ref = torch.cat([g[k].flatten() for k in sorted(g)]).numpy()
     np.testing.assert_allclose(res[0], ref, rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(res[1], ref, rtol=1e-9, atol=1e-12)
+
+
+def test_bucket_allreduce_on_collective_stream(monkeypatch):
+    """During the backward each completed bucket's all-reduce is enqueued on the collective
+    stream (ops.comm_stream: ordered after the compute and weight-gradient side streams), never
+    on the side stream itself, in backward-completion (arena) order, each bucket exactly once;
+    leftovers at finish() go on the current stream.  (Streams stubbed: CPU.)"""
+    import contextlib
+    from optical_flow_amd import dist as D
+    from optical_flow_amd import ops
+    from optical_flow_amd.model import ParamStore, backward_order
+    from optical_flow_amd.params import flow_net_spec
+    calls = []
+
+    class FakeComm:
+        kind, world = "fake", 2
+
+        def allreduce_(self, t):
+            calls.append(("allreduce", t.data_ptr(), t.numel()))
+
+        def wait(self):
+            calls.append(("wait",))
+
+    st = ParamStore(flow_net_spec(), device="cpu", order=backward_order())
+    red = D.GradBucketReducer(st, bucket_bytes=2 << 20, comm=FakeComm())
+    monkeypatch.setattr(D, "_device_tensor", lambda t: True)
+    monkeypatch.setattr(ops, "comm_stream", lambda *t: calls.append(("comm_stream", t[0].data_ptr())) or "S")
+    monkeypatch.setattr(ops, "side_stream", lambda *t: (_ for _ in ()).throw(AssertionError("side")))
+    monkeypatch.setattr(torch.cuda, "stream", lambda s: contextlib.nullcontext())
+    red.begin()
+    names = st.arena_order
+    held = names[-1]                             # one parameter never reports: a leftover
+    for name in names[:-1]:
+        ops._grad_ready(st.params[name])
+    assert red.finish() == 0.5
+    nb = len(red.buckets)
+    assert [b for b, _ in red.launch_log] == list(range(nb))
+    assert all(own for _, own in red.launch_log[:-1]) and red.launch_log[-1] == (nb - 1, False)
+    ar = [c for c in calls if c[0] == "allreduce"]
+    cs = [c for c in calls if c[0] == "comm_stream"]
+    assert len(ar) == nb and len(cs) == nb - 1
+    for (lo, hi), c in zip(red.ranges, ar):
+        assert c[1] == st.grad_arena[lo:hi].data_ptr() and c[2] == hi - lo
+    # every collective-stream fork precedes its all-reduce
+    for i in range(nb - 1):
+        k = calls.index(("comm_stream", ar[i][1]))
+        assert calls[k + 1] == ar[i]
+    assert held in red.buckets[-1]

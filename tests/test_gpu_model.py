@@ -338,3 +338,27 @@ def test_bn_gamma_near_zero(precision):
         if name.startswith("ResNet18") and e >= tol:
             bad.append((name, e))
     assert not bad, bad
+
+
+def test_two_forwards_one_backward():
+    """Two forwards of the same net before one backward (micro-batch accumulation):
+    each forward's flow heads own their loss-gradient buffers (ops.FlowGrad), so the summed
+    loss's gradients equal the sum of the two batches' separate gradients."""
+    from optical_flow_amd.loss import LossLayer
+    net, vals, batch, blocks = _setup(64, 128, 2, seed=3)
+    from optical_flow_amd.data import synthetic_batch
+    b1 = dev(torch.from_numpy(batch))
+    b2 = dev(torch.from_numpy(synthetic_batch(2, 64, 128, seed=777)))
+    sep = []
+    for b in (b1, b2):
+        net.store.zero_grad()
+        LossLayer()(b, net(b)).backward()
+        torch.cuda.synchronize()
+        sep.append(net.store.grad_arena.clone())
+    net.store.zero_grad()
+    loss = LossLayer()(b1, net(b1)) + LossLayer()(b2, net(b2))
+    loss.backward()
+    torch.cuda.synchronize()
+    err = rel_l2(net.store.grad_arena, sep[0] + sep[1])
+    print("two forwards, one backward: grad rel_l2 %.2e" % err)
+    assert err < 1e-5, err
