@@ -170,3 +170,95 @@ def test_config5_768x1024_bf16():
     assert errs[0][0] < BF16_GRAD_WORST, errs[0]
     kinds = {k for _, k in launches}
     assert any(96 <= k < 128 for k in kinds), sorted(kinds)      # bf16 halo-tiled kernels ran
+
+
+def test_config3_384x512_b32_bf16():
+    """Config 3 (384 x 512, B = 32, bf16) at its own size: the kernel forms the B = 32 plans
+    pick (the bf16-image flow heads at levels 2-3, conv_halo_b16 / conv_wgrad_b16i) checked
+    against the bf16-rounded oracle on 2 of the 32 pairs -- the forward is per pair, and so is
+    every gradient when the output gradient is zero on the other 30 pairs:
+      * the whole net's forward: flows of pairs 3 and 17 (oracle on those 2 pairs);
+      * the level-3 flow module (model.py:80-116; 54.7 % of the FLOPs) teacher-forced with the
+        HIP encoder's features at B = 32 and an output gradient that is nonzero on pairs 3
+        and 17 only: outputs, input gradients and all 12 weight / bias gradients against the
+        oracle on those 2 pairs (the LeakyReLU slopes the HIP head took given to the oracle,
+        as test_gpu_bf16_modules.py), 1e-2 relative L2."""
+    from optical_flow_amd import _lib, ops
+    from optical_flow_amd.data import synthetic_batch
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params, perturb_params
+    H, W, B, pick = 384, 512, 32, [3, 17]
+    vals = perturb_params(init_params(flow_net_spec(), 11), 12)
+    batch = synthetic_batch(B, H, W, seed=4321)
+    net = FlowNet(H, W, values=vals, precision="bf16")
+    lib = _lib.lib()
+    bd = dev(torch.from_numpy(batch))
+    lib.of_timing_read(0, None, None, None)
+    lib.of_timing_enable(1)
+    try:
+        with torch.no_grad():
+            flows = net(bd)
+            torch.cuda.synchronize()
+    finally:
+        lib.of_timing_enable(0)
+    cap = 4096
+    kk, ff, mm = (C.c_int * cap)(), (C.c_double * cap)(), (C.c_float * cap)()
+    kinds = {kk[i] for i in range(lib.of_timing_read(cap, kk, ff, mm))}
+    assert {288, 289, 290, 291} <= kinds, sorted(kinds)     # bf16-image forward, BN 128..32
+    p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+    R.set_conv_precision("bf16")
+    try:
+        with torch.no_grad():
+            fo = R.flow_net(torch.tensor(batch[pick], dtype=torch.float64), p,
+                            list(encoder_blocks()))
+    finally:
+        R.set_conv_precision("fp32")
+    for k in range(4):
+        fh = flows[k][pick].double().cpu()
+        e = rel_inf(fh, fo[k])
+        print("cfg3 flow%d (pairs %s) rel_inf %.2e EPE %.3e px" % (3 - k, pick, e, _epe(fh, fo[k])))
+        assert e < BF16_FLOW_TOL, (k, e)
+    # ---- level-3 module, teacher-forced at B = 32, gradient on 2 pairs
+    with torch.no_grad():
+        feats = net.encoder.forward4(ops.split_pair(bd))
+        f1, f2 = feats[0][:B].contiguous(), feats[0][B:].contiguous()
+        prev = flows[1].contiguous()                        # level 2's flow (H/4)
+    g = torch.zeros(B, H // 2, W // 2, 2, dtype=torch.float64)
+    g[pick] = torch.tensor(np.random.default_rng(5).standard_normal((2, H // 2, W // 2, 2)))
+    ins = [f1, f2, prev]
+    hin = [t.detach().clone().requires_grad_(True) for t in ins]
+    net.store.zero_grad()
+    lib.of_timing_read(0, None, None, None)
+    lib.of_timing_enable(1)
+    try:
+        out = net.heads[3](hin[0], hin[1], hin[2])
+        acts = out.grad_fn.saved_tensors
+        assert acts[1].dtype == torch.bfloat16               # the bf16-image path ran
+        masks = [(a[pick] > 0).cpu() for a in acts[1:6]]
+        (out * dev(g.float())).sum().backward()
+        torch.cuda.synchronize()
+    finally:
+        lib.of_timing_enable(0)
+    n = lib.of_timing_read(cap, kk, ff, mm)
+    kinds = {kk[i] for i in range(n)}
+    assert {296, 304} <= kinds, sorted(kinds)                # image dgrad + weight gradient
+    prefix = "flow_module_3"
+    names = ["%s/conv%d/%s" % (prefix, i, k) for i in range(6) for k in ("kernel", "bias")]
+    grads = net.store.grads()
+    leaves = [t[pick].detach().cpu().double().requires_grad_(True) for t in ins]
+    ws = {nme: p[nme].clone().requires_grad_(True) for nme in names}
+    pp = dict(p)
+    pp.update(ws)
+    R.set_conv_precision("bf16")
+    try:
+        o = R.flow_module(leaves[0], leaves[1], leaves[2], 3, pp, prefix, masks=masks)
+        (o * g[pick]).sum().backward()
+    finally:
+        R.set_conv_precision("fp32")
+    errs = [("out", rel_l2(out[pick], o.detach()))]
+    errs += [("d_in%d" % i, rel_l2(h.grad[pick], l.grad)) for i, (h, l) in enumerate(zip(hin, leaves))]
+    errs += [(nme, rel_l2(grads[nme], ws[nme].grad)) for nme in names]
+    for e in errs:
+        print("cfg3 level-3 module %-32s rel_l2 %.2e" % e)
+    bad = [e for e in errs if not e[1] < 1e-2]
+    assert not bad, bad
