@@ -68,6 +68,7 @@ __device__ __forceinline__ float4 bload_quad(rsrc_t r, bool ok, uint32_t off, in
 extern int g_warp_win;   // of_set_tuning key 7 (flow_ops.hip: warp backward form)
 extern int g_corr_blk;   // of_set_tuning key 9 (flow_ops.hip: cost-volume kernel form)
 extern int g_corr_ty8;   // of_set_tuning key 19 (flow_ops.hip: corr_bwd_kernel tile height)
+extern int g_b16i_abl;   // of_set_tuning key 21 (conv_b16i.hip: timing ablations, wrong results)
 
 }  // namespace oflow
 

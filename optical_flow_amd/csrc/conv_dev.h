@@ -61,6 +61,7 @@ struct GemmArgs {
   uint16_t* C16; int ldc16;
   const uint16_t* act16; int ld_act16;
   float* col_part;
+  int abl;                // conv_b16i.hip timing ablations (of_set_tuning key 21; 0 = none)
   Group grp[MAX_GROUPS];
 };
 

@@ -4645,7 +4645,7 @@ int of_conv_pack_weights(const of_conv_desc* d, const float* w_hwio, float* w_fw
 int of_set_tuning(int key, int value) {
   if (key == 8 && value >= 0 && value <= 2) { g_stem_x3 = value; return OF_OK; }
   if (key == 7 && (value == 0 || value == 1)) { g_warp_win = value; return OF_OK; }
-  if (key == 9 && value >= 0 && value <= 3) { g_corr_blk = value; return OF_OK; }
+  if (key == 9 && value >= 0 && value <= 7) { g_corr_blk = value; return OF_OK; }
   if (key == 19 && (value == 0 || value == 1)) { g_corr_ty8 = value; return OF_OK; }
   if (key == 10 && value >= 1 && value <= 16) { g_wgrad_wgs = value; return OF_OK; }
   if (key == 11 && (value == 0 || value == 1)) { g_wgx3_c4 = value; return OF_OK; }
@@ -4663,6 +4663,7 @@ int of_set_tuning(int key, int value) {
   if (key == 18 && (value == 0 || value == 1)) { g_tall16_dgrad = value; return OF_OK; }
   if (key == 17 && (value == 0 || value == 1)) { g_wgt_pf = value; return OF_OK; }
   if (key == 20 && (value == 0 || value == 1)) { g_tile16_pf = value; return OF_OK; }
+  if (key == 21 && value >= 0 && value <= 3) { g_b16i_abl = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

@@ -695,6 +695,202 @@ __global__ __launch_bounds__(CBB_NT, 2) void corr_bwd_blk(CorrBwdArgs a, int sla
   }
 }
 
+// ---- fused backward (of_set_tuning key 9 bit 2, the default when both gradients are wanted) --
+// d/d(f1) and d/d(f2) of one 8 x 16 tile and one 32-channel slab in one workgroup, from one
+// staging of the tile's 14 x 22 coefficient halo:
+//   df1[p] = sum_k g[p][k] f2[p + d_k]          (waves 0-3: f2 halo, G1[p][k] = g[p][k])
+//   df2[q] = sum_k g[q - d_k][k] f1[q - d_k]    (waves 4-7: f1 halo, H[q][k] = g[q - d_k][k])
+// The coefficient halo (all 49 values of each of its 308 pixels, coalesced rows) is read once
+// per tile and scattered into both tables; the f1 / f2 halo slabs once per (tile, slab).  A
+// thread owns 4 adjacent pixels x one channel quad: per offset row, 10 src + 8 coefficient
+// ds_read_b128 feed 112 FMAs.  Coefficient tables are [pixel][offset row][8] with a 60-float
+// pixel pitch, halo pixels have a 40-float pitch: the b128 reads of every 16-lane group hit
+// distinct slots.  160,000 B of LDS, one 512-thread workgroup per CU, persistent: workgroup
+// w walks items [w * items / grid, (w + 1) * items / grid) (items = (tile, slab), slabs of a
+// tile adjacent; XCD-remapped, so neighbouring tiles share an L2), and loads the next item's
+// halos (and, for a new tile, coefficients) into registers while the current one computes.
+constexpr int FB_Y = 8, FB_X = 16, FB_PIX = FB_Y * FB_X;
+constexpr int FB_HY = FB_Y + 6, FB_HX = FB_X + 6, FB_HPIX = FB_HY * FB_HX;   // 14 x 22
+constexpr int FB_SC = 32, FB_PS = 40, FB_GP = 60, FB_NT = 512;
+constexpr int FB_HQ = FB_HPIX * (FB_SC / 4), FB_HU = (FB_HQ + FB_NT - 1) / FB_NT;   // 2464, 5
+constexpr int FB_GQ = FB_HPIX * 49, FB_GU = (FB_GQ + FB_NT - 1) / FB_NT;           // 15092, 30
+constexpr int FB_LDS = 2 * FB_HPIX * FB_PS + 2 * FB_PIX * FB_GP;                    // floats
+
+struct CorrFusedArgs {
+  const float* g; int ldg;
+  const float* f1; int ld1;
+  const float* f2; int ld2;
+  float* df1; int lddf1;
+  const float* init1; int ldinit1;    // NULL, or added to df1 (may alias df1)
+  float* df2; int lddf2;
+  const float* init2; int ldinit2;
+  int h, w, c, slabs, tiles_x, tiles_y, items;
+};
+
+// One role's 7 offset rows: ROLE 0 = df1 (src f2 at p + d), 1 = df2 (src f1 at q - d).
+template <int ROLE>
+__device__ __forceinline__ void corr_fused_rows(const float* hal, const float* gt, int row,
+                                                int col0, int cq, f32x2 (&acc)[8]) {
+#pragma unroll 1
+  for (int i = 0; i < 7; ++i) {
+    const int hr = ROLE == 0 ? row + i : row + 6 - i;
+    const float* sb = &hal[(hr * FB_HX + col0) * FB_PS + 4 * cq];
+    float4 sv[10];
+#pragma unroll
+    for (int u = 0; u < 10; ++u) sv[u] = *reinterpret_cast<const float4*>(sb + u * FB_PS);
+    float cf[4][8];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float* cb = &gt[(row * FB_X + col0 + m) * FB_GP + 8 * i];
+      const float4 lo = *reinterpret_cast<const float4*>(cb);
+      const float4 hi = *reinterpret_cast<const float4*>(cb + 4);
+      cf[m][0] = lo.x, cf[m][1] = lo.y, cf[m][2] = lo.z, cf[m][3] = lo.w;
+      cf[m][4] = hi.x, cf[m][5] = hi.y, cf[m][6] = hi.z, cf[m][7] = hi.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int u0 = ROLE == 0 ? j : 6 - j;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const float4 v = sv[u0 + m];
+        const f32x2 c2 = {cf[m][j], cf[m][j]};
+        acc[2 * m] = __builtin_elementwise_fma(c2, f32x2{v.x, v.y}, acc[2 * m]);
+        acc[2 * m + 1] = __builtin_elementwise_fma(c2, f32x2{v.z, v.w}, acc[2 * m + 1]);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
+  __shared__ float4 lds4[FB_LDS / 4];
+  float* hal1 = reinterpret_cast<float*>(lds4);   // f1 halo slab (df2's source)
+  float* hal2 = hal1 + FB_HPIX * FB_PS;           // f2 halo slab (df1's source)
+  float* G1 = hal2 + FB_HPIX * FB_PS;             // [p][i][8]: g[p][7i + j]
+  float* H = G1 + FB_PIX * FB_GP;                 // [q][i][8]: g[q - d_k][k], k = 7i + j
+  const int tid = threadIdx.x, h = a.h, w = a.w;
+  const int tiles = a.tiles_x * a.tiles_y;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int it0 = (int)((int64_t)wg * a.items / gridDim.x);
+  const int it1 = (int)((int64_t)(wg + 1) * a.items / gridDim.x);
+  if (it0 >= it1) return;                         // uniform over the workgroup
+  auto decode = [&](int it, int& b, int& y0, int& x0, int& c_lo) {
+    const int t = it / a.slabs;
+    c_lo = (it - t * a.slabs) * FB_SC;
+    b = t / tiles;
+    const int tl = t - b * tiles;
+    y0 = (tl / a.tiles_x) * FB_Y, x0 = (tl % a.tiles_x) * FB_X;
+  };
+  float4 hv1[FB_HU], hv2[FB_HU];
+  float gv[FB_GU];
+  auto load_halo = [&](int it) {
+    int b, y0, x0, c_lo;
+    decode(it, b, y0, x0, c_lo);
+    const int64_t img = (int64_t)b * h * w;
+    const rsrc_t r1 = make_rsrc(a.f1 + img * a.ld1, (int64_t)h * w * a.ld1 * 4);
+    const rsrc_t r2 = make_rsrc(a.f2 + img * a.ld2, (int64_t)h * w * a.ld2 * 4);
+#pragma unroll
+    for (int u = 0; u < FB_HU; ++u) {
+      const int q = tid + FB_NT * u;
+      const int hp = q >> 3, cq = q & 7;
+      const int sy = y0 - 3 + hp / FB_HX, sx = x0 - 3 + hp % FB_HX;
+      const bool ok = q < FB_HQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
+      const int pix = sy * w + sx, ch = c_lo + 4 * cq;
+      hv1[u] = bload4(r1, ok ? 4 * (pix * a.ld1 + ch) : kOOB);
+      hv2[u] = bload4(r2, ok ? 4 * (pix * a.ld2 + ch) : kOOB);
+    }
+  };
+  auto load_coef = [&](int it) {
+    int b, y0, x0, c_lo;
+    decode(it, b, y0, x0, c_lo);
+    const int64_t img = (int64_t)b * h * w;
+    const rsrc_t rg = make_rsrc(a.g + img * a.ldg, (int64_t)h * w * a.ldg * 4);
+#pragma unroll
+    for (int u = 0; u < FB_GU; ++u) {
+      const int q = tid + FB_NT * u;
+      const int hp = q / 49, k = q - hp * 49;
+      const int sy = y0 - 3 + hp / FB_HX, sx = x0 - 3 + hp % FB_HX;
+      const bool ok = q < FB_GQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
+      gv[u] = bload1(rg, ok ? 4 * ((sy * w + sx) * a.ldg + k) : kOOB);
+    }
+  };
+  const int role = tid >> 8, r = tid & 255, cq = r & 7, pg = r >> 3;
+  const int row = pg >> 2, col0 = (pg & 3) * 4;
+  int it = it0, cur_tile = -1;
+  load_halo(it);
+  load_coef(it);
+  for (;;) {
+    const int tile = it / a.slabs;
+#pragma unroll
+    for (int u = 0; u < FB_HU; ++u) {
+      const int q = tid + FB_NT * u;
+      if (q < FB_HQ) {
+        const int o = (q >> 3) * FB_PS + 4 * (q & 7);
+        *reinterpret_cast<float4*>(&hal1[o]) = hv1[u];
+        *reinterpret_cast<float4*>(&hal2[o]) = hv2[u];
+      }
+    }
+    if (tile != cur_tile) {                       // uniform: scatter the new coefficients
+#pragma unroll
+      for (int u = 0; u < FB_GU; ++u) {
+        const int q = tid + FB_NT * u;
+        if (q < FB_GQ) {
+          const int hp = q / 49, k = q - hp * 49;
+          const int i = k / 7, j = k - 7 * i;
+          const int hy = hp / FB_HX, hx = hp - hy * FB_HX;
+          if ((unsigned)(hy - 3) < (unsigned)FB_Y && (unsigned)(hx - 3) < (unsigned)FB_X)
+            G1[((hy - 3) * FB_X + hx - 3) * FB_GP + 8 * i + j] = gv[u];
+          const int ty = hy + i - 6, tx = hx + j - 6;   // target q = p + d_k
+          if ((unsigned)ty < (unsigned)FB_Y && (unsigned)tx < (unsigned)FB_X)
+            H[(ty * FB_X + tx) * FB_GP + 8 * i + j] = gv[u];
+        }
+      }
+      cur_tile = tile;
+    }
+    __syncthreads();
+    const int nit = it + 1;
+    const bool more = nit < it1;
+    if (more) {
+      load_halo(nit);
+      if (nit / a.slabs != tile) load_coef(nit);
+    }
+    int b, y0, x0, c_lo;
+    decode(it, b, y0, x0, c_lo);
+    const int64_t img = (int64_t)b * h * w;
+    const int y = y0 + row, ch = c_lo + 4 * cq;
+    const float* init = role == 0 ? a.init1 : a.init2;
+    const int ldi = role == 0 ? a.ldinit1 : a.ldinit2;
+    float4 iv[4];
+    {
+      const rsrc_t ri = make_rsrc(init ? init + img * ldi : nullptr, init ? (int64_t)h * w * ldi * 4 : 0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int x = x0 + col0 + m;
+        iv[m] = bload4(ri, y < h && x < w ? 4 * ((y * w + x) * ldi + ch) : kOOB);
+      }
+    }
+    f32x2 acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = f32x2{0.f, 0.f};
+    if (role == 0)
+      corr_fused_rows<0>(hal2, G1, row, col0, cq, acc);
+    else
+      corr_fused_rows<1>(hal1, H, row, col0, cq, acc);
+    float* df = role == 0 ? a.df1 : a.df2;
+    const int ldd = role == 0 ? a.lddf1 : a.lddf2;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int x = x0 + col0 + m;
+      if (y < h && x < w)
+        *reinterpret_cast<float4*>(df + (img + y * w + x) * ldd + ch) =
+            make_float4(iv[m].x + acc[2 * m].x, iv[m].y + acc[2 * m].y,
+                        iv[m].z + acc[2 * m + 1].x, iv[m].w + acc[2 * m + 1].y);
+    }
+    if (!more) break;
+    __syncthreads();                              // halo / coefficients no longer read
+    it = nit;
+  }
+}
+
 // ===================================================================== warp (K7) =======
 // transformations.py:85-129 with the grid of model.py:65-71 (P1, P2):
 //   x = i + flow0 (i = ROW index), y = j + flow1 (j = COLUMN index), sampled as column x,
@@ -959,7 +1155,8 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
 // exceeds WG_CAP slots adds each corner's row straight to global memory.
 constexpr int WG_T = 8, WG_CAP = 1024, WG_NT = 256;
 int g_warp_win = 1;   // of_set_tuning key 7: warp_bwd_gather (1) or warp_bwd_agg (0)
-int g_corr_blk = 1;   // of_set_tuning key 9: bit 0 corr_fwd_blk (else corr_fwd_kernel), bit 1 corr_bwd_blk
+int g_corr_blk = 5;   // of_set_tuning key 9: bit 0 corr_fwd_blk (else corr_fwd_kernel), bit 1 corr_bwd_blk,
+                      // bit 2 corr_bwd_fused when both gradients are wanted
 int g_corr_ty8 = 0;   // of_set_tuning key 19: corr_bwd_kernel on 8 x 16 tiles, 512 threads (1)
 
 __device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes of a DPP row
@@ -1544,6 +1741,31 @@ static int corr_bwd_launch(int sign, CorrBwdArgs a, int n, hipStream_t s) {
   return check_launch(sign > 0 ? "corr_bwd_f1" : "corr_bwd_f2");
 }
 
+// Both gradients in one pass (corr_bwd_fused); false: the caller runs the per-gradient kernels.
+static bool corr_fused_ok(int c, const float* f1, int ld1, const float* f2, int ld2,
+                          const float* df1, int lddf1, const float* init1, int ldinit1,
+                          const float* df2, int lddf2) {
+  return (g_corr_blk & 4) && df1 && df2 && c % FB_SC == 0 && ld1 % 4 == 0 && ld2 % 4 == 0 &&
+         lddf1 % 4 == 0 && lddf2 % 4 == 0 && (!init1 || (ldinit1 % 4 == 0 && al16(init1))) &&
+         al16(f1) && al16(f2) && al16(df1) && al16(df2);
+}
+
+static int corr_fused_launch(CorrFusedArgs a, int n, hipStream_t s) {
+  OF_CHECK_ARG((int64_t)a.h * a.w *
+                       std::max(std::max(std::max(a.ldg, a.ld1), std::max(a.ld2, a.lddf1)),
+                                std::max(std::max(a.lddf2, a.ldinit1), a.ldinit2)) <
+                   (1LL << 29),
+               "corr: one image must hold < 2^29 elements (32-bit buffer offsets)");
+  a.slabs = a.c / FB_SC;
+  a.tiles_x = (int)cdiv(a.w, FB_X), a.tiles_y = (int)cdiv(a.h, FB_Y);
+  const int64_t items = (int64_t)n * a.tiles_x * a.tiles_y * a.slabs;
+  OF_CHECK_ARG(items < INT32_MAX / 2, "corr bwd: too many tiles");
+  a.items = (int)items;
+  const int grid = (int)std::min<int64_t>(items, device_cus());
+  hipLaunchKernelGGL(corr_bwd_fused, dim3(grid), dim3(FB_NT), 0, s, a);
+  return check_launch("corr_bwd_fused");
+}
+
 size_t of_corr_fwd_workspace(int n, int h, int w, int c, int max_disp) {
   (void)max_disp;
   return n > 0 && h > 0 && w > 0 && c > 0 ? corr_fwd_ws(n, h, w, c) : 0;
@@ -1572,6 +1794,15 @@ int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const flo
   OF_CHECK_ARG(ld1 >= c && ld2 >= c && lddcv >= 49, "corr bwd: strides");
   hipStream_t s = as_stream(stream);
   int st;
+  if (corr_fused_ok(c, f1, ld1, f2, ld2, df1, lddf1, acc1 ? df1 : nullptr, lddf1, df2, lddf2)) {
+    OF_CHECK_ARG(lddf1 >= c && lddf2 >= c, "corr bwd: df strides");
+    CorrFusedArgs a{};
+    a.g = dcv, a.ldg = lddcv, a.f1 = f1, a.ld1 = ld1, a.f2 = f2, a.ld2 = ld2;
+    a.df1 = df1, a.lddf1 = lddf1, a.init1 = acc1 ? df1 : nullptr, a.ldinit1 = lddf1;
+    a.df2 = df2, a.lddf2 = lddf2, a.init2 = acc2 ? df2 : nullptr, a.ldinit2 = lddf2;
+    a.h = h, a.w = w, a.c = c;
+    return corr_fused_launch(a, n, s);
+  }
   if (df1) {
     OF_CHECK_ARG(lddf1 >= c, "corr bwd: df1 stride");
     CorrBwdArgs a{};
@@ -1615,6 +1846,17 @@ int of_corr_concat_bwd(const float* dcat, int cp, const float* f1, const float* 
   hipStream_t s = as_stream(stream);
   const bool vec = c % 4 == 0 && cp % 4 == 0 && al16(f1) && al16(f2) && al16(dcat) && al16(df1);
   int st;
+  if (corr_fused_ok(c, f1, c, f2, c, df1, c, dcat, cp, df2, c)) {
+    CorrFusedArgs f{};
+    f.g = dcat + c, f.ldg = cp, f.f1 = f1, f.ld1 = c, f.f2 = f2, f.ld2 = c;
+    f.df1 = df1, f.lddf1 = c, f.init1 = dcat, f.ldinit1 = cp;
+    f.df2 = df2, f.lddf2 = c;
+    f.h = h, f.w = w, f.c = c;
+    if ((st = corr_fused_launch(f, n, s))) return st;
+    if (dflow)
+      return of_copy_strided(dcat + c + 49, cp, dflow, 2, (int64_t)n * h * w, 2, stream);
+    return OF_OK;
+  }
   CorrBwdArgs a{};
   a.g = dcat + c, a.ldg = cp, a.src = f2, a.lds = c, a.h = h, a.w = w, a.c = c;
   a.df = df1, a.lddf = c, a.init = dcat, a.ldinit = cp, a.vec = vec;

@@ -466,6 +466,107 @@ def test_conv_bf16_prefetch_forms(n, h, w, cin, cout):
         assert torch.equal(a_, b_), what
 
 
+# Every conv_halo_b16 N tile (128 / 96 / 64 / 32) and conv_wgrad_b16i form (Cout tile 128 /
+# 64 / 32: (2,4) / (4,2) / (4,1) waves), ragged tiles and padded channels.
+B16I_CASES = [(2, 40, 70, 128, 128), (1, 37, 45, 20, 24), (2, 24, 48, 128, 96),
+              (2, 32, 40, 96, 64), (2, 20, 36, 64, 32), (1, 16, 32, 256, 256), (3, 17, 33, 115, 128)]
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout", B16I_CASES)
+def test_conv_b16i(n, h, w, cin, cout):
+    """The bf16-activation-image 3x3 kernels (of_conv2d_b16i fwd / dgrad, of_conv2d_wgrad_b16i)
+    through the C ABI against float64 convolutions of the same bf16-rounded operands (the
+    oracle's bf16 rounding points, R._Bf16Conv): forward with bias + LeakyReLU, input gradient
+    with the producer's act' from an fp32 or a bf16 source and the bias-gradient column sums,
+    weight gradient; fp32 and bf16-image outputs (the image is the RNE of the fp32 output)."""
+    import ctypes as C
+    import torch.nn.functional as Fn
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_LEAKY, B16iIO, ConvDesc, call
+    lib = _lib.load()
+    P, st = ops._ptr, ops._stream()
+    seed = zlib.crc32(repr((n, h, w, cin, cout)).encode()) % 1000
+    cin_p, cout_p = (cin + 3) // 4 * 4, (cout + 3) // 4 * 4
+    lx, ly = (cin_p + 31) // 32 * 32, (cout_p + 31) // 32 * 32
+    d = ConvDesc(n, h, w, cin, cin_p, cout, 3, 3, 1, 1, 1, h, w)
+    bf = lambda t: f64(t.to(torch.bfloat16).float())
+    nchw = lambda t: t.permute(0, 3, 1, 2)
+    nhwc = lambda t: t.permute(0, 2, 3, 1)
+
+    def img16(t, c, ld):
+        out = torch.zeros(t.numel() // t.shape[-1] * ld, dtype=torch.bfloat16, device="cuda")
+        call("of_to_bf16_image", P(t), t.numel() // t.shape[-1], c, t.shape[-1], P(out), ld, st)
+        return out
+
+    def io(**kw):
+        r = B16iIO()
+        for k, v in kw.items():
+            setattr(r, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
+        return r
+
+    x = rng_tensor((n, h, w, cin), seed)
+    wt = rng_tensor((3, 3, cin, cout), seed + 1, scale=(2.0 / (9 * cin)) ** 0.5)
+    bias = rng_tensor((cout,), seed + 2, scale=0.1)
+    dy = rng_tensor((n, h, w, cout), seed + 3)
+    src = rng_tensor((n, h, w, cin), seed + 4)
+    wk = bf(wt).permute(3, 2, 0, 1).contiguous()                  # (cout, cin, 3, 3)
+    y_o = nhwc(Fn.conv2d(nchw(bf(x)), wk, f64(bias), padding=1))
+    y_o = torch.where(y_o > 0, y_o, 0.3 * y_o)
+    slope = torch.where(f64(src) > 0, 1.0, 0.3).double()
+    dx_o = nhwc(torch.nn.grad.conv2d_input((n, cin, h, w), wk, nchw(bf(dy)), padding=1)) * slope
+    dw_o = torch.nn.grad.conv2d_weight(nchw(bf(x)), wk.shape, nchw(bf(dy)), padding=1)
+    dw_o = dw_o.permute(2, 3, 1, 0)                                # (3, 3, cin, cout)
+
+    wd = dev(wt)
+    wf = torch.empty(lib.of_conv_wfwd16_elems(C.byref(d)), dtype=torch.bfloat16, device="cuda")
+    wb = torch.empty(lib.of_conv_wbwd16_elems(C.byref(d)), dtype=torch.bfloat16, device="cuda")
+    call("of_conv_pack_weights_bf16", C.byref(d), P(wd), P(wf), P(wb), st)
+    xd = torch.zeros(n, h, w, cin_p, device="cuda")
+    xd[..., :cin] = dev(x)
+    dyd = torch.zeros(n, h, w, cout_p, device="cuda")
+    dyd[..., :cout] = dev(dy)
+    srcd = torch.zeros(n, h, w, cin_p, device="cuda")
+    srcd[..., :cin] = dev(src)
+    x16, dy16 = img16(xd, cin_p, lx), img16(dyd, cout_p, ly)
+    bd = dev(bias)
+    # forward: fp32 output and bf16 image
+    y32 = torch.empty(n, h, w, cout, device="cuda")
+    y16 = torch.empty(n, h, w, cout, dtype=torch.bfloat16, device="cuda")
+    for o in (io(a16=x16, lda16=lx, y=y32, ldy=cout), io(a16=x16, lda16=lx, y16=y16, ldy16=cout)):
+        call("of_conv2d_b16i", 0, C.byref(d), C.byref(o), P(wf), P(bd), None, None, None, None,
+             0.0, ACT_LEAKY, 0.3, st)
+    # input gradient: act' from the fp32 source / from its bf16 image with the column sums
+    dx32 = torch.empty(n, h, w, cin_p, device="cuda")
+    dx16 = torch.empty(n, h, w, cin_p, dtype=torch.bfloat16, device="cuda")
+    src16 = srcd.bfloat16()
+    tiles = lib.of_conv2d_b16i_tiles(1, C.byref(d))
+    part = torch.empty(tiles, cin_p, device="cuda")
+    db = torch.empty(cin_p, device="cuda")
+    call("of_conv2d_b16i", 1, C.byref(d),
+         C.byref(io(a16=dy16, lda16=ly, y=dx32, ldy=cin_p, act_src=srcd, ld_act=cin_p)), P(wb),
+         None, None, None, None, None, 0.0, ACT_LEAKY, 0.3, st)
+    call("of_conv2d_b16i", 1, C.byref(d),
+         C.byref(io(a16=dy16, lda16=ly, y16=dx16, ldy16=cin_p, act16=src16, ld_act16=cin_p,
+                    col_part=part)), P(wb), None, None, None, None, None, 0.0, ACT_LEAKY, 0.3, st)
+    call("of_col_part_reduce", P(part), tiles, cin_p, P(db), 0, st)
+    # weight gradient
+    dw = torch.empty(3, 3, cin, cout, device="cuda")
+    wsb = lib.of_conv2d_wgrad_b16i_workspace(C.byref(d))
+    ws = torch.empty(wsb // 4 + 4, device="cuda")
+    call("of_conv2d_wgrad_b16i", C.byref(d), P(x16), lx, P(dy16), ly, P(dw), 0, None, None, 0.0,
+         P(ws), wsb, st)
+    torch.cuda.synchronize()
+    tol = 1e-4                     # same bf16 operands: fp32 summation order only
+    assert rel_inf(y32, y_o) < tol, "forward"
+    assert torch.equal(y16, y32.bfloat16()), "forward image != RNE of the fp32 output"
+    assert rel_inf(dx32[..., :cin], dx_o) < tol, "dgrad"
+    assert dx32[..., cin:].abs().max().item() == 0.0 if cin < cin_p else True
+    assert torch.equal(dx16, dx32.bfloat16()), "dgrad image != RNE of the fp32 output"
+    assert rel_l2(db[:cin], f64(dx32[..., :cin]).sum((0, 1, 2))) < tol, "column sums"
+    assert rel_l2(dw, dw_o) < tol, "wgrad"
+
+
 @pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (3, 38, 130), (8, 384, 512)])
 def test_conv_stem_b16(n, h, w):
     """The bf16 stem (configs 3-5) on the one-plane stem kernels (conv_stem_x3<32, 1>,
@@ -1125,20 +1226,21 @@ def test_conv_bf16_tall_dgrad():
 
 
 # ----------------------------------------------------------------------- cost volume ----
-CORR_FORM_DEFAULT = 1      # of_set_tuning key 9: bit 0 corr_fwd_blk, bit 1 corr_bwd_blk
+CORR_FORM_DEFAULT = 5      # of_set_tuning key 9: bit 0 corr_fwd_blk, bit 1 corr_bwd_blk, bit 2 fused bwd
 
 
 class _corr_form:
-    """Select the cost-volume kernel forms for a block, restoring the defaults: bits 0-1 are
-    of_set_tuning key 9, bit 2 key 19 (the gather backward on 8 x 16 tiles)."""
+    """Select the cost-volume kernel forms for a block, restoring the defaults: bits 0-2 are
+    of_set_tuning key 9 (bit 2: corr_bwd_fused), bit 3 key 19 (the gather backward on 8 x 16
+    tiles)."""
 
     def __init__(self, form):
         self.form = form
 
     def __enter__(self):
         from optical_flow_amd import _lib
-        assert _lib.lib().of_set_tuning(9, self.form & 3) == 0
-        assert _lib.lib().of_set_tuning(19, (self.form >> 2) & 1) == 0
+        assert _lib.lib().of_set_tuning(9, self.form & 7) == 0
+        assert _lib.lib().of_set_tuning(19, (self.form >> 3) & 1) == 0
 
     def __exit__(self, *exc):
         from optical_flow_amd import _lib
@@ -1146,7 +1248,7 @@ class _corr_form:
         _lib.lib().of_set_tuning(19, 0)
 
 
-@pytest.mark.parametrize("form", [1, 3, 0, 5])
+@pytest.mark.parametrize("form", [1, 3, 0, 9, 5, 4])
 @pytest.mark.parametrize("shape", [(2, 12, 20, 64), (1, 24, 32, 256), (2, 9, 13, 6), (1, 19, 70, 32),
                                    (3, 40, 56, 64), (1, 17, 35, 100)])
 def test_cost_volume(form, shape):
@@ -1181,7 +1283,7 @@ def test_cost_volume(form, shape):
                                                   (1, 4, 8, 128, 180, True),
                                                   (1, 2, 4, 256, 308, False),
                                                   (8, 48, 64, 128, 180, True)])
-@pytest.mark.parametrize("form", [1, 3, 0, 5])
+@pytest.mark.parametrize("form", [1, 3, 0, 9, 5, 4])
 def test_corr_concat(form, n, h, w, c, cp, has_flow):
     """The fused concat([f1, cost volume, flow]) kernel and its gradient, for both kernel
     forms (key 9): multi-tile and ragged shapes, 1 to 8 channel slabs (and slab groups with

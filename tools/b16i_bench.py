@@ -146,14 +146,30 @@ def case(n, h, w, cin, cout, reps, lib):
               n, h, w, cin, cout, ef, tf_ref, tf(tf_ref), tf_new, tf(tf_new), tf_16, tf(tf_16),
               ed, td_ref, tf(td_ref), td_new, tf(td_new), td_16, tf(td_16),
               ew, tw_ref, tf(tw_ref), tw_new, tf(tw_new)), flush=True)
+    if ABLATE:
+        # timing ablations of conv_halo_b16 (of_set_tuning key 21; results are wrong): what the
+        # epilogue's global traffic (1) and the main loop's DMAs (2) cost on this shape
+        out = []
+        for abl in (1, 2, 3):
+            call("of_set_tuning", 21, abl)
+            out.append((timeit(new_f16, reps), timeit(new_d16, reps)))
+        call("of_set_tuning", 21, 0)
+        print("   ablation (fwd16, dgrad16 ms): no-epilogue %.3f %.3f | no-DMA %.3f %.3f | neither"
+              " %.3f %.3f" % tuple(v for p_ in out for v in p_), flush=True)
     return ef, max(ed, ew)
+
+
+ABLATE = False
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--ablate", action="store_true")
     args = ap.parse_args()
+    global ABLATE
+    ABLATE = args.ablate
     lib = _lib.load()
     n = args.batch
     worst = 0.0

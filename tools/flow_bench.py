@@ -70,6 +70,11 @@ def main():
         res["corr_bwd"] = (timeit(lambda: call(
             "of_corr_concat_bwd", P(dcat), cp, P(f1), P(f2), n, h, w, c, 3, P(df1), P(df2),
             P(dfl), st), args.reps), 4 * npx * (2 * (c + 49) + 4 * c + (4 if has_flow else 0)))
+        if _lib.lib().of_set_tuning(9, 1) == 0:        # the two per-gradient kernels (r3)
+            res["corr_bwd_sep"] = (timeit(lambda: call(
+                "of_corr_concat_bwd", P(dcat), cp, P(f1), P(f2), n, h, w, c, 3, P(df1), P(df2),
+                P(dfl), st), args.reps), res["corr_bwd"][1])
+            _lib.lib().of_set_tuning(9, args.corr_form if args.corr_form is not None else 5)
         if has_flow:
             wout = torch.empty_like(f2)
             dw = torch.empty_like(f2)

@@ -6,8 +6,14 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/r4c}
 mkdir -p "$OUT"
-run() { local t=$1; shift; timeout -k 10 "$t" "$@"; }
-run 300 python tools/b16i_bench.py --batch 32 > "$OUT/b16i_b32.txt" 2>&1; echo "b16i b32 rc $?"; grep -v amdgpu.ids "$OUT/b16i_b32.txt" | tail -14
+# A step that faulted, aborted, crashed or ran out of time ends the call (test failures do not).
+run() {
+  local t=$1; shift
+  timeout -k 10 "$t" "$@"; local rc=$?
+  case $rc in 124|134|137|139) echo "step '$*' rc $rc: stopping"; exit $rc;; esac
+  return $rc
+}
+run 300 python tools/b16i_bench.py --batch 32 --ablate > "$OUT/b16i_b32.txt" 2>&1; echo "b16i b32 rc $?"; grep -v amdgpu.ids "$OUT/b16i_b32.txt" | tail -14
 run 900 python -u -m pytest -v -s --timeout 300 --timeout-method thread tests/test_gpu_bf16_modules.py \
   "tests/test_gpu_model.py::test_bn_gamma_near_zero" "tests/test_gpu_model.py::test_resnet_block_bn_guard" \
   "tests/test_gpu_model.py::test_two_forwards_one_backward" "tests/test_gpu_model.py::test_flow_net_forward_backward" \
