@@ -378,7 +378,13 @@ int of_timing_enable(int on);
  * split-GEMM forms conv_gemm_x3<..., 1> / conv_wgrad_x3<..., 1> (timing kinds 240 + 8 mode +
  * cfg): bit 0 forward, bit 1 input gradient, bit 2 weight gradient (default 6);
  * key 18 = bf16 3x3 input gradients with N tiles of 128 on the tall 8 x 32 output tiles where
- * the grid allows (1) or on 4 x 32 tiles (0, default). */
+ * the grid allows (1) or on 4 x 32 tiles (0, default);
+ * key 9 bit 2 = the fused cost-volume backward corr_bwd_fused when both gradients are wanted
+ * (default on: key 9 = 5);
+ * key 21 = conv_halo_b16 timing ablations (bit 0: no epilogue loads / stores, bit 1: no main-loop
+ * DMAs; RESULTS ARE WRONG, A/B timing only; default 0);
+ * key 22 = conv_halo_b16's direct epilogue for forwards with a bf16 image output alone (1,
+ * default; the input gradient takes it whenever it is given mask_in). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 
@@ -393,8 +399,9 @@ int of_to_bf16_image(const float* x, int64_t npix, int c, int ldx, void* y16, in
  * channels per pixel, a multiple of 32 and >= round_up(kc, 32), kc = cin_p (fwd) /
  * round_up(cout, 4) (dgrad); channels past kc zero), the weights the packed bf16 images of
  * of_conv_pack_weights_bf16.  Epilogue as of_conv2d_fwd (bias, BN, aux = residual, act) /
- * of_conv2d_dgrad (the producer's act' from act_src (fp32) or act16 (bf16 image), aux = an
- * added gradient); the result goes to y (fp32) and / or y16 (bf16 image, RNE).  col_part
+ * of_conv2d_dgrad (the producer's act' from act_src (fp32), act16 (bf16 image) or mask_in (the
+ * signs its b16i forward wrote); no added gradient); the result goes to y (fp32) and / or y16
+ * (bf16 image, RNE).  col_part
  * (dgrad, optional): per output tile the column sums of the fp32 result, [tiles][N] with tiles =
  * of_conv2d_b16i_tiles(1, d) -- the bias gradient of the layer that produced dy, reduced by
  * of_col_part_reduce.  No workspace (one K slice). */
@@ -406,8 +413,12 @@ typedef struct of_b16i_io {
   const float* act_src; int ld_act;
   const void* act16; int ld_act16;
   float* col_part;
+  void* mask_out;        /* fwd (optional): the output's act' signs, of_conv2d_b16i_mask_bytes */
+  const void* mask_in;   /* dgrad (optional): mask_out of the forward that produced the act'
+                          * source (same N = its cout, same n, h, w); replaces act16 / act_src */
 } of_b16i_io;
 int of_conv2d_b16i_tiles(int mode, const of_conv_desc* d);
+size_t of_conv2d_b16i_mask_bytes(const of_conv_desc* d);
 int of_conv2d_b16i(int mode, const of_conv_desc* d, const of_b16i_io* io, const void* w16,
                    const float* bias, const float* bn_gamma, const float* bn_beta,
                    const float* bn_mean, const float* bn_var, float bn_eps, int act, float alpha,

@@ -23,7 +23,8 @@ class B16iIO(C.Structure):
     _fields_ = [("a16", C.c_void_p), ("lda16", C.c_int), ("y", C.c_void_p), ("ldy", C.c_int),
                 ("y16", C.c_void_p), ("ldy16", C.c_int), ("aux", C.c_void_p), ("ldr", C.c_int),
                 ("act_src", C.c_void_p), ("ld_act", C.c_int), ("act16", C.c_void_p),
-                ("ld_act16", C.c_int), ("col_part", C.c_void_p)]
+                ("ld_act16", C.c_int), ("col_part", C.c_void_p), ("mask_out", C.c_void_p),
+                ("mask_in", C.c_void_p)]
 
 
 class ConvDesc(C.Structure):
@@ -100,6 +101,7 @@ PROTOTYPES = {
     "of_bilinear_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
     "of_to_bf16_image": (I, [P, I64, I, I, P, I, P]),
     "of_conv2d_b16i_tiles": (I, [I, PD]),
+    "of_conv2d_b16i_mask_bytes": (SZ, [PD]),
     "of_conv2d_b16i": (I, [I, PD, P, P, P, P, P, P, P, F, I, F, P]),
     "of_col_part_reduce": (I, [P, I, I, P, I, P]),
     "of_conv2d_wgrad_b16i_workspace": (SZ, [PD]),

@@ -69,6 +69,7 @@ extern int g_warp_win;   // of_set_tuning key 7 (flow_ops.hip: warp backward for
 extern int g_corr_blk;   // of_set_tuning key 9 (flow_ops.hip: cost-volume kernel form)
 extern int g_corr_ty8;   // of_set_tuning key 19 (flow_ops.hip: corr_bwd_kernel tile height)
 extern int g_b16i_abl;   // of_set_tuning key 21 (conv_b16i.hip: timing ablations, wrong results)
+extern int g_b16i_direct;   // of_set_tuning key 22 (conv_b16i.hip: forward direct epilogue)
 
 }  // namespace oflow
 

@@ -28,6 +28,8 @@ namespace oflow {
 // of_set_tuning key 21: timing ablations of conv_halo_b16 (WRONG results, A/B only): bit 0
 // skips the epilogue's global loads and stores, bit 1 the main loop's DMAs.
 int g_b16i_abl = 0;
+// of_set_tuning key 22: the forward's direct epilogue for bf16-image-only outputs (1, default)
+int g_b16i_direct = 1;
 
 namespace {
 
@@ -57,8 +59,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
                                                                                      : 1;
   constexpr int EPW = 16 * EJ;
   constexpr int EP_U4 = NW * WM * EPW / 4 + WAVES_M * BN / 4;     // + the column-sum buffer
-  constexpr int SM_U4 = LOOP_U4 > EP_U4 ? LOOP_U4 : EP_U4;
+  // direct epilogue (bf16 image out): per-wave bf16 rows of WN columns, 16-byte padded pitch
+  constexpr int P16 = WN * 2 + 16;
+  constexpr int D_U4 = NW * WM * P16 / 16 + WAVES_M * BN / 4;
+  constexpr int SM_U4 = (LOOP_U4 > EP_U4 ? LOOP_U4 : EP_U4) > D_U4 ? (LOOP_U4 > EP_U4 ? LOOP_U4 : EP_U4)
+                                                                   : D_U4;
   static_assert(SM_U4 * 16 <= 160 * 1024, "LDS");
+  static_assert(SM * SN * 4 <= 128, "sign mask: 128 bits per lane");
   __shared__ uint4 smem[SM_U4];
   uint4* Hs = smem;                        // [2][HPD pixels][4 octets]
   uint4* Bs = smem + 2 * H_U4;             // [2][3 taps][BN rows][4 octets]
@@ -189,6 +196,111 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of the next step landed
     __syncthreads();
+  }
+
+  if (a.direct16) {
+    // ---- direct epilogue (bf16 image output only, no residual / BN): the epilogue math on
+    // the accumulators in their MFMA layout (lane: column 16 j + l16, rows 16 i + 4 lq + r),
+    // bf16 pairs of adjacent columns swapped between lane pairs (DPP) into 32-bit LDS writes,
+    // then whole 16-byte row chunks out: every store instruction writes full 128-byte lines
+    // (the per-pass fp32 transposes below store 32-byte row pieces, which measured ~2.4 TB/s).
+    // fwd also writes the act' signs of its output (mask_out: 128 bits per lane, the input
+    // gradient of the next layer reads them as mask_in in the same layout); dgrad takes
+    // act' from those signs and sums its columns (bias gradient) in registers.
+    char* E16 = reinterpret_cast<char*>(smem) + wave * WM * P16;
+    float* colb = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + NW * WM * P16);
+    const int64_t img = (int64_t)b * OH * OW;
+    // dgrad: the producer forward's act' signs of this tile, in this lane's MFMA layout
+    const uint4 mk = MODE == MODE_DGRAD ? a.mask_in[(int64_t)tile * NT + tid]
+                                        : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t mki[4] = {mk.x, mk.y, mk.z, mk.w};
+    uint32_t mo[4] = {0u, 0u, 0u, 0u};
+    float bj[SN];
+#pragma unroll
+    for (int j = 0; j < SN; ++j) {
+      const int nn = n0 + wn0 + 16 * j + l16;
+      bj[j] = MODE == MODE_FWD && a.bias && nn < a.N ? a.bias[nn] : 0.f;
+    }
+    float cs[SN];
+#pragma unroll
+    for (int j = 0; j < SN; ++j) cs[j] = 0.f;
+    const bool even = !(l16 & 1);
+#pragma unroll
+    for (int i = 0; i < SM; ++i) {
+      unsigned rv = 0;                     // row validity of rows 16 i + 4 lq + r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mt = wm0 + 16 * i + 4 * lq + r;
+        rv |= (oy0 + mt / TW < OH && ox0 + mt % TW < OW ? 1u : 0u) << r;
+      }
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        const bool cv = n0 + wn0 + 16 * j + l16 < a.N;
+        float x[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int bit = (i * SN + j) * 4 + r;
+          if (MODE == MODE_FWD) {
+            x[r] = act_fwd(acc[i][j][r] + bj[j], a.act, a.alpha);
+            mo[bit >> 5] |= (x[r] > 0.f ? 1u : 0u) << (bit & 31);
+          } else {
+            const bool pos = (mki[bit >> 5] >> (bit & 31)) & 1u;
+            x[r] = dgrad_ep(a, acc[i][j][r], pos ? 1.f : -1.f, 0.f);
+            if (cv && ((rv >> r) & 1)) cs[j] += x[r];
+          }
+        }
+        const float p0 = even ? x[2] : x[0], p1 = even ? x[3] : x[1];
+        const float q0 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                       __builtin_bit_cast(int, p0), 0xB1, 0xF, 0xF, false));
+        const float q1 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                       __builtin_bit_cast(int, p1), 0xB1, 0xF, 0xF, false));
+        const uint2 w = even ? pack_bf16x4(make_float4(x[0], q0, x[1], q1))
+                             : pack_bf16x4(make_float4(q0, x[2], q1, x[3]));
+        const int row0 = 16 * i + 4 * lq + (even ? 0 : 2);
+        char* d = E16 + row0 * P16 + (16 * j + (l16 & ~1)) * 2;
+        *reinterpret_cast<uint32_t*>(d) = w.x;
+        *reinterpret_cast<uint32_t*>(d + P16) = w.y;
+      }
+      // pin the sign words / column sums here: left free, the compiler sinks their updates
+      // past every LDS write and keeps all 128 values live (spills)
+      if (MODE == MODE_FWD) asm volatile("" : "+v"(mo[0]), "+v"(mo[1]), "+v"(mo[2]), "+v"(mo[3]));
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+        if (MODE == MODE_DGRAD) asm volatile("" : "+v"(cs[j]));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int LR = WN / 8;                       // 16-byte chunks per row
+    static_assert((WM * LR) % 64 == 0, "whole store instructions");
+#pragma unroll
+    for (int it = 0; it < WM * LR / 64; ++it) {
+      const int c = lane + 64 * it, row = c / LR, part = c - row * LR;
+      const uint4 v = *reinterpret_cast<const uint4*>(E16 + row * P16 + 16 * part);
+      const int mt = wm0 + row;
+      const int oy = oy0 + mt / TW, ox = ox0 + mt % TW;
+      const int ch = n0 + wn0 + 8 * part;
+      if (oy < OH && ox < OW && ch < a.N)
+        *reinterpret_cast<uint4*>(&a.C16[(img + (int64_t)oy * OW + ox) * a.ldc16 + ch]) = v;
+    }
+    if (MODE == MODE_FWD && a.mask_out)
+      a.mask_out[(int64_t)tile * NT + tid] = make_uint4(mo[0], mo[1], mo[2], mo[3]);
+    if (MODE == MODE_DGRAD && a.col_part != nullptr) {
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {        // fixed order: lq 0+1, 2+3, then the halves
+        cs[j] += __shfl_xor(cs[j], 16, 64);
+        cs[j] += __shfl_xor(cs[j], 32, 64);
+        if (lq == 0) colb[(wave / WAVES_N) * BN + wn0 + 16 * j + l16] = cs[j];
+      }
+      __syncthreads();
+      if (tid < BN && n0 + tid < a.N) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WAVES_M; ++w) v += colb[w * BN + tid];
+        a.col_part[(int64_t)tile_m * a.N + n0 + tid] = v;
+      }
+    }
+    return;
   }
 
   // ---- epilogue: the wave's accumulators through a private LDS image (EJ 16-column blocks
@@ -603,6 +715,12 @@ static int b16i_plan(int mode, const of_conv_desc* d, GemmArgs& a) {
   return OF_OK;
 }
 
+size_t of_conv2d_b16i_mask_bytes(const of_conv_desc* d) {
+  GemmArgs a;
+  if (!d || b16i_plan(0, d, a)) return 0;
+  return (size_t)a.tiles_total * 512 * 16;
+}
+
 int of_conv2d_b16i_tiles(int mode, const of_conv_desc* d) {
   GemmArgs a;
   if (!d || b16i_plan(mode, d, a)) return -1;
@@ -653,6 +771,19 @@ int of_conv2d_b16i(int mode, const of_conv_desc* d, const of_b16i_io* io, const 
   a.act = act, a.alpha = alpha;
   a.vec_ep = 1;
   a.abl = g_b16i_abl;
+  // the direct epilogue: a bf16 image output alone, N and its pitch in whole 16-byte chunks
+  const bool direct_ok = io->y16 && !io->y && a.N % 8 == 0 && io->ldy16 % 8 == 0 &&
+                         ((uintptr_t)io->y16 & 15) == 0 && (mode == 1 || (!io->aux && !bn_gamma));
+  OF_CHECK_ARG(!io->mask_out || (mode == 0 && direct_ok),
+               "conv b16i: mask_out needs the forward with a bf16 image output alone (N % 8 == 0)");
+  OF_CHECK_ARG(!io->mask_in || (mode == 1 && direct_ok),
+               "conv b16i: mask_in needs the input gradient with a bf16 image output alone");
+  OF_CHECK_ARG(!io->mask_out || ((uintptr_t)io->mask_out & 15) == 0, "conv b16i: mask alignment");
+  OF_CHECK_ARG(!io->mask_in || ((uintptr_t)io->mask_in & 15) == 0, "conv b16i: mask alignment");
+  a.direct16 = direct_ok && (mode == 0 ? g_b16i_direct : io->mask_in != nullptr) && !(a.abl & 1);
+  OF_CHECK_ARG(!io->mask_out || a.direct16, "conv b16i: mask_out with the direct epilogue off");
+  a.mask_out = static_cast<uint4*>(io->mask_out);
+  a.mask_in = static_cast<const uint4*>(io->mask_in);
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * 9 * d->cin;
   const int bn = b16i_bn(a.N);

@@ -62,6 +62,11 @@ struct GemmArgs {
   const uint16_t* act16; int ld_act16;
   float* col_part;
   int abl;                // conv_b16i.hip timing ablations (of_set_tuning key 21; 0 = none)
+  // conv_b16i.hip direct epilogue (bf16 image output only): fwd writes its output's act' signs
+  // (mask_out), the next layer's input gradient reads them (mask_in) instead of act16
+  int direct16;
+  uint4* mask_out;
+  const uint4* mask_in;
   Group grp[MAX_GROUPS];
 };
 

@@ -4664,6 +4664,7 @@ int of_set_tuning(int key, int value) {
   if (key == 17 && (value == 0 || value == 1)) { g_wgt_pf = value; return OF_OK; }
   if (key == 20 && (value == 0 || value == 1)) { g_tile16_pf = value; return OF_OK; }
   if (key == 21 && value >= 0 && value <= 3) { g_b16i_abl = value; return OF_OK; }
+  if (key == 22 && (value == 0 || value == 1)) { g_b16i_direct = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

@@ -700,7 +700,8 @@ __global__ __launch_bounds__(CBB_NT, 2) void corr_bwd_blk(CorrBwdArgs a, int sla
 // staging of the tile's 14 x 22 coefficient halo:
 //   df1[p] = sum_k g[p][k] f2[p + d_k]          (waves 0-3: f2 halo, G1[p][k] = g[p][k])
 //   df2[q] = sum_k g[q - d_k][k] f1[q - d_k]    (waves 4-7: f1 halo, H[q][k] = g[q - d_k][k])
-// The coefficient halo (all 49 values of each of its 308 pixels, coalesced rows) is read once
+// The coefficient halo (all 49 values of each of its 308 pixels as 13 16-byte quads, the
+// last one reading 3 channels past the cost volume) is read once
 // per tile and scattered into both tables; the f1 / f2 halo slabs once per (tile, slab).  A
 // thread owns 4 adjacent pixels x one channel quad: per offset row, 10 src + 8 coefficient
 // ds_read_b128 feed 112 FMAs.  Coefficient tables are [pixel][offset row][8] with a 60-float
@@ -713,7 +714,7 @@ constexpr int FB_Y = 8, FB_X = 16, FB_PIX = FB_Y * FB_X;
 constexpr int FB_HY = FB_Y + 6, FB_HX = FB_X + 6, FB_HPIX = FB_HY * FB_HX;   // 14 x 22
 constexpr int FB_SC = 32, FB_PS = 40, FB_GP = 60, FB_NT = 512;
 constexpr int FB_HQ = FB_HPIX * (FB_SC / 4), FB_HU = (FB_HQ + FB_NT - 1) / FB_NT;   // 2464, 5
-constexpr int FB_GQ = FB_HPIX * 49, FB_GU = (FB_GQ + FB_NT - 1) / FB_NT;           // 15092, 30
+constexpr int FB_GQ = FB_HPIX * 13, FB_GU = (FB_GQ + FB_NT - 1) / FB_NT;   // 4004 quads, 8
 constexpr int FB_LDS = 2 * FB_HPIX * FB_PS + 2 * FB_PIX * FB_GP;                    // floats
 
 struct CorrFusedArgs {
@@ -738,22 +739,17 @@ __device__ __forceinline__ void corr_fused_rows(const float* hal, const float* g
     float4 sv[10];
 #pragma unroll
     for (int u = 0; u < 10; ++u) sv[u] = *reinterpret_cast<const float4*>(sb + u * FB_PS);
-    float cf[4][8];
+    // pixel by pixel: its 7 coefficients of row i (two b128 reads), 14 packed FMAs
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const float* cb = &gt[(row * FB_X + col0 + m) * FB_GP + 8 * i];
       const float4 lo = *reinterpret_cast<const float4*>(cb);
       const float4 hi = *reinterpret_cast<const float4*>(cb + 4);
-      cf[m][0] = lo.x, cf[m][1] = lo.y, cf[m][2] = lo.z, cf[m][3] = lo.w;
-      cf[m][4] = hi.x, cf[m][5] = hi.y, cf[m][6] = hi.z, cf[m][7] = hi.w;
-    }
+      const float cf[7] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z};
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const int u0 = ROLE == 0 ? j : 6 - j;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const float4 v = sv[u0 + m];
-        const f32x2 c2 = {cf[m][j], cf[m][j]};
+      for (int j = 0; j < 7; ++j) {
+        const float4 v = sv[(ROLE == 0 ? j : 6 - j) + m];
+        const f32x2 c2 = {cf[j], cf[j]};
         acc[2 * m] = __builtin_elementwise_fma(c2, f32x2{v.x, v.y}, acc[2 * m]);
         acc[2 * m + 1] = __builtin_elementwise_fma(c2, f32x2{v.z, v.w}, acc[2 * m + 1]);
       }
@@ -781,7 +777,7 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
     y0 = (tl / a.tiles_x) * FB_Y, x0 = (tl % a.tiles_x) * FB_X;
   };
   float4 hv1[FB_HU], hv2[FB_HU];
-  float gv[FB_GU];
+  float4 gv[FB_GU];            // coefficient quads k = 4 kq .. 4 kq + 3 (k < 49 kept)
   auto load_halo = [&](int it) {
     int b, y0, x0, c_lo;
     decode(it, b, y0, x0, c_lo);
@@ -807,10 +803,10 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
 #pragma unroll
     for (int u = 0; u < FB_GU; ++u) {
       const int q = tid + FB_NT * u;
-      const int hp = q / 49, k = q - hp * 49;
+      const int hp = q / 13, kq = q - hp * 13;
       const int sy = y0 - 3 + hp / FB_HX, sx = x0 - 3 + hp % FB_HX;
       const bool ok = q < FB_GQ && (unsigned)sy < (unsigned)h && (unsigned)sx < (unsigned)w;
-      gv[u] = bload1(rg, ok ? 4 * ((sy * w + sx) * a.ldg + k) : kOOB);
+      gv[u] = bload4(rg, ok ? 4 * ((sy * w + sx) * a.ldg + 4 * kq) : kOOB);
     }
   };
   const int role = tid >> 8, r = tid & 255, cq = r & 7, pg = r >> 3;
@@ -834,14 +830,20 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
       for (int u = 0; u < FB_GU; ++u) {
         const int q = tid + FB_NT * u;
         if (q < FB_GQ) {
-          const int hp = q / 49, k = q - hp * 49;
-          const int i = k / 7, j = k - 7 * i;
+          const int hp = q / 13, kq = q - hp * 13;
           const int hy = hp / FB_HX, hx = hp - hy * FB_HX;
-          if ((unsigned)(hy - 3) < (unsigned)FB_Y && (unsigned)(hx - 3) < (unsigned)FB_X)
-            G1[((hy - 3) * FB_X + hx - 3) * FB_GP + 8 * i + j] = gv[u];
-          const int ty = hy + i - 6, tx = hx + j - 6;   // target q = p + d_k
-          if ((unsigned)ty < (unsigned)FB_Y && (unsigned)tx < (unsigned)FB_X)
-            H[(ty * FB_X + tx) * FB_GP + 8 * i + j] = gv[u];
+          const float gq[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = 4 * kq + e;
+            if (k >= 49) break;
+            const int i = k / 7, j = k - 7 * i;
+            if ((unsigned)(hy - 3) < (unsigned)FB_Y && (unsigned)(hx - 3) < (unsigned)FB_X)
+              G1[((hy - 3) * FB_X + hx - 3) * FB_GP + 8 * i + j] = gq[e];
+            const int ty = hy + i - 6, tx = hx + j - 6;   // target q = p + d_k
+            if ((unsigned)ty < (unsigned)FB_Y && (unsigned)tx < (unsigned)FB_X)
+              H[(ty * FB_X + tx) * FB_GP + 8 * i + j] = gq[e];
+          }
         }
       }
       cur_tile = tile;
@@ -857,7 +859,14 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
     decode(it, b, y0, x0, c_lo);
     const int64_t img = (int64_t)b * h * w;
     const int y = y0 + row, ch = c_lo + 4 * cq;
-    const float* init = role == 0 ? a.init1 : a.init2;
+    f32x2 acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = f32x2{0.f, 0.f};
+    if (role == 0)
+      corr_fused_rows<0>(hal2, G1, row, col0, cq, acc);
+    else
+      corr_fused_rows<1>(hal1, H, row, col0, cq, acc);
+    const float* init = role == 0 ? a.init1 : a.init2;   // loaded here: registers
     const int ldi = role == 0 ? a.ldinit1 : a.ldinit2;
     float4 iv[4];
     {
@@ -868,13 +877,6 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
         iv[m] = bload4(ri, y < h && x < w ? 4 * ((y * w + x) * ldi + ch) : kOOB);
       }
     }
-    f32x2 acc[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = f32x2{0.f, 0.f};
-    if (role == 0)
-      corr_fused_rows<0>(hal2, G1, row, col0, cq, acc);
-    else
-      corr_fused_rows<1>(hal1, H, row, col0, cq, acc);
     float* df = role == 0 ? a.df1 : a.df2;
     const int ldd = role == 0 ? a.lddf1 : a.lddf2;
 #pragma unroll
@@ -1742,10 +1744,12 @@ static int corr_bwd_launch(int sign, CorrBwdArgs a, int n, hipStream_t s) {
 }
 
 // Both gradients in one pass (corr_bwd_fused); false: the caller runs the per-gradient kernels.
-static bool corr_fused_ok(int c, const float* f1, int ld1, const float* f2, int ld2,
-                          const float* df1, int lddf1, const float* init1, int ldinit1,
-                          const float* df2, int lddf2) {
-  return (g_corr_blk & 4) && df1 && df2 && c % FB_SC == 0 && ld1 % 4 == 0 && ld2 % 4 == 0 &&
+static bool corr_fused_ok(const float* g, int ldg, int c, const float* f1, int ld1,
+                          const float* f2, int ld2, const float* df1, int lddf1,
+                          const float* init1, int ldinit1, const float* df2, int lddf2) {
+  // (the coefficient quads read g[48 .. 51] of each pixel: ldg >= 52)
+  return (g_corr_blk & 4) && df1 && df2 && c % FB_SC == 0 && ldg % 4 == 0 && ldg >= 52 &&
+         al16(g) && ld1 % 4 == 0 && ld2 % 4 == 0 &&
          lddf1 % 4 == 0 && lddf2 % 4 == 0 && (!init1 || (ldinit1 % 4 == 0 && al16(init1))) &&
          al16(f1) && al16(f2) && al16(df1) && al16(df2);
 }
@@ -1794,7 +1798,8 @@ int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const flo
   OF_CHECK_ARG(ld1 >= c && ld2 >= c && lddcv >= 49, "corr bwd: strides");
   hipStream_t s = as_stream(stream);
   int st;
-  if (corr_fused_ok(c, f1, ld1, f2, ld2, df1, lddf1, acc1 ? df1 : nullptr, lddf1, df2, lddf2)) {
+  if (corr_fused_ok(dcv, lddcv, c, f1, ld1, f2, ld2, df1, lddf1, acc1 ? df1 : nullptr, lddf1, df2,
+                    lddf2)) {
     OF_CHECK_ARG(lddf1 >= c && lddf2 >= c, "corr bwd: df strides");
     CorrFusedArgs a{};
     a.g = dcv, a.ldg = lddcv, a.f1 = f1, a.ld1 = ld1, a.f2 = f2, a.ld2 = ld2;
@@ -1846,7 +1851,7 @@ int of_corr_concat_bwd(const float* dcat, int cp, const float* f1, const float* 
   hipStream_t s = as_stream(stream);
   const bool vec = c % 4 == 0 && cp % 4 == 0 && al16(f1) && al16(f2) && al16(dcat) && al16(df1);
   int st;
-  if (corr_fused_ok(c, f1, c, f2, c, df1, c, dcat, cp, df2, c)) {
+  if (corr_fused_ok(dcat + c, cp, c, f1, c, f2, c, df1, c, dcat, cp, df2, c)) {
     CorrFusedArgs f{};
     f.g = dcat + c, f.ldg = cp, f.f1 = f1, f.ld1 = c, f.f2 = f2, f.ld2 = c;
     f.df1 = df1, f.lddf1 = c, f.init1 = dcat, f.ldinit1 = cp;

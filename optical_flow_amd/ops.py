@@ -989,6 +989,10 @@ def res_block(x, a: ConvLayer, b: ConvLayer, p: Optional[ConvLayer] = None):
 # kernels with K splits); OFLOW_B16I=0 turns it off, OFLOW_B16I_MIN_TILES overrides the size.
 B16I = os.environ.get("OFLOW_B16I", "1") == "1"
 B16I_MIN_TILES = int(os.environ.get("OFLOW_B16I_MIN_TILES", "256"))
+# The forwards of the bf16-image heads write their outputs' act' signs (of_b16i_io mask_out)
+# and the input gradients read those (mask_in) on conv_halo_b16's direct epilogue;
+# OFLOW_B16I_MASK=0 keeps the act16 form (the general epilogue).
+B16I_MASK = os.environ.get("OFLOW_B16I_MASK", "1") == "1"
 
 
 def _img16_ok(layers, x) -> bool:
@@ -1029,17 +1033,21 @@ def _stack_fwd_img16(layers, x):
     nb, h, w, cx = x.shape
     s = _stream()
     x16 = _to_img16(x, (cx + 31) // 32 * 32)
-    imgs = [x16]
+    imgs, masks = [x16], []
     cur = x16
     for i, layer in enumerate(layers[:-2]):
         d = layer.desc(nb, h, w)
         wf, _ = layer.packed(d)
         y16 = _img((nb, h, w, layer.cout), x.device)
+        # the output's act' signs, in the layout the next layer's input gradient reads them
+        mask = (torch.empty(_lib.lib().of_conv2d_b16i_mask_bytes(C.byref(d)) // 4,
+                            dtype=torch.int32, device=x.device) if B16I_MASK else None)
         _tag(layer, 0)
-        io = _b16i_io(a16=cur, lda16=cur.shape[-1], y16=y16, ldy16=layer.cout)
+        io = _b16i_io(a16=cur, lda16=cur.shape[-1], y16=y16, ldy16=layer.cout, mask_out=mask)
         call("of_conv2d_b16i", 0, C.byref(d), C.byref(io), _ptr(wf), _ptr(layer.bias), None, None,
              None, None, BN_EPS, layer.act, layer.alpha, s)
         imgs.append(y16)
+        masks.append(mask)
         cur = y16
     l4 = layers[-2]                      # fp32 output: the narrow flow conv reads it
     d = l4.desc(nb, h, w)
@@ -1058,7 +1066,7 @@ def _stack_fwd_img16(layers, x):
     wsk, wsp, wsb = _workspace(wsz, x.device)
     call(entry, C.byref(d), _ptr(y4), l4.cout, _ptr(wf), _ptr(l5.bias), None, None, None, None,
          BN_EPS, None, 0, l5.act, l5.alpha, None, 0, _ptr(y5), l5.cout, wsp, wsb, s)
-    return imgs + [y4, y5], y5
+    return imgs + masks + [y4, y5], y5
 
 
 def _wgrad_img16(layer, d, x16, dy16, tk, part=None, dy32=None):
@@ -1090,7 +1098,8 @@ def _wgrad_img16(layer, d, x16, dy16, tk, part=None, dy32=None):
 
 def _stack_bwd_img16(layers, saved, g, need_x):
     """Backward of _stack_fwd_img16 (g: the padded flow gradient of the last conv)."""
-    imgs, y4, y5 = saved[:-2], saved[-2], saved[-1]
+    nimg = len(layers) - 1                 # x16 and the outputs of the bf16-image layers
+    imgs, masks, y4, y5 = saved[:nimg], saved[nimg:-2], saved[-2], saved[-1]
     nb, h, w, _ = y4.shape
     s = _stream()
     rets = {}
@@ -1127,8 +1136,11 @@ def _stack_bwd_img16(layers, saved, g, need_x):
             part = torch.empty((tiles, layer.cin_p), device=y4.device)
             gx16 = _img((nb, h, w, layer.cin_p), y4.device)
             _tag(layer, 1)
+            # act' of the producer (layer i - 1): the signs its forward wrote, or its image
+            mk = masks[i - 1] if masks[i - 1] is not None else None
             io = _b16i_io(a16=dy16, lda16=dy16.shape[-1], y16=gx16, ldy16=layer.cin_p,
-                          act16=x16, ld_act16=x16.shape[-1], col_part=part)
+                          act16=None if mk is not None else x16, ld_act16=x16.shape[-1],
+                          col_part=part, mask_in=mk)
             call("of_conv2d_b16i", 1, C.byref(d), C.byref(io), _ptr(wd), None, None, None, None,
                  None, 0.0, prev.act, prev.alpha, s)
             dy16, dy32 = gx16, None

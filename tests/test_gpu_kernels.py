@@ -567,6 +567,80 @@ def test_conv_b16i(n, h, w, cin, cout):
     assert rel_l2(dw, dw_o) < tol, "wgrad"
 
 
+@pytest.mark.parametrize("n,h,w,c0,c1,c2", [(2, 40, 70, 115, 128, 128), (1, 37, 45, 64, 96, 64),
+                                             (2, 20, 36, 96, 64, 32), (1, 16, 32, 128, 32, 64)])
+def test_conv_b16i_direct_masks(n, h, w, c0, c1, c2):
+    """conv_halo_b16's direct epilogue (bf16 image output alone): layer A (c0 -> c1) forward
+    writes its output image and its act' signs (mask_out); the input gradient of layer B
+    (c1 -> c2) reads the signs (mask_in).  Against the general epilogue (of_set_tuning key 22
+    = 0 for the forward; act_src = A's fp32 output for the gradient): the images bitwise, the
+    bias-gradient column sums to fp32 summation order."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_LEAKY, B16iIO, ConvDesc, call
+    lib = _lib.load()
+    P, st = ops._ptr, ops._stream()
+    seed = zlib.crc32(repr((n, h, w, c0, c1, c2)).encode()) % 1000
+    l0, l1, l2 = [(c + 31) // 32 * 32 for c in ((c0 + 3) // 4 * 4, c1, c2)]
+    dA = ConvDesc(n, h, w, c0, (c0 + 3) // 4 * 4, c1, 3, 3, 1, 1, 1, h, w)
+    dB = ConvDesc(n, h, w, c1, c1, c2, 3, 3, 1, 1, 1, h, w)
+
+    def io(**kw):
+        r = B16iIO()
+        for k, v in kw.items():
+            setattr(r, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
+        return r
+
+    def packed(d, cin, cout, sd):
+        wt = dev(rng_tensor((3, 3, cin, cout), sd, scale=(2.0 / (9 * cin)) ** 0.5))
+        wf = torch.empty(lib.of_conv_wfwd16_elems(C.byref(d)), dtype=torch.bfloat16, device="cuda")
+        wb = torch.empty(lib.of_conv_wbwd16_elems(C.byref(d)), dtype=torch.bfloat16, device="cuda")
+        call("of_conv_pack_weights_bf16", C.byref(d), P(wt), P(wf), P(wb), st)
+        return wf, wb
+
+    wfA, _ = packed(dA, c0, c1, seed + 1)
+    _, wbB = packed(dB, c1, c2, seed + 2)
+    bias = dev(rng_tensor((c1,), seed + 3, scale=0.1))
+    x = torch.zeros(n, h, w, (c0 + 3) // 4 * 4, device="cuda")
+    x[..., :c0] = dev(rng_tensor((n, h, w, c0), seed))
+    x16 = torch.zeros(n * h * w * l0, dtype=torch.bfloat16, device="cuda")
+    call("of_to_bf16_image", P(x), n * h * w, x.shape[-1], x.shape[-1], P(x16), l0, st)
+    dy = torch.zeros(n, h, w, c2, device="cuda")
+    dy[...] = dev(rng_tensor((n, h, w, c2), seed + 4))
+    dy16 = torch.zeros(n * h * w * l2, dtype=torch.bfloat16, device="cuda")
+    call("of_to_bf16_image", P(dy), n * h * w, c2, c2, P(dy16), l2, st)
+    mask = torch.empty(lib.of_conv2d_b16i_mask_bytes(C.byref(dA)) // 4, dtype=torch.int32,
+                       device="cuda")
+    yA16 = torch.empty(n, h, w, c1, dtype=torch.bfloat16, device="cuda")
+    yA16g = torch.empty_like(yA16)
+    yA32 = torch.empty(n, h, w, c1, device="cuda")
+    fwd = lambda o: call("of_conv2d_b16i", 0, C.byref(dA), C.byref(o), P(wfA), P(bias), None,
+                         None, None, None, 0.0, ACT_LEAKY, 0.3, st)
+    fwd(io(a16=x16, lda16=l0, y16=yA16, ldy16=c1, mask_out=mask))          # direct
+    fwd(io(a16=x16, lda16=l0, y=yA32, ldy=c1))                             # general, fp32
+    assert lib.of_set_tuning(22, 0) == 0
+    try:
+        fwd(io(a16=x16, lda16=l0, y16=yA16g, ldy16=c1))                    # general, bf16
+    finally:
+        lib.of_set_tuning(22, 1)
+    tiles = lib.of_conv2d_b16i_tiles(1, C.byref(dB))
+    parts = [torch.empty(tiles, c1, device="cuda") for _ in range(2)]
+    dbs = [torch.empty(c1, device="cuda") for _ in range(2)]
+    gx = [torch.empty(n, h, w, c1, dtype=torch.bfloat16, device="cuda") for _ in range(2)]
+    dgrad = lambda o: call("of_conv2d_b16i", 1, C.byref(dB), C.byref(o), P(wbB), None, None, None,
+                           None, None, 0.0, ACT_LEAKY, 0.3, st)
+    dgrad(io(a16=dy16, lda16=l2, y16=gx[0], ldy16=c1, mask_in=mask, col_part=parts[0]))
+    dgrad(io(a16=dy16, lda16=l2, y16=gx[1], ldy16=c1, act_src=yA32, ld_act=c1, col_part=parts[1]))
+    for k in range(2):
+        call("of_col_part_reduce", P(parts[k]), tiles, c1, P(dbs[k]), 0, st)
+    torch.cuda.synchronize()
+    assert torch.equal(yA16, yA16g), "direct forward image != the general epilogue's"
+    assert torch.equal(yA16, yA32.bfloat16()), "forward image != RNE of the fp32 output"
+    assert torch.equal(gx[0], gx[1]), "mask_in input gradient != act_src input gradient"
+    assert rel_l2(dbs[0], dbs[1]) < 1e-6, "column sums"
+
+
 @pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (3, 38, 130), (8, 384, 512)])
 def test_conv_stem_b16(n, h, w):
     """The bf16 stem (configs 3-5) on the one-plane stem kernels (conv_stem_x3<32, 1>,
