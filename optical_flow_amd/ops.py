@@ -1066,7 +1066,7 @@ def _stack_fwd_img16(layers, x):
     wsk, wsp, wsb = _workspace(wsz, x.device)
     call(entry, C.byref(d), _ptr(y4), l4.cout, _ptr(wf), _ptr(l5.bias), None, None, None, None,
          BN_EPS, None, 0, l5.act, l5.alpha, None, 0, _ptr(y5), l5.cout, wsp, wsb, s)
-    return imgs + masks + [y4, y5], y5
+    return imgs + [y4, y5] + masks, y5
 
 
 def _wgrad_img16(layer, d, x16, dy16, tk, part=None, dy32=None):
@@ -1099,7 +1099,7 @@ def _wgrad_img16(layer, d, x16, dy16, tk, part=None, dy32=None):
 def _stack_bwd_img16(layers, saved, g, need_x):
     """Backward of _stack_fwd_img16 (g: the padded flow gradient of the last conv)."""
     nimg = len(layers) - 1                 # x16 and the outputs of the bf16-image layers
-    imgs, masks, y4, y5 = saved[:nimg], saved[nimg:-2], saved[-2], saved[-1]
+    imgs, (y4, y5), masks = saved[:nimg], saved[nimg:nimg + 2], saved[nimg + 2:]
     nb, h, w, _ = y4.shape
     s = _stream()
     rets = {}

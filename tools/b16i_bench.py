@@ -116,6 +116,29 @@ def case(n, h, w, cin, cout, reps, lib):
         call("of_conv2d_b16i", 1, C.byref(d), C.byref(iod16), P(wb), None, None, None, None,
              None, 0.0, 2, 0.3, st)
         call("of_col_part_reduce", P(part), tiles, cin_p, P(db), 0, st)
+    # direct epilogue: act' signs written by a forward producing this layer's input (mask_in)
+    td_m = float("nan")
+    if cin_p % 8 == 0 and cin_p == cin:
+        dp = ConvDesc(n, h, w, 32, 32, cin, 3, 3, 1, 1, 1, h, w)
+        wp = torch.randn(3, 3, 32, cin, device="cuda") * 0.1
+        wfp = torch.empty(lib.of_conv_wfwd16_elems(C.byref(dp)), dtype=torch.bfloat16, device="cuda")
+        wbp = torch.empty(lib.of_conv_wbwd16_elems(C.byref(dp)), dtype=torch.bfloat16, device="cuda")
+        call("of_conv_pack_weights_bf16", C.byref(dp), P(wp), P(wfp), P(wbp), st)
+        xp16 = torch.randn(n * h * w * 32, device="cuda").bfloat16()
+        yp16 = torch.empty(n, h, w, cin, dtype=torch.bfloat16, device="cuda")
+        mask = torch.empty(lib.of_conv2d_b16i_mask_bytes(C.byref(dp)) // 4, dtype=torch.int32,
+                           device="cuda")
+        call("of_conv2d_b16i", 0, C.byref(dp),
+             C.byref(io(a16=xp16, lda16=32, y16=yp16, ldy16=cin, mask_out=mask)), P(wfp), None,
+             None, None, None, None, 0.0, 2, 0.3, st)
+        iodm = io(a16=dy16, lda16=ly, y16=dx16, ldy16=cin_p, mask_in=mask, col_part=part)
+
+        def new_dm():
+            call("of_conv2d_b16i", 1, C.byref(d), C.byref(iodm), P(wb), None, None, None, None,
+                 None, 0.0, 2, 0.3, st)
+            call("of_col_part_reduce", P(part), tiles, cin_p, P(db), 0, st)
+        new_dm()
+        td_m = timeit(new_dm, reps)
     ref_d()
     new_d()
     new_d16()
@@ -142,9 +165,10 @@ def case(n, h, w, cin, cout, reps, lib):
     tw_ref, tw_new = timeit(ref_w, reps), timeit(new_w, reps)
     print("n%d %dx%d %d->%d | fwd err %.1e ref %.3f ms (%.0f TF) new %.3f (%.0f) bf16-out %.3f (%.0f)"
           " | dgrad err %.1e ref %.3f (%.0f) new %.3f (%.0f) bf16-ends+bias %.3f (%.0f)"
+          " masks+bias %.3f (%.0f)"
           " | wgrad err %.1e ref %.3f (%.0f) new %.3f (%.0f)" % (
               n, h, w, cin, cout, ef, tf_ref, tf(tf_ref), tf_new, tf(tf_new), tf_16, tf(tf_16),
-              ed, td_ref, tf(td_ref), td_new, tf(td_new), td_16, tf(td_16),
+              ed, td_ref, tf(td_ref), td_new, tf(td_new), td_16, tf(td_16), td_m, tf(td_m),
               ew, tw_ref, tf(tw_ref), tw_new, tf(tw_new)), flush=True)
     if ABLATE:
         # timing ablations of conv_halo_b16 (of_set_tuning key 21; results are wrong): what the
