@@ -20,6 +20,7 @@
 //   * epilogue: the fp32 epilogues of conv_dev.h (bias, BN, residual, activation / the
 //     producer's activation derivative) through a per-wave LDS transpose as 16-byte rows.
 #include <algorithm>
+#include <type_traits>
 
 #include "conv_dev.h"
 
@@ -59,9 +60,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
                                                                                      : 1;
   constexpr int EPW = 16 * EJ;
   constexpr int EP_U4 = NW * WM * EPW / 4 + WAVES_M * BN / 4;     // + the column-sum buffer
-  // direct epilogue (bf16 image out): per-wave bf16 rows of WN columns, 16-byte padded pitch
-  constexpr int P16 = WN * 2 + 16;
-  constexpr int D_U4 = NW * WM * P16 / 16 + WAVES_M * BN / 4;
+  // direct epilogue: per-wave row images of WN columns -- bf16 all WM rows (16-byte padded
+  // pitch), fp32 WM / 2 rows per pass (32-byte padded: conflict-free 64-bit writes)
+  constexpr int P16 = WN * 2 + 16, P32 = WN * 4 + 32;
+  static_assert(SM % 2 == 0, "fp32 direct epilogue: two passes of SM / 2 row blocks");
+  constexpr int DE_B = NW * WM * P16 > NW * (WM / 2) * P32 ? NW * WM * P16 : NW * (WM / 2) * P32;
+  constexpr int D_U4 = DE_B / 16 + WAVES_M * BN / 4;
   constexpr int SM_U4 = (LOOP_U4 > EP_U4 ? LOOP_U4 : EP_U4) > D_U4 ? (LOOP_U4 > EP_U4 ? LOOP_U4 : EP_U4)
                                                                    : D_U4;
   static_assert(SM_U4 * 16 <= 160 * 1024, "LDS");
@@ -199,20 +203,21 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   }
 
   if (a.direct16) {
-    // ---- direct epilogue (bf16 image output only, no residual / BN): the epilogue math on
-    // the accumulators in their MFMA layout (lane: column 16 j + l16, rows 16 i + 4 lq + r),
-    // bf16 pairs of adjacent columns swapped between lane pairs (DPP) into 32-bit LDS writes,
-    // then whole 16-byte row chunks out: every store instruction writes full 128-byte lines
-    // (the per-pass fp32 transposes below store 32-byte row pieces, which measured ~2.4 TB/s).
-    // fwd also writes the act' signs of its output (mask_out: 128 bits per lane, the input
-    // gradient of the next layer reads them as mask_in in the same layout); dgrad takes
-    // act' from those signs and sums its columns (bias gradient) in registers.
-    char* E16 = reinterpret_cast<char*>(smem) + wave * WM * P16;
-    float* colb = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + NW * WM * P16);
+    // ---- direct epilogue (one output, bf16 image or fp32; no residual / BN): the epilogue
+    // math on the accumulators in their MFMA layout (lane: column 16 j + l16, rows
+    // 16 i + 4 lq + r); adjacent columns swapped between lane pairs (DPP) so each lane writes
+    // 2 rows x 2 columns into a per-wave LDS row image (bf16: 32-bit writes, whole wave rows
+    // at once; fp32: 64-bit writes, half the rows per pass), then whole 16-byte row chunks
+    // out: every store instruction writes full 128-byte lines (the per-pass transposes of the
+    // general epilogue store 32-byte row pieces, measured ~2.4 TB/s).  fwd also writes the
+    // act' signs of its output (mask_out: 128 bits per lane, the input gradient of the next
+    // layer reads them as mask_in in the same layout); dgrad takes act' from those signs
+    // (or none: ACT_NONE) and sums its columns (bias gradient) in registers.
+    char* Ew = reinterpret_cast<char*>(smem);
+    float* colb = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + DE_B);
     const int64_t img = (int64_t)b * OH * OW;
-    // dgrad: the producer forward's act' signs of this tile, in this lane's MFMA layout
-    const uint4 mk = MODE == MODE_DGRAD ? a.mask_in[(int64_t)tile * NT + tid]
-                                        : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 mk = MODE == MODE_DGRAD && a.mask_in ? a.mask_in[(int64_t)tile * NT + tid]
+                                                     : make_uint4(~0u, ~0u, ~0u, ~0u);
     const uint32_t mki[4] = {mk.x, mk.y, mk.z, mk.w};
     uint32_t mo[4] = {0u, 0u, 0u, 0u};
     float bj[SN];
@@ -225,63 +230,93 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
 #pragma unroll
     for (int j = 0; j < SN; ++j) cs[j] = 0.f;
     const bool even = !(l16 & 1);
+    // rows [16 i0, 16 i1) of the wave: epilogue values -> the LDS row image (pitch P bytes,
+    // E bytes per value) -> global
+    auto emit = [&](auto I0, auto I1, auto PB, auto EB) {
+      constexpr int i0 = decltype(I0)::value, i1 = decltype(I1)::value;
+      constexpr int P = decltype(PB)::value, E = decltype(EB)::value;
+      char* Ewv = Ew + wave * (16 * (i1 - i0)) * P;
 #pragma unroll
-    for (int i = 0; i < SM; ++i) {
-      unsigned rv = 0;                     // row validity of rows 16 i + 4 lq + r
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int mt = wm0 + 16 * i + 4 * lq + r;
-        rv |= (oy0 + mt / TW < OH && ox0 + mt % TW < OW ? 1u : 0u) << r;
-      }
-#pragma unroll
-      for (int j = 0; j < SN; ++j) {
-        const bool cv = n0 + wn0 + 16 * j + l16 < a.N;
-        float x[4];
+      for (int i = i0; i < i1; ++i) {
+        unsigned rv = 0;                   // row validity of rows 16 i + 4 lq + r
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int bit = (i * SN + j) * 4 + r;
-          if (MODE == MODE_FWD) {
-            x[r] = act_fwd(acc[i][j][r] + bj[j], a.act, a.alpha);
-            mo[bit >> 5] |= (x[r] > 0.f ? 1u : 0u) << (bit & 31);
+          const int mt = wm0 + 16 * i + 4 * lq + r;
+          rv |= (oy0 + mt / TW < OH && ox0 + mt % TW < OW ? 1u : 0u) << r;
+        }
+#pragma unroll
+        for (int j = 0; j < SN; ++j) {
+          const bool cv = n0 + wn0 + 16 * j + l16 < a.N;
+          float x[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int bit = (i * SN + j) * 4 + r;
+            if (MODE == MODE_FWD) {
+              x[r] = act_fwd(acc[i][j][r] + bj[j], a.act, a.alpha);
+              mo[bit >> 5] |= (x[r] > 0.f ? 1u : 0u) << (bit & 31);
+            } else {
+              const bool pos = (mki[bit >> 5] >> (bit & 31)) & 1u;
+              x[r] = dgrad_ep(a, acc[i][j][r], pos ? 1.f : -1.f, 0.f);
+              if (cv && ((rv >> r) & 1)) cs[j] += x[r];
+            }
+          }
+          const float p0 = even ? x[2] : x[0], p1 = even ? x[3] : x[1];
+          const float q0 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                         __builtin_bit_cast(int, p0), 0xB1, 0xF, 0xF, false));
+          const float q1 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                         __builtin_bit_cast(int, p1), 0xB1, 0xF, 0xF, false));
+          const float4 w = even ? make_float4(x[0], q0, x[1], q1) : make_float4(q0, x[2], q1, x[3]);
+          const int row0 = 16 * (i - i0) + 4 * lq + (even ? 0 : 2);
+          char* d = Ewv + row0 * P + (16 * j + (l16 & ~1)) * E;
+          if (E == 2) {
+            const uint2 u = pack_bf16x4(w);
+            *reinterpret_cast<uint32_t*>(d) = u.x;
+            *reinterpret_cast<uint32_t*>(d + P) = u.y;
           } else {
-            const bool pos = (mki[bit >> 5] >> (bit & 31)) & 1u;
-            x[r] = dgrad_ep(a, acc[i][j][r], pos ? 1.f : -1.f, 0.f);
-            if (cv && ((rv >> r) & 1)) cs[j] += x[r];
+            *reinterpret_cast<float2*>(d) = make_float2(w.x, w.y);
+            *reinterpret_cast<float2*>(d + P) = make_float2(w.z, w.w);
           }
         }
-        const float p0 = even ? x[2] : x[0], p1 = even ? x[3] : x[1];
-        const float q0 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
-                                                       __builtin_bit_cast(int, p0), 0xB1, 0xF, 0xF, false));
-        const float q1 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
-                                                       __builtin_bit_cast(int, p1), 0xB1, 0xF, 0xF, false));
-        const uint2 w = even ? pack_bf16x4(make_float4(x[0], q0, x[1], q1))
-                             : pack_bf16x4(make_float4(q0, x[2], q1, x[3]));
-        const int row0 = 16 * i + 4 * lq + (even ? 0 : 2);
-        char* d = E16 + row0 * P16 + (16 * j + (l16 & ~1)) * 2;
-        *reinterpret_cast<uint32_t*>(d) = w.x;
-        *reinterpret_cast<uint32_t*>(d + P16) = w.y;
+        // pin the sign words / column sums here: left free, the compiler sinks their updates
+        // past every LDS write and keeps all the values live (spills)
+        if (MODE == MODE_FWD) asm volatile("" : "+v"(mo[0]), "+v"(mo[1]), "+v"(mo[2]), "+v"(mo[3]));
+#pragma unroll
+        for (int j = 0; j < SN; ++j)
+          if (MODE == MODE_DGRAD) asm volatile("" : "+v"(cs[j]));
       }
-      // pin the sign words / column sums here: left free, the compiler sinks their updates
-      // past every LDS write and keeps all 128 values live (spills)
-      if (MODE == MODE_FWD) asm volatile("" : "+v"(mo[0]), "+v"(mo[1]), "+v"(mo[2]), "+v"(mo[3]));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int LR = WN * E / 16, NR = 16 * (i1 - i0);   // 16-byte chunks per row, rows
+      static_assert((NR * LR) % 64 == 0, "whole store instructions");
 #pragma unroll
-      for (int j = 0; j < SN; ++j)
-        if (MODE == MODE_DGRAD) asm volatile("" : "+v"(cs[j]));
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    constexpr int LR = WN / 8;                       // 16-byte chunks per row
-    static_assert((WM * LR) % 64 == 0, "whole store instructions");
-#pragma unroll
-    for (int it = 0; it < WM * LR / 64; ++it) {
-      const int c = lane + 64 * it, row = c / LR, part = c - row * LR;
-      const uint4 v = *reinterpret_cast<const uint4*>(E16 + row * P16 + 16 * part);
-      const int mt = wm0 + row;
-      const int oy = oy0 + mt / TW, ox = ox0 + mt % TW;
-      const int ch = n0 + wn0 + 8 * part;
-      if (oy < OH && ox < OW && ch < a.N)
-        *reinterpret_cast<uint4*>(&a.C16[(img + (int64_t)oy * OW + ox) * a.ldc16 + ch]) = v;
+      for (int it = 0; it < NR * LR / 64; ++it) {
+        const int c = lane + 64 * it, row = c / LR, part = c - row * LR;
+        const uint4 v = *reinterpret_cast<const uint4*>(Ewv + row * P + 16 * part);
+        const int mt = wm0 + 16 * i0 + row;
+        const int oy = oy0 + mt / TW, ox = ox0 + mt % TW;
+        const int ch = n0 + wn0 + 16 / E * part;
+        if (oy < OH && ox < OW && ch < a.N) {
+          const int64_t pix = img + (int64_t)oy * OW + ox;
+          if (E == 2)
+            *reinterpret_cast<uint4*>(&a.C16[pix * a.ldc16 + ch]) = v;
+          else
+            *reinterpret_cast<uint4*>(&a.C[pix * a.ldc + ch]) = v;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    using std::integral_constant;
+    if (a.C16) {
+      emit(integral_constant<int, 0>{}, integral_constant<int, SM>{}, integral_constant<int, P16>{},
+           integral_constant<int, 2>{});
+    } else {
+      emit(integral_constant<int, 0>{}, integral_constant<int, SM / 2>{},
+           integral_constant<int, P32>{}, integral_constant<int, 4>{});
+      emit(integral_constant<int, SM / 2>{}, integral_constant<int, SM>{},
+           integral_constant<int, P32>{}, integral_constant<int, 4>{});
     }
     if (MODE == MODE_FWD && a.mask_out)
       a.mask_out[(int64_t)tile * NT + tid] = make_uint4(mo[0], mo[1], mo[2], mo[3]);
@@ -771,16 +806,23 @@ int of_conv2d_b16i(int mode, const of_conv_desc* d, const of_b16i_io* io, const 
   a.act = act, a.alpha = alpha;
   a.vec_ep = 1;
   a.abl = g_b16i_abl;
-  // the direct epilogue: a bf16 image output alone, N and its pitch in whole 16-byte chunks
-  const bool direct_ok = io->y16 && !io->y && a.N % 8 == 0 && io->ldy16 % 8 == 0 &&
-                         ((uintptr_t)io->y16 & 15) == 0 && (mode == 1 || (!io->aux && !bn_gamma));
+  // the direct epilogue: one output (a bf16 image, or fp32), N and its pitch in whole 16-byte
+  // chunks; fwd without residual / BN; dgrad with act' from mask_in or no activation
+  const bool one16 = io->y16 && !io->y && a.N % 8 == 0 && io->ldy16 % 8 == 0 &&
+                     ((uintptr_t)io->y16 & 15) == 0;
+  const bool one32 = io->y && !io->y16 && a.N % 4 == 0 && io->ldy % 4 == 0 &&
+                     ((uintptr_t)io->y & 15) == 0;
+  const bool direct_ok = (one16 || one32) && (mode == 1 || (!io->aux && !bn_gamma));
   OF_CHECK_ARG(!io->mask_out || (mode == 0 && direct_ok),
-               "conv b16i: mask_out needs the forward with a bf16 image output alone (N % 8 == 0)");
+               "conv b16i: mask_out needs the forward with one output (N % 8 == 0 for bf16)");
   OF_CHECK_ARG(!io->mask_in || (mode == 1 && direct_ok),
-               "conv b16i: mask_in needs the input gradient with a bf16 image output alone");
+               "conv b16i: mask_in needs the input gradient with one output");
   OF_CHECK_ARG(!io->mask_out || ((uintptr_t)io->mask_out & 15) == 0, "conv b16i: mask alignment");
   OF_CHECK_ARG(!io->mask_in || ((uintptr_t)io->mask_in & 15) == 0, "conv b16i: mask alignment");
-  a.direct16 = direct_ok && (mode == 0 ? g_b16i_direct : io->mask_in != nullptr) && !(a.abl & 1);
+  a.direct16 = direct_ok && !(a.abl & 1) &&
+               (mode == 0 ? g_b16i_direct != 0
+                          : io->mask_in != nullptr ||
+                                (g_b16i_direct && act == OF_ACT_NONE && !io->act_src && !io->act16));
   OF_CHECK_ARG(!io->mask_out || a.direct16, "conv b16i: mask_out with the direct epilogue off");
   a.mask_out = static_cast<uint4*>(io->mask_out);
   a.mask_in = static_cast<const uint4*>(io->mask_in);

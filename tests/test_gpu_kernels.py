@@ -550,6 +550,10 @@ def test_conv_b16i(n, h, w, cin, cout):
          C.byref(io(a16=dy16, lda16=ly, y16=dx16, ldy16=cin_p, act16=src16, ld_act16=cin_p,
                     col_part=part)), P(wb), None, None, None, None, None, 0.0, ACT_LEAKY, 0.3, st)
     call("of_col_part_reduce", P(part), tiles, cin_p, P(db), 0, st)
+    # no activation (the first head conv's input gradient): the direct fp32 epilogue
+    dxn = torch.empty(n, h, w, cin_p, device="cuda")
+    call("of_conv2d_b16i", 1, C.byref(d), C.byref(io(a16=dy16, lda16=ly, y=dxn, ldy=cin_p)),
+         P(wb), None, None, None, None, None, 0.0, 0, 0.0, st)
     # weight gradient
     dw = torch.empty(3, 3, cin, cout, device="cuda")
     wsb = lib.of_conv2d_wgrad_b16i_workspace(C.byref(d))
@@ -564,6 +568,7 @@ def test_conv_b16i(n, h, w, cin, cout):
     assert dx32[..., cin:].abs().max().item() == 0.0 if cin < cin_p else True
     assert torch.equal(dx16, dx32.bfloat16()), "dgrad image != RNE of the fp32 output"
     assert rel_l2(db[:cin], f64(dx32[..., :cin]).sum((0, 1, 2))) < tol, "column sums"
+    assert rel_inf(dxn[..., :cin], dx_o / slope) < tol, "dgrad, no activation"
     assert rel_l2(dw, dw_o) < tol, "wgrad"
 
 
