@@ -320,6 +320,75 @@ __device__ __forceinline__ uint2 pack_bf16x4(const float4& v) {
   return __builtin_bit_cast(uint2, r);
 }
 
+// Direct fp32 forward epilogue of a 16x16x32-MFMA tile kernel (conv_f32.hip tile_x3_body;
+// conv_b16i.hip has its own, with the bf16 image and sign-mask outputs): bias / BN / act on
+// the accumulators in their MFMA layout (lane: column 16 j + l16, rows 16 i + 4 lq + r),
+// adjacent columns swapped between lane pairs (DPP) so each lane writes 2 rows x 2 columns
+// with 64-bit LDS writes into the wave's row image (half the rows per pass, 32-byte padded
+// pitch: conflict-free), then whole 16-byte row chunks to C: every store instruction writes
+// full 128-byte lines, where the per-pass transposes store 64-byte row pieces.  lds: this
+// wave's region, (WM / 2) * (WN * 4 + 32) bytes.  Rows: tile pixel m -> (oy0 + m / TW,
+// ox0 + m % TW) of image `img` (OH x OW).
+template <int SM, int SN, int WM, int WN, int TW>
+__device__ __forceinline__ void direct_fwd_f32(const GemmArgs& a, f32x4 (&acc)[SM][SN], char* lds,
+                                               int lane, int wm0, int wn0, int n0, int oy0,
+                                               int ox0, int OH, int OW, int64_t img) {
+  static_assert(SM % 2 == 0, "two passes of SM / 2 row blocks");
+  constexpr int P = WN * 4 + 32, LR = WN / 4, NR = WM / 2;
+  static_assert((NR * LR) % 64 == 0, "whole store instructions");
+  const int l16 = lane & 15, lq = lane >> 4;
+  const bool even = !(l16 & 1);
+  float cb[SN], cs[SN], ct[SN];
+#pragma unroll
+  for (int j = 0; j < SN; ++j) {
+    const int n = n0 + wn0 + 16 * j + l16;
+    cb[j] = 0.f, cs[j] = 1.f, ct[j] = 0.f;
+    if (n < a.N) column_params<MODE_FWD>(a, n, cb[j], cs[j], ct[j]);
+  }
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int ii = 0; ii < SM / 2; ++ii) {
+      const int i = hf * (SM / 2) + ii;
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        float x[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = acc[i][j][r] + cb[j];
+          if (a.bn_g) t = t * cs[j] + ct[j];
+          x[r] = act_fwd(t, a.act, a.alpha);
+        }
+        const float p0 = even ? x[2] : x[0], p1 = even ? x[3] : x[1];
+        const float q0 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                       __builtin_bit_cast(int, p0), 0xB1, 0xF, 0xF, false));
+        const float q1 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                       __builtin_bit_cast(int, p1), 0xB1, 0xF, 0xF, false));
+        const int row0 = 16 * ii + 4 * lq + (even ? 0 : 2);
+        char* d = lds + row0 * P + (16 * j + (l16 & ~1)) * 4;
+        *reinterpret_cast<float2*>(d) = even ? make_float2(x[0], q0) : make_float2(q0, x[2]);
+        *reinterpret_cast<float2*>(d + P) = even ? make_float2(x[1], q1) : make_float2(q1, x[3]);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < NR * LR / 64; ++it) {
+      const int c = lane + 64 * it, row = c / LR, part = c - row * LR;
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + row * P + 16 * part);
+      const int mt = wm0 + 16 * (hf * (SM / 2)) + row;
+      const int oy = oy0 + mt / TW, ox = ox0 + mt % TW;
+      const int ch = n0 + wn0 + 4 * part;
+      if (oy < OH && ox < OW && ch < a.N)
+        *reinterpret_cast<uint4*>(&a.C[(img + (int64_t)oy * OW + ox) * a.ldc + ch]) = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // conv_ws.hip: launch conv_tile_ws for a planned bf16 3x3 fwd / dgrad (no timing, no split-K
 // epilogue: the caller's)
 int launch_tile_ws_kernel(const GemmArgs& a, int mode, hipStream_t s);

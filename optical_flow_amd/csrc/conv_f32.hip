@@ -1312,6 +1312,16 @@ __device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
     a.C[(img + (int64_t)oy0 * OW + ox0) * a.ldc + (n0 + wn0 + (lane & 31)) % a.N] = v;
     return;
   }
+  if constexpr (MODE == MODE_FWD && SM % 2 == 0 &&
+                (NT / 64) * (WM / 2) * (WN * 4 + 32) <= LDS_B &&
+                ((WM / 2) * (WN / 4)) % 64 == 0) {
+    if (a.direct16) {      // fp32 forward, one output, no residual / z: conv_dev.h
+      direct_fwd_f32<SM, SN, WM, WN, TF_W>(
+          a, acc4, reinterpret_cast<char*>(smem) + wave * (WM / 2) * (WN * 4 + 32), lane, wm0,
+          wn0, n0, oy0, ox0, OH, OW, img);
+      return;
+    }
+  }
   if (a.vec_ep) {
     // The wave's accumulator block goes through a private LDS image, EJ column blocks per
     // pass (every wave passed the main loop's last barrier after its last halo / B read), and
@@ -4470,6 +4480,9 @@ int stem_wg_tiles(const of_conv_desc* d) {
 
 // of_set_tuning key 10: fp32 / bf16 GEMM weight-gradient split-K target workgroups per CU.
 static int g_wgrad_wgs = 4;
+// of_set_tuning key 23: the split 3x3 forward's direct epilogue (1, default; conv_dev.h
+// direct_fwd_f32) or the per-pass transposes (0).
+static int g_x3_direct = 1;
 
 // of_set_tuning key 16: which bf16 implicit GEMMs (stride-2 block convs, 1x1 projections; the
 // stem when key 15 = 0) run on the one-plane conv_gemm_x3 / conv_wgrad_x3 forms instead of
@@ -4665,6 +4678,7 @@ int of_set_tuning(int key, int value) {
   if (key == 20 && (value == 0 || value == 1)) { g_tile16_pf = value; return OF_OK; }
   if (key == 21 && value >= 0 && value <= 3) { g_b16i_abl = value; return OF_OK; }
   if (key == 22 && (value == 0 || value == 1)) { g_b16i_direct = value; return OF_OK; }
+  if (key == 23 && (value == 0 || value == 1)) { g_x3_direct = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -4826,6 +4840,9 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   a.vec_ep = vec_ep_ok(a);
+  // split 3x3 forward, one K slice, fp32 output only: the direct epilogue (conv_dev.h)
+  a.direct16 = x3 && tile && g_x3_direct && a.splits == 1 && a.vec_ep && !residual && !z &&
+               d->cout % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)y & 15) == 0;
   if (stem) {
     const int64_t tiles = (int64_t)d->n * cdiv(d->ho, ST_TH) * cdiv(d->wo, ST_TW);
     OF_CHECK_ARG(tiles < INT32_MAX, "conv stem: too many tiles");
