@@ -241,8 +241,17 @@ int of_corr_bwd(const float* dcv, int lddcv, const float* f1, int ld1, const flo
 int of_corr_concat_fwd(const float* f1, const float* f2, const float* flow, int n, int h, int w,
                        int c, int max_disp, float* cat, int cp, void* workspace,
                        size_t ws_bytes, void* stream);
-/* Its gradient from dcat (row stride cp): df1 = dcat[:, :c] + d(cv)/d(f1); df2 = d(cv)/d(f2)
- * (skipped if NULL); dflow = dcat[:, c+49 : c+51] (skipped if NULL).  All written. */
+/* The concat row [f1 | cost volume | flow | 0] of of_corr_concat_fwd written as a bf16 NHWC
+ * image with ld16 channels per pixel (>= c + 49 (+ 2), a multiple of 4; channels past the row
+ * zero): the only form the bf16 flow head's first conv reads (ops._stack_fwd_img16), so no
+ * fp32 row is written and converted (round 4).  Grids that need slab groups (small levels,
+ * of_corr_concat_fwd16_ok(n, h, w, c) == 0) are refused. */
+int of_corr_concat_fwd16(const float* f1, const float* f2, const float* flow, int n, int h,
+                         int w, int c, int max_disp, void* cat16, int ld16, void* stream);
+int of_corr_concat_fwd16_ok(int n, int h, int w, int c);
+/* The gradient of of_corr_concat_fwd from dcat (row stride cp): df1 = dcat[:, :c] +
+ * d(cv)/d(f1); df2 = d(cv)/d(f2) (skipped if NULL); dflow = dcat[:, c+49 : c+51] (skipped if
+ * NULL).  All written. */
 int of_corr_concat_bwd(const float* dcat, int cp, const float* f1, const float* f2, int n,
                        int h, int w, int c, int max_disp, float* df1, float* df2, float* dflow,
                        void* stream);

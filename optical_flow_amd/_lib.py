@@ -94,6 +94,8 @@ PROTOTYPES = {
     "of_corr_bwd": (I, [P, I, P, I, P, I, I, I, I, I, I, P, I, I, P, I, I, P]),
     "of_corr_concat_fwd": (I, [P, P, P, I, I, I, I, I, P, I, P, SZ, P]),
     "of_corr_concat_bwd": (I, [P, I, P, P, I, I, I, I, I, P, P, P, P]),
+    "of_corr_concat_fwd16": (I, [P, P, P, I, I, I, I, I, P, I, P]),
+    "of_corr_concat_fwd16_ok": (I, [I, I, I, I]),
     "of_warp_fwd": (I, [P, I, I, I, I, P, P, P]),
     "of_warp_bwd": (I, [P, P, I, I, I, I, P, P, P, P]),
     "of_warp_bwd_add": (I, [P, P, I, I, I, I, P, P, P, P, I, P]),

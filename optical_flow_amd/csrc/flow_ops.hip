@@ -22,6 +22,14 @@ constexpr int CT_Y = 4, CT_X = 16, CT_PIX = CT_Y * CT_X;
 constexpr int CSLAB = 64, CSPS = CSLAB + 4;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// 4 fp32 -> 4 bf16 (RNE), element 0 in the low half of .x (as conv_dev.h pack_bf16x4)
+__device__ __forceinline__ uint2 pack4_bf16(const float4& v) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 r;
+  r[0] = (__bf16)v.x, r[1] = (__bf16)v.y, r[2] = (__bf16)v.z, r[3] = (__bf16)v.w;
+  return __builtin_bit_cast(uint2, r);
+}
+
 __device__ __forceinline__ float quad_sum(float v) {   // sum over the 4 lanes of a quad
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF,
                                                           0xF, false));   // quad_perm(1,0,3,2)
@@ -45,6 +53,10 @@ struct CorrFwdArgs {
   // Flow-module concat (model.py:97-102), optional: cat row = [f1 | cv | flow | zero pad].
   float* cat;         // row stride ldcv; cv == cat + c
   const float* flow;  // (.., 2) or NULL
+  // or the concat row as a bf16 image (corr_fwd_blk, one slab group): [f1 | cv | flow | 0]
+  // with ld16 channels per pixel (cat, cv NULL)
+  uint16_t* cat16;
+  int ld16;
 };
 
 template <int D, bool VEC>
@@ -290,6 +302,11 @@ __global__ __launch_bounds__(CB_NT, 2) void corr_fwd_blk(CorrBlkArgs p) {
       const int pp = q >> 3, cq = q & 7;
       if (q < CB_FQ) {
         *reinterpret_cast<float4*>(&f1s[((pp / CB_X) * CB_F1P + pp % CB_X) * CB_PS + 4 * cq]) = fv[u];
+        if (a.cat16) {                               // f1 slice of the bf16 concat image
+          const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X, ch = c_lo + 4 * cq;
+          if (sy < h && sx < w && ch < a.c)          // (c % 4 == 0)
+            *reinterpret_cast<uint2*>(a.cat16 + (img + sy * w + sx) * a.ld16 + ch) = pack4_bf16(fv[u]);
+        }
         if (a.cat) {                                 // f1 slice of the concat row
           const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X, ch = c_lo + 4 * cq;
           const int n = a.c - ch;
@@ -345,6 +362,31 @@ __global__ __launch_bounds__(CB_NT, 2) void corr_fwd_blk(CorrBlkArgs p) {
         for (int j = 0; j < 7; ++j)
           hal[(cty * CB_X + ctx + m) * 49 + oi * 7 + j] = acc[m * 7 + j].x + acc[m * 7 + j].y;
       __syncthreads();
+      if (a.cat16) {                               // bf16 image: cv, flow, zero padding
+        __bf16* o16 = reinterpret_cast<__bf16*>(a.cat16);
+        for (int q = tid; q < CB_PIX * 49; q += CB_NT) {
+          const int pp = q / 49, k = q - pp * 49;
+          const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X;
+          if (sy < h && sx < w) o16[(img + sy * w + sx) * a.ld16 + a.c + k] = (__bf16)hal[q];
+        }
+        for (int pp = tid; pp < CB_PIX; pp += CB_NT) {
+          const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X;
+          if (sy >= h || sx >= w) continue;
+          const int64_t pl = img + sy * w + sx;
+          __bf16* row = o16 + pl * a.ld16;
+          int ch = a.c + 49;
+          if (a.flow) {
+            row[ch] = (__bf16)a.flow[2 * pl];
+            row[ch + 1] = (__bf16)a.flow[2 * pl + 1];
+            ch += 2;
+          }
+          for (; ch < a.ld16; ++ch) row[ch] = (__bf16)0.f;
+        }
+        __syncthreads();
+        if (!more) break;
+        lt = nlt, it = nit, s = ns;
+        continue;
+      }
       float* out;
       int64_t ld;
       if (p.groups == 1) {
@@ -1839,6 +1881,33 @@ int of_corr_concat_fwd(const float* f1, const float* f2, const float* flow, int 
   a.cv = cat + c, a.ldcv = cp, a.cat = cat, a.flow = flow;
   a.vec = c % 4 == 0 && cp % 4 == 0 && al16(f1) && al16(f2) && al16(cat);
   return corr_fwd_launch(a, n, workspace, ws_bytes, stream);
+}
+
+int of_corr_concat_fwd16(const float* f1, const float* f2, const float* flow, int n, int h,
+                         int w, int c, int max_disp, void* cat16, int ld16, void* stream) {
+  OF_CHECK_ARG(f1 && f2 && cat16, "corr concat fwd16: NULL pointer");
+  OF_CHECK_ARG(max_disp == 3, "corr: only max_disp=3 (the reference default) is compiled");
+  OF_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "corr concat fwd16: dims");
+  OF_CHECK_ARG(ld16 >= c + 49 + (flow ? 2 : 0) && ld16 % 4 == 0, "corr concat fwd16: ld16");
+  OF_CHECK_ARG(al16(f1) && al16(f2) && ((uintptr_t)cat16 & 7) == 0, "corr concat fwd16: alignment");
+  OF_CHECK_ARG((int64_t)h * w * std::max(c, ld16) < (1LL << 29),
+               "corr: one image must hold < 2^29 elements (32-bit buffer offsets)");
+  CorrBlkArgs p{};
+  p.a.f1 = f1, p.a.ld1 = c, p.a.f2 = f2, p.a.ld2 = c, p.a.h = h, p.a.w = w, p.a.c = c;
+  p.a.flow = flow, p.a.vec = 1;
+  p.a.cat16 = static_cast<uint16_t*>(cat16), p.a.ld16 = ld16;
+  corr_blk_plan(n, h, w, c, p);
+  if (p.groups != 1) return fail(OF_EINVAL, "corr concat fwd16: the grid needs slab groups "
+                                 "(small level): use of_corr_concat_fwd");
+  const int grid = corr_blk_grid(p.items);
+  hipLaunchKernelGGL(corr_fwd_blk<true>, dim3(grid), dim3(CB_NT), 0, as_stream(stream), p);
+  return check_launch("corr_fwd_blk (bf16 image)");
+}
+
+int of_corr_concat_fwd16_ok(int n, int h, int w, int c) {
+  CorrBlkArgs p{};
+  corr_blk_plan(n, h, w, c, p);
+  return c % 4 == 0 && p.groups == 1;
 }
 
 int of_corr_concat_bwd(const float* dcat, int cp, const float* f1, const float* f2, int n, int h,

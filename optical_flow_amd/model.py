@@ -308,7 +308,7 @@ def flow_module(features1, features2, previous_flow, max_disp, head: Optional[Fl
         flow_up = None
         features2_warped = features2
     x = ops.corr_concat(features1, features2_warped, flow_up, max_disp, head.cp,
-                        head.convs[0].precision)
+                        head.convs[0].precision, layers=head.convs)
     return ops.conv_stack(x, head.convs)
 
 

@@ -993,6 +993,10 @@ B16I_MIN_TILES = int(os.environ.get("OFLOW_B16I_MIN_TILES", "256"))
 # and the input gradients read those (mask_in) on conv_halo_b16's direct epilogue;
 # OFLOW_B16I_MASK=0 keeps the act16 form (the general epilogue).
 B16I_MASK = os.environ.get("OFLOW_B16I_MASK", "1") == "1"
+# The bf16-image heads' input, concat([f1, cost volume, flow]), written as its bf16 image by the
+# cost-volume kernel (of_corr_concat_fwd16) instead of an fp32 row plus a conversion pass;
+# OFLOW_CONCAT_IMG16=0 keeps the fp32 row.
+CONCAT_IMG16 = os.environ.get("OFLOW_CONCAT_IMG16", "1") == "1"
 
 
 def _img16_ok(layers, x) -> bool:
@@ -1032,7 +1036,9 @@ def _stack_fwd_img16(layers, x):
     """Forward of a bf16 flow head on images: returns (saved tensors, output)."""
     nb, h, w, cx = x.shape
     s = _stream()
-    x16 = _to_img16(x, (cx + 31) // 32 * 32)
+    x16 = getattr(x, "_of_img16", None)   # written by corr_concat directly
+    if x16 is None:
+        x16 = _to_img16(x, (cx + 31) // 32 * 32)
     imgs, masks = [x16], []
     cur = x16
     for i, layer in enumerate(layers[:-2]):
@@ -1378,7 +1384,7 @@ class _CorrConcat(torch.autograd.Function):
     as the initial value of df1 (no copy or concat passes)."""
 
     @staticmethod
-    def forward(ctx, f1, f2w, flow_up, max_disp, cp, fa, df1_side=False):
+    def forward(ctx, f1, f2w, flow_up, max_disp, cp, fa, df1_side=False, img=None):
         _check_dev(f1, f2w, flow_up)
         ctx.fa = fa
         ctx.df1_side = df1_side
@@ -1390,9 +1396,18 @@ class _CorrConcat(torch.autograd.Function):
         x = torch.empty((n, h, w, cp), device=f1.device)
         ctx.dst = (grad_dst(f1), grad_dst(f2w))
         fu = flow_up.contiguous() if flow_up is not None else None
-        ws, wp, wb = _workspace(_lib.lib().of_corr_fwd_workspace(n, h, w, c, max_disp), f1.device)
-        call("of_corr_concat_fwd", _ptr(f1), _ptr(f2w), _ptr(fu), n, h, w, c, max_disp, _ptr(x),
-             cp, wp, wb, _stream())
+        if img is not None:
+            # the consumer (a bf16-image flow head) reads only the row's bf16 image: written
+            # directly, x stays unwritten (its shape and gradient are the autograd interface)
+            x16 = _img((n, h, w, img["ld"]), f1.device)
+            call("of_corr_concat_fwd16", _ptr(f1), _ptr(f2w), _ptr(fu), n, h, w, c, max_disp,
+                 _ptr(x16), img["ld"], _stream())
+            img["x16"] = x16
+        else:
+            ws, wp, wb = _workspace(_lib.lib().of_corr_fwd_workspace(n, h, w, c, max_disp),
+                                    f1.device)
+            call("of_corr_concat_fwd", _ptr(f1), _ptr(f2w), _ptr(fu), n, h, w, c, max_disp,
+                 _ptr(x), cp, wp, wb, _stream())
         ctx.save_for_backward(f1, f2w)
         ctx.meta = (max_disp, cp, nk, flow_up is not None)
         return x
@@ -1426,17 +1441,28 @@ class _CorrConcat(torch.autograd.Function):
             with torch.cuda.stream(corr_side_stream(dx, f1, f2w, df1)):
                 call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c,
                      max_disp, _ptr(df1), None, None, _stream())
-            return df1, df2, dflow, None, None, None, None
+            return df1, df2, dflow, None, None, None, None, None
         call("of_corr_concat_bwd", _ptr(dx), cp, _ptr(f1), _ptr(f2w), n, h, w, c, max_disp,
              _ptr(df1), _ptr(df2), _ptr(dflow), _stream())
-        return df1, df2, dflow, None, None, None, None
+        return df1, df2, dflow, None, None, None, None, None
 
 
-def corr_concat(f1, f2w, flow_up, max_disp, cp, precision="fp32"):
+def corr_concat(f1, f2w, flow_up, max_disp, cp, precision="fp32", layers=None):
     """``precision``: that of the flow module's convs; it picks whether df1 runs on a stream
-    of its own (corr_df1_side)."""
+    of its own (corr_df1_side).  ``layers``: the head convs that will read the result; when
+    they run on bf16 images (_img16_ok) the concat is written as that image directly
+    (of_corr_concat_fwd16, attached to the result as ``_of_img16``) and the fp32 row is not
+    written."""
     fa = getattr(flow_up, "_of_flowadd", None) if flow_up is not None else None
-    return _CorrConcat.apply(f1, f2w, flow_up, max_disp, cp, fa, corr_df1_side(precision))
+    img = None
+    if (layers is not None and CONCAT_IMG16 and f1.is_cuda and
+            _img16_ok(layers, f1) and layers[0].cin_p == cp and
+            _lib.lib().of_corr_concat_fwd16_ok(*f1.shape) == 1):
+        img = {"ld": (cp + 31) // 32 * 32}
+    x = _CorrConcat.apply(f1, f2w, flow_up, max_disp, cp, fa, corr_df1_side(precision), img)
+    if img is not None:
+        x._of_img16 = img["x16"]
+    return x
 
 
 # ============================================================================ warp =====

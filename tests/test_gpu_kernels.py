@@ -1390,6 +1390,33 @@ def test_corr_concat(form, n, h, w, c, cp, has_flow):
         assert rel_inf(d_.grad, o_.grad) < REL_TOL
 
 
+@pytest.mark.parametrize("n,h,w,c,cp,has_flow", [(2, 24, 32, 64, 116, True), (1, 40, 72, 64, 116, True),
+                                                  (4, 48, 64, 128, 180, True), (2, 96, 64, 64, 113, False)])
+def test_corr_concat_fwd16(n, h, w, c, cp, has_flow):
+    """of_corr_concat_fwd16: the concat row written as a bf16 image (ld16 channels) equals the
+    RNE of of_corr_concat_fwd's fp32 row, with zeros past the row."""
+    ops = _ops()
+    from optical_flow_amd import _lib
+    lib = _lib.lib()
+    if lib.of_corr_concat_fwd16_ok(n, h, w, c) != 1:
+        pytest.skip("grid needs slab groups")
+    f1, f2, fl = [dev(rng_tensor(s_, 40 + k)) for k, s_ in
+                  enumerate([(n, h, w, c), (n, h, w, c), (n, h, w, 2)])]
+    fu = fl if has_flow else None
+    ld16 = (cp + 31) // 32 * 32
+    x = torch.empty(n, h, w, cp, device="cuda")
+    wsb = lib.of_corr_fwd_workspace(n, h, w, c, 3)
+    ws = torch.empty(wsb // 4 + 4, device="cuda")
+    P, st = ops._ptr, ops._stream()
+    from optical_flow_amd._lib import call
+    call("of_corr_concat_fwd", P(f1), P(f2), P(fu), n, h, w, c, 3, P(x), cp, P(ws), wsb, st)
+    x16 = torch.full((n, h, w, ld16), 7.0, dtype=torch.bfloat16, device="cuda")
+    call("of_corr_concat_fwd16", P(f1), P(f2), P(fu), n, h, w, c, 3, P(x16), ld16, st)
+    torch.cuda.synchronize()
+    assert torch.equal(x16[..., :cp], x.bfloat16()), "image != RNE of the fp32 row"
+    assert (x16[..., cp:] == 0).all(), "channels past the row must be zero"
+
+
 # ------------------------------------------------------------------------------ warp ----
 @pytest.mark.parametrize("shape,flow_scale", [((2, 12, 20, 64), 3.0), ((2, 16, 16, 128), 1.5),
                                               ((1, 10, 14, 3), 4.0), ((2, 8, 24, 32), 20.0),

@@ -21,7 +21,7 @@ if [ -f "$IN/pmc_traffic.json" ]; then
 else
   python tools/pmc_traffic.py "$IN/fetch/bench_counter_collection.csv" "$IN/write/bench_counter_collection.csv" 384 512 8
 fi
-for f in conv_bench conv_bench_bf16 conv_bench_f32mfma flow_bench x3_accuracy; do
+for f in conv_bench conv_bench_bf16 conv_bench_f32mfma flow_bench x3_accuracy b16i_bench; do
   [ -f "$IN/$f.txt" ] && grep -v amdgpu.ids "$IN/$f.txt" > profiles/${R}_$f.txt
 done
 true
