@@ -31,6 +31,9 @@ namespace oflow {
 int g_b16i_abl = 0;
 // of_set_tuning key 22: the forward's direct epilogue for bf16-image-only outputs (1, default)
 int g_b16i_direct = 1;
+// of_set_tuning key 24: conv_halo_b16 persistent over tile ranges (1; 2: on 8 workgroups,
+// for tests) or one tile per workgroup (0, default: the persistent form measured even)
+int g_b16i_persist = 0;
 
 namespace {
 
@@ -41,7 +44,7 @@ __device__ __forceinline__ float4 bf16x4_to_f4(uint2 u) {
                      __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
 
-template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int TW>
+template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int TW, bool PERSIST = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmArgs a) {
   constexpr int KS = 3;
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = NT / 64;
@@ -70,6 +73,20 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
                                                                    : D_U4;
   static_assert(SM_U4 * 16 <= 160 * 1024, "LDS");
   static_assert(SM * SN * 4 <= 128, "sign mask: 128 bits per lane");
+  // PERSIST: a workgroup per CU walks a contiguous range of tiles; after a tile's main loop it
+  // issues the next tile's first B and halo DMAs into the buffers the last step did not read,
+  // then runs the direct epilogue in the halo buffer it did read (passes of RB row blocks per
+  // wave), so the next tile's first loads are in flight during the epilogue.
+  // rows blocks per pass, by output element size e: whole store instructions, one halo buffer
+  constexpr auto rb_ok = [](int rb, int e, int sm, int wn, int nw, int hb) {
+    return sm % rb == 0 && (16 * rb * (wn * e / 16)) % 64 == 0 &&
+           nw * 16 * rb * (wn * e + 16 * (e / 2)) <= hb;
+  };
+  constexpr int HB = H_U4 * 16;
+  constexpr int PRB16 = rb_ok(1, 2, SM, WN, NW, HB) ? 1 : rb_ok(2, 2, SM, WN, NW, HB) ? 2 : 0;
+  constexpr int PRB32 = rb_ok(1, 4, SM, WN, NW, HB) ? 1 : rb_ok(2, 4, SM, WN, NW, HB) ? 2 : 0;
+  static_assert(!PERSIST || (PRB16 > 0 && PRB32 > 0), "persistent epilogue passes must fit a halo buffer");
+  static_assert(!PERSIST || WAVES_M * BN * 4 <= B_U4 * 16, "column sums in a B buffer");
   __shared__ uint4 smem[SM_U4];
   uint4* Hs = smem;                        // [2][HPD pixels][4 octets]
   uint4* Bs = smem + 2 * H_U4;             // [2][3 taps][BN rows][4 octets]
@@ -78,22 +95,31 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = wgid / a.tiles_total;
-  const int tile = wgid - split * a.tiles_total;
-  const int tile_n = tile % a.n_tiles;
-  const int tile_m = tile / a.n_tiles;
-  const int n0 = tile_n * BN;
   const int OH = MODE == MODE_FWD ? a.ho : a.h, OW = MODE == MODE_FWD ? a.wo : a.w;
   const int SH = MODE == MODE_FWD ? a.h : a.ho, SW = MODE == MODE_FWD ? a.w : a.wo;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
-  const int b = tile_m / (tiles_x * tiles_y);
-  const int trem = tile_m - b * tiles_x * tiles_y;
-  const int oy0 = (trem / tiles_x) * TH, ox0 = (trem % tiles_x) * TW;
-  const int hy0 = MODE == MODE_FWD ? oy0 - a.pt : oy0 + a.pt - (KS - 1);
-  const int hx0 = MODE == MODE_FWD ? ox0 - a.pl : ox0 + a.pl - (KS - 1);
-  const int c_begin = split * a.k_per_split;
-  const int c_end = min(a.K, c_begin + a.k_per_split);
-  const int nsteps = c_end > c_begin ? (c_end - c_begin) * KS : 0;
+  // work items: split * tiles_total + tile (PERSIST: one split, this workgroup's range)
+  const int w_begin = PERSIST ? (int)((int64_t)wgid * a.tiles_total / gridDim.x) : wgid;
+  const int w_end = PERSIST ? (int)((int64_t)(wgid + 1) * a.tiles_total / gridDim.x) : wgid + 1;
+  if (w_begin >= w_end) return;                     // (uniform over the workgroup)
+  struct Geo { int tile, tile_m, n0, b, oy0, ox0, hy0, hx0, c_begin, c_end; };
+  auto geo_of = [&](int wid) {
+    Geo g;
+    const int split = wid / a.tiles_total;
+    g.tile = wid - split * a.tiles_total;
+    const int tile_n = g.tile % a.n_tiles;
+    g.tile_m = g.tile / a.n_tiles;
+    g.n0 = tile_n * BN;
+    g.b = g.tile_m / (tiles_x * tiles_y);
+    const int trem = g.tile_m - g.b * tiles_x * tiles_y;
+    g.oy0 = (trem / tiles_x) * TH, g.ox0 = (trem % tiles_x) * TW;
+    g.hy0 = MODE == MODE_FWD ? g.oy0 - a.pt : g.oy0 + a.pt - (KS - 1);
+    g.hx0 = MODE == MODE_FWD ? g.ox0 - a.pl : g.ox0 + a.pl - (KS - 1);
+    g.c_begin = split * a.k_per_split;
+    g.c_end = min(a.K, g.c_begin + a.k_per_split);
+    return g;
+  };
+  Geo G = geo_of(w_begin);
 
   // a.A: the bf16 image, a.lda channels (bf16 elements) per pixel
   const rsrc_t ra = make_rsrc(a.A, a.a_bytes);
@@ -103,15 +129,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   // loads octet (L & 3) ^ x3_sw(pixel) of pixel 16 g + (L >> 2) (the swizzled image stays
   // lane-linear in LDS)
   uint32_t h_off[HDW];
+  auto set_halo = [&](const Geo& t) {
 #pragma unroll
-  for (int k = 0; k < HDW; ++k) {
-    const int g = wave + NW * k;
-    const int hp = 16 * g + (lane >> 2);
-    const int oct = (lane & 3) ^ x3_sw(hp);
-    const int sy = hy0 + hp / HW, sx = hx0 + hp % HW;
-    const bool ok = g < HDI && hp < HP && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
-    h_off[k] = ok ? (uint32_t)((((int64_t)(b * SH + sy) * SW + sx) * a.lda + 8 * oct) * 2) : kOOB;
-  }
+    for (int k = 0; k < HDW; ++k) {
+      const int g = wave + NW * k;
+      const int hp = 16 * g + (lane >> 2);
+      const int oct = (lane & 3) ^ x3_sw(hp);
+      const int sy = t.hy0 + hp / HW, sx = t.hx0 + hp % HW;
+      const bool ok = g < HDI && hp < HP && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+      h_off[k] = ok ? (uint32_t)((((int64_t)(t.b * SH + sy) * SW + sx) * a.lda + 8 * oct) * 2) : kOOB;
+    }
+  };
   auto dma_halo = [&](int c, int buf) {
 #pragma unroll
     for (int k = 0; k < HDW; ++k) {
@@ -123,14 +151,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   // loads octet (L & 3) ^ x3_sw(L >> 2) of row (L >> 2)
   uint32_t b_off[BDW];
   int b_tap[BDW];
+  auto set_b = [&](const Geo& t) {
 #pragma unroll
-  for (int k = 0; k < BDW; ++k) {
-    const int g = wave + NW * k;
-    const int s = g / (BN / 16), rbk = g % (BN / 16);
-    const int n = rbk * 16 + (lane >> 2), o = (lane & 3) ^ x3_sw(lane >> 2);
-    b_tap[k] = s;
-    b_off[k] = g < BDI && n0 + n < a.nb ? (uint32_t)(((int64_t)(n0 + n) * a.ldb + 8 * o) * 2) : kOOB;
-  }
+    for (int k = 0; k < BDW; ++k) {
+      const int g = wave + NW * k;
+      const int s = g / (BN / 16), rbk = g % (BN / 16);
+      const int n = rbk * 16 + (lane >> 2), o = (lane & 3) ^ x3_sw(lane >> 2);
+      b_tap[k] = s;
+      b_off[k] = g < BDI && t.n0 + n < a.nb ? (uint32_t)(((int64_t)(t.n0 + n) * a.ldb + 8 * o) * 2)
+                                            : kOOB;
+    }
+  };
   auto dma_b = [&](int c, int r, int buf) {
 #pragma unroll
     for (int k = 0; k < BDW; ++k) {
@@ -141,13 +172,6 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
     }
   };
 
-  f32x4 acc[SM][SN];
-#pragma unroll
-  for (int i = 0; i < SM; ++i)
-#pragma unroll
-    for (int j = 0; j < SN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
   const int wm0 = (wave / WAVES_N) * WM;
   const int wn0 = (wave % WAVES_N) * WN;
   const int l16 = lane & 15, lq = lane >> 4;
@@ -158,19 +182,39 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
     const int ty = wm0 / TW, tx = wm0 % TW + l16;
     return MODE == MODE_FWD ? ty * HW + tx : (ty + KS - 1) * HW + tx + KS - 1;
   }();
-  auto frag_hp = [&](int i) { return a_hp0 + ((16 * i) / TW) * HW + (16 * i) % TW; };
-  const int b_frag = (wn0 + l16) * 4 + (lq ^ x3_sw(l16));
+  const int b_frag0 = (wn0 + l16) * 4 + (lq ^ x3_sw(l16));
 
-  if (nsteps > 0) {
-    dma_b(c_begin, 0, 0);
-    dma_halo(c_begin, 0);
+  int hoff = 0, boff = 0;          // buffer parity of the tile's first chunk / step (PERSIST)
+  for (int wid = w_begin;; ++wid) {
+  // (recomputed per tile: nothing but wid and the parities lives across the epilogue)
+  G = geo_of(wid);
+  set_halo(G);
+  set_b(G);
+  if (wid == w_begin && G.c_end > G.c_begin) {
+    dma_b(G.c_begin, 0, 0);
+    dma_halo(G.c_begin, 0);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int tile = G.tile, tile_m = G.tile_m, n0 = G.n0, b = G.b, oy0 = G.oy0, ox0 = G.ox0;
+  // the fragment bases, opaque per tile: left loop-invariant, the addresses derived from them
+  // are hoisted out of the tile loop and stay live through the epilogue (PERSIST: spills)
+  int a_hp = a_hp0, b_frag = b_frag0;
+  if (PERSIST) asm volatile("" : "+v"(a_hp), "+v"(b_frag));
+  auto frag_hp = [&](int i) { return a_hp + ((16 * i) / TW) * HW + (16 * i) % TW; };
+  const int c_begin = G.c_begin, c_end = G.c_end;
+  const int nsteps = c_end > c_begin ? (c_end - c_begin) * KS : 0;
+  f32x4 acc[SM][SN];
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+#pragma unroll
+    for (int j = 0; j < SN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tile's first B and halo landed
   __syncthreads();
   for (int q = 0; q < nsteps; ++q) {
     const int cc = q / KS, r = q - cc * KS;
     const int c = c_begin + cc;
-    const int hbuf = cc & 1, bbuf = q & 1;
+    const int hbuf = (cc + hoff) & 1, bbuf = (q + boff) & 1;
     // prefetch: the next step's B, then (at a chunk's first row) the next chunk's halo; the
     // buffers they overwrite were last read before the previous step's closing barrier
     if (!(a.abl & 2)) {
@@ -201,20 +245,42 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of the next step landed
     __syncthreads();
   }
+  // PERSIST: the next tile's first B and halo go into the buffers the last step did not read
+  // (every wave passed the last step's barrier); the epilogue works in the other halo buffer
+  const bool more = PERSIST && wid + 1 < w_end;
+  const int hl = ((nsteps > 0 ? nsteps / KS - 1 : 0) + hoff) & 1;
+  const int bl = ((nsteps > 0 ? nsteps - 1 : 0) + boff) & 1;
+  if (more) {
+    const Geo Gn = geo_of(wid + 1);
+    set_halo(Gn);
+    set_b(Gn);
+    if (Gn.c_end > Gn.c_begin) {
+      dma_b(Gn.c_begin, 0, bl ^ 1);
+      dma_halo(Gn.c_begin, hl ^ 1);
+    }
+  }
 
   if (a.direct16) {
+    // the lane's column / row-group indices, opaque per tile: left loop-invariant, the LDS and
+    // row addresses derived from them are hoisted out of the tile loop (PERSIST: spills)
+    int lanee = lane;
+    if (PERSIST) asm volatile("" : "+v"(lanee));
+    const int l16e = lanee & 15, lqe = lanee >> 4;
     // ---- direct epilogue (one output, bf16 image or fp32; no residual / BN): the epilogue
-    // math on the accumulators in their MFMA layout (lane: column 16 j + l16, rows
-    // 16 i + 4 lq + r); adjacent columns swapped between lane pairs (DPP) so each lane writes
+    // math on the accumulators in their MFMA layout (lanee: column 16 j + l16e, rows
+    // 16 i + 4 lqe + r); adjacent columns swapped between lanee pairs (DPP) so each lanee writes
     // 2 rows x 2 columns into a per-wave LDS row image (bf16: 32-bit writes, whole wave rows
     // at once; fp32: 64-bit writes, half the rows per pass), then whole 16-byte row chunks
     // out: every store instruction writes full 128-byte lines (the per-pass transposes of the
     // general epilogue store 32-byte row pieces, measured ~2.4 TB/s).  fwd also writes the
-    // act' signs of its output (mask_out: 128 bits per lane, the input gradient of the next
+    // act' signs of its output (mask_out: 128 bits per lanee, the input gradient of the next
     // layer reads them as mask_in in the same layout); dgrad takes act' from those signs
     // (or none: ACT_NONE) and sums its columns (bias gradient) in registers.
-    char* Ew = reinterpret_cast<char*>(smem);
-    float* colb = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + DE_B);
+    // (PERSIST with a next tile: the halo buffer the last step read, and the B buffer likewise
+    // for the column sums; the next tile's first DMAs are writing the other two)
+    char* Ew = PERSIST ? reinterpret_cast<char*>(Hs + hl * H_U4) : reinterpret_cast<char*>(smem);
+    float* colb = PERSIST ? reinterpret_cast<float*>(Bs + bl * B_U4)
+                          : reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + DE_B);
     const int64_t img = (int64_t)b * OH * OW;
     const uint4 mk = MODE == MODE_DGRAD && a.mask_in ? a.mask_in[(int64_t)tile * NT + tid]
                                                      : make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -223,13 +289,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
     float bj[SN];
 #pragma unroll
     for (int j = 0; j < SN; ++j) {
-      const int nn = n0 + wn0 + 16 * j + l16;
+      const int nn = n0 + wn0 + 16 * j + l16e;
       bj[j] = MODE == MODE_FWD && a.bias && nn < a.N ? a.bias[nn] : 0.f;
     }
     float cs[SN];
 #pragma unroll
     for (int j = 0; j < SN; ++j) cs[j] = 0.f;
-    const bool even = !(l16 & 1);
+    const bool even = !(l16e & 1);
     // rows [16 i0, 16 i1) of the wave: epilogue values -> the LDS row image (pitch P bytes,
     // E bytes per value) -> global
     auto emit = [&](auto I0, auto I1, auto PB, auto EB) {
@@ -238,15 +304,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
       char* Ewv = Ew + wave * (16 * (i1 - i0)) * P;
 #pragma unroll
       for (int i = i0; i < i1; ++i) {
-        unsigned rv = 0;                   // row validity of rows 16 i + 4 lq + r
+        unsigned rv = 0;                   // row validity of rows 16 i + 4 lqe + r
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int mt = wm0 + 16 * i + 4 * lq + r;
+          const int mt = wm0 + 16 * i + 4 * lqe + r;
           rv |= (oy0 + mt / TW < OH && ox0 + mt % TW < OW ? 1u : 0u) << r;
         }
 #pragma unroll
         for (int j = 0; j < SN; ++j) {
-          const bool cv = n0 + wn0 + 16 * j + l16 < a.N;
+          const bool cv = n0 + wn0 + 16 * j + l16e < a.N;
           float x[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -266,8 +332,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
           const float q1 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
                                                          __builtin_bit_cast(int, p1), 0xB1, 0xF, 0xF, false));
           const float4 w = even ? make_float4(x[0], q0, x[1], q1) : make_float4(q0, x[2], q1, x[3]);
-          const int row0 = 16 * (i - i0) + 4 * lq + (even ? 0 : 2);
-          char* d = Ewv + row0 * P + (16 * j + (l16 & ~1)) * E;
+          const int row0 = 16 * (i - i0) + 4 * lqe + (even ? 0 : 2);
+          char* d = Ewv + row0 * P + (16 * j + (l16e & ~1)) * E;
           if (E == 2) {
             const uint2 u = pack_bf16x4(w);
             *reinterpret_cast<uint32_t*>(d) = u.x;
@@ -291,7 +357,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
       static_assert((NR * LR) % 64 == 0, "whole store instructions");
 #pragma unroll
       for (int it = 0; it < NR * LR / 64; ++it) {
-        const int c = lane + 64 * it, row = c / LR, part = c - row * LR;
+        const int c = lanee + 64 * it, row = c / LR, part = c - row * LR;
         const uint4 v = *reinterpret_cast<const uint4*>(Ewv + row * P + 16 * part);
         const int mt = wm0 + 16 * i0 + row;
         const int oy = oy0 + mt / TW, ox = ox0 + mt % TW;
@@ -309,7 +375,25 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     using std::integral_constant;
-    if (a.C16) {
+    // passes of RB row blocks (PERSIST with a next tile: PRB16 / PRB32, inside one halo buffer)
+    auto passes = [&](auto RBc, auto PB, auto EB) {
+      constexpr int RB = decltype(RBc)::value;
+      auto pass = [&](auto K) {
+        constexpr int k = decltype(K)::value;
+        if constexpr (RB > 0 && k * RB < SM)
+          emit(integral_constant<int, k * RB>{}, integral_constant<int, (k + 1) * RB>{}, PB, EB);
+      };
+      pass(integral_constant<int, 0>{}), pass(integral_constant<int, 1>{});
+      pass(integral_constant<int, 2>{}), pass(integral_constant<int, 3>{});
+      pass(integral_constant<int, 4>{}), pass(integral_constant<int, 5>{});
+      pass(integral_constant<int, 6>{}), pass(integral_constant<int, 7>{});
+    };
+    if (PERSIST) {                       // (the last tile too: one code path)
+      if (a.C16)
+        passes(integral_constant<int, PRB16>{}, integral_constant<int, P16>{}, integral_constant<int, 2>{});
+      else
+        passes(integral_constant<int, PRB32>{}, integral_constant<int, P32>{}, integral_constant<int, 4>{});
+    } else if (a.C16) {
       emit(integral_constant<int, 0>{}, integral_constant<int, SM>{}, integral_constant<int, P16>{},
            integral_constant<int, 2>{});
     } else {
@@ -322,10 +406,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
       a.mask_out[(int64_t)tile * NT + tid] = make_uint4(mo[0], mo[1], mo[2], mo[3]);
     if (MODE == MODE_DGRAD && a.col_part != nullptr) {
 #pragma unroll
-      for (int j = 0; j < SN; ++j) {        // fixed order: lq 0+1, 2+3, then the halves
+      for (int j = 0; j < SN; ++j) {        // fixed order: lqe 0+1, 2+3, then the halves
         cs[j] += __shfl_xor(cs[j], 16, 64);
         cs[j] += __shfl_xor(cs[j], 32, 64);
-        if (lq == 0) colb[(wave / WAVES_N) * BN + wn0 + 16 * j + l16] = cs[j];
+        if (lqe == 0) colb[(wave / WAVES_N) * BN + wn0 + 16 * j + l16e] = cs[j];
       }
       __syncthreads();
       if (tid < BN && n0 + tid < a.N) {
@@ -335,8 +419,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
         a.col_part[(int64_t)tile_m * a.N + n0 + tid] = v;
       }
     }
-    return;
+    if (!more) return;
+    hoff = hl ^ 1, boff = bl ^ 1;
+    continue;
   }
+  if constexpr (PERSIST) return;         // (the host runs PERSIST with the direct epilogue only)
 
   // ---- epilogue: the wave's accumulators through a private LDS image (EJ 16-column blocks
   // per pass), back as float4 rows (16-byte loads / stores, 4 EJ lanes per pixel row).  Every
@@ -476,6 +563,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
       a.col_part[(int64_t)tile_m * a.N + n0 + tid] = v;
     }
   }
+  return;
+  }   // tile loop
 }
 
 // ---- weight gradient from bf16 images: dW[r][s][ci][co] = sum_p x(p + (r, s) - pad)[ci] .
@@ -832,15 +921,21 @@ int of_conv2d_b16i(int mode, const of_conv_desc* d, const of_b16i_io* io, const 
   const int cfg = bn == 128 ? 0 : bn == 96 ? 1 : bn == 64 ? 2 : 3;
   const dim3 grid(a.tiles_total), block(512);
   if (timing_on()) timing_begin(s);
-#define B16I_LAUNCH(MODE)                                                                        \
-  if (cfg == 0) hipLaunchKernelGGL((conv_halo_b16<128, 4, 2, MODE, BI_TH, BI_TW>), grid, block, 0, s, a); \
-  else if (cfg == 1) hipLaunchKernelGGL((conv_halo_b16<96, 4, 2, MODE, BI_TH, BI_TW>), grid, block, 0, s, a); \
-  else if (cfg == 2) hipLaunchKernelGGL((conv_halo_b16<64, 8, 1, MODE, BI_TH, BI_TW>), grid, block, 0, s, a); \
-  else hipLaunchKernelGGL((conv_halo_b16<32, 8, 1, MODE, BI_TH, BI_TW>), grid, block, 0, s, a);
+  // persistent form (key 24): one workgroup per CU over contiguous tile ranges, the next
+  // tile's first loads in flight during the epilogue; direct epilogue only
+  // (key 24 = 2: a grid of 8 workgroups whatever the size: the tests' multi-tile walks)
+  const int pg = g_b16i_persist == 2 ? 8 : device_cus();
+  const bool persist = g_b16i_persist && a.direct16 && a.splits == 1 && a.tiles_total > pg;
+  const dim3 pgrid(persist ? pg : 1);
+#define B16I_LAUNCH(MODE, P, G)                                                                  \
+  if (cfg == 0) hipLaunchKernelGGL((conv_halo_b16<128, 4, 2, MODE, BI_TH, BI_TW, P>), G, block, 0, s, a); \
+  else if (cfg == 1) hipLaunchKernelGGL((conv_halo_b16<96, 4, 2, MODE, BI_TH, BI_TW, P>), G, block, 0, s, a); \
+  else if (cfg == 2) hipLaunchKernelGGL((conv_halo_b16<64, 8, 1, MODE, BI_TH, BI_TW, P>), G, block, 0, s, a); \
+  else hipLaunchKernelGGL((conv_halo_b16<32, 8, 1, MODE, BI_TH, BI_TW, P>), G, block, 0, s, a);
   if (mode == 0) {
-    B16I_LAUNCH(MODE_FWD)
+    if (persist) { B16I_LAUNCH(MODE_FWD, true, pgrid) } else { B16I_LAUNCH(MODE_FWD, false, grid) }
   } else {
-    B16I_LAUNCH(MODE_DGRAD)
+    if (persist) { B16I_LAUNCH(MODE_DGRAD, true, pgrid) } else { B16I_LAUNCH(MODE_DGRAD, false, grid) }
   }
 #undef B16I_LAUNCH
   if (timing_on()) timing_end(s, 288 + 8 * mode + cfg, flops);   // bench.py kind_parts

@@ -4679,6 +4679,7 @@ int of_set_tuning(int key, int value) {
   if (key == 21 && value >= 0 && value <= 3) { g_b16i_abl = value; return OF_OK; }
   if (key == 22 && (value == 0 || value == 1)) { g_b16i_direct = value; return OF_OK; }
   if (key == 23 && (value == 0 || value == 1)) { g_x3_direct = value; return OF_OK; }
+  if (key == 24 && value >= 0 && value <= 2) { g_b16i_persist = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

@@ -473,7 +473,7 @@ B16I_CASES = [(2, 40, 70, 128, 128), (1, 37, 45, 20, 24), (2, 24, 48, 128, 96),
 
 
 @pytest.mark.parametrize("n,h,w,cin,cout", B16I_CASES)
-def test_conv_b16i(n, h, w, cin, cout):
+def test_conv_b16i(n, h, w, cin, cout, b16i_persist):
     """The bf16-activation-image 3x3 kernels (of_conv2d_b16i fwd / dgrad, of_conv2d_wgrad_b16i)
     through the C ABI against float64 convolutions of the same bf16-rounded operands (the
     oracle's bf16 rounding points, R._Bf16Conv): forward with bias + LeakyReLU, input gradient
@@ -572,9 +572,21 @@ def test_conv_b16i(n, h, w, cin, cout):
     assert rel_l2(dw, dw_o) < tol, "wgrad"
 
 
+@pytest.fixture(params=[0, 2], ids=["tile", "persist"])
+def b16i_persist(request):
+    """conv_halo_b16 one tile per workgroup, or persistent on 8 workgroups (of_set_tuning key 24
+    = 2: multi-tile walks at test sizes, the next tile's loads in flight during the epilogue)."""
+    from optical_flow_amd import _lib
+    lib = _lib.lib()
+    assert lib.of_set_tuning(24, request.param) == 0
+    yield request.param
+    lib.of_set_tuning(24, 0)
+
+
 @pytest.mark.parametrize("n,h,w,c0,c1,c2", [(2, 40, 70, 115, 128, 128), (1, 37, 45, 64, 96, 64),
-                                             (2, 20, 36, 96, 64, 32), (1, 16, 32, 128, 32, 64)])
-def test_conv_b16i_direct_masks(n, h, w, c0, c1, c2):
+                                             (2, 20, 36, 96, 64, 32), (1, 16, 32, 128, 32, 64),
+                                             (4, 48, 96, 64, 128, 96)])
+def test_conv_b16i_direct_masks(n, h, w, c0, c1, c2, b16i_persist):
     """conv_halo_b16's direct epilogue (bf16 image output alone): layer A (c0 -> c1) forward
     writes its output image and its act' signs (mask_out); the input gradient of layer B
     (c1 -> c2) reads the signs (mask_in).  Against the general epilogue (of_set_tuning key 22
