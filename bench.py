@@ -336,6 +336,11 @@ def main():
                          "launches through the Python glue")
     ap.add_argument("--side-stream", type=int, choices=[0, 1], default=1,
                     help="1: weight-gradient kernels on a second HIP stream (ops.side_stream)")
+    ap.add_argument("--main-prio", type=int, choices=[0, 1],
+                    default=int(os.environ.get("OFLOW_MAIN_PRIO", "0")),
+                    help="1: run the step on a high-priority HIP stream, so the hardware "
+                         "dispatches its workgroups ahead of the side streams' (weight "
+                         "gradients, the cost volume's df1) when both have work queued")
     ap.add_argument("--deterministic", type=int, choices=[0, 1], default=0,
                     help="1: the deterministic (sort + fixed-order gather) warp backward "
                          "(ops.DETERMINISTIC)")
@@ -357,6 +362,8 @@ def main():
 
     rank, world, local = init_from_env()
     torch.cuda.set_device(local)
+    if args.main_prio:
+        torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     _lib.load()
     H, W, B = args.height, args.width, args.batch
     vals = init_params(flow_net_spec(levels=args.levels), 0)   # identical weights on all ranks

@@ -54,6 +54,11 @@ __device__ __forceinline__ float4 bload4(rsrc_t r, uint32_t voff) {
 __device__ __forceinline__ float bload1(rsrc_t r, uint32_t voff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
 }
+// Store counterpart: an out-of-range offset (kOOB) drops the write, no branch around it.
+__device__ __forceinline__ void bstore4(float4 v, rsrc_t r, uint32_t voff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                         r, voff, 0, 0);
+}
 // Channel quad at byte offset `off` with `n` valid channels (n >= 4: all), zero elsewhere;
 // `ok` false -> zeros.  vec: 16-byte aligned rows and whole quads (the caller guarantees
 // n <= 0 or n >= 4), one b128 and no selects on the loaded value -- a select right after

@@ -757,7 +757,7 @@ constexpr int FB_HY = FB_Y + 6, FB_HX = FB_X + 6, FB_HPIX = FB_HY * FB_HX;   // 
 constexpr int FB_SC = 32, FB_PS = 40, FB_GP = 60, FB_NT = 512;
 constexpr int FB_HQ = FB_HPIX * (FB_SC / 4), FB_HU = (FB_HQ + FB_NT - 1) / FB_NT;   // 2464, 5
 constexpr int FB_GQ = FB_HPIX * 13, FB_GU = (FB_GQ + FB_NT - 1) / FB_NT;   // 4004 quads, 8
-constexpr int FB_LDS = 2 * FB_HPIX * FB_PS + 2 * FB_PIX * FB_GP;                    // floats
+constexpr int FB_LDS = 2 * FB_HPIX * FB_PS + 2 * FB_PIX * FB_GP + 64;   // floats (+ dummy words)
 
 struct CorrFusedArgs {
   const float* g; int ldg;
@@ -786,7 +786,8 @@ __device__ __forceinline__ void corr_fused_rows(const float* hal, const float* g
     for (int m = 0; m < 4; ++m) {
       const float* cb = &gt[(row * FB_X + col0 + m) * FB_GP + 8 * i];
       const float4 lo = *reinterpret_cast<const float4*>(cb);
-      const float4 hi = *reinterpret_cast<const float4*>(cb + 4);
+      float4 hi = *reinterpret_cast<const float4*>(cb + 4);
+      asm volatile("" : "+v"(hi.w));   // keep the 4th word: a b128 read, not a slower b96
       const float cf[7] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z};
 #pragma unroll
       for (int j = 0; j < 7; ++j) {
@@ -851,7 +852,8 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
       gv[u] = bload4(rg, ok ? 4 * ((sy * w + sx) * a.ldg + 4 * kq) : kOOB);
     }
   };
-  const int role = tid >> 8, r = tid & 255, cq = r & 7, pg = r >> 3;
+  const int role = __builtin_amdgcn_readfirstlane(tid >> 8);   // wave-uniform: scalar rsrcs
+  const int r = tid & 255, cq = r & 7, pg = r >> 3;
   const int row = pg >> 2, col0 = (pg & 3) * 4;
   int it = it0, cur_tile = -1;
   load_halo(it);
@@ -868,24 +870,28 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
       }
     }
     if (tile != cur_tile) {                       // uniform: scatter the new coefficients
+      // straight-line: a value with no slot in a table goes to this lane's dummy word (a
+      // guarded store per value compiled to a branch, an exec save and a wait each)
+      float* const dummy = H + FB_PIX * FB_GP + (tid & 63);
 #pragma unroll
       for (int u = 0; u < FB_GU; ++u) {
         const int q = tid + FB_NT * u;
-        if (q < FB_GQ) {
-          const int hp = q / 13, kq = q - hp * 13;
-          const int hy = hp / FB_HX, hx = hp - hy * FB_HX;
-          const float gq[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+        const int hp = q / 13, kq = q - hp * 13;
+        const int hy = hp / FB_HX, hx = hp - hy * FB_HX;
+        const bool live = q < FB_GQ;
+        const bool own = live && (unsigned)(hy - 3) < (unsigned)FB_Y && (unsigned)(hx - 3) < (unsigned)FB_X;
+        const float gq[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int k = 4 * kq + e;
-            if (k >= 49) break;
-            const int i = k / 7, j = k - 7 * i;
-            if ((unsigned)(hy - 3) < (unsigned)FB_Y && (unsigned)(hx - 3) < (unsigned)FB_X)
-              G1[((hy - 3) * FB_X + hx - 3) * FB_GP + 8 * i + j] = gq[e];
-            const int ty = hy + i - 6, tx = hx + j - 6;   // target q = p + d_k
-            if ((unsigned)ty < (unsigned)FB_Y && (unsigned)tx < (unsigned)FB_X)
-              H[(ty * FB_X + tx) * FB_GP + 8 * i + j] = gq[e];
-          }
+        for (int e = 0; e < 4; ++e) {
+          const int k = 4 * kq + e;
+          const int i = k / 7, j = k - 7 * i;
+          const bool kk = k < 49;
+          float* g1 = own && kk ? &G1[((hy - 3) * FB_X + hx - 3) * FB_GP + 8 * i + j] : dummy;
+          *g1 = gq[e];
+          const int ty = hy + i - 6, tx = hx + j - 6;   // target q = p + d_k
+          const bool hit = live && kk && (unsigned)ty < (unsigned)FB_Y && (unsigned)tx < (unsigned)FB_X;
+          float* hq = hit ? &H[(ty * FB_X + tx) * FB_GP + 8 * i + j] : dummy;
+          *hq = gq[e];
         }
       }
       cur_tile = tile;
@@ -908,7 +914,9 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
       corr_fused_rows<0>(hal2, G1, row, col0, cq, acc);
     else
       corr_fused_rows<1>(hal1, H, row, col0, cq, acc);
-    const float* init = role == 0 ? a.init1 : a.init2;   // loaded here: registers
+    // the added gradients (issued before the rows they would land during the compute, but
+    // their 16 registers push the kernel past 256 VGPRs: 23 spills)
+    const float* init = role == 0 ? a.init1 : a.init2;
     const int ldi = role == 0 ? a.ldinit1 : a.ldinit2;
     float4 iv[4];
     {
@@ -921,13 +929,16 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
     }
     float* df = role == 0 ? a.df1 : a.df2;
     const int ldd = role == 0 ? a.lddf1 : a.lddf2;
+    // unguarded buffer stores (edge pixels dropped by offset): with a guarded store the
+    // wait for iv sat on one path only, and the compiler then waited for every load in
+    // flight -- the next item's prefetch -- at the top of the next item's row loop
+    const rsrc_t rd = make_rsrc(df + img * ldd, (int64_t)h * w * ldd * 4);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const int x = x0 + col0 + m;
-      if (y < h && x < w)
-        *reinterpret_cast<float4*>(df + (img + y * w + x) * ldd + ch) =
-            make_float4(iv[m].x + acc[2 * m].x, iv[m].y + acc[2 * m].y,
-                        iv[m].z + acc[2 * m + 1].x, iv[m].w + acc[2 * m + 1].y);
+      bstore4(make_float4(iv[m].x + acc[2 * m].x, iv[m].y + acc[2 * m].y,
+                          iv[m].z + acc[2 * m + 1].x, iv[m].w + acc[2 * m + 1].y),
+              rd, y < h && x < w ? 4 * ((y * w + x) * ldd + ch) : kOOB);
     }
     if (!more) break;
     __syncthreads();                              // halo / coefficients no longer read
@@ -968,20 +979,23 @@ __device__ __forceinline__ WarpTap warp_tap(int i, int j, float f0, float f1, in
 }
 
 // One thread per (pixel, channel quad); C % 4 == 0.
+// I: index type, 32-bit unsigned when the element count fits (64-bit divisions per element
+// made the kernel ALU-bound)
+template <typename I>
 __global__ __launch_bounds__(256) void warp_fwd_vec(const float* __restrict__ inp, int n, int h,
                                                     int w, int c,
                                                     const float* __restrict__ flow,
                                                     float* __restrict__ out, int absolute) {
-  const int nq = c >> 2;
-  const int64_t total = (int64_t)n * h * w * nq;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t p = idx / nq;
-    const int q = (int)(idx - p * nq);
-    const int j = (int)(p % w);
-    const int64_t t2 = p / w;
-    const int i = (int)(t2 % h);
-    const int64_t img = (t2 / h) * h * w;
+  const I nq = c >> 2;
+  const I total = (I)n * h * w * nq;
+  for (I idx = blockIdx.x * (I)blockDim.x + threadIdx.x; idx < total;
+       idx += (I)gridDim.x * blockDim.x) {
+    const int64_t p = (int64_t)(idx / nq);
+    const int q = (int)(idx % nq);
+    const int j = (int)((I)p % (I)w);
+    const I t2 = (I)p / (I)w;
+    const int i = (int)(t2 % (I)h);
+    const int64_t img = (int64_t)(t2 / (I)h) * h * w;
     const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
     const WarpTap t = warp_tap(i, j, f.x, f.y, h, w, img, absolute);
     const float4 v00 = *reinterpret_cast<const float4*>(inp + t.o00 * c + 4 * q);
@@ -1252,18 +1266,42 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
     return img + (int64_t)min(i, h - 1) * w + min(j, w - 1);
   };
 
-  // ---- flow-gradient lanes: pixel group pg of 4, channel quad q; corner loads issued first
-  constexpr int IT = NP / (4 * WG_NT / 64);
+  // ---- loads in three batches, each waited for once (tile pixels are clamped into the
+  // image, so every address is valid and no load sits behind a branch; a guarded load per
+  // element compiled to a wait per element, and each flow wait also drained the corner loads
+  // issued before it): (1) the flows, the tile's dout rows and the added flow gradients,
+  // (2) the corner rows, which need the flows, (3) nothing: dout and dfa arrive meanwhile.
+  constexpr int IT = NP / (4 * WG_NT / 64), DU = NP * 16 / WG_NT;
   const int q = lane & 15, pg = lane >> 4;
-  bool okg[IT];
+  const int pe = tid >> 2, ke = tid & 3;               // this thread's (pixel, corner) entry
+  bool okg[IT], oke;
   int64_t pixg[IT];
+  float2 fg[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    pixg[it] = tile_pix((it * (WG_NT / 64) + wave) * 4 + pg, okg[it]);
+    fg[it] = *reinterpret_cast<const float2*>(flow + 2 * pixg[it]);
+  }
+  const int64_t pxe = tile_pix(pe, oke);
+  const float2 fe = *reinterpret_cast<const float2*>(flow + 2 * pxe);
+  float4 dv[DU];
+#pragma unroll
+  for (int u = 0; u < DU; ++u) {
+    bool ok;
+    const int v = tid + u * WG_NT;
+    dv[u] = *reinterpret_cast<const float4*>(dout + tile_pix(v >> 4, ok) * c + cc + 4 * (v & 15));
+  }
+  float fax[IT], fay[IT];                              // dfa (passes == 1 only; else unused)
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    fax[it] = dfa ? dfa[pixg[it] * ldfa] : 0.f;
+    fay[it] = dfa ? dfa[pixg[it] * ldfa + 1] : 0.f;
+  }
   float ag[IT], bg[IT];
   float4 pv[IT][4];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int pr = (it * (WG_NT / 64) + wave) * 4 + pg;
-    pixg[it] = tile_pix(pr, okg[it]);
-    const float2 f = okg[it] ? *reinterpret_cast<const float2*>(flow + 2 * pixg[it]) : make_float2(0.f, 0.f);
+    const float2 f = okg[it] ? fg[it] : make_float2(0.f, 0.f);
     int y0, y1, x0, x1;
     corners((int)(pixg[it] - img) / w, (int)((pixg[it] - img) % w), f, y0, y1, x0, x1, ag[it], bg[it]);
     const int ys[4] = {y0, y1, y0, y1}, xs[4] = {x0, x0, x1, x1};
@@ -1271,29 +1309,25 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
     for (int k = 0; k < 4; ++k)
       pv[it][k] = *reinterpret_cast<const float4*>(inp + (img + (int64_t)ys[k] * w + xs[k]) * c + cc + 4 * q);
   }
-  // ---- dout rows of the tile -> LDS
-#pragma unroll
-  for (int u = tid; u < NP * 16; u += WG_NT) {
-    const int p = u >> 4, qq = u & 15;
-    bool ok;
-    const int64_t px = tile_pix(p, ok);
-    const float4 g = ok ? *reinterpret_cast<const float4*>(dout + px * c + cc + 4 * qq) : make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(&dtile[p * 64 + 4 * qq]) = g;
-  }
-  // ---- this thread's entry: pixel tid >> 2, corner tid & 3
-  const int pe = tid >> 2, ke = tid & 3;
-  bool oke;
-  const int64_t pxe = tile_pix(pe, oke);
   int ye = 0, xe = 0;
   float wte = 0.f;
   {
-    const float2 f = oke ? *reinterpret_cast<const float2*>(flow + 2 * pxe) : make_float2(0.f, 0.f);
     int y0, y1, x0, x1;
     float a, bq;
-    corners((int)(pxe - img) / w, (int)((pxe - img) % w), f, y0, y1, x0, x1, a, bq);
+    corners((int)(pxe - img) / w, (int)((pxe - img) % w), oke ? fe : make_float2(0.f, 0.f), y0,
+            y1, x0, x1, a, bq);
     ye = (ke & 1) ? y1 : y0;
     xe = (ke & 2) ? x1 : x0;
     wte = ((ke & 2) ? 1.f - a : a) * ((ke & 1) ? 1.f - bq : bq);
+  }
+  // ---- dout rows of the tile -> LDS (out-of-image pixels: zero rows)
+#pragma unroll
+  for (int u = 0; u < DU; ++u) {
+    const int v = tid + u * WG_NT;
+    bool ok;
+    (void)tile_pix(v >> 4, ok);
+    *reinterpret_cast<float4*>(&dtile[(v >> 4) * 64 + 4 * (v & 15)]) =
+        ok ? dv[u] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (dinp) {
     if (tid == 0) bb[0] = INT32_MAX, bb[1] = -1, bb[2] = INT32_MAX, bb[3] = -1;
@@ -1382,11 +1416,7 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
     gy = row16_sum(gy);
     if (q == 0 && okg[it]) {
       if (passes == 1) {
-        if (dfa) {
-          gx = dfa[(int64_t)pixg[it] * ldfa] + gx;
-          gy = dfa[(int64_t)pixg[it] * ldfa + 1] + gy;
-        }
-        *reinterpret_cast<float2*>(dflow + 2 * pixg[it]) = make_float2(gx, gy);
+        *reinterpret_cast<float2*>(dflow + 2 * pixg[it]) = make_float2(fax[it] + gx, fay[it] + gy);
       } else {                                         // dflow preset by the launcher
         atomicAdd(dflow + 2 * pixg[it], gx);
         atomicAdd(dflow + 2 * pixg[it] + 1, gy);
@@ -1951,8 +1981,13 @@ static int warp_fwd_impl(const float* inp, int n, int h, int w, int c, const flo
   hipStream_t s = as_stream(stream);
   const int64_t npix = (int64_t)n * h * w;
   if (c % 4 == 0 && ((uintptr_t)inp & 15) == 0 && ((uintptr_t)out & 15) == 0) {
-    hipLaunchKernelGGL(warp_fwd_vec, dim3(grid_for(npix * (c / 4))), dim3(256), 0, s, inp, n, h,
-                       w, c, flow, out, absolute);
+    const int64_t total = npix * (c / 4);
+    if (total + (int64_t)grid_for(total) * 256 < (int64_t)UINT32_MAX)
+      hipLaunchKernelGGL(warp_fwd_vec<uint32_t>, dim3(grid_for(total)), dim3(256), 0, s, inp, n,
+                         h, w, c, flow, out, absolute);
+    else
+      hipLaunchKernelGGL(warp_fwd_vec<int64_t>, dim3(grid_for(total)), dim3(256), 0, s, inp, n,
+                         h, w, c, flow, out, absolute);
   } else {
     hipLaunchKernelGGL(warp_fwd_scalar, dim3(grid_for(npix)), dim3(256), 0, s, inp, n, h, w, c,
                        flow, out, absolute);

@@ -242,13 +242,18 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
       bt = *reinterpret_cast<const float4*>(beta + ch);
       ig = make_float4(1.f / gm.x, 1.f / gm.y, 1.f / gm.z, 1.f / gm.w);
     }
+    // window cursor (b, oy, ox) of p, stepped by `rows` without a division per pixel (64-bit
+    // divisions, three per pooled pixel, made this kernel ALU-bound at ~2.1 TB/s)
+    int ox = (int)((p0 + r) % wo), oy = (int)((p0 + r) / wo % ho);
+    int64_t b = (p0 + r) / wo / ho;
+    const int dox = rows % wo, doy = rows / wo;
 #pragma unroll MPB_UNROLL
     for (int64_t p = p0 + r; p < p1; p += rows) {
-      const int ox = (int)(p % wo);
-      const int64_t t2 = p / wo;
-      const int oy = (int)(t2 % ho);
-      const int64_t b = t2 / ho;
       const int64_t o0 = ((b * h + 2 * oy) * (int64_t)w + 2 * ox) * c + ch;
+      ox += dox;
+      oy += doy;
+      if (ox >= wo) ox -= wo, ++oy;
+      while (oy >= ho) oy -= ho, ++b;
       const int64_t offs[4] = {o0, o0 + c, o0 + (int64_t)w * c, o0 + (int64_t)w * c + c};
       float4 yv[4], zv[4], gv[4];
 #pragma unroll
@@ -365,19 +370,23 @@ __global__ __launch_bounds__(BNF_Q * BNF_G) void bn_act_bwd_final(const float* _
 }
 
 // ------------------------------------------------------------------------- max pool ----
+// I: the index type -- 32-bit unsigned whenever the element count fits (64-bit division is a
+// software routine of ~100 instructions, and three of them per element made this kernel
+// ALU-bound at ~2.6 TB/s).
+template <typename I>
 __global__ __launch_bounds__(256) void maxpool2_fwd_kernel(const float* __restrict__ x, int n,
                                                            int h, int w, int c,
                                                            float* __restrict__ y) {
-  const int ho = h / 2, wo = w / 2, cq = c / 4;
-  const int64_t total = (int64_t)n * ho * wo * cq;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  const I ho = h / 2, wo = w / 2, cq = c / 4;
+  const I total = (I)n * ho * wo * cq;
+  for (I idx = blockIdx.x * (I)blockDim.x + threadIdx.x; idx < total;
+       idx += (I)gridDim.x * blockDim.x) {
     const int q = (int)(idx % cq);
-    const int64_t p = idx / cq;
+    const I p = idx / cq;
     const int ox = (int)(p % wo);
-    const int64_t t2 = p / wo;
+    const I t2 = p / wo;
     const int oy = (int)(t2 % ho);
-    const int64_t b = t2 / ho;
+    const int64_t b = (int64_t)(t2 / ho);
     const float* base = x + ((b * h + 2 * oy) * (int64_t)w + 2 * ox) * c + 4 * q;
     const float4 a = *reinterpret_cast<const float4*>(base);
     const float4 bb = *reinterpret_cast<const float4*>(base + c);
@@ -388,7 +397,7 @@ __global__ __launch_bounds__(256) void maxpool2_fwd_kernel(const float* __restri
     r.y = fmaxf(fmaxf(a.y, bb.y), fmaxf(cc.y, d.y));
     r.z = fmaxf(fmaxf(a.z, bb.z), fmaxf(cc.z, d.z));
     r.w = fmaxf(fmaxf(a.w, bb.w), fmaxf(cc.w, d.w));
-    *reinterpret_cast<float4*>(y + p * c + 4 * q) = r;
+    *reinterpret_cast<float4*>(y + (int64_t)p * c + 4 * q) = r;
   }
 }
 
@@ -718,8 +727,12 @@ int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const f
 int of_maxpool2_fwd(const float* x, int n, int h, int w, int c, float* y, void* stream) {
   OF_CHECK_ARG(x && y && h % 2 == 0 && w % 2 == 0 && c % 4 == 0, "maxpool fwd: args");
   const int64_t total = (int64_t)n * (h / 2) * (w / 2) * (c / 4);
-  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_of(total)), dim3(256), 0, as_stream(stream),
-                     x, n, h, w, c, y);
+  if (total < (int64_t)UINT32_MAX - (int64_t)grid_of(total) * 256)
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<uint32_t>, dim3(grid_of(total)), dim3(256), 0,
+                       as_stream(stream), x, n, h, w, c, y);
+  else
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<int64_t>, dim3(grid_of(total)), dim3(256), 0,
+                       as_stream(stream), x, n, h, w, c, y);
   return check_launch("maxpool2_fwd");
 }
 

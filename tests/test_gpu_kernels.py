@@ -1661,7 +1661,8 @@ def test_conv_split_k_matches_unsplit(stride):
     assert rel_inf(dx1, ref) < REL_TOL and rel_inf(dx2, ref) < REL_TOL
 
 
-@pytest.mark.parametrize("n,h,w,c,with_g", [(2, 8, 12, 64, True), (1, 6, 10, 16, False)])
+@pytest.mark.parametrize("n,h,w,c,with_g", [(2, 8, 12, 64, True), (1, 6, 10, 16, False),
+                                            (3, 34, 70, 64, True)])
 def test_maxpool_bn_act_bwd_fused(n, h, w, c, with_g):
     """The stem's fused backward (max-pool backward + out0's second gradient + BN/ReLU
     backward) against torch autograd of relu(bn(z)) -> {out0, maxpool} in float64."""
