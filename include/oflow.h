@@ -394,7 +394,8 @@ int of_timing_enable(int on);
  * DMAs; RESULTS ARE WRONG, A/B timing only; default 0);
  * key 22 = conv_halo_b16's direct epilogue for forwards with a bf16 image output alone (1,
  * default; the input gradient takes it whenever it is given mask_in);
- * key 23 = the split 3x3 forward's direct fp32 epilogue (1, default);
+ * key 23 = the split 3x3 kernels' direct fp32 epilogues, bit 0 forward, bit 1 input
+ * gradient (1, default: the input gradient's measured slower; 0 = per-pass transposes);
  * key 24 = conv_halo_b16 persistent over contiguous tile ranges, the next tile's first loads
  * in flight during the epilogue (1; 2: on 8 workgroups, for tests) or one tile per workgroup
  * (0, default: the persistent form measured even). */

@@ -389,6 +389,83 @@ __device__ __forceinline__ void direct_fwd_f32(const GemmArgs& a, f32x4 (&acc)[S
   }
 }
 
+// Direct fp32 input-gradient epilogue, the counterpart of direct_fwd_f32: the raw sums go
+// through the same row image; then each lane takes whole 16-byte row chunks, loads the
+// activation source and residual quads of all its chunks first (addresses clamped into the
+// tensors, so no load sits behind a branch and all are in flight together), and stores
+// dgrad_ep of each element -- full 128-byte lines for the loads and the stores, where the
+// per-pass transposes move 64-byte row pieces with one chunk's loads in flight.
+template <int SM, int SN, int WM, int WN, int TW>
+__device__ __forceinline__ void direct_dgrad_f32(const GemmArgs& a, f32x4 (&acc)[SM][SN],
+                                                 char* lds, int lane, int wm0, int wn0, int n0,
+                                                 int oy0, int ox0, int OH, int OW, int64_t img) {
+  static_assert(SM % 2 == 0, "two passes of SM / 2 row blocks");
+  constexpr int P = WN * 4 + 32, LR = WN / 4, NR = WM / 2, IT = NR * LR / 64;
+  static_assert((NR * LR) % 64 == 0, "whole store instructions");
+  const int l16 = lane & 15, lq = lane >> 4;
+  const bool even = !(l16 & 1);
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int ii = 0; ii < SM / 2; ++ii) {
+      const int i = hf * (SM / 2) + ii;
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        const f32x4 x = acc[i][j];
+        const float p0 = even ? x[2] : x[0], p1 = even ? x[3] : x[1];
+        const float q0 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                       __builtin_bit_cast(int, p0), 0xB1, 0xF, 0xF, false));
+        const float q1 = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                       __builtin_bit_cast(int, p1), 0xB1, 0xF, 0xF, false));
+        const int row0 = 16 * ii + 4 * lq + (even ? 0 : 2);
+        char* d = lds + row0 * P + (16 * j + (l16 & ~1)) * 4;
+        *reinterpret_cast<float2*>(d) = even ? make_float2(x[0], q0) : make_float2(q0, x[2]);
+        *reinterpret_cast<float2*>(d + P) = even ? make_float2(x[1], q1) : make_float2(q1, x[3]);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // chunks in groups of G: the group's activation-source / residual quads are all loaded
+    // before its first store (G = 4 bounds the registers: 8 chunks spilled the 4-wave form)
+    constexpr int G = IT < 4 ? IT : 4;
+    static_assert(IT % G == 0, "whole groups");
+#pragma unroll
+    for (int g0 = 0; g0 < IT; g0 += G) {
+      int64_t prow[G];
+      int chs[G];
+      bool ok[G];
+      float4 s4[G], r4[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int c = lane + 64 * (g0 + g), row = c / LR, part = c - row * LR;
+        const int mt = wm0 + 16 * (hf * (SM / 2)) + row;
+        const int oy = oy0 + mt / TW, ox = ox0 + mt % TW;
+        const int ch = n0 + wn0 + 4 * part;
+        ok[g] = oy < OH && ox < OW && ch < a.N;
+        prow[g] = img + (int64_t)min(oy, OH - 1) * OW + min(ox, OW - 1);
+        chs[g] = min(ch, a.N - 4);
+        s4[g] = a.act_src ? *reinterpret_cast<const float4*>(&a.act_src[prow[g] * a.ld_act + chs[g]])
+                          : make_float4(1.f, 1.f, 1.f, 1.f);
+        r4[g] = a.res ? *reinterpret_cast<const float4*>(&a.res[prow[g] * a.ldr + chs[g]])
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int c = lane + 64 * (g0 + g), row = c / LR, part = c - row * LR;
+        const float4 v = *reinterpret_cast<const float4*>(lds + row * P + 16 * part);
+        if (ok[g])
+          *reinterpret_cast<float4*>(&a.C[prow[g] * a.ldc + chs[g]]) =
+              make_float4(dgrad_ep(a, v.x, s4[g].x, r4[g].x), dgrad_ep(a, v.y, s4[g].y, r4[g].y),
+                          dgrad_ep(a, v.z, s4[g].z, r4[g].z), dgrad_ep(a, v.w, s4[g].w, r4[g].w));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // conv_ws.hip: launch conv_tile_ws for a planned bf16 3x3 fwd / dgrad (no timing, no split-K
 // epilogue: the caller's)
 int launch_tile_ws_kernel(const GemmArgs& a, int mode, hipStream_t s);

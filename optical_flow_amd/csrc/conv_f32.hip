@@ -1322,6 +1322,17 @@ __device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
       return;
     }
   }
+  // (not the 4-wave forms: at 256 VGPRs already, the chunk registers raised their spills)
+  if constexpr (MODE == MODE_DGRAD && NT >= 512 && SM % 2 == 0 &&
+                (NT / 64) * (WM / 2) * (WN * 4 + 32) <= LDS_B &&
+                ((WM / 2) * (WN / 4)) % 64 == 0) {
+    if (a.direct16) {      // fp32 input gradient, one K slice: conv_dev.h
+      direct_dgrad_f32<SM, SN, WM, WN, TF_W>(
+          a, acc4, reinterpret_cast<char*>(smem) + wave * (WM / 2) * (WN * 4 + 32), lane, wm0,
+          wn0, n0, oy0, ox0, OH, OW, img);
+      return;
+    }
+  }
   if (a.vec_ep) {
     // The wave's accumulator block goes through a private LDS image, EJ column blocks per
     // pass (every wave passed the main loop's last barrier after its last halo / B read), and
@@ -4480,8 +4491,10 @@ int stem_wg_tiles(const of_conv_desc* d) {
 
 // of_set_tuning key 10: fp32 / bf16 GEMM weight-gradient split-K target workgroups per CU.
 static int g_wgrad_wgs = 4;
-// of_set_tuning key 23: the split 3x3 forward's direct epilogue (1, default; conv_dev.h
-// direct_fwd_f32) or the per-pass transposes (0).
+// of_set_tuning key 23: the split 3x3 kernels' direct epilogues (conv_dev.h), bit 0 the
+// forward's (direct_fwd_f32), bit 1 the input gradient's (direct_dgrad_f32); a clear bit keeps
+// the per-pass transposes.  Default 1: the input gradient's measured slower (per layer dec3.c1
+// 0.506 -> 0.531 ms, c2 0.413 -> 0.426; fp32 step 651.8 -> 650.6 pairs/s, gpurun_out/misc6).
 static int g_x3_direct = 1;
 
 // of_set_tuning key 16: which bf16 implicit GEMMs (stride-2 block convs, 1x1 projections; the
@@ -4678,7 +4691,7 @@ int of_set_tuning(int key, int value) {
   if (key == 20 && (value == 0 || value == 1)) { g_tile16_pf = value; return OF_OK; }
   if (key == 21 && value >= 0 && value <= 3) { g_b16i_abl = value; return OF_OK; }
   if (key == 22 && (value == 0 || value == 1)) { g_b16i_direct = value; return OF_OK; }
-  if (key == 23 && (value == 0 || value == 1)) { g_x3_direct = value; return OF_OK; }
+  if (key == 23 && value >= 0 && value <= 3) { g_x3_direct = value; return OF_OK; }
   if (key == 24 && value >= 0 && value <= 2) { g_b16i_persist = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
@@ -4842,7 +4855,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   a.vec_ep = vec_ep_ok(a);
   // split 3x3 forward, one K slice, fp32 output only: the direct epilogue (conv_dev.h)
-  a.direct16 = x3 && tile && g_x3_direct && a.splits == 1 && a.vec_ep && !residual && !z &&
+  a.direct16 = x3 && tile && (g_x3_direct & 1) && a.splits == 1 && a.vec_ep && !residual && !z &&
                d->cout % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)y & 15) == 0;
   if (stem) {
     const int64_t tiles = (int64_t)d->n * cdiv(d->ho, ST_TH) * cdiv(d->wo, ST_TW);
@@ -4943,6 +4956,8 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   a.vec_ep = vec_ep_ok(a);
+  // split 3x3 input gradient, one K slice: the direct epilogue (conv_dev.h direct_dgrad_f32)
+  a.direct16 = x3 && tile && (g_x3_direct & 2) && a.splits == 1 && a.vec_ep;
   st = x3     ? (tile ? launch_tile_x3<MODE_DGRAD>(a, s, flops)
                      : launch_gemm_x3<MODE_DGRAD>(a, s, flops))
        : ws   ? launch_tile_ws<MODE_DGRAD>(a, s, flops)

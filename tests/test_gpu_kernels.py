@@ -1057,6 +1057,56 @@ def test_conv_x3_vec_epilogue(n, h, w, cin, cout):
 
 
 @pytest.mark.parametrize("n,h,w,cin,cout", [
+    (8, 128, 256, 128, 128),  # 8-wave <128, 4, 2> dgrad, 8 x 32 tiles
+    (4, 67, 250, 96, 128),    # ragged bottom / right edges
+    (8, 64, 128, 96, 96),     # BN 96, 12 waves
+])
+def test_conv_x3_direct_dgrad(n, h, w, cin, cout):
+    """The split input gradient's direct epilogue (of_set_tuning key 23 bit 1, off by default:
+    row image + whole 16-byte chunks with the activation-source / added-gradient quads loaded
+    ahead) is bitwise the per-pass transposes' result: activation derivative, added gradient, and the
+    added gradient in place."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_LEAKY, call
+    lib = _lib.lib()
+    wt = dev(rng_tensor((3, 3, cin, cout), 52, scale=(2.0 / (9 * cin)) ** 0.5))
+    b = dev(rng_tensor((cout,), 53, scale=0.1))
+    dy = dev(rng_tensor((n, h, w, cout), 54))
+    act_src = dev(rng_tensor((n, h, w, cin), 55))
+    add = dev(rng_tensor((n, h, w, cin), 56))
+    layer = ops.ConvLayer(wt, b, stride=1, act=ACT_LEAKY, cin_p=cin, f32_split=True)
+    d = layer.desc(n, h, w)
+    assert layer.mode(d) == 2
+    _, wd = layer.packed(d)
+    dws = lib.of_conv2d_dgrad_x3_workspace(C.byref(d))
+    assert dws == 0                       # one K slice: the direct epilogue's precondition
+    P, st = ops._ptr, ops._stream()
+    outs = []
+    try:
+        for key in (3, 1):
+            assert lib.of_set_tuning(23, key) == 0
+            dx = torch.full((n, h, w, cin), 7.0, device="cuda")
+            dx2 = torch.full((n, h, w, cin), 7.0, device="cuda")
+            dx3 = add.clone()
+            call("of_conv2d_dgrad_x3", C.byref(d), P(dy), cout, P(wd), P(act_src), cin,
+                 ACT_LEAKY, 0.3, P(dx), cin, None, 0, st)
+            call("of_conv2d_dgrad_add_x3", C.byref(d), P(dy), cout, P(wd), P(add), cin,
+                 P(dx2), cin, None, 0, st)
+            call("of_conv2d_dgrad_add_x3", C.byref(d), P(dy), cout, P(wd), P(dx3), cin,
+                 P(dx3), cin, None, 0, st)
+            torch.cuda.synchronize()
+            outs.append((dx, dx2, dx3))
+    finally:
+        lib.of_set_tuning(23, 1)
+    for name, a1, a0 in zip(("dx", "dx_add", "dx_add_in_place"), *outs):
+        assert torch.equal(a1, a0), (name, (a1 - a0).abs().max().item())
+    assert torch.equal(outs[0][1], outs[0][2])
+    # (the per-pass form is pinned against fp64 by test_conv_x3_large_grids / _accuracy)
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout", [
     (2, 20, 45, 128, 128),   # <2,4,8>: ragged right edge, 2 channel tiles
     (1, 13, 32, 64, 96),     # <2,3,8>: odd rows (half k-step at the bottom)
     (2, 24, 32, 64, 64),     # <4,2,4>
