@@ -752,6 +752,11 @@ __global__ __launch_bounds__(CBB_NT, 2) void corr_bwd_blk(CorrBwdArgs a, int sla
 // w walks items [w * items / grid, (w + 1) * items / grid) (items = (tile, slab), slabs of a
 // tile adjacent; XCD-remapped, so neighbouring tiles share an L2), and loads the next item's
 // halos (and, for a new tile, coefficients) into registers while the current one computes.
+// Timing ablations of corr_bwd_fused (tools/ab_build.sh -DCORR_ABL=mask; wrong results, never
+// in the shipped build): 1 no coefficient scatter, 2 no row compute, 4 no added-gradient loads.
+#ifndef CORR_ABL
+#define CORR_ABL 0
+#endif
 constexpr int FB_Y = 8, FB_X = 16, FB_PIX = FB_Y * FB_X;
 constexpr int FB_HY = FB_Y + 6, FB_HX = FB_X + 6, FB_HPIX = FB_HY * FB_HX;   // 14 x 22
 constexpr int FB_SC = 32, FB_PS = 40, FB_GP = 60, FB_NT = 512;
@@ -869,7 +874,7 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
         *reinterpret_cast<float4*>(&hal2[o]) = hv2[u];
       }
     }
-    if (tile != cur_tile) {                       // uniform: scatter the new coefficients
+    if (!(CORR_ABL & 1) && tile != cur_tile) {    // uniform: scatter the new coefficients
       // straight-line: a value with no slot in a table goes to this lane's dummy word (a
       // guarded store per value compiled to a branch, an exec save and a wait each)
       float* const dummy = H + FB_PIX * FB_GP + (tid & 63);
@@ -910,10 +915,12 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
     f32x2 acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = f32x2{0.f, 0.f};
-    if (role == 0)
+    if (CORR_ABL & 2) {
+    } else if (role == 0) {
       corr_fused_rows<0>(hal2, G1, row, col0, cq, acc);
-    else
+    } else {
       corr_fused_rows<1>(hal1, H, row, col0, cq, acc);
+    }
     // the added gradients (issued before the rows they would land during the compute, but
     // their 16 registers push the kernel past 256 VGPRs: 23 spills)
     const float* init = role == 0 ? a.init1 : a.init2;
@@ -924,7 +931,7 @@ __global__ __launch_bounds__(FB_NT, 1) void corr_bwd_fused(CorrFusedArgs a) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int x = x0 + col0 + m;
-        iv[m] = bload4(ri, y < h && x < w ? 4 * ((y * w + x) * ldi + ch) : kOOB);
+        iv[m] = bload4(ri, !(CORR_ABL & 4) && y < h && x < w ? 4 * ((y * w + x) * ldi + ch) : kOOB);
       }
     }
     float* df = role == 0 ? a.df1 : a.df2;
@@ -1211,6 +1218,11 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
 // addresses serialise.)  The flow gradient: lanes work 4 pixels x 16 channel quads (16-byte
 // corner loads, a DPP row reduction over the 16 lanes of a pixel).  A tile whose window
 // exceeds WG_CAP slots adds each corner's row straight to global memory.
+// Timing ablations of warp_bwd_gather (tools/ab_build.sh -DWARP_ABL=mask; wrong results):
+// 1 no d(features) atomics (the sums still formed), 2 no d(flow) part.
+#ifndef WARP_ABL
+#define WARP_ABL 0
+#endif
 constexpr int WG_T = 8, WG_CAP = 1024, WG_NT = 256;
 int g_warp_win = 1;   // of_set_tuning key 7: warp_bwd_gather (1) or warp_bwd_agg (0)
 int g_corr_blk = 5;   // of_set_tuning key 9: bit 0 corr_fwd_blk (else corr_fwd_kernel), bit 1 corr_bwd_blk,
@@ -1388,7 +1400,11 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
           acc += __int_as_float(en.y) * dtile[en.x * 64 + lane];
         }
         const int yy = wy0 + k / wwx, xx = wx0 + k % wwx;
-        atomicAdd(dinp + (img + (int64_t)yy * w + xx) * c + cc + lane, acc);
+        if (WARP_ABL & 1) {
+          if (acc == 12345.f) dinp[0] = acc;             // keep the sum live
+        } else {
+          atomicAdd(dinp + (img + (int64_t)yy * w + xx) * c + cc + lane, acc);
+        }
       }
     } else {                                           // spread flows: one add per corner
       ent[tid] = make_int2(oke ? (ye * w + xe) : -1, __float_as_int(wte));
@@ -1403,7 +1419,7 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
   }
   // ---- flow gradient
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
+  for (int it = 0; it < (WARP_ABL & 2 ? 0 : IT); ++it) {
     const int pr = (it * (WG_NT / 64) + wave) * 4 + pg;
     const float a = ag[it], bq = bg[it];
     const float4 g = *reinterpret_cast<const float4*>(&dtile[pr * 64 + 4 * q]);
