@@ -4494,7 +4494,7 @@ static int g_wgrad_wgs = 4;
 // of_set_tuning key 23: the split 3x3 kernels' direct epilogues (conv_dev.h), bit 0 the
 // forward's (direct_fwd_f32), bit 1 the input gradient's (direct_dgrad_f32); a clear bit keeps
 // the per-pass transposes.  Default 1: the input gradient's measured slower (per layer dec3.c1
-// 0.506 -> 0.531 ms, c2 0.413 -> 0.426; fp32 step 651.8 -> 650.6 pairs/s, gpurun_out/misc6).
+// 0.506 -> 0.531 ms, c2 0.413 -> 0.426; fp32 step 651.8 -> 650.6 pairs/s, profiles/r4_late/step_ab.txt).
 static int g_x3_direct = 1;
 
 // of_set_tuning key 16: which bf16 implicit GEMMs (stride-2 block convs, 1x1 projections; the

@@ -247,7 +247,7 @@ def side_stream(*tensors):
 # fill the chip; the memory-bound df1 only slows them), bf16 B=32 1353 -> 1363 (round 2) and
 # 1422.7 / 1426.9 -> 1430.9 / 1435.9 (round 3, tools/gpu_r3q.sh).  Round 4 fused both
 # gradients into one kernel (corr_bwd_fused, main stream): bf16 B=32 side 1745.8 / 1745.3 ->
-# fused 1748.5 / 1750.8 (gpurun_out/misc4), and with the H/8 heads on images 1703.9 -> 1716.4
+# fused 1748.5 / 1750.8 (profiles/r4_late/step_ab.txt), and with the H/8 heads on images 1703.9 -> 1716.4
 # (misc5, a slower box): off for both precisions.  CORR_DF1_SIDE (env OFLOW_CORR_DF1_SIDE =
 # 0 / 1) forces it either way.
 _DF1_ENV = os.environ.get("OFLOW_CORR_DF1_SIDE")
@@ -991,7 +991,7 @@ def res_block(x, a: ConvLayer, b: ConvLayer, p: Optional[ConvLayer] = None):
 # B16I_MIN_TILES 16 x 32 tiles (the kernels take one K slice: smaller grids keep the halo
 # kernels with K splits); OFLOW_B16I=0 turns it off, OFLOW_B16I_MIN_TILES overrides the size.
 # 128 (round 4, with the fused cost-volume backward): the H/8 head at B = 32 (192 tiles) too,
-# bf16 B=32 1703.9 (256) -> 1716.4 (128) / 1712.0 (64) pairs/s, gpurun_out/misc5.
+# bf16 B=32 1703.9 (256) -> 1716.4 (128) / 1712.0 (64) pairs/s, profiles/r4_late/step_ab.txt.
 B16I = os.environ.get("OFLOW_B16I", "1") == "1"
 B16I_MIN_TILES = int(os.environ.get("OFLOW_B16I_MIN_TILES", "128"))
 # The forwards of the bf16-image heads write their outputs' act' signs (of_b16i_io mask_out)
