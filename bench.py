@@ -121,6 +121,7 @@ KIND_STEM_WG_B16 = 187  # conv_wgrad_stem_x3<1> (its bf16 weight gradient)
 
 
 HALO_B16 = {0: "128, 4, 2", 1: "96, 4, 2", 2: "64, 8, 1", 3: "32, 8, 1"}  # conv_halo_b16<BN, waves>
+HALO_PERSIST = False   # of_set_tuning key 24 = 1 (set from --tune in main)
 WGRAD_B16I = {0: "2, 4", 1: "4, 2", 2: "4, 1"}                          # conv_wgrad_b16i<waves>
 
 
@@ -158,9 +159,9 @@ def kind_name(kind):
 def kernel_symbol(kind):
     """rocprofv3 name of the conv kernel instance behind a timing kind."""
     mode, cfg, fam = kind_parts(kind)
-    if fam == "halo_b16":
-        return "void oflow::(anonymous namespace)::conv_halo_b16<%s, %d, 16, 32>(oflow::GemmArgs)" % (
-            HALO_B16[cfg], mode)
+    if fam == "halo_b16":    # last template argument: the persistent form (key 24, default off)
+        return ("void oflow::(anonymous namespace)::conv_halo_b16<%s, %d, 16, 32, %s>"
+                "(oflow::GemmArgs)" % (HALO_B16[cfg], mode, "true" if HALO_PERSIST else "false"))
     if fam == "wgrad_b16i":
         return "void oflow::(anonymous namespace)::conv_wgrad_b16i<%s>(oflow::GemmArgs)" % WGRAD_B16I[cfg]
     if fam == "stem_x3":
@@ -353,6 +354,9 @@ def main():
         for kv in args.tune.split(","):
             k, v = kv.split("=")
             _lib.lib().of_set_tuning(int(k), int(v))
+            if int(k) == 24:
+                global HALO_PERSIST
+                HALO_PERSIST = int(v) != 0
     from optical_flow_amd.data import synthetic_batch
     from optical_flow_amd.dist import init_from_env
     from optical_flow_amd.loss import LossLayer

@@ -116,6 +116,15 @@ def test_bench_kernel_symbols_match_pmc_keys():
         names.add(bench.kernel_symbol(kind))
     x3_keys = {k for k in keys if "_x3<" in k or "_x3b<" in k}
     assert x3_keys and x3_keys <= names, sorted(x3_keys - names)
+    # the bf16 image kernels (conv_b16i.hip; their template also carries the persistent flag)
+    b16i = set()
+    for mode in (0, 1):
+        for cfg in bench.HALO_B16:
+            b16i.add(bench.kernel_symbol(288 + mode * 8 + cfg))
+    for cfg in bench.WGRAD_B16I:
+        b16i.add(bench.kernel_symbol(304 + cfg))
+    b16i_keys = {k for k in keys if "conv_halo_b16<" in k or "conv_wgrad_b16i<" in k}
+    assert b16i_keys and b16i_keys <= b16i, sorted(b16i_keys - b16i)
 
 
 def test_draw_all_arrows_geometry():
