@@ -782,6 +782,12 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #ifndef X3_EPB
 #define X3_EPB 1
 #endif
+// tile_x3_body's 4-wave split form recomputes its halo slot offsets per chunk (1) instead of
+// keeping them live (0: the round-3 form, 14-16 VGPRs spilled to scratch and reloaded at every
+// chunk's halo store behind a vmcnt(0)); -DX3_HREC=0 builds the old form for A/B timing
+#ifndef X3_HREC
+#define X3_HREC 1
+#endif
 
 
 // PF (of_set_tuning key 20, default 1): the MFMA loop's fragments read one sub-step ahead.
@@ -1117,24 +1123,44 @@ __device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
   const rsrc_t rb_src = make_rsrc(a.B, a.b_bytes);
 
   // ---- halo slots: quad (q & 7) of halo pixel (q >> 3)
-  int h_off[HS];
+  float4 hv[HS];
+  // HREC (the 4-wave split form): the slot offsets recomputed per chunk from a lane index made
+  // opaque there, instead of HS offsets live through the main loop (that form spilled)
+  constexpr bool HREC = X3_HREC && NT == 256 && NP == 3;
+  int h_off[HREC ? 1 : HS];
   unsigned h_ok = 0;
   const int hcq = tid & 7;
-#pragma unroll
-  for (int j = 0; j < HS; ++j) {
-    const int q = tid + NT * j;
+  auto halo_slot = [&](int t, int j, bool& ok) {
+    const int q = t + NT * j;
     const int hp = q >> 3;
     const int sy = hy0 + hp / HW, sx = hx0 + hp % HW;
-    const bool ok = q < HQ && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
-    h_off[j] = ok ? (((b * SH + sy) * SW + sx) * a.lda + 4 * hcq) * 4 : 0;
-    h_ok |= (ok ? 1u : 0u) << j;
+    ok = q < HQ && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+    return ok ? (((b * SH + sy) * SW + sx) * a.lda + 4 * (t & 7)) * 4 : 0;
+  };
+  if constexpr (!HREC) {
+#pragma unroll
+    for (int j = 0; j < HS; ++j) {
+      bool ok;
+      h_off[j] = halo_slot(tid, j, ok);
+      h_ok |= (ok ? 1u : 0u) << j;
+    }
   }
-  float4 hv[HS];
   auto load_halo = [&](int c) {
     const bool cok = 32 * c + 4 * hcq < a.kc;
+    if constexpr (HREC) {
+      int t = tid;
+      asm volatile("" : "+v"(t));
 #pragma unroll
-    for (int j = 0; j < HS; ++j)
-      hv[j] = bload4(ra_src, cok && ((h_ok >> j) & 1) ? (uint32_t)(h_off[j] + 128 * c) : kOOB);
+      for (int j = 0; j < HS; ++j) {
+        bool ok;
+        const int off = halo_slot(t, j, ok);
+        hv[j] = bload4(ra_src, cok && ok ? (uint32_t)(off + 128 * c) : kOOB);
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < HS; ++jj)
+        hv[jj] = bload4(ra_src, cok && ((h_ok >> jj) & 1) ? (uint32_t)(h_off[jj] + 128 * c) : kOOB);
+    }
   };
   auto store_halo = [&]() {
 #pragma unroll

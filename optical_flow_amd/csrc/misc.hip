@@ -273,14 +273,17 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
         }
       }
       const float4 d = *reinterpret_cast<const float4*>(dyp + p * c + ch);
-      // first maximum per channel
+      // first maximum per channel (the running maxima kept as values: indexing yv by the
+      // running argmax made the arrays dynamically indexed, and the compiler put them in LDS
+      // with a wait after every load -- four serial memory round trips per pooled pixel)
       int bx = 0, by = 0, bz = 0, bw = 0;
+      float4 mx = yv[0];
 #pragma unroll
       for (int k = 1; k < 4; ++k) {
-        if (yv[k].x > yv[bx].x) bx = k;
-        if (yv[k].y > yv[by].y) by = k;
-        if (yv[k].z > yv[bz].z) bz = k;
-        if (yv[k].w > yv[bw].w) bw = k;
+        if (yv[k].x > mx.x) bx = k, mx.x = yv[k].x;
+        if (yv[k].y > mx.y) by = k, mx.y = yv[k].y;
+        if (yv[k].z > mx.z) bz = k, mx.z = yv[k].z;
+        if (yv[k].w > mx.w) bw = k, mx.w = yv[k].w;
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
