@@ -348,12 +348,6 @@ int of_fill(float* y, float v, int64_t n, void* stream);
  * device scope only (the side-stream forks and joins of the backward; torch's
  * Stream.wait_stream records a default event).  Works inside a stream capture. */
 int of_stream_wait(void* waiter, void* signaller);
-/* A stream whose kernels may use all CUs but `withhold` of them (hipExtStreamCreateWithCUMask;
- * the withheld CUs spread over the device): the side stream of the weight gradients, so the
- * main stream's short kernels find free CUs while a side-stream kernel holds the rest
- * (ops.SIDE_CU_WITHHOLD).  Destroy with of_stream_destroy. */
-int of_stream_create_cu_masked(int withhold, void** stream);
-int of_stream_destroy(void* stream);
 
 /* Per-launch timing of the conv kernels (bench instrumentation): when enabled (on = 1), every
  * conv launch records a hipEvent pair on its stream; on = 2 times the next conv launch only

@@ -126,8 +126,6 @@ PROTOTYPES = {
     "of_copy_strided": (I, [P, I, P, I, I64, I, P]),
     "of_fill": (I, [P, F, I64, P]),
     "of_stream_wait": (I, [P, P]),
-    "of_stream_create_cu_masked": (I, [I, C.POINTER(C.c_void_p)]),
-    "of_stream_destroy": (I, [P]),
     "of_timing_enable": (I, [I]),
     "of_set_tuning": (I, [I, I]),
     "of_timing_read": (I, [I, C.POINTER(I), C.POINTER(C.c_double), C.POINTER(F)]),

@@ -131,31 +131,6 @@ int of_same_pads(int n, int k, int s, int* before, int* after, int* out) {
   return OF_OK;
 }
 
-int of_stream_create_cu_masked(int withhold, void** stream) {
-  OF_CHECK_ARG(stream, "stream_create_cu_masked: NULL out pointer");
-  const int n = device_cus();
-  OF_CHECK_ARG(withhold >= 0 && withhold < n, "stream_create_cu_masked: 0 <= withhold < CUs");
-  // withhold every (n / withhold)-th CU index, so the free ones spread over the XCDs
-  std::vector<uint32_t> mask((n + 31) / 32, 0u);
-  const int step = withhold > 0 ? n / withhold : n + 1;
-  int kept = 0;
-  for (int i = 0; i < n; ++i) {
-    const bool free_cu = withhold > 0 && i % step == step - 1 && (i / step) < withhold;
-    if (!free_cu) mask[i / 32] |= 1u << (i % 32), ++kept;
-  }
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess)
-    return check_launch("stream_create_cu_masked: hipExtStreamCreateWithCUMask");
-  *stream = s;
-  return kept > 0 ? OF_OK : fail(OF_EINVAL, "stream_create_cu_masked: no CU left");
-}
-
-int of_stream_destroy(void* stream) {
-  if (stream && hipStreamDestroy(static_cast<hipStream_t>(stream)) != hipSuccess)
-    return check_launch("stream_destroy");
-  return OF_OK;
-}
-
 int of_stream_wait(void* waiter, void* signaller) {
   OF_CHECK_ARG(waiter != signaller, "stream_wait: waiter and signaller are one stream");
   int dev = 0;

@@ -252,6 +252,59 @@ __device__ __forceinline__ void epilogue_rows4(const GemmArgs& a, int split, con
   }
 }
 
+// epilogue_rows4 for rows and a column clamped into the tensors (row[r] always a valid pixel,
+// nl = min(n, N - 4)): every residual / activation-source quad is loaded unconditionally, all
+// of them before the first store, and only the stores are masked by ok -- a guarded load per
+// row was compiled to a branch and a wait per row (the loads reuse the address registers).
+template <int MODE, int R>
+__device__ __forceinline__ void epilogue_rows4c(const GemmArgs& a, int split, const int64_t* row,
+                                                unsigned ok, int n, int nl, const float4* v) {
+  if (a.splits > 1) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if ((ok >> r) & 1)
+        *reinterpret_cast<float4*>(&a.slab[(int64_t)split * a.split_stride + row[r] * a.slab_ld + n]) = v[r];
+    return;
+  }
+  float4 s4[R], r4[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) s4[r] = make_float4(1.f, 1.f, 1.f, 1.f), r4[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (MODE == MODE_DGRAD && a.act_src) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) s4[r] = *reinterpret_cast<const float4*>(&a.act_src[row[r] * a.ld_act + nl]);
+  }
+  if (a.res) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) r4[r] = *reinterpret_cast<const float4*>(&a.res[row[r] * a.ldr + nl]);
+  }
+  if (MODE == MODE_FWD) {
+    float bias[4], scale[4], shift[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) column_params<MODE>(a, nl + e, bias[e], scale[e], shift[e]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (!((ok >> r) & 1)) continue;
+      float x[4] = {v[r].x + bias[0], v[r].y + bias[1], v[r].z + bias[2], v[r].w + bias[3]};
+      if (a.z) *reinterpret_cast<float4*>(&a.z[row[r] * a.ldz + n]) = make_float4(x[0], x[1], x[2], x[3]);
+      const float rr[4] = {r4[r].x, r4[r].y, r4[r].z, r4[r].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (a.bn_g) x[e] = x[e] * scale[e] + shift[e];
+        x[e] = act_fwd(x[e] + rr[e], a.act, a.alpha);
+      }
+      *reinterpret_cast<float4*>(&a.C[row[r] * a.ldc + n]) = make_float4(x[0], x[1], x[2], x[3]);
+    }
+  } else if (MODE == MODE_DGRAD) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (!((ok >> r) & 1)) continue;
+      *reinterpret_cast<float4*>(&a.C[row[r] * a.ldc + n]) =
+          make_float4(dgrad_ep(a, v[r].x, s4[r].x, r4[r].x), dgrad_ep(a, v[r].y, s4[r].y, r4[r].y),
+                      dgrad_ep(a, v[r].z, s4[r].z, r4[r].z), dgrad_ep(a, v[r].w, s4[r].w, r4[r].w));
+    }
+  }
+}
+
 // One wave's 32 x 32 accumulator block in the v_mfma_f32_32x32x* layout (column lane & 31,
 // rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) through a private 4 KB LDS image E, back as
 // float4 rows: f(row 0..31, column quad 0..7, value) for the 4 rows x 1 quad each lane owns.

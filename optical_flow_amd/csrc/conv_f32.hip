@@ -775,12 +775,17 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #ifndef X3_BDMA
 #define X3_BDMA 1
 #endif
-// tile_x3_body's 16-byte epilogue: rows per epilogue_rows4 batch (1: one row per
-// epilogue_store4, the round-2 form)
-// (4 measured -0.3 % on the fp32 step and -1-4 % on dgrad per layer: the stores, not the aux
-// loads, bound that epilogue with one workgroup per CU)
+// tile_x3_body's 16-byte epilogue: rows per epilogue_rows4c batch (1: one row per
+// epilogue_store4, the round-2 form).  (Round 2 measured 4 at -0.3 % on the fp32 step, but
+// with guarded loads that the compiler still waited for one by one; round 4 batches them
+// unguarded, epilogue_rows4c.)
 #ifndef X3_EPB
 #define X3_EPB 1
+#endif
+// conv_tile_bf16's 16-byte epilogue: each 32 x 32 block's 4 rows per lane through
+// epilogue_rows4c (1) or one row at a time (0, the round-2 form; A/B builds)
+#ifndef TB16_EPC
+#define TB16_EPC 1
 #endif
 // tile_x3_body's 4-wave split form recomputes its halo slot offsets per chunk (1) instead of
 // keeping them live (0: the round-3 form, 14-16 VGPRs spilled to scratch and reloaded at every
@@ -984,7 +989,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES
 
   // ---- epilogue
   const int64_t img = (int64_t)b * OH * OW;
-  if (a.vec_ep) {   // 16-byte rows through LDS (the loop's last barrier freed the images)
+  if (a.vec_ep && !TB16_EPC) {   // the round-2 form (one row at a time), for A/B builds
     float* E = reinterpret_cast<float*>(smem) + wave * 1024;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -996,6 +1001,32 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES
           if (oy < OH && ox < OW && n < a.N)
             epilogue_store4<MODE>(a, split, img + (int64_t)oy * OW + ox, n, v);
         });
+    return;
+  }
+  if (a.vec_ep) {   // 16-byte rows through LDS (the loop's last barrier freed the images)
+    float* E = reinterpret_cast<float*>(smem) + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        // the block's 4 rows per lane through epilogue_rows4: their residual / activation-
+        // source quads are loaded before the first store (one row at a time, each row's load
+        // sat behind a branch and waited: 4 TM TN serial memory round trips per tile)
+        float4 vv[4];
+        int64_t rows[4];
+        unsigned ok = 0;
+        int ncol = 0;
+        transpose32(E, acc[i][j], lane, [&](int row, int c4, float4 v) {
+          const int q = row >> 3;
+          const int mt = wm0 + 32 * i + row, n = n0 + wn0 + 32 * j + 4 * c4;
+          const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
+          rows[q] = img + (int64_t)min(oy, OH - 1) * OW + min(ox, OW - 1);
+          ok |= (oy < OH && ox < OW && n < a.N ? 1u : 0u) << q;
+          vv[q] = v;
+          ncol = n;
+        });
+        epilogue_rows4c<MODE, 4>(a, split, rows, ok, ncol, min(ncol, a.N - 4), vv);
+      }
     return;
   }
 #pragma unroll
@@ -1393,10 +1424,10 @@ __device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
             v[g] = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
             const int mt = wm0 + m;
             const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
-            row[g] = img + (int64_t)oy * OW + ox;
+            row[g] = img + (int64_t)min(oy, OH - 1) * OW + min(ox, OW - 1);   // clamped: loads
             ok |= (oy < OH && ox < OW && n < a.N ? 1u : 0u) << g;
           }
-          epilogue_rows4<MODE, X3_EPB>(a, split, row, ok, n, v);
+          epilogue_rows4c<MODE, X3_EPB>(a, split, row, ok, n, min(n, a.N - 4), v);
         }
       } else {
 #pragma unroll

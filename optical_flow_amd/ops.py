@@ -220,22 +220,6 @@ def comm_stream(*tensors):
     return s
 
 
-# SIDE_CU_WITHHOLD (env OFLOW_SIDE_CU_WITHHOLD): CUs the wgrad side stream's kernels may not
-# use (of_stream_create_cu_masked), so the main stream's short kernels are not queued behind
-# a side-stream kernel holding every CU's registers (the bf16 trace: a 20 µs upscale backward
-# took 106 µs beside conv_wgrad_b16i).  0 (default): an ordinary stream.
-SIDE_CU_WITHHOLD = int(os.environ.get("OFLOW_SIDE_CU_WITHHOLD", "0"))
-
-
-def _new_side_stream(device):
-    if SIDE_CU_WITHHOLD <= 0:
-        return torch.cuda.Stream(device)
-    h = C.c_void_p()
-    with torch.cuda.device(device):
-        call("of_stream_create_cu_masked", SIDE_CU_WITHHOLD, C.byref(h))
-    return torch.cuda.ExternalStream(h.value, device=device)
-
-
 def side_stream(*tensors):
     """The wgrad side stream of the current device, ordered after all work enqueued so far on
     the current stream; ``tensors`` (read by the side stream's kernels) are marked in use by
@@ -244,7 +228,7 @@ def side_stream(*tensors):
     cur = torch.cuda.current_stream()
     s = _SIDE.get(cur.device)
     if s is None:
-        s = _SIDE[cur.device] = _new_side_stream(cur.device)
+        s = _SIDE[cur.device] = torch.cuda.Stream(cur.device)
     stream_wait(s, cur)
     for t in tensors:
         if t is not None:
