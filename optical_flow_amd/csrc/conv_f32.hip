@@ -685,18 +685,46 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_bf16(GemmArgs a) {
     float* E = reinterpret_cast<float*>(smem) + wave * 1024;
     float* S = a.slab + (int64_t)split * a.split_stride;
     const int row_base = G.tiles_begin * BM;
+    if constexpr (!EPC_BATCH) {        // the round-2 form (one row at a time), for A/B builds
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          transpose32(E, acc[i][j], lane, [&](int row, int c4, float4 v) {
+            const int m = m0 + wm0 + 32 * i + row, n = n0 + wn0 + 32 * j + 4 * c4;
+            if (m >= M || n >= a.N) return;
+            if (a.splits > 1)
+              *reinterpret_cast<float4*>(&S[(int64_t)(row_base + m) * a.slab_ld + n]) = v;
+            else
+              epilogue_store4<MODE>(a, 0, out_row(a, G, m), n, v);
+          });
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j) {
+        // one 32 x 32 block's 4 rows per lane through epilogue_rows4c (the aux quads loaded
+        // before the first store; row by row each load waited behind its row's guard)
+        float4 vv[4];
+        int64_t rows[4];
+        unsigned ok = 0;
+        int ncol = 0;
         transpose32(E, acc[i][j], lane, [&](int row, int c4, float4 v) {
+          const int q = row >> 3;
           const int m = m0 + wm0 + 32 * i + row, n = n0 + wn0 + 32 * j + 4 * c4;
-          if (m >= M || n >= a.N) return;
-          if (a.splits > 1)
-            *reinterpret_cast<float4*>(&S[(int64_t)(row_base + m) * a.slab_ld + n]) = v;
-          else
-            epilogue_store4<MODE>(a, 0, out_row(a, G, m), n, v);
+          if (a.splits > 1) {
+            if (m < M && n < a.N)
+              *reinterpret_cast<float4*>(&S[(int64_t)(row_base + m) * a.slab_ld + n]) = v;
+            return;
+          }
+          rows[q] = out_row(a, G, min(m, M - 1));
+          ok |= (m < M && n < a.N ? 1u : 0u) << q;
+          vv[q] = v;
+          ncol = n;
         });
+        if (a.splits == 1) epilogue_rows4c<MODE, 4>(a, 0, rows, ok, ncol, min(ncol, a.N - 4), vv);
+      }
     return;
   }
   if (a.splits > 1) {
@@ -782,10 +810,10 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #ifndef X3_EPB
 #define X3_EPB 1
 #endif
-// conv_tile_bf16's 16-byte epilogue: each 32 x 32 block's 4 rows per lane through
-// epilogue_rows4c (1) or one row at a time (0, the round-2 form; A/B builds)
-#ifndef TB16_EPC
-#define TB16_EPC 1
+// The 16-byte epilogues of conv_tile_bf16, conv_gemm_bf16 and conv_gemm_x3: rows in groups
+// through epilogue_rows4c (1) or one row at a time (0, the round-2 form; A/B builds)
+#ifndef EPC_BATCH
+#define EPC_BATCH 1
 #endif
 // tile_x3_body's 4-wave split form recomputes its halo slot offsets per chunk (1) instead of
 // keeping them live (0: the round-3 form, 14-16 VGPRs spilled to scratch and reloaded at every
@@ -989,7 +1017,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES
 
   // ---- epilogue
   const int64_t img = (int64_t)b * OH * OW;
-  if (a.vec_ep && !TB16_EPC) {   // the round-2 form (one row at a time), for A/B builds
+  if (a.vec_ep && !EPC_BATCH) {   // the round-2 form (one row at a time), for A/B builds
     float* E = reinterpret_cast<float*>(smem) + wave * 1024;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1946,16 +1974,46 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NP == 1 ? 2 : 1) void conv_
     constexpr int LPR = WN / 4, RPI = 64 / LPR;
     const int c4 = lane % LPR, rr = lane / LPR;
     const int n = n0 + wn0 + 4 * c4;
+    if (a.splits > 1) {
 #pragma unroll
-    for (int q = 0; q < WM / RPI; ++q) {
-      const int ml = q * RPI + rr;
-      const int m = m0 + wm0 + ml;
-      const float4 v = *reinterpret_cast<const float4*>(&E[ml * WN + 4 * c4]);
-      if (m >= M || n >= a.N) continue;
-      if (a.splits > 1)
+      for (int q = 0; q < WM / RPI; ++q) {
+        const int ml = q * RPI + rr;
+        const int m = m0 + wm0 + ml;
+        const float4 v = *reinterpret_cast<const float4*>(&E[ml * WN + 4 * c4]);
+        if (m >= M || n >= a.N) continue;
         *reinterpret_cast<float4*>(&S[(int64_t)(row_base + m) * a.slab_ld + n]) = v;
-      else
+      }
+      return;
+    }
+    // rows in groups of GR through epilogue_rows4c: each group's residual / activation-source
+    // quads loaded before its first store (row by row, every load sat behind the row's guard
+    // and waited: WM / RPI serial memory round trips per wave)
+    if constexpr (!EPC_BATCH) {        // the round-2 form, for A/B builds
+#pragma unroll
+      for (int q = 0; q < WM / RPI; ++q) {
+        const int ml = q * RPI + rr;
+        const int m = m0 + wm0 + ml;
+        const float4 v = *reinterpret_cast<const float4*>(&E[ml * WN + 4 * c4]);
+        if (m >= M || n >= a.N) continue;
         epilogue_store4<MODE>(a, 0, out_row(a, G, m), n, v);
+      }
+      return;
+    }
+    constexpr int NQ = WM / RPI, GR = NQ % 4 == 0 ? 4 : NQ % 2 == 0 ? 2 : 1;
+#pragma unroll
+    for (int q0 = 0; q0 < NQ; q0 += GR) {
+      float4 v[GR];
+      int64_t row[GR];
+      unsigned ok = 0;
+#pragma unroll
+      for (int g = 0; g < GR; ++g) {
+        const int ml = (q0 + g) * RPI + rr;
+        const int m = m0 + wm0 + ml;
+        v[g] = *reinterpret_cast<const float4*>(&E[ml * WN + 4 * c4]);
+        row[g] = out_row(a, G, min(m, M - 1));           // clamped: the loads stay in range
+        ok |= (m < M && n < a.N ? 1u : 0u) << g;
+      }
+      epilogue_rows4c<MODE, GR>(a, 0, row, ok, n, min(n, a.N - 4), v);
     }
     return;
   }

@@ -13,7 +13,7 @@ case $rc in 0) ;; *) exit 1;; esac
 timeout -k 10 300 python tools/conv_bench.py > $O/conv_f32.txt 2>&1 || exit 1
 OFLOW_LIB=optical_flow_amd/_build/ab_epb4/liboflow.so timeout -k 10 300 python tools/conv_bench.py > $O/conv_f32_epb4.txt 2>&1 || exit 1
 timeout -k 10 300 python tools/conv_bench.py --bf16 > $O/conv_bf16.txt 2>&1 || exit 1
-OFLOW_LIB=optical_flow_amd/_build/ab_tb0/liboflow.so timeout -k 10 300 python tools/conv_bench.py --bf16 > $O/conv_bf16_tb0.txt 2>&1 || exit 1
+OFLOW_LIB=optical_flow_amd/_build/ab_epc0/liboflow.so timeout -k 10 300 python tools/conv_bench.py --bf16 > $O/conv_bf16_epc0.txt 2>&1 || exit 1
 echo conv ok
-bash tools/gpu_ab.sh $O/ab 2 'f|OFLOW_MAIN_PRIO=0|' 'fepb4|OFLOW_LIB=optical_flow_amd/_build/ab_epb4/liboflow.so|' \
-  'b|OFLOW_MAIN_PRIO=0|--precision bf16 --batch 32' 'btb0|OFLOW_LIB=optical_flow_amd/_build/ab_tb0/liboflow.so|--precision bf16 --batch 32'
+bash tools/gpu_ab.sh $O/ab 2 'f|OFLOW_MAIN_PRIO=0|' 'fepb4|OFLOW_LIB=optical_flow_amd/_build/ab_epb4/liboflow.so|' 'fepc0|OFLOW_LIB=optical_flow_amd/_build/ab_epc0/liboflow.so|' \
+  'b|OFLOW_MAIN_PRIO=0|--precision bf16 --batch 32' 'bepc0|OFLOW_LIB=optical_flow_amd/_build/ab_epc0/liboflow.so|--precision bf16 --batch 32'
