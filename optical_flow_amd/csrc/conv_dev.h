@@ -9,6 +9,13 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+// The 16-byte epilogues of conv_tile_bf16, conv_gemm_bf16 and conv_gemm_x3 (conv_f32.hip):
+// rows in groups through epilogue_rows4c (1) or one row at a time (0, the round-2 form; A/B
+// builds)
+#ifndef EPC_BATCH
+#define EPC_BATCH 1
+#endif
 constexpr int BK = 16;
 constexpr int MAX_GROUPS = 4;
 

@@ -810,11 +810,7 @@ constexpr int X3_TH0 = OF_X3_TH0;   // conv_tile_x3 BN = 128 tiles: X3_TH0 rows 
 #ifndef X3_EPB
 #define X3_EPB 1
 #endif
-// The 16-byte epilogues of conv_tile_bf16, conv_gemm_bf16 and conv_gemm_x3: rows in groups
-// through epilogue_rows4c (1) or one row at a time (0, the round-2 form; A/B builds)
-#ifndef EPC_BATCH
-#define EPC_BATCH 1
-#endif
+
 // tile_x3_body's 4-wave split form recomputes its halo slot offsets per chunk (1) instead of
 // keeping them live (0: the round-3 form, 14-16 VGPRs spilled to scratch and reloaded at every
 // chunk's halo store behind a vmcnt(0)); -DX3_HREC=0 builds the old form for A/B timing
