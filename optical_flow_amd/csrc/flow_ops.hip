@@ -226,16 +226,6 @@ struct CorrBlkArgs {
   int tiles_x, tiles_y, items;
 };
 
-// corr_fwd_blk's bf16 concat epilogue in whole 16-byte chunks (1) or per element (0, the
-// first form; A/B builds)
-#ifndef CAT16_CHUNK
-#define CAT16_CHUNK 1
-#endif
-
-__device__ __forceinline__ __bf16* o16_base(const CorrFwdArgs& a) {
-  return reinterpret_cast<__bf16*>(a.cat16);
-}
-
 template <bool VEC>
 __global__ __launch_bounds__(CB_NT, 2) void corr_fwd_blk(CorrBlkArgs p) {
   __shared__ float4 lds4[(CB_LDS_HALO + CB_LDS_F1) / 4];
@@ -372,53 +362,6 @@ __global__ __launch_bounds__(CB_NT, 2) void corr_fwd_blk(CorrBlkArgs p) {
         for (int j = 0; j < 7; ++j)
           hal[(cty * CB_X + ctx + m) * 49 + oi * 7 + j] = acc[m * 7 + j].x + acc[m * 7 + j].y;
       __syncthreads();
-      if (CAT16_CHUNK && a.cat16 && (a.c & 7) == 0 && (a.ld16 & 7) == 0) {
-        // bf16 image, channels c .. ld16 of each pixel (cv, flow, zero padding) as whole
-        // 16-byte chunks, 4 per thread in flight; the flows loaded first, unguarded (pixels
-        // clamped into the image).  (The per-element form below wrote 2-byte pieces, one
-        // pixel's padding per thread, and waited for each pixel's flow load.)
-        const int cpp = (a.ld16 - a.c) >> 3, nchunk = CB_PIX * cpp;
-        for (int t0 = 0; t0 < nchunk; t0 += 4 * CB_NT) {
-          float2 fl[4];
-          int64_t pls[4];
-          int pps[4], js[4];
-          bool oks[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int t = min(t0 + tid + u * CB_NT, nchunk - 1);
-            const int pp = t / cpp, j = t - pp * cpp;
-            const int sy = y0 + pp / CB_X, sx = x0 + pp % CB_X;
-            oks[u] = t0 + tid + u * CB_NT < nchunk && sy < h && sx < w;
-            pls[u] = img + (int64_t)min(sy, h - 1) * w + min(sx, w - 1);
-            pps[u] = pp, js[u] = j;
-            fl[u] = a.flow ? *reinterpret_cast<const float2*>(a.flow + 2 * pls[u])
-                           : make_float2(0.f, 0.f);
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-            bf16x8_t v;
-            float cv[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) cv[e] = hal[pps[u] * 49 + min(8 * js[u] + e, 48)];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(cv[e]));   // reads unguarded
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int k = 8 * js[u] + e;
-              const float x = k < 49 ? cv[e]
-                              : a.flow && k == 49 ? fl[u].x : a.flow && k == 50 ? fl[u].y : 0.f;
-              v[e] = (__bf16)x;
-            }
-            if (oks[u])
-              *reinterpret_cast<bf16x8_t*>(o16_base(a) + pls[u] * a.ld16 + a.c + 8 * js[u]) = v;
-          }
-        }
-        __syncthreads();
-        if (!more) break;
-        lt = nlt, it = nit, s = ns;
-        continue;
-      }
       if (a.cat16) {                               // bf16 image: cv, flow, zero padding
         __bf16* o16 = reinterpret_cast<__bf16*>(a.cat16);
         for (int q = tid; q < CB_PIX * 49; q += CB_NT) {
