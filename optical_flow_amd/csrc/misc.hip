@@ -18,11 +18,6 @@ namespace oflow {
 #ifndef MPB_UNROLL
 #define MPB_UNROLL 2   // the stem's max-pool + BN backward: 2 pooled pixels (18 float4 loads) in flight
 #endif
-// the stem's max-pool + BN backward workgroups: 512 (the BN reductions' count) left it at 8
-// waves per CU and ~2 TB/s, each thread walking ~100 pooled pixels two at a time
-#ifndef MPB_BLOCKS
-#define MPB_BLOCKS 2048
-#endif
 constexpr int RED_TARGET_BLOCKS = RED_BLOCKS;
 
 struct RedGeo {
@@ -32,14 +27,14 @@ struct RedGeo {
   int64_t ppb;  // pixels per workgroup (multiple of rows)
 };
 
-inline RedGeo red_geo(int64_t npix, int c, int target_blocks = RED_TARGET_BLOCKS) {
+inline RedGeo red_geo(int64_t npix, int c) {
   RedGeo g;
   const int cq = (c + 3) / 4;
   g.qw = 1;
   while (g.qw < cq && g.qw < 64) g.qw <<= 1;
   g.rows = 256 / g.qw;
   const int64_t min_ppb = (int64_t)g.rows * 8;
-  int64_t nb = std::min<int64_t>(target_blocks, cdiv(npix, min_ppb));
+  int64_t nb = std::min<int64_t>(RED_TARGET_BLOCKS, cdiv(npix, min_ppb));
   nb = std::max<int64_t>(nb, 1);
   g.ppb = round_up(cdiv(npix, nb), g.rows);
   g.nblk = (int)cdiv(npix, g.ppb);
@@ -657,8 +652,7 @@ int of_min_abs_segments(const float* const* dev_ptrs, const int* dev_lens, int n
 }
 
 size_t of_maxpool_bn_act_bwd_workspace(int n, int h, int w, int c) {
-  return (size_t)red_geo((int64_t)n * (h / 2) * (w / 2), c, MPB_BLOCKS).nblk * 2 * c *
-         sizeof(float);
+  return of_bn_act_bwd_workspace((int64_t)n * (h / 2) * (w / 2), c);
 }
 
 int of_maxpool_bn_act_bwd(int n, int h, int w, int c, const float* dyp, const float* g,
@@ -674,7 +668,7 @@ int of_maxpool_bn_act_bwd(int n, int h, int w, int c, const float* dyp, const fl
                "maxpool_bn_act_bwd: 16-byte alignment");
   hipStream_t s = as_stream(stream);
   const int64_t npix = (int64_t)n * (h / 2) * (w / 2);
-  const RedGeo geo = red_geo(npix, c, MPB_BLOCKS);
+  const RedGeo geo = red_geo(npix, c);
   float* part = static_cast<float*>(workspace);
   hipLaunchKernelGGL(maxpool_bn_act_bwd_partial<false>, dim3(geo.nblk, cdiv(c / 4, geo.qw)),
                      dim3(256), 0, s, npix, h, w, c, dyp, g, y, z, gamma, nullptr, mean, var, eps,
@@ -721,7 +715,7 @@ int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const f
                "maxpool_bn_relu_bwd: 16-byte alignment");
   hipStream_t s = as_stream(stream);
   const int64_t npix = (int64_t)n * (h / 2) * (w / 2);
-  const RedGeo geo = red_geo(npix, c, MPB_BLOCKS);
+  const RedGeo geo = red_geo(npix, c);
   float* part = static_cast<float*>(workspace);
   hipLaunchKernelGGL(maxpool_bn_act_bwd_partial<true>, dim3(geo.nblk, cdiv(c / 4, geo.qw)),
                      dim3(256), 0, s, npix, h, w, c, dyp, g, y, nullptr, gamma, beta, nullptr,
