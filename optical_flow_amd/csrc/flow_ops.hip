@@ -1223,6 +1223,27 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
 #ifndef WARP_ABL
 #define WARP_ABL 0
 #endif
+#ifndef WARP_WPE
+#define WARP_WPE
+#endif
+#ifndef WARP_PV_GROUP
+#define WARP_PV_GROUP 2
+#endif
+#ifndef WARP_LATE_PV
+#define WARP_LATE_PV 2
+#endif
+// the flow gradient's corner rows: pv[it][k] = inp row of corner k of pixel group it (lanes
+// = 16 channel quads x 4 pixels)
+#define warp_corner_rows(I0_, I1_)                                                              \
+  _Pragma("unroll") for (int i_ = (I0_); i_ < (I1_); ++i_) {                                   \
+    const float2 f = okg[i_] ? fg[i_] : make_float2(0.f, 0.f);                                 \
+    int y0, y1, x0, x1;                                                                        \
+    float a_, b_;                                                                              \
+    corners(pixg[i_] / w, pixg[i_] % w, f, y0, y1, x0, x1, a_, b_);                            \
+    const int ys[4] = {y0, y1, y0, y1}, xs[4] = {x0, x0, x1, x1};                              \
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) pv[i_][k] =                                  \
+        *reinterpret_cast<const float4*>(inp + (img + (int64_t)ys[k] * w + xs[k]) * c + cc + 4 * q); \
+  }
 constexpr int WG_T = 8, WG_CAP = 1024, WG_NT = 256;
 int g_warp_win = 1;   // of_set_tuning key 7: warp_bwd_gather (1) or warp_bwd_agg (0)
 int g_corr_blk = 5;   // of_set_tuning key 9: bit 0 corr_fwd_blk (else corr_fwd_kernel), bit 1 corr_bwd_blk,
@@ -1237,7 +1258,7 @@ __device__ __forceinline__ float row16_sum(float v) {   // sum over the 16 lanes
   return v;                                              // row_ror 8, 4, 2, 1
 }
 
-__global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict__ dout,
+__global__ __launch_bounds__(WG_NT) WARP_WPE void warp_bwd_gather(const float* __restrict__ dout,
                                                          const float* __restrict__ inp, int n,
                                                          int h, int w, int c,
                                                          const float* __restrict__ flow,
@@ -1287,12 +1308,12 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
   const int q = lane & 15, pg = lane >> 4;
   const int pe = tid >> 2, ke = tid & 3;               // this thread's (pixel, corner) entry
   bool okg[IT], oke;
-  int64_t pixg[IT];
+  int pixg[IT];                                        // pixel index within the image
   float2 fg[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    pixg[it] = tile_pix((it * (WG_NT / 64) + wave) * 4 + pg, okg[it]);
-    fg[it] = *reinterpret_cast<const float2*>(flow + 2 * pixg[it]);
+    pixg[it] = (int)(tile_pix((it * (WG_NT / 64) + wave) * 4 + pg, okg[it]) - img);
+    fg[it] = *reinterpret_cast<const float2*>(flow + 2 * (img + pixg[it]));
   }
   const int64_t pxe = tile_pix(pe, oke);
   const float2 fe = *reinterpret_cast<const float2*>(flow + 2 * pxe);
@@ -1306,21 +1327,13 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
   float fax[IT], fay[IT];                              // dfa (passes == 1 only; else unused)
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    fax[it] = dfa ? dfa[pixg[it] * ldfa] : 0.f;
-    fay[it] = dfa ? dfa[pixg[it] * ldfa + 1] : 0.f;
+    fax[it] = dfa ? dfa[(img + pixg[it]) * ldfa] : 0.f;
+    fay[it] = dfa ? dfa[(img + pixg[it]) * ldfa + 1] : 0.f;
   }
-  float ag[IT], bg[IT];
+#if !WARP_LATE_PV
   float4 pv[IT][4];
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const float2 f = okg[it] ? fg[it] : make_float2(0.f, 0.f);
-    int y0, y1, x0, x1;
-    corners((int)(pixg[it] - img) / w, (int)((pixg[it] - img) % w), f, y0, y1, x0, x1, ag[it], bg[it]);
-    const int ys[4] = {y0, y1, y0, y1}, xs[4] = {x0, x0, x1, x1};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      pv[it][k] = *reinterpret_cast<const float4*>(inp + (img + (int64_t)ys[k] * w + xs[k]) * c + cc + 4 * q);
-  }
+  warp_corner_rows(0, IT);
+#endif
   int ye = 0, xe = 0;
   float wte = 0.f;
   {
@@ -1360,6 +1373,13 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
     }
   }
   __syncthreads();                                     // dtile and the bounding box
+#if WARP_LATE_PV == 1
+  // the corner rows for the flow gradient are loaded here, after the dout rows went to LDS:
+  // they arrive during the destination sort and the gather, and the 64 registers they take
+  // are not live together with the dout rows (156 -> fewer VGPRs, more workgroups per CU)
+  float4 pv[IT][4];
+  warp_corner_rows(0, IT);
+#endif
   if (dinp) {
     const int wy0 = bb[0], wx0 = bb[2], wwx = bb[3] - wx0 + 1;
     const int wsz = (bb[1] - wy0 + 1) * wwx;
@@ -1418,10 +1438,24 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
     }
   }
   // ---- flow gradient
+#if WARP_LATE_PV == 2
+  float4 pv[IT][4];
+#endif
 #pragma unroll
   for (int it = 0; it < (WARP_ABL & 2 ? 0 : IT); ++it) {
+#if WARP_LATE_PV == 2
+    if (it % WARP_PV_GROUP == 0) {                     // corner rows in groups: fewer VGPRs
+      asm volatile("" ::: "memory");
+      warp_corner_rows(it, it + WARP_PV_GROUP);
+    }
+#endif
     const int pr = (it * (WG_NT / 64) + wave) * 4 + pg;
-    const float a = ag[it], bq = bg[it];
+    float a, bq;                                       // recomputed: 8 registers fewer
+    {
+      int y0, y1, x0, x1;
+      corners(pixg[it] / w, pixg[it] % w, okg[it] ? fg[it] : make_float2(0.f, 0.f), y0, y1, x0,
+              x1, a, bq);
+    }
     const float4 g = *reinterpret_cast<const float4*>(&dtile[pr * 64 + 4 * q]);
     const float4* P = pv[it];
     auto dot = [](float4 u, float4 v) { return u.x * v.x + u.y * v.y + u.z * v.z + u.w * v.w; };
@@ -1432,10 +1466,10 @@ __global__ __launch_bounds__(WG_NT) void warp_bwd_gather(const float* __restrict
     gy = row16_sum(gy);
     if (q == 0 && okg[it]) {
       if (passes == 1) {
-        *reinterpret_cast<float2*>(dflow + 2 * pixg[it]) = make_float2(fax[it] + gx, fay[it] + gy);
+        *reinterpret_cast<float2*>(dflow + 2 * (img + pixg[it])) = make_float2(fax[it] + gx, fay[it] + gy);
       } else {                                         // dflow preset by the launcher
-        atomicAdd(dflow + 2 * pixg[it], gx);
-        atomicAdd(dflow + 2 * pixg[it] + 1, gy);
+        atomicAdd(dflow + 2 * (img + pixg[it]), gx);
+        atomicAdd(dflow + 2 * (img + pixg[it]) + 1, gy);
       }
     }
   }
