@@ -12,6 +12,12 @@ namespace oflow {
 #ifndef RED_BLOCKS
 #define RED_BLOCKS 512
 #endif
+#ifndef MPB_BATCH
+#define MPB_BATCH 1
+#endif
+#ifndef BNP_BATCH
+#define BNP_BATCH 1
+#endif
 #ifndef BNP_UNROLL
 #define BNP_UNROLL 4   // 4 pixel rows of 3 float4 loads in flight per thread (2: -8 % on the step's BN backward)
 #endif
@@ -167,36 +173,88 @@ __global__ __launch_bounds__(256) void bn_act_bwd_partial(
       ig = make_float4(1.f / gm.x, 1.f / gm.y, 1.f / gm.z, 1.f / gm.w);
     }
     const bool relu = act == OF_ACT_RELU;
-#pragma unroll BNP_UNROLL
-    for (int64_t p = p0 + r; p < p1; p += rows) {
-      const int64_t o = p * c + ch;
-      const float4 g = *reinterpret_cast<const float4*>(dy + o);
-      const float4 yy = *reinterpret_cast<const float4*>(y + o);
-      float4 zh;                                   // normalised pre-BN value
-      if (FROM_Y) {
-        const float4 rr = res ? *reinterpret_cast<const float4*>(res + o)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-        zh = make_float4((yy.x - rr.x - bt.x) * ig.x, (yy.y - rr.y - bt.y) * ig.y,
-                         (yy.z - rr.z - bt.z) * ig.z, (yy.w - rr.w - bt.w) * ig.w);
-      } else {
-        const float4 zz = *reinterpret_cast<const float4*>(z + o);
-        zh = make_float4((zz.x - mu.x) * is.x, (zz.y - mu.y) * is.y, (zz.z - mu.z) * is.z,
-                         (zz.w - mu.w) * is.w);
+    // BNP_UNROLL pixel rows per round, every load of the round issued before any use: buffer
+    // loads on resources based at this block's first pixel (a row past the block's range, or
+    // a null tensor, reads 0 -> t = 0 and adds nothing; its stores are dropped).  The pointer
+    // form (kept for blocks of 2 GB and more, and as BNP_BATCH=0) put each row's res load and
+    // dz / dres stores behind a branch, and the compiler then waited for every load in flight
+    // (vmcnt(0)) once per row.
+    const int64_t nb = (p1 - p0) * c * 4;              // this block's bytes per tensor
+    if (BNP_BATCH && nb < (int64_t)kOOB) {
+      const int64_t ob = p0 * c;
+      const rsrc_t rdy = make_rsrc(dy + ob, nb), ry = make_rsrc(y + ob, nb);
+      const rsrc_t rx = FROM_Y ? make_rsrc(res ? res + ob : dy, res ? nb : 0)
+                               : make_rsrc(z + ob, nb);
+      const rsrc_t rdz = make_rsrc(dz ? dz + ob : dy, dz ? nb : 0);
+      const rsrc_t rdr = make_rsrc(dres ? dres + ob : dy, dres ? nb : 0);
+      const int np = (int)(p1 - p0);
+      constexpr int U = BNP_UNROLL;
+      for (int pl = r; pl < np; pl += U * rows) {
+        uint32_t off[U];
+        float4 g[U], yy[U], xx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int pu = pl + u * rows;
+          off[u] = pu < np ? (uint32_t)(pu * c + ch) * 4u : kOOB;
+          g[u] = bload4(rdy, off[u]);
+          yy[u] = bload4(ry, off[u]);
+          xx[u] = bload4(rx, off[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float4 zh;
+          if (FROM_Y)
+            zh = make_float4((yy[u].x - xx[u].x - bt.x) * ig.x, (yy[u].y - xx[u].y - bt.y) * ig.y,
+                             (yy[u].z - xx[u].z - bt.z) * ig.z, (yy[u].w - xx[u].w - bt.w) * ig.w);
+          else
+            zh = make_float4((xx[u].x - mu.x) * is.x, (xx[u].y - mu.y) * is.y,
+                             (xx[u].z - mu.z) * is.z, (xx[u].w - mu.w) * is.w);
+          float4 t;
+          t.x = (!relu || yy[u].x > 0.f) ? g[u].x : 0.f;
+          t.y = (!relu || yy[u].y > 0.f) ? g[u].y : 0.f;
+          t.z = (!relu || yy[u].z > 0.f) ? g[u].z : 0.f;
+          t.w = (!relu || yy[u].w > 0.f) ? g[u].w : 0.f;
+          bstore4(make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w), rdz, off[u]);
+          bstore4(t, rdr, off[u]);
+          add4(sb, t);
+          sg.x += t.x * zh.x;
+          sg.y += t.y * zh.y;
+          sg.z += t.z * zh.z;
+          sg.w += t.w * zh.w;
+        }
       }
-      float4 t;
-      t.x = (!relu || yy.x > 0.f) ? g.x : 0.f;
-      t.y = (!relu || yy.y > 0.f) ? g.y : 0.f;
-      t.z = (!relu || yy.z > 0.f) ? g.z : 0.f;
-      t.w = (!relu || yy.w > 0.f) ? g.w : 0.f;
-      if (dz)
-        *reinterpret_cast<float4*>(dz + o) =
-            make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
-      if (dres) *reinterpret_cast<float4*>(dres + o) = t;
-      add4(sb, t);
-      sg.x += t.x * zh.x;
-      sg.y += t.y * zh.y;
-      sg.z += t.z * zh.z;
-      sg.w += t.w * zh.w;
+    } else {
+  #pragma unroll BNP_UNROLL
+      for (int64_t p = p0 + r; p < p1; p += rows) {
+        const int64_t o = p * c + ch;
+        const float4 g = *reinterpret_cast<const float4*>(dy + o);
+        const float4 yy = *reinterpret_cast<const float4*>(y + o);
+        float4 zh;                                   // normalised pre-BN value
+        if (FROM_Y) {
+          const float4 rr = res ? *reinterpret_cast<const float4*>(res + o)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+          zh = make_float4((yy.x - rr.x - bt.x) * ig.x, (yy.y - rr.y - bt.y) * ig.y,
+                           (yy.z - rr.z - bt.z) * ig.z, (yy.w - rr.w - bt.w) * ig.w);
+        } else {
+          const float4 zz = *reinterpret_cast<const float4*>(z + o);
+          zh = make_float4((zz.x - mu.x) * is.x, (zz.y - mu.y) * is.y, (zz.z - mu.z) * is.z,
+                           (zz.w - mu.w) * is.w);
+        }
+        float4 t;
+        t.x = (!relu || yy.x > 0.f) ? g.x : 0.f;
+        t.y = (!relu || yy.y > 0.f) ? g.y : 0.f;
+        t.z = (!relu || yy.z > 0.f) ? g.z : 0.f;
+        t.w = (!relu || yy.w > 0.f) ? g.w : 0.f;
+        if (dz)
+          *reinterpret_cast<float4*>(dz + o) =
+              make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
+        if (dres) *reinterpret_cast<float4*>(dres + o) = t;
+        add4(sb, t);
+        sg.x += t.x * zh.x;
+        sg.y += t.y * zh.y;
+        sg.z += t.z * zh.z;
+        sg.w += t.w * zh.w;
+      }
     }
   }
   sb = rows_reduce(sb, q, r, qw, rows, red);
@@ -247,58 +305,138 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
     int ox = (int)((p0 + r) % wo), oy = (int)((p0 + r) / wo % ho);
     int64_t b = (p0 + r) / wo / ho;
     const int dox = rows % wo, doy = rows / wo;
-#pragma unroll MPB_UNROLL
-    for (int64_t p = p0 + r; p < p1; p += rows) {
-      const int64_t o0 = ((b * h + 2 * oy) * (int64_t)w + 2 * ox) * c + ch;
-      ox += dox;
-      oy += doy;
-      if (ox >= wo) ox -= wo, ++oy;
-      while (oy >= ho) oy -= ho, ++b;
-      const int64_t offs[4] = {o0, o0 + c, o0 + (int64_t)w * c, o0 + (int64_t)w * c + c};
-      float4 yv[4], zv[4], gv[4];
+    // Batched form (MPB_BATCH): MPB_UNROLL pooled pixels per round, their 9 loads each issued
+    // before any use, on buffer resources based at the block's first full-resolution row (a
+    // pixel past the block, or a null g, reads 0 and its dz stores are dropped).  The pointer
+    // form below put g's loads behind a branch and waited for all loads once per pixel.
+    // The block's full-resolution span: at most (its pooled rows + 2) x 2 image rows.
+    const int64_t e0 = ((p0 / wo) * 2) * (int64_t)w * c;   // (b, 2 oy0, 0, 0): p0 / wo = b ho + oy0
+    const int64_t span = ((p1 - p0) / wo + 2) * 2 * (int64_t)w * c * 4;
+    if (MPB_BATCH && span < (int64_t)kOOB && (p1 - p0) * c * 4 < (int64_t)kOOB) {
+      const int64_t tot = npix * 4 * c * 4 - e0 * 4;   // bytes of y from e0 to the end
+      const int64_t nb = min(tot, span);
+      const rsrc_t ry = make_rsrc(y + e0, nb), rg = make_rsrc(g ? g + e0 : y, g ? nb : 0);
+      const rsrc_t rz = make_rsrc(FROM_Y ? y : z + e0, FROM_Y ? 0 : nb);
+      const rsrc_t rdz = make_rsrc(dz + e0, nb);
+      const rsrc_t rd = make_rsrc(dyp + p0 * c, (p1 - p0) * c * 4);
+      const int np = (int)(p1 - p0);
+      constexpr int U = MPB_UNROLL;
+      for (int pl = r; pl < np; pl += U * rows) {
+        uint32_t o[U], od[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        yv[k] = *reinterpret_cast<const float4*>(y + offs[k]);
-        gv[k] = g ? *reinterpret_cast<const float4*>(g + offs[k]) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+        for (int u = 0; u < U; ++u) {
+          const bool in = pl + u * rows < np;
+          o[u] = in ? (uint32_t)(((b * h + 2 * oy) * (int64_t)w + 2 * ox) * c + ch - e0) * 4u : kOOB;
+          od[u] = in ? (uint32_t)((pl + u * rows) * c + ch) * 4u : kOOB;
+          ox += dox;
+          oy += doy;
+          if (ox >= wo) ox -= wo, ++oy;
+          while (oy >= ho) oy -= ho, ++b;
+        }
+        const uint32_t dxo = (uint32_t)c * 4u, dyo = (uint32_t)w * c * 4u;
+        auto at = [&](uint32_t base, int k) {           // corner k of a window (kOOB stays out)
+          return base == kOOB ? kOOB : base + (k & 1 ? dxo : 0u) + (k & 2 ? dyo : 0u);
+        };
+        float4 yv[U][4], gv[U][4], zr[U][4], d[U];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {   // zv: the normalised pre-BN values
-        if (FROM_Y) {
-          zv[k] = make_float4((yv[k].x - bt.x) * ig.x, (yv[k].y - bt.y) * ig.y,
-                              (yv[k].z - bt.z) * ig.z, (yv[k].w - bt.w) * ig.w);
-        } else {
-          const float4 zz = *reinterpret_cast<const float4*>(z + offs[k]);
-          zv[k] = make_float4((zz.x - mu.x) * is.x, (zz.y - mu.y) * is.y, (zz.z - mu.z) * is.z,
-                              (zz.w - mu.w) * is.w);
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            yv[u][k] = bload4(ry, at(o[u], k));
+            gv[u][k] = bload4(rg, at(o[u], k));
+            if (!FROM_Y) zr[u][k] = bload4(rz, at(o[u], k));
+          }
+          d[u] = bload4(rd, od[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          int bx = 0, by = 0, bz = 0, bw = 0;           // first maximum per channel
+          float4 mx = yv[u][0];
+#pragma unroll
+          for (int k = 1; k < 4; ++k) {
+            if (yv[u][k].x > mx.x) bx = k, mx.x = yv[u][k].x;
+            if (yv[u][k].y > mx.y) by = k, mx.y = yv[u][k].y;
+            if (yv[u][k].z > mx.z) bz = k, mx.z = yv[u][k].z;
+            if (yv[u][k].w > mx.w) bw = k, mx.w = yv[u][k].w;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float4 yk = yv[u][k];
+            float4 zk;
+            if (FROM_Y)
+              zk = make_float4((yk.x - bt.x) * ig.x, (yk.y - bt.y) * ig.y, (yk.z - bt.z) * ig.z,
+                               (yk.w - bt.w) * ig.w);
+            else
+              zk = make_float4((zr[u][k].x - mu.x) * is.x, (zr[u][k].y - mu.y) * is.y,
+                               (zr[u][k].z - mu.z) * is.z, (zr[u][k].w - mu.w) * is.w);
+            float4 t;
+            t.x = yk.x > 0.f ? gv[u][k].x + (k == bx ? d[u].x : 0.f) : 0.f;
+            t.y = yk.y > 0.f ? gv[u][k].y + (k == by ? d[u].y : 0.f) : 0.f;
+            t.z = yk.z > 0.f ? gv[u][k].z + (k == bz ? d[u].z : 0.f) : 0.f;
+            t.w = yk.w > 0.f ? gv[u][k].w + (k == bw ? d[u].w : 0.f) : 0.f;
+            bstore4(make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w), rdz, at(o[u], k));
+            add4(sb, t);
+            sg.x += t.x * zk.x;
+            sg.y += t.y * zk.y;
+            sg.z += t.z * zk.z;
+            sg.w += t.w * zk.w;
+          }
         }
       }
-      const float4 d = *reinterpret_cast<const float4*>(dyp + p * c + ch);
-      // first maximum per channel (the running maxima kept as values: indexing yv by the
-      // running argmax made the arrays dynamically indexed, and the compiler put them in LDS
-      // with a wait after every load -- four serial memory round trips per pooled pixel)
-      int bx = 0, by = 0, bz = 0, bw = 0;
-      float4 mx = yv[0];
-#pragma unroll
-      for (int k = 1; k < 4; ++k) {
-        if (yv[k].x > mx.x) bx = k, mx.x = yv[k].x;
-        if (yv[k].y > mx.y) by = k, mx.y = yv[k].y;
-        if (yv[k].z > mx.z) bz = k, mx.z = yv[k].z;
-        if (yv[k].w > mx.w) bw = k, mx.w = yv[k].w;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float4 t;
-        t.x = yv[k].x > 0.f ? gv[k].x + (k == bx ? d.x : 0.f) : 0.f;
-        t.y = yv[k].y > 0.f ? gv[k].y + (k == by ? d.y : 0.f) : 0.f;
-        t.z = yv[k].z > 0.f ? gv[k].z + (k == bz ? d.z : 0.f) : 0.f;
-        t.w = yv[k].w > 0.f ? gv[k].w + (k == bw ? d.w : 0.f) : 0.f;
-        *reinterpret_cast<float4*>(dz + offs[k]) =
-            make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
-        add4(sb, t);
-        sg.x += t.x * zv[k].x;
-        sg.y += t.y * zv[k].y;
-        sg.z += t.z * zv[k].z;
-        sg.w += t.w * zv[k].w;
+    } else {
+  #pragma unroll MPB_UNROLL
+      for (int64_t p = p0 + r; p < p1; p += rows) {
+        const int64_t o0 = ((b * h + 2 * oy) * (int64_t)w + 2 * ox) * c + ch;
+        ox += dox;
+        oy += doy;
+        if (ox >= wo) ox -= wo, ++oy;
+        while (oy >= ho) oy -= ho, ++b;
+        const int64_t offs[4] = {o0, o0 + c, o0 + (int64_t)w * c, o0 + (int64_t)w * c + c};
+        float4 yv[4], zv[4], gv[4];
+  #pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          yv[k] = *reinterpret_cast<const float4*>(y + offs[k]);
+          gv[k] = g ? *reinterpret_cast<const float4*>(g + offs[k]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+  #pragma unroll
+        for (int k = 0; k < 4; ++k) {   // zv: the normalised pre-BN values
+          if (FROM_Y) {
+            zv[k] = make_float4((yv[k].x - bt.x) * ig.x, (yv[k].y - bt.y) * ig.y,
+                                (yv[k].z - bt.z) * ig.z, (yv[k].w - bt.w) * ig.w);
+          } else {
+            const float4 zz = *reinterpret_cast<const float4*>(z + offs[k]);
+            zv[k] = make_float4((zz.x - mu.x) * is.x, (zz.y - mu.y) * is.y, (zz.z - mu.z) * is.z,
+                                (zz.w - mu.w) * is.w);
+          }
+        }
+        const float4 d = *reinterpret_cast<const float4*>(dyp + p * c + ch);
+        // first maximum per channel (the running maxima kept as values: indexing yv by the
+        // running argmax made the arrays dynamically indexed, and the compiler put them in LDS
+        // with a wait after every load -- four serial memory round trips per pooled pixel)
+        int bx = 0, by = 0, bz = 0, bw = 0;
+        float4 mx = yv[0];
+  #pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          if (yv[k].x > mx.x) bx = k, mx.x = yv[k].x;
+          if (yv[k].y > mx.y) by = k, mx.y = yv[k].y;
+          if (yv[k].z > mx.z) bz = k, mx.z = yv[k].z;
+          if (yv[k].w > mx.w) bw = k, mx.w = yv[k].w;
+        }
+  #pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float4 t;
+          t.x = yv[k].x > 0.f ? gv[k].x + (k == bx ? d.x : 0.f) : 0.f;
+          t.y = yv[k].y > 0.f ? gv[k].y + (k == by ? d.y : 0.f) : 0.f;
+          t.z = yv[k].z > 0.f ? gv[k].z + (k == bz ? d.z : 0.f) : 0.f;
+          t.w = yv[k].w > 0.f ? gv[k].w + (k == bw ? d.w : 0.f) : 0.f;
+          *reinterpret_cast<float4*>(dz + offs[k]) =
+              make_float4(t.x * sc.x, t.y * sc.y, t.z * sc.z, t.w * sc.w);
+          add4(sb, t);
+          sg.x += t.x * zv[k].x;
+          sg.y += t.y * zv[k].y;
+          sg.z += t.z * zv[k].z;
+          sg.w += t.w * zv[k].w;
+        }
       }
     }
   }

@@ -1711,11 +1711,15 @@ def test_conv_split_k_matches_unsplit(stride):
     assert rel_inf(dx1, ref) < REL_TOL and rel_inf(dx2, ref) < REL_TOL
 
 
+@pytest.mark.parametrize("from_y", [False, True])
 @pytest.mark.parametrize("n,h,w,c,with_g", [(2, 8, 12, 64, True), (1, 6, 10, 16, False),
-                                            (3, 34, 70, 64, True)])
-def test_maxpool_bn_act_bwd_fused(n, h, w, c, with_g):
+                                            (3, 34, 70, 64, True),
+                                            # many workgroups, a ragged last one; 8 quads
+                                            (2, 96, 130, 64, True), (1, 40, 52, 32, False)])
+def test_maxpool_bn_act_bwd_fused(n, h, w, c, with_g, from_y):
     """The stem's fused backward (max-pool backward + out0's second gradient + BN/ReLU
-    backward) against torch autograd of relu(bn(z)) -> {out0, maxpool} in float64."""
+    backward) against torch autograd of relu(bn(z)) -> {out0, maxpool} in float64; from_y:
+    of_maxpool_bn_relu_bwd, z not stored (zhat recovered from y)."""
     import ctypes as C
     from optical_flow_amd._lib import call, lib
     torch.manual_seed(0)
@@ -1738,8 +1742,13 @@ def test_maxpool_bn_act_bwd_fused(n, h, w, c, with_g):
     ws = torch.empty(lib().of_maxpool_bn_act_bwd_workspace(n, h, w, c) // 4 + 1, device="cuda")
     P = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
     args = [dv(dyp), dv(g) if with_g else None, dv(yv), dv(z), dv(gamma), dv(mean), dv(var)]
-    call("of_maxpool_bn_act_bwd", n, h, w, c, *[P(t) for t in args], 1e-3, P(outs[0]), P(outs[1]),
-         P(outs[2]), P(outs[3]), 0, P(ws), None)
+    if from_y:
+        call("of_maxpool_bn_relu_bwd", n, h, w, c, P(args[0]), P(args[1]), P(args[2]),
+             P(args[4]), P(dv(beta)), P(args[6]), 1e-3, P(outs[0]), P(outs[1]), P(outs[2]),
+             P(outs[3]), 0, P(ws), None)
+    else:
+        call("of_maxpool_bn_act_bwd", n, h, w, c, *[P(t) for t in args], 1e-3, P(outs[0]),
+             P(outs[1]), P(outs[2]), P(outs[3]), 0, P(ws), None)
     torch.cuda.synchronize()
     dz, dg, db, dbias = [o.double().cpu() for o in outs]
     exp_dbias = zr.grad.sum(dim=(0, 1, 2))
