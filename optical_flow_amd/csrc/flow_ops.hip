@@ -1244,7 +1244,10 @@ __global__ __launch_bounds__(64 * WH_WAVES) void warp_bwd_agg(const float* __res
     _Pragma("unroll") for (int k = 0; k < 4; ++k) pv[i_][k] =                                  \
         *reinterpret_cast<const float4*>(inp + (img + (int64_t)ys[k] * w + xs[k]) * c + cc + 4 * q); \
   }
-constexpr int WG_T = 8, WG_CAP = 1024, WG_NT = 256;
+#ifndef WARP_CAP
+#define WARP_CAP 512   // destination slots: 23.7 KB of LDS = 6 workgroups per CU (1024: 5)
+#endif
+constexpr int WG_T = 8, WG_CAP = WARP_CAP, WG_NT = 256;
 int g_warp_win = 1;   // of_set_tuning key 7: warp_bwd_gather (1) or warp_bwd_agg (0)
 int g_corr_blk = 5;   // of_set_tuning key 9: bit 0 corr_fwd_blk (else corr_fwd_kernel), bit 1 corr_bwd_blk,
                       // bit 2 corr_bwd_fused when both gradients are wanted
