@@ -32,7 +32,7 @@ extern "C" {
 
 #define OF_ABI_VERSION 1
 
-enum { OF_OK = 0, OF_EINVAL = 1, OF_EHIP = 2, OF_EUNSUPPORTED = 3 };
+enum { OF_OK = 0, OF_EINVAL = 1, OF_EHIP = 2, OF_EUNSUPPORTED = 3, OF_ETIMEOUT = 4 };
 enum { OF_ACT_NONE = 0, OF_ACT_RELU = 1, OF_ACT_LEAKY = 2 };
 
 /* Convolution geometry.  Replaces layers.Conv2D(padding='same') (model.py:12,104-114 and the
@@ -398,7 +398,9 @@ int of_timing_enable(int on);
  * gradient (1, default: the input gradient's measured slower; 0 = per-pass transposes);
  * key 24 = conv_halo_b16 persistent over contiguous tile ranges, the next tile's first loads
  * in flight during the epilogue (1; 2: on 8 workgroups, for tests) or one tile per workgroup
- * (0, default: the persistent form measured even). */
+ * (0, default: the persistent form measured even);
+ * keys 25 / 26 = the K-split cost models' slab-pass term (tenths of a chunk per slice and tile
+ * round; default 5) of the fp32 halo-tile kernels and of the split implicit GEMMs. */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 
@@ -562,6 +564,32 @@ int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const f
                            const float* var, float eps, float* dz, float* dgamma, float* dbeta,
                            float* dbias, int accumulate, void* workspace, void* stream);
 
+/* ==== SURVEY.md §8 P5: BatchNormalization in training mode (bn_mode = "training") ========= */
+/* keras BatchNormalization called with training=True (old/train.py:59; the reference's
+ * train.py:51 runs inference mode, the build default): z is the conv output (bias included),
+ * npix rows x c channels (NHWC, c % 4 == 0, c <= 1024), split into `groups` contiguous row
+ * ranges with separate statistics (the Siamese (2B) batch: model.py:131-132 calls the encoder
+ * once per image).  Fixed-order reductions (bitwise reproducible).
+ * Workspace of all three: of_bn_train_workspace(npix, c, groups) bytes. */
+size_t of_bn_train_workspace(int64_t npix, int c, int groups);
+/* mean[g][c], invstd[g][c] = 1 / sqrt(biased var + eps); moving statistics (NULL to skip)
+ * updated group by group in order as FusedBatchNormV3 does with exponential_avg_factor
+ * f = 1 - momentum: moving = (1 - f) moving + f stat, the variance Bessel-corrected. */
+int of_bn_train_stats(int64_t npix, int c, int groups, const float* z, float eps, float momentum,
+                      float* mean, float* invstd, float* moving_mean, float* moving_var,
+                      void* workspace, void* stream);
+/* y = act(gamma (z - mean[g]) invstd[g] + beta + res)   (res may be NULL; act OF_ACT_*) */
+int of_bn_train_apply(int64_t npix, int c, int groups, const float* z, const float* mean,
+                      const float* invstd, const float* gamma, const float* beta,
+                      const float* res, int act, float* y, void* stream);
+/* FusedBatchNormGradV3 (is_training): t = dy act'(y) (to t_out if non-NULL: the residual's
+ * gradient); per group st = sum t, stz = sum t zhat; dz = gamma invstd (t - st/n - zhat stz/n);
+ * dgamma (+)= sum over groups of stz, dbeta (+)= sum of st (NULL to skip). */
+int of_bn_train_bwd(int64_t npix, int c, int groups, int act, const float* dy, const float* y,
+                    const float* z, const float* mean, const float* invstd, const float* gamma,
+                    float* dz, float* t_out, float* dgamma, float* dbeta, int accumulate,
+                    void* workspace, void* stream);
+
 /* ==== SURVEY.md §8 b / §8 e: gradient all-reduce over RCCL (build-added K14) ============= */
 /* The reference is single-process (train.py:47-61); batch data parallelism sums the
  * gradients tape.gradient() returns (train.py:55) across ranks before the Adam update
@@ -571,8 +599,17 @@ int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const f
 typedef struct of_comm of_comm;
 int of_comm_id_bytes(void);                      /* bytes of a unique id (128) */
 int of_comm_get_unique_id(void* id);
+/* OF_OK when librccl loads with every entry point used here and a HIP device is current:
+ * checked (and agreed on over the rendezvous store) before any rank enters of_comm_init. */
+int of_comm_probe(void);
 /* Collective over the nranks processes; binds the communicator to the current HIP device. */
 int of_comm_init(of_comm** comm, const void* id, int nranks, int rank);
+/* The same with a deadline: a non-blocking RCCL init (ncclConfig_t.blocking = 0) polled until
+ * it completes; a rendezvous a peer never reaches is aborted after timeout_s seconds and
+ * OF_ETIMEOUT is returned (timeout_s <= 0 or an RCCL without ncclCommInitRankConfig: the
+ * blocking of_comm_init). */
+int of_comm_init_timeout(of_comm** comm, const void* id, int nranks, int rank,
+                         double timeout_s);
 int of_comm_info(const of_comm* comm, int* nranks, int* rank, int* device);
 /* recv = sum over ranks of send (count fp32 elements; send == recv is in place), enqueued on
  * `stream` and ordered after the work already on it; returns without waiting. */

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # OFLOW_LIB: an alternative build of the same library (A/B experiments with tools/ab_build.sh)
 LIB_PATH = os.environ.get("OFLOW_LIB") or os.path.join(HERE, "liboflow.so")
 
-OF_OK, OF_EINVAL, OF_EHIP, OF_EUNSUPPORTED = 0, 1, 2, 3
+OF_OK, OF_EINVAL, OF_EHIP, OF_EUNSUPPORTED, OF_ETIMEOUT = 0, 1, 2, 3, 4
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
 
 
@@ -154,10 +154,17 @@ PROTOTYPES = {
     "of_conv2d_dgrad_add_act": (I, [PD, I, P, I, P, P, I, P, I, I, F, P, I, P, SZ, P]),
     "of_bn_bwd_reduce": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     "of_maxpool_bn_relu_bwd": (I, [I, I, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
+    # BatchNormalization in training mode (bn_mode="training")
+    "of_bn_train_workspace": (SZ, [I64, I, I]),
+    "of_bn_train_stats": (I, [I64, I, I, P, F, F, P, P, P, P, P, P]),
+    "of_bn_train_apply": (I, [I64, I, I, P, P, P, P, P, P, I, P, P]),
+    "of_bn_train_bwd": (I, [I64, I, I, I, P, P, P, P, P, P, P, P, P, P, I, P, P]),
     # gradient all-reduce over RCCL (SURVEY §8 b / e)
     "of_comm_id_bytes": (I, []),
     "of_comm_get_unique_id": (I, [P]),
+    "of_comm_probe": (I, []),
     "of_comm_init": (I, [C.POINTER(P), P, I, I]),
+    "of_comm_init_timeout": (I, [C.POINTER(P), P, I, I, C.c_double]),
     "of_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "of_comm_allreduce_async": (I, [P, P, P, I64, P]),
     "of_comm_async_error": (I, [P]),
@@ -167,6 +174,10 @@ PROTOTYPES = {
 
 class OflowError(RuntimeError):
     pass
+
+
+class OflowTimeout(OflowError):
+    """OF_ETIMEOUT: a collective setup or wait passed its deadline (and was aborted)."""
 
 
 _lib = None
@@ -207,6 +218,8 @@ def check(status: int, what: str = ""):
         msg = lib().of_last_error().decode(errors="replace")
         if status == OF_EINVAL:
             raise AssertionError("%s: %s" % (what, msg))
+        if status == OF_ETIMEOUT:
+            raise OflowTimeout("%s timed out: %s" % (what, msg))
         raise OflowError("%s failed (%d): %s" % (what, status, msg))
 
 

@@ -13,14 +13,130 @@ backend on CPU tensors for the multi-process CPU tests, and for two ranks that s
 from __future__ import annotations
 
 import ctypes as C
+import datetime
 import itertools
+import os
+import threading
+import time
 
 import torch
 
 from . import _lib
-from ._lib import call
+from ._lib import OF_OK, OflowTimeout, call
 
 _ids = itertools.count()
+_votes = itertools.count()
+
+# Deadline (seconds) for every step of the N > 1 communicator that waits on peers: the probe
+# exchange and the RCCL rendezvous at init, the self-test all-reduce, and each step's bucket
+# all-reduces (CommWatchdog).  A peer that never arrives then ends in an error on every rank
+# instead of a hang.  OFLOW_COMM_TIMEOUT overrides.
+COMM_TIMEOUT_S = float(os.environ.get("OFLOW_COMM_TIMEOUT", "300"))
+
+
+class CommError(RuntimeError):
+    """The gradient communicator failed or timed out (SURVEY.md §5 failure detection)."""
+
+
+def _store_wait(store, keys, timeout):
+    try:
+        store.wait(list(keys), datetime.timedelta(seconds=timeout))
+    except Exception as e:  # noqa: BLE001 -- the store raises its own timeout types
+        raise CommError("rendezvous store: %d key(s) %s not set within %.0f s (a peer is "
+                        "missing or failed before reaching this point): %r" % (
+                            len(keys), list(keys)[:3], timeout, e)) from e
+
+
+def vote(store, tag: str, rank: int, world: int, ok: bool, timeout: float = None) -> bool:
+    """All ranks' verdicts through the rendezvous store (no collective on any process group,
+    so it works whatever backend the default group has): True iff every rank voted ok.  A
+    rank that never votes makes every other rank raise CommError after ``timeout``."""
+    timeout = COMM_TIMEOUT_S if timeout is None else timeout
+    store.set("%s/%d" % (tag, rank), b"1" if ok else b"0")
+    keys = ["%s/%d" % (tag, r) for r in range(world)]
+    _store_wait(store, keys, timeout)
+    return all(bytes(store.get(k)) == b"1" for k in keys)
+
+
+class CommWatchdog:
+    """Bounds the waits a data-parallel step cannot bound itself: each step's
+    collectives are stream-ordered, so nothing on the host waits for them -- a peer that never
+    joins would hang the next synchronize.  ``watch(done)`` registers a completion predicate
+    (an event recorded after the step's last collective); a daemon thread polls it, and the
+    communicator's asynchronous error state, and after ``timeout`` seconds calls
+    ``on_expire(reason)`` (RcclComm: abort the communicator, which makes its in-flight kernels
+    return) and remembers the reason; ``check()`` raises CommError with it in the caller's
+    thread (GradBucketReducer.finish, once per step)."""
+
+    def __init__(self, timeout: float, on_expire, poll_s: float = 0.01, error_probe=None):
+        self.timeout = timeout
+        self.on_expire = on_expire
+        self.error_probe = error_probe
+        self.poll_s = poll_s
+        self.failed = None
+        self._q = []
+        self._cv = threading.Condition()
+        self._stop = False
+        self._t = threading.Thread(target=self._run, name="oflow-comm-watchdog", daemon=True)
+        self._t.start()
+
+    def watch(self, done):
+        with self._cv:
+            self._q.append((done, time.monotonic() + self.timeout))
+            self._cv.notify()
+
+    def pending(self) -> int:
+        with self._cv:
+            return len(self._q)
+
+    def check(self):
+        if self.failed is not None:
+            raise CommError(self.failed)
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._t.join(timeout=5)
+
+    def _fail(self, reason):
+        with self._cv:
+            if self.failed is not None:
+                return
+            self.failed = reason
+            self._q.clear()
+        try:
+            self.on_expire(reason)
+        except Exception:  # noqa: BLE001 -- the reason is kept for check()
+            pass
+
+    def _run(self):
+        while True:
+            with self._cv:
+                while not self._q and not self._stop:
+                    self._cv.wait()
+                if self._stop:
+                    return
+                done, deadline = self._q[0]
+            try:
+                finished = done()
+            except Exception as e:  # noqa: BLE001
+                self._fail("collective completion check raised %r" % (e,))
+                continue
+            if finished:
+                with self._cv:
+                    if self._q and self._q[0][0] is done:
+                        self._q.pop(0)
+                continue
+            err = self.error_probe() if self.error_probe is not None else None
+            if err:
+                self._fail(err)
+            elif time.monotonic() > deadline:
+                self._fail("a step's gradient all-reduce did not complete within %.0f s (a "
+                           "peer stopped joining the collectives); communicator aborted" %
+                           self.timeout)
+            else:
+                time.sleep(self.poll_s)
 
 
 def _store():
@@ -39,29 +155,76 @@ class RcclComm:
 
     kind = "rccl"
 
-    def __init__(self, rank: int = 0, world: int = 1, store=None, key: str = None):
+    def __init__(self, rank: int = 0, world: int = 1, store=None, key: str = None,
+                 timeout: float = None):
         lib = _lib.lib()
         self.rank, self.world = rank, world
+        self.timeout = COMM_TIMEOUT_S if timeout is None else timeout
+        self._h = None
+        self.watchdog = None
         nb = lib.of_comm_id_bytes()
         uid = (C.c_char * nb)()
         key = key or "oflow/rccl_id/%d" % next(_ids)
+        if world > 1:
+            store = store or _store()
+            # every rank checks that it can make a communicator at all (librccl, a device)
+            # and the ranks agree on it through the store BEFORE any of them enters the RCCL
+            # rendezvous, which would otherwise wait for a rank that already gave up
+            ok = lib.of_comm_probe() == OF_OK
+            why = "" if ok else lib.of_last_error().decode(errors="replace")
+            if not vote(store, key + "/probe", rank, world, ok, self.timeout):
+                raise CommError("C-ABI RCCL communicator unavailable on at least one rank%s" % (
+                    (" (this rank: %s)" % why) if why else ""))
         if rank == 0:
             call("of_comm_get_unique_id", uid)
             if world > 1:
-                (store or _store()).set(key, bytes(uid))
+                store.set(key, bytes(uid))
         else:
-            raw = (store or _store()).get(key)          # blocks until rank 0 has set it
+            _store_wait(store, [key], self.timeout)
+            raw = store.get(key)
             assert len(raw) == nb, "RCCL unique id: %d bytes, expected %d" % (len(raw), nb)
             C.memmove(uid, raw, nb)
         h = C.c_void_p()
-        call("of_comm_init", C.byref(h), uid, world, rank)
+        try:
+            call("of_comm_init_timeout", C.byref(h), uid, world, rank,
+                 self.timeout if world > 1 else 0.0)
+        except OflowTimeout as e:
+            raise CommError(str(e)) from e
         self._h = h
         n, r, d = C.c_int(), C.c_int(), C.c_int()
         call("of_comm_info", h, C.byref(n), C.byref(r), C.byref(d))
         self.device = d.value
         assert (n.value, r.value) == (world, rank)
+        self._lock = threading.Lock()
+        if world > 1:
+            self.watchdog = CommWatchdog(self.timeout, self._expire, error_probe=self._probe)
+
+    def _probe(self):
+        """The communicator's asynchronous error, as text (None while healthy)."""
+        with self._lock:
+            if self._h is None:
+                return None
+            st = _lib.lib().of_comm_async_error(self._h)
+            if st == OF_OK:
+                return None
+            return "RCCL communicator failed: " + _lib.lib().of_last_error().decode(
+                errors="replace")
+
+    def _expire(self, reason):
+        self.close(abort=True)
+
+    def watch_stream(self, stream):
+        """Bound the collectives enqueued so far on ``stream`` (an event recorded there; the
+        watchdog aborts the communicator if it is not reached within the timeout)."""
+        if self.watchdog is None:
+            return
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self.watchdog.watch(ev.query)
 
     def allreduce_(self, t: torch.Tensor):
+        if self.watchdog is not None:
+            self.watchdog.check()
         if self._h is None:
             raise RuntimeError("RcclComm used after close()")
         if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
@@ -71,12 +234,18 @@ class RcclComm:
              C.c_void_p(torch.cuda.current_stream().cuda_stream))
 
     def wait(self):
+        if self.watchdog is not None:
+            self.watchdog.check()
         if self._h is not None:
             call("of_comm_async_error", self._h)
 
     def close(self, abort: bool = False):
-        if self._h is not None:
+        lock = getattr(self, "_lock", None)
+        with lock if lock is not None else _nolock():
             h, self._h = self._h, None
+        if self.watchdog is not None and threading.current_thread() is not self.watchdog._t:
+            self.watchdog.close()
+        if h is not None:
             call("of_comm_destroy", h, int(abort))
 
     def __del__(self):
@@ -84,6 +253,14 @@ class RcclComm:
             self.close()
         except Exception:
             pass
+
+
+class _nolock:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 class TorchComm:
@@ -120,39 +297,49 @@ def selftest(comm, rank: int, world: int, n: int = 4096) -> bool:
     the first step (it has only ever run at N = 1 on the development boxes)."""
     t = (torch.arange(n, dtype=torch.float32, device="cuda") + (rank + 1)).contiguous()
     comm.allreduce_(t)
-    torch.cuda.current_stream().synchronize()
+    ev = torch.cuda.Event()
+    ev.record()
+    deadline = time.monotonic() + getattr(comm, "timeout", COMM_TIMEOUT_S)
+    while not ev.query():          # bounded: a hung peer must not hang this rank's init
+        if time.monotonic() > deadline:
+            comm.close(abort=True)
+            raise CommError("RCCL self-test all-reduce did not complete within %.0f s" %
+                            getattr(comm, "timeout", COMM_TIMEOUT_S))
+        time.sleep(0.001)
     comm.wait()
     want = torch.arange(n, dtype=torch.float32, device="cuda") * world + world * (world + 1) / 2
     return bool(torch.equal(t, want))
 
 
-def make_comm(kind: str, rank: int = 0, world: int = 1):
+def make_comm(kind: str, rank: int = 0, world: int = 1, fallback: str = "torch-nccl",
+              timeout: float = None):
     """"rccl" -> RcclComm(rank, world) on the current device, self-tested (``selftest``) when
-    world > 1; if that fails on any rank (the decision is taken jointly over the default
-    process group), every rank falls back to torch.distributed's own RCCL (a "nccl" process
-    group) with a warning.  "torch" -> TorchComm over the default process group;
+    world > 1; if making or testing it fails on any rank, every rank falls back together to
+    ``fallback`` (default torch.distributed's own RCCL, a "nccl" process group) with a warning.
+    The decision is a ``vote`` through the rendezvous store, not a collective on the default
+    process group (whatever its backend), and every wait on a peer has a deadline (``timeout``,
+    default COMM_TIMEOUT_S): a rank that dies or hangs before voting makes the others raise
+    CommError instead of hanging.  "torch" -> TorchComm over the default process group;
     "torch-nccl" -> TorchComm over a new "nccl" group (RCCL through torch)."""
     if kind == "rccl":
         if world <= 1:
             return RcclComm(rank, world)
-        import torch.distributed as dist
+        import warnings
+        timeout = COMM_TIMEOUT_S if timeout is None else timeout
+        tag = "oflow/make_comm/%d" % next(_votes)
         comm, ok = None, False
         try:
-            comm = RcclComm(rank, world)
+            comm = RcclComm(rank, world, timeout=timeout)
             ok = selftest(comm, rank, world)
         except Exception as e:  # noqa: BLE001 -- any failure means: fall back
-            import warnings
             warnings.warn("C-ABI RCCL communicator failed on rank %d: %r" % (rank, e))
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)        # control plane (gloo)
-        if int(flag) == 1:
+        if vote(_store(), tag, rank, world, ok, timeout):
             return comm
-        import warnings
-        warnings.warn("C-ABI RCCL communicator self-test failed: gradients go over "
-                      "torch.distributed's nccl (RCCL) backend instead")
+        warnings.warn("C-ABI RCCL communicator failed its set-up or self-test on at least one "
+                      "rank: gradients go over %s instead (all ranks)" % fallback)
         if comm is not None:
             comm.close(abort=True)
-        kind = "torch-nccl"
+        kind = fallback
     if kind == "torch":
         return TorchComm()
     if kind == "torch-nccl":

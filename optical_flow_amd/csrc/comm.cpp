@@ -12,9 +12,11 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include "common.h"
 
@@ -23,6 +25,7 @@ using namespace oflow;
 struct of_comm {
   ncclComm_t nccl;
   int nranks, rank, device;
+  int nonblocking;   // made by of_comm_init_timeout with a deadline (ncclConfig_t.blocking = 0)
 };
 
 namespace {
@@ -30,6 +33,8 @@ namespace {
 struct RcclApi {
   ncclResult_t (*get_unique_id)(ncclUniqueId*);
   ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+  // optional (non-blocking init with a deadline); absent in old RCCL builds
+  ncclResult_t (*comm_init_rank_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*);
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t);
   ncclResult_t (*comm_destroy)(ncclComm_t);
@@ -53,6 +58,8 @@ RcclApi& rccl() {
     auto sym = [&](const char* n) { return dlsym(h, n); };
     api.get_unique_id = (decltype(api.get_unique_id))sym("ncclGetUniqueId");
     api.comm_init_rank = (decltype(api.comm_init_rank))sym("ncclCommInitRank");
+    api.comm_init_rank_config =
+        (decltype(api.comm_init_rank_config))sym("ncclCommInitRankConfig");
     api.all_reduce = (decltype(api.all_reduce))sym("ncclAllReduce");
     api.comm_destroy = (decltype(api.comm_destroy))sym("ncclCommDestroy");
     api.comm_abort = (decltype(api.comm_abort))sym("ncclCommAbort");
@@ -67,6 +74,25 @@ RcclApi& rccl() {
 
 int rccl_fail(const char* what, ncclResult_t r) {
   return fail(OF_EHIP, std::string(what) + ": " + rccl().error_string(r));
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// A non-blocking communicator's state: poll until it leaves ncclInProgress or the deadline
+// passes (deadline <= 0: no deadline).  Returns ncclSuccess, the failure, or ncclInProgress on
+// expiry.
+ncclResult_t settle(ncclComm_t c, double deadline) {
+  for (;;) {
+    ncclResult_t e = ncclSuccess;
+    ncclResult_t r = rccl().async_error(c, &e);
+    if (r != ncclSuccess) return r;
+    if (e != ncclInProgress) return e;
+    if (deadline > 0 && now_s() > deadline) return ncclInProgress;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
 }
 
 }  // namespace
@@ -86,7 +112,16 @@ int of_comm_get_unique_id(void* id) {
   return OF_OK;
 }
 
-int of_comm_init(of_comm** comm, const void* id, int nranks, int rank) {
+int of_comm_probe(void) {
+  RcclApi& api = rccl();
+  if (!api.ok) return fail(OF_EUNSUPPORTED, api.why);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(OF_EHIP, "comm_probe: no current HIP device");
+  return OF_OK;
+}
+
+int of_comm_init_timeout(of_comm** comm, const void* id, int nranks, int rank,
+                         double timeout_s) {
   OF_CHECK_ARG(comm && id, "comm_init: comm, id");
   OF_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "comm_init: rank / nranks");
   *comm = nullptr;
@@ -97,10 +132,40 @@ int of_comm_init(of_comm** comm, const void* id, int nranks, int rank) {
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
   ncclComm_t c = nullptr;
+  if (timeout_s > 0 && api.comm_init_rank_config) {
+    // non-blocking: the call returns at once (ncclInProgress) and the rendezvous with the
+    // other ranks completes in RCCL's own threads; a peer that never arrives leaves it in
+    // progress, and at the deadline the half-made communicator is aborted
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const double deadline = now_s() + timeout_s;
+    ncclResult_t r = api.comm_init_rank_config(&c, nranks, u, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (c) api.comm_abort(c);
+      return rccl_fail("ncclCommInitRankConfig", r);
+    }
+    r = settle(c, deadline);
+    if (r == ncclInProgress) {
+      api.comm_abort(c);
+      return fail(OF_ETIMEOUT, "ncclCommInitRankConfig: the " + std::to_string(nranks) +
+                                   "-rank rendezvous did not complete within " +
+                                   std::to_string(timeout_s) + " s (aborted)");
+    }
+    if (r != ncclSuccess) {
+      api.comm_abort(c);
+      return rccl_fail("ncclCommInitRankConfig", r);
+    }
+    *comm = new of_comm{c, nranks, rank, dev, 1};
+    return OF_OK;
+  }
   ncclResult_t r = api.comm_init_rank(&c, nranks, u, rank);   // collective over the ranks
   if (r != ncclSuccess) return rccl_fail("ncclCommInitRank", r);
-  *comm = new of_comm{c, nranks, rank, dev};
+  *comm = new of_comm{c, nranks, rank, dev, 0};
   return OF_OK;
+}
+
+int of_comm_init(of_comm** comm, const void* id, int nranks, int rank) {
+  return of_comm_init_timeout(comm, id, nranks, rank, 0.0);
 }
 
 int of_comm_info(const of_comm* comm, int* nranks, int* rank, int* device) {
@@ -117,6 +182,9 @@ int of_comm_allreduce_async(of_comm* comm, const float* send, float* recv, int64
   if (count == 0) return OF_OK;
   ncclResult_t r = rccl().all_reduce(send, recv, (size_t)count, ncclFloat32, ncclSum, comm->nccl,
                                      as_stream(stream));
+  // a non-blocking communicator may return while the enqueue is still in progress: it must
+  // settle before the next call on the communicator (host-side only; the GPU work stays async)
+  if (r == ncclInProgress && comm->nonblocking) r = settle(comm->nccl, 0.0);
   if (r != ncclSuccess) return rccl_fail("ncclAllReduce", r);
   return OF_OK;
 }

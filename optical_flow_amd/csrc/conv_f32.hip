@@ -4357,6 +4357,10 @@ bool ws_ok(const of_conv_desc* d, int mode) {
   return (g_tile_b16 == 2 || (g_tile_b16 == 3 && mode == MODE_FWD)) && pick_bn(N) >= 96;
 }
 
+// of_set_tuning keys 25 / 26: the K-split cost models' slab-pass term, in tenths of a chunk per
+// slice and tile round, of the halo-tile kernels (tile_args) and of conv_gemm_x3 (gemm_x3_plan).
+static int g_x3t_ep = 5;
+static int g_x3g_ep = 5;
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false,
                    bool b16 = false, bool ws = false) {
   GemmArgs a = base_args(d);
@@ -4404,7 +4408,7 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
       if (cdiv(a.K, per) != sp) continue;            // not a distinct slice count
       const int64_t w = (int64_t)a.tiles_total * sp;
       const double cost = (double)cdiv(w, slots) * (per + 1.0) +
-                          (sp > 1 ? 0.5 * sp * a.tiles_total / (double)slots : 0.0);
+                          (sp > 1 ? 0.1 * g_x3t_ep * sp * a.tiles_total / (double)slots : 0.0);
       if (cost < best_cost - 1e-9) {
         best_cost = cost;
         best = sp;
@@ -4534,7 +4538,7 @@ void gemm_x3_plan(GemmArgs& a) {
     if (cdiv(chunks, per) != sp) continue;
     const int64_t w = plan_tiles * sp;
     const double cost = (double)cdiv(w, device_cus()) * (per + 1.0) +
-                        (sp > 1 ? 0.5 * sp * plan_tiles / (double)device_cus() : 0.0);
+                        (sp > 1 ? 0.1 * g_x3g_ep * sp * plan_tiles / (double)device_cus() : 0.0);
     if (cost < best_cost - 1e-9) {
       best_cost = cost;
       best = sp;
@@ -4804,6 +4808,8 @@ int of_set_tuning(int key, int value) {
   if (key == 22 && (value == 0 || value == 1)) { g_b16i_direct = value; return OF_OK; }
   if (key == 23 && value >= 0 && value <= 3) { g_x3_direct = value; return OF_OK; }
   if (key == 24 && value >= 0 && value <= 2) { g_b16i_persist = value; return OF_OK; }
+  if (key == 25 && value >= 0 && value <= 1000) { g_x3t_ep = value; return OF_OK; }
+  if (key == 26 && value >= 0 && value <= 1000) { g_x3g_ep = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

@@ -101,6 +101,11 @@ class GradBucketReducer:
                 self._launch(bi, in_backward=False)
         if torch.cuda.is_available() and torch.cuda.is_initialized():
             ops.side_join_now()
+            # the current stream now waits for every bucket's collective: bound that wait
+            # (comm.CommWatchdog aborts the communicator if a peer never joins)
+            watch = getattr(self.comm, "watch_stream", None)
+            if watch is not None:
+                watch(torch.cuda.current_stream())
         self.comm.wait()
         return 1.0 / self.world
 

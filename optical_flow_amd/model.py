@@ -136,7 +136,7 @@ class Encoder:
     max-pool; three resnet_layer_simple stages -> H/4 x64, H/8 x128, H/16 x256.
     The stage body is the assumed standard basic block (params.py)."""
 
-    def __init__(self, store: ParamStore, name="ResNet18", levels=4):
+    def __init__(self, store: ParamStore, name="ResNet18", levels=4, bn_mode="inference"):
         self.store = store
         self.name = name
         self.levels = levels
@@ -147,9 +147,29 @@ class Encoder:
                                    act=ACT_RELU, bn=stem_bn, cin_p=4,
                                    version_of=lambda: store.version, name="conv1")
         self.blocks = block_layers(store, encoder_blocks(levels))
+        self.set_bn_mode(bn_mode)
 
-    def forward4(self, x4):
-        """x4: (N, H, W, 4) images with a zero 4th channel -> 4 feature maps."""
+    def bn_layers(self):
+        out = [self.conv1]
+        for a, b, p in self.blocks:
+            out += [a, b] + ([p] if p is not None else [])
+        return out
+
+    def set_bn_mode(self, bn_mode):
+        """"inference" (the reference's train.py:51: moving statistics, the default) or
+        "training" (old/train.py:59: batch statistics, moving statistics updated; P5)."""
+        assert bn_mode in ("inference", "training"), bn_mode
+        self.bn_mode = bn_mode
+        for L in self.bn_layers():
+            L.bn_train = bn_mode == "training"
+            L._pack_key = None
+
+    def forward4(self, x4, groups=1):
+        """x4: (N, H, W, 4) images with a zero 4th channel -> 4 feature maps.  groups: the
+        number of separate encoder calls x4 stacks (the FlowNet's image1s / image2s: 2), each
+        with its own batch statistics in bn_mode "training"."""
+        if self.bn_mode == "training":
+            return ops.encoder_forward_train(x4, self.conv1, self.blocks, groups)
         if not _PER_LAYER_BLOCKS:
             return ops.encoder_forward(x4, self.conv1, self.blocks)
         x = self.conv1(x4)
@@ -198,14 +218,15 @@ def block_layers(store: ParamStore, blocks):
 
 
 def resnet_layer_simple(x, nblocks, downsample, idx, store: Optional[ParamStore] = None,
-                        seed: int = 0):
+                        seed: int = 0, precision: str = "fp32", bn_mode: str = "inference"):
     """``resnet.models.resnet_layer_simple(x, nblocks, downsample, idx)`` (model.py:2,18,20,22).
     The ``resnet`` submodule is not vendored, so this is the assumed ResNet-18 basic stage
     (parity unpinned): ``nblocks`` blocks of [conv3x3(s) + BN + ReLU,
     conv3x3 + BN] + shortcut (1x1/s conv + BN when downsampling or when the channel count
     changes) -> add -> ReLU, with 64 * 2^(idx-2) output channels; BN in inference mode (P5).
 
-    x: (N, H, W, C) NHWC float32 on the GPU.  Like the Keras functional call, a call with no
+    x: (N, H, W, C) NHWC float32 on the GPU; ``precision`` "bf16" runs the block convs on the
+    bf16 kernels (configs 3-5).  Like the Keras functional call, a call with no
     ``store`` creates fresh layers (Keras-default init from ``seed``; the store is kept on
     the returned tensor as ``_resnet_store``); a ``store`` holding the stage's weights under
     ``ResNet18/res{idx}_{j}/...`` (e.g. a FlowNet's) reuses them."""
@@ -215,6 +236,17 @@ def resnet_layer_simple(x, nblocks, downsample, idx, store: Optional[ParamStore]
         store = ParamStore(blocks_spec(blocks), seed=seed, device=x.device)
     layers = block_layers(store, blocks)
     flat = [L for blk in layers for L in blk if L is not None]
+    assert bn_mode in ("inference", "training"), bn_mode
+    for L in flat:                      # "bf16": the convs on bf16 MFMA (configs 3-5)
+        L.precision = precision
+        L.bn_train = bn_mode == "training"
+    if bn_mode == "training":           # batch statistics (P5): z always kept, no guard
+        for a, b, p in layers:
+            ya = ops.conv_bn_train(a, x)
+            sc = ops.conv_bn_train(p, x) if p is not None else x
+            x = ops.conv_bn_train(b, ya, residual=sc)
+        x._resnet_store = store
+        return x
     if store.bn_guard is None:          # z kept for BN layers with gamma ~ 0 (ops.BNZGuard)
         store.bn_guard = ops.BNZGuard(flat)
     store.bn_guard.poll()
@@ -317,9 +349,10 @@ class FlowNet:
     """The Keras ``Model`` returned by build_flow_net (model.py:119-143)."""
 
     def __init__(self, height, width, max_disp=3, seed=0, device="cuda", values=None,
-                 precision="fp32", levels=4):
+                 precision="fp32", levels=4, bn_mode="inference"):
         """levels=5 enables the reference's commented-out 5th pyramid level (model.py:24-25,
-        138, 141): encoder stage 5 (512 channels at H/32) and flow4 at H/2."""
+        138, 141): encoder stage 5 (512 channels at H/32) and flow4 at H/2.  bn_mode:
+        "inference" (train.py:51, the default) or "training" (old/train.py:59; P5)."""
         assert levels in (4, 5), levels
         m = 2 ** levels
         assert height % m == 0 and width % m == 0, \
@@ -328,7 +361,7 @@ class FlowNet:
         self.levels = levels
         self.store = ParamStore(flow_net_spec(max_disp, levels), values=values, device=device,
                                 order=backward_order(max_disp, levels), seed=seed)
-        self.encoder = Encoder(self.store, levels=levels)
+        self.encoder = Encoder(self.store, levels=levels, bn_mode=bn_mode)
         self.heads = [FlowHead(self.store, level, max_disp, levels) for level in range(levels)]
         self.name = "flow_net"
         self._packer = None
@@ -345,6 +378,15 @@ class FlowNet:
             L._wf = L._wd = None
             L._pack_key = None
         self._packer = None
+
+    def set_bn_mode(self, bn_mode):
+        """BatchNormalization "inference" (train.py:51, default) or "training" (P5)."""
+        self.encoder.set_bn_mode(bn_mode)
+        self._packer = None
+
+    @property
+    def bn_mode(self):
+        return self.encoder.bn_mode
 
     def conv_layers(self):
         layers = [self.encoder.conv1]
@@ -369,12 +411,14 @@ class FlowNet:
         assert batch_imgs.shape[3] == 6
         if self._packer is None:
             self._packer = ops.ConvPacker(self.conv_layers(), lambda: self.store.version)
-        if self.store.bn_guard is None:              # z kept for BN layers with gamma ~ 0
-            self.store.bn_guard = ops.BNZGuard(self.conv_layers())
-        self.store.bn_guard.poll()
+        if self.encoder.bn_mode == "inference":
+            if self.store.bn_guard is None:          # z kept for BN layers with gamma ~ 0
+                self.store.bn_guard = ops.BNZGuard(self.conv_layers())
+            self.store.bn_guard.poll()
         self._packer.ensure()                        # all conv weights packed in one launch
         imgs = ops.split_pair(batch_imgs)            # image1s then image2s (model.py:122-123)
-        feats = self.encoder.forward4(imgs)          # shared encoder, both images (P12)
+        # shared encoder, both images (P12); training-mode BN: two calls' statistics
+        feats = self.encoder.forward4(imgs, groups=2)
         flows = []
         prev = None
         L = self.levels
@@ -426,13 +470,13 @@ class FlowNet:
 
 
 def build_flow_net(height, width, pretrained_weights_path=None, max_disp=3, seed=0,
-                   device="cuda", precision="fp32", levels=4):
+                   device="cuda", precision="fp32", levels=4, bn_mode="inference"):
     """model.py:119-143.  ``pretrained_weights_path``: the stand-alone ResNet18 encoder's
     weights, as a TF checkpoint (Keras object-based keys, checkpoint.py) or an .npz of
     encoder parameter names; like the reference (model.py:128-129) every encoder weight must
     be matched."""
     net = FlowNet(height, width, max_disp, seed=seed, device=device, precision=precision,
-                  levels=levels)
+                  levels=levels, bn_mode=bn_mode)
     if pretrained_weights_path is not None:
         enc_names = [p.name for p in encoder_spec(levels)]
         if (os.path.exists(pretrained_weights_path + ".index")

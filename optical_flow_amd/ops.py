@@ -184,6 +184,14 @@ def _side_join():
     global _side_armed
     _side_armed = False
     side_join_now()
+    # buffers read by side-stream kernels of this backward go back to their pools only now,
+    # after the current stream has been ordered behind those streams (FlowGrad.release)
+    while _DEFERRED_RELEASE:
+        key, buf = _DEFERRED_RELEASE.pop()
+        FlowGrad._pool.setdefault(key, []).append(buf)
+
+
+_DEFERRED_RELEASE = []
 
 
 def side_join_now():
@@ -343,6 +351,7 @@ class ConvLayer:
         self._mode = None
         self.f32_split = F32_SPLIT if f32_split is None else bool(f32_split)
         self.store_z = False              # BN layers: keep z for the backward (BNZGuard)
+        self.bn_train = False             # BN in training mode (bn_mode="training", P5)
 
     def desc(self, n, h, w) -> ConvDesc:
         key = (n, h, w)
@@ -396,7 +405,7 @@ class ConvLayer:
         if self._wf is None:
             self.alloc_packed(d)
         if key != self._pack_key or self.version_of is None:
-            if self.bn is not None:       # BN scale folded into the dgrad image (see _bn_backward)
+            if self.bn is not None and not self.bn_train:   # BN scale folded (_conv_backward)
                 call("of_conv_pack_weights_bn", C.byref(d), self.mode(d), _ptr(self.kernel),
                      _ptr(self._wf), _ptr(self._wd), _ptr(self.bn[0]), _ptr(self.bn[3]),
                      BN_EPS, _stream())
@@ -466,7 +475,7 @@ class ConvPacker:
             wp[i], fp[i], bp[i] = L.kernel.data_ptr(), L._wf.data_ptr(), L._wd.data_ptr()
         gp, vp = (C.c_void_p * n)(), (C.c_void_p * n)()
         for i, L in enumerate(self.layers):
-            if L.bn is not None:
+            if L.bn is not None and not L.bn_train:      # training-mode BN: plain weights
                 gp[i], vp[i] = L.bn[0].data_ptr(), L.bn[3].data_ptr()
         nbytes = lib.of_conv_pack_table_bytes(n)
         host = (C.c_char * nbytes)()
@@ -530,7 +539,7 @@ class BNZGuard:
 
     def _apply(self, mins, thr):
         for L, m in zip(self.layers, mins):
-            if m < thr:
+            if not m >= thr:            # (a NaN gamma is flagged too)
                 L.store_z = True
                 self.flagged.add(L.name)
 
@@ -590,9 +599,11 @@ def _pad_channels(t: torch.Tensor, cp: int) -> torch.Tensor:
     return out
 
 
-def _conv_forward(layer: "ConvLayer", x, residual=None):
+def _conv_forward(layer: "ConvLayer", x, residual=None, stream=None):
     """Conv2D + BiasAdd [+ FusedBatchNorm(inference)] [+ AddV2 residual] [+ Relu/LeakyRelu]:
-    one fused kernel.  Returns (y, z); z = the pre-BN conv output (BN layers only)."""
+    one fused kernel.  Returns (y, z); z = the pre-BN conv output (BN layers only).
+    stream: launch on this stream instead of the current one (the outputs are allocated on
+    the current stream, which must wait for ``stream`` before reading them)."""
     _check_dev(x, residual)
     n, h, w, cx = x.shape
     assert cx == layer.cin_p, "conv %s: input has %d channels, expected %d (cin_p)" % (
@@ -610,12 +621,53 @@ def _conv_forward(layer: "ConvLayer", x, residual=None):
     _tag(layer, 0)
     entry, wsz = layer.fwd_entry(d)
     wsk, wsp, wsb = _workspace(wsz, x.device)
+    st = _stream()
+    if stream is not None:
+        for t in (x, y, z, wsk, residual):
+            if t is not None:
+                t.record_stream(stream)
+        st = C.c_void_p(stream.cuda_stream)
     call(entry, C.byref(d), _ptr(x), cx, _ptr(wf), _ptr(layer.bias),
          _ptr(bn[0]) if bn else None, _ptr(bn[1]) if bn else None,
          _ptr(bn[2]) if bn else None, _ptr(bn[3]) if bn else None, BN_EPS,
          _ptr(residual), layer.cout, layer.act, layer.alpha,
-         _ptr(z), layer.cout, _ptr(y), layer.cout, wsp, wsb, _stream())
+         _ptr(z), layer.cout, _ptr(y), layer.cout, wsp, wsb, st)
     return y, z
+
+
+# The encoder's 1x1 stride-2 projections (res3_0 / res4_0 proj, model.py:20,22) read the same
+# block input as conv_a and are independent of it until conv_b adds them: their forward runs on
+# a stream of its own beside conv_a (a 0.8-GFLOP conv is launch/latency-bound on its own).
+# OFLOW_PROJ_SIDE=0 keeps them on the current stream.
+PROJ_SIDE = os.environ.get("OFLOW_PROJ_SIDE", "1") == "1"
+_FWD_SIDE = {}
+
+
+def _fwd_side_stream():
+    """The forward's side stream of the current device, ordered after the current stream's
+    work so far (no end-of-backward join: the caller waits for it, stream_wait)."""
+    cur = torch.cuda.current_stream()
+    s = _FWD_SIDE.get(cur.device)
+    if s is None:
+        s = _FWD_SIDE[cur.device] = torch.cuda.Stream(cur.device)
+    stream_wait(s, cur)
+    return s
+
+
+def _block_forward(a, b, p, x):
+    """One residual block's forward: (ya, za, y, zb, yp, zp)."""
+    yp = zp = None
+    side = None
+    if p is not None and PROJ_SIDE and x.is_cuda:
+        side = _fwd_side_stream()
+        yp, zp = _conv_forward(p, x, stream=side)
+    ya, za = _conv_forward(a, x)
+    if p is not None and side is None:
+        yp, zp = _conv_forward(p, x)
+    if side is not None:
+        stream_wait(torch.cuda.current_stream(), side)
+    y, zb = _conv_forward(b, ya, residual=yp if p is not None else x)
+    return ya, za, y, zb, yp, zp
 
 
 def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx_out=None,
@@ -821,13 +873,7 @@ class _ResBlockFn(torch.autograd.Function):
     def forward(ctx, x, *args):
         a, b, p = args[-1]
         x = x.contiguous()
-        ya, za = _conv_forward(a, x)
-        yp = zp = None
-        sc = x
-        if p is not None:
-            yp, zp = _conv_forward(p, x)
-            sc = yp
-        y, zb = _conv_forward(b, ya, residual=sc)
+        ya, za, y, zb, yp, zp = _block_forward(a, b, p, x)
         ctx.block = (a, b, p)
         ctx.save_for_backward(x, ya, za, y, zb, yp, zp)
         return y
@@ -897,13 +943,7 @@ class _EncoderFn(torch.autograd.Function):
         saved = [x4, y0, z0]
         outs = [y0]
         for i, (a, b, p) in enumerate(blocks):
-            ya, za = _conv_forward(a, x)
-            yp = zp = None
-            sc = x
-            if p is not None:
-                yp, zp = _conv_forward(p, x)
-                sc = yp
-            y, zb = _conv_forward(b, ya, residual=sc)
+            ya, za, y, zb, yp, zp = _block_forward(a, b, p, x)
             saved += [x, ya, za, y, zb, yp, zp]
             x = y
             if i % 2 == 1:
@@ -962,6 +1002,121 @@ class _EncoderFn(torch.autograd.Function):
                                            (False, nk, nbias, ng, nbe, False), dz_given=dz0)
         stem = [gk, tbias[2], tg[2], tb[2]]
         return (None, *stem, *grads, None)
+
+
+# ------------------------------------------------- BatchNormalization, training mode ----
+# bn_mode="training" (SURVEY.md §8 P5): keras BatchNormalization(training=True) as the legacy
+# loop calls it (old/train.py:59); the reference's own train.py:51 runs inference mode, the
+# default above.  Each BN layer normalises with the statistics of the batch it is called on --
+# per Siamese half (``groups`` = 2 on the (2B) encoder batch: model.py:131-132 calls the
+# encoder once per image) -- and updates its moving statistics in place (momentum 0.99, Keras'
+# default).  The conv writes z (bias included, no BN epilogue), of_bn_train_stats /
+# of_bn_train_apply normalise, and the backward is FusedBatchNormGradV3's (of_bn_train_bwd)
+# followed by the plain conv gradients of dz: nothing of the inference path's BN fold applies.
+# Not the benchmarked configuration: one autograd node per conv, gradients summed by autograd.
+BN_MOMENTUM = 0.99
+
+
+class _ConvBNTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kernel, bias, gamma, beta, residual, layer: ConvLayer, groups: int):
+        _check_dev(x, kernel, bias, residual)
+        x = x.contiguous()
+        n, h, w, cx = x.shape
+        assert cx == layer.cin_p and layer.bn is not None and layer.bn_train
+        d = layer.desc(n, h, w)
+        wf, _ = layer.packed(d)
+        z = torch.empty((n, d.ho, d.wo, layer.cout), device=x.device)
+        entry, wsz = layer.fwd_entry(d)
+        wsk, wsp, wsb = _workspace(wsz, x.device)
+        s = _stream()
+        _tag(layer, 0)
+        call(entry, C.byref(d), _ptr(x), cx, _ptr(wf), _ptr(layer.bias), None, None, None, None,
+             BN_EPS, None, layer.cout, ACT_NONE, 0.0, None, layer.cout, _ptr(z), layer.cout, wsp,
+             wsb, s)
+        npix, c = n * d.ho * d.wo, layer.cout
+        assert n % groups == 0
+        g_, be, mm, mv = layer.bn
+        mean = torch.empty((groups, c), device=x.device)
+        invstd = torch.empty((groups, c), device=x.device)
+        ws = torch.empty(_lib.lib().of_bn_train_workspace(npix, c, groups) // 4 + 1,
+                         device=x.device)
+        call("of_bn_train_stats", npix, c, groups, _ptr(z), BN_EPS, BN_MOMENTUM, _ptr(mean),
+             _ptr(invstd), _ptr(mm), _ptr(mv), _ptr(ws), s)
+        if residual is not None:
+            residual = residual.contiguous()
+            assert residual.shape == z.shape
+        y = torch.empty_like(z)
+        call("of_bn_train_apply", npix, c, groups, _ptr(z), _ptr(mean), _ptr(invstd), _ptr(g_),
+             _ptr(be), _ptr(residual), layer.act, _ptr(y), s)
+        ctx.layer, ctx.groups = layer, groups
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, z, y, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, y, mean, invstd = ctx.saved_tensors
+        layer, groups = ctx.layer, ctx.groups
+        need_x, need_k, need_b, need_g, need_be, need_res = ctx.needs_input_grad[:6]
+        dy = dy.contiguous()
+        n, h, w, cx = x.shape
+        d = layer.desc(n, h, w)
+        _, wd = layer.packed(d)
+        npix, c = n * d.ho * d.wo, layer.cout
+        s = _stream()
+        g_ = layer.bn[0]
+        tg = grad_target(g_) if need_g else (None, 0, None)
+        tb = grad_target(layer.bn[1]) if need_be else (None, 0, None)
+        acc = tg[1] if need_g else tb[1]
+        assert tb[0] is None or tb[1] == acc
+        dz = torch.empty_like(z)
+        t = torch.empty_like(z) if (ctx.has_res and need_res) else None
+        ws = torch.empty(_lib.lib().of_bn_train_workspace(npix, c, groups) // 4 + 1,
+                         device=z.device)
+        call("of_bn_train_bwd", npix, c, groups, layer.act, _ptr(dy), _ptr(y), _ptr(z),
+             _ptr(mean), _ptr(invstd), _ptr(g_), _ptr(dz), _ptr(t), _ptr(tg[0]), _ptr(tb[0]),
+             acc, _ptr(ws), s)
+        ret_k = ret_b = dx = None
+        if need_k or need_b:
+            tk = grad_target(layer.kernel)
+            tbias = grad_target(layer.bias)
+            assert tk[1] == tbias[1]
+            went, wsb = layer.wgrad_entry(d)
+            wsw = torch.empty(wsb // 4 + 1, device=z.device)
+            _tag(layer, 2)
+            call(went, C.byref(d), _ptr(x), cx, _ptr(dz), c, _ptr(tk[0]), _ptr(tbias[0]), tk[1],
+                 _ptr(wsw), wsb, s)
+            ret_k, ret_b = tk[2], tbias[2]
+            _grad_ready(layer.kernel, layer.bias, g_, layer.bn[1])
+        if need_x:
+            dx = torch.empty_like(x)
+            entry, wsz = layer.dgrad_entry(d)
+            wsk, wsp, wsb = _workspace(wsz, z.device)
+            _tag(layer, 1)
+            call(entry, C.byref(d), _ptr(dz), c, _ptr(wd), None, 0, ACT_NONE, 0.0, _ptr(dx), cx,
+                 wsp, wsb, s)
+        return dx, ret_k, ret_b, tg[2], tb[2], t, None, None
+
+
+def conv_bn_train(layer: ConvLayer, x, residual=None, groups: int = 1):
+    """Conv2D + BiasAdd + BatchNormalization(training=True) [+ residual] [+ activation]."""
+    g_, be = layer.bn[0], layer.bn[1]
+    return _ConvBNTrainFn.apply(x, layer.kernel, layer.bias, g_, be, residual, layer, groups)
+
+
+def encoder_forward_train(x4, conv1: ConvLayer, blocks, groups: int = 2):
+    """reset18_encoder (model.py:10-26) with BN in training mode: [out0, out1, ...]."""
+    y = conv_bn_train(conv1, x4, groups=groups)
+    outs = [y]
+    x = maxpool2(y)
+    for i, (a, b, p) in enumerate(blocks):
+        ya = conv_bn_train(a, x, groups=groups)
+        sc = conv_bn_train(p, x, groups=groups) if p is not None else x
+        x = conv_bn_train(b, ya, residual=sc, groups=groups)
+        if i % 2 == 1:
+            outs.append(x)
+    return outs
 
 
 def encoder_forward(x4, conv1: ConvLayer, blocks):
@@ -1043,7 +1198,7 @@ def _stack_fwd_img16(layers, x):
     s = _stream()
     x16 = getattr(x, "_of_img16", None)   # written by corr_concat directly
     if x16 is None:
-        x16 = _to_img16(x, (cx + 31) // 32 * 32)
+        x16 = _to_img16(x.contiguous(), (cx + 31) // 32 * 32)
     imgs, masks = [x16], []
     cur = x16
     for i, layer in enumerate(layers[:-2]):
@@ -1180,13 +1335,17 @@ class _ConvStackFn(torch.autograd.Function):
         args = args[:-1]
         n = len(layers)
         _check_dev(x)
-        x = x.contiguous()
         ctx.img16 = _img16_ok(layers, x)
         if ctx.img16:
             saved, out = _stack_fwd_img16(layers, x)
             ctx.layers = layers
             ctx.save_for_backward(*saved)
             return out
+        if getattr(x, "_of_img16", None) is not None:
+            # corr_concat wrote only the bf16 image (its fp32 output is a placeholder)
+            raise RuntimeError("conv stack: the input carries only a bf16 concat image, but "
+                               "this stack does not run on images")
+        x = x.contiguous()
         s = _stream()
         acts = [x]
         for i, layer in enumerate(layers):
@@ -1398,7 +1557,12 @@ class _CorrConcat(torch.autograd.Function):
         nk = (2 * max_disp + 1) ** 2
         used = c + nk + (2 if flow_up is not None else 0)
         assert used <= cp
-        x = torch.empty((n, h, w, cp), device=f1.device)
+        if img is not None:
+            # the fp32 row is never written on this path: a zero-stride placeholder of the
+            # row's shape is the autograd output (no (n, h, w, cp) allocation per level)
+            x = torch.empty((1, 1, 1, 1), device=f1.device).expand(n, h, w, cp)
+        else:
+            x = torch.empty((n, h, w, cp), device=f1.device)
         ctx.dst = (grad_dst(f1), grad_dst(f2w))
         fu = flow_up.contiguous() if flow_up is not None else None
         if img is not None:
@@ -1661,9 +1825,17 @@ class FlowGrad:
         return self._buf
 
     def release(self):
-        """Return the buffer to the pool (its consumers are enqueued; channels 2-3 stay 0)."""
+        """Return the buffer to the pool (its consumers are enqueued; channels 2-3 stay 0).
+        Inside a backward that forked side streams the head's weight gradient may still read
+        the buffer there, and the next pop would write it on the current stream with nothing
+        ordering the two (two forwards, one backward: loss 1's FlowGrad pops the buffer that
+        forward 2's backward released).  The buffer is then pooled at the end-of-backward
+        join (_side_join), after the current stream waits for the side streams."""
         if self._buf is not None:
-            FlowGrad._pool.setdefault(self._key(), []).append(self._buf)
+            if _side_armed:
+                _DEFERRED_RELEASE.append((self._key(), self._buf))
+            else:
+                FlowGrad._pool.setdefault(self._key(), []).append(self._buf)
             self._buf = None
 
     def __del__(self):

@@ -147,19 +147,39 @@ class GraphedStep:
             for i in range(warmup):                  # capture rule), creates the side streams
                 trainer.train_step(batch_imgs, i)
         cur.wait_stream(s)
+        self.captures = 0
+        self._capture(capture_ctx)
+
+    def _capture(self, capture_ctx=None):
         self.graph = torch.cuda.CUDAGraph()
         with capture_ctx() if capture_ctx is not None else contextlib.nullcontext():
             with torch.cuda.graph(self.graph):
-                self.loss, self.flows = trainer.train_step(batch_imgs)
+                self.loss, self.flows = self.trainer.train_step(self.batch)
+        self.captures += 1
 
     def load(self, batch_imgs):
         self.batch.copy_(batch_imgs, non_blocking=True)
 
     def __call__(self, batch_imgs=None, step_count=0):
+        """One replay.  The BN gamma guard (ops.BNZGuard) is driven from here: the captured
+        step bakes in which BN layers store z, so every BNZGuard.EVERY replays the guard's
+        min |gamma| check is launched after the replay (read back asynchronously), and when a
+        check flags a new layer the step is captured again before the next replay, so that
+        layer's backward reads the stored z instead of recovering it through gamma ~ 0."""
+        store = self.trainer.flow_net.store
+        guard = store.bn_guard
+        if guard is not None and guard.layers:
+            before = len(guard.flagged)
+            guard.poll()
+            if len(guard.flagged) != before:
+                torch.cuda.synchronize()
+                self._capture()
         if batch_imgs is not None and batch_imgs.data_ptr() != self.batch.data_ptr():
             self.load(batch_imgs)
         self.graph.replay()
-        self.trainer.flow_net.store.version += 1
+        store.version += 1
+        if guard is not None:
+            guard.after_update(self.trainer.optimizer.learning_rate)
         return self.loss, self.flows
 
 

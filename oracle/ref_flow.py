@@ -136,6 +136,44 @@ class _Bf16ConvBN(torch.autograd.Function):
         return xv.grad, dw, db, dgamma, dbeta, None, None, None
 
 
+# BatchNormalization mode of the build under test: "inference" -- the
+# reference's train.py:51 calls flow_net(batch_imgs) without training=True -- or "training",
+# the legacy loop's model(images, training=True) (old/train.py:59).
+BN_MODE = "inference"
+BN_MOMENTUM = 0.99       # keras BatchNormalization default momentum
+
+
+def set_bn_mode(m):
+    global BN_MODE
+    assert m in ("inference", "training"), m
+    BN_MODE = m
+
+
+def batchnorm_training(x, p: Dict[str, torch.Tensor], prefix: str):
+    """keras BatchNormalization called with training=True (old/train.py:59), on Keras' fused
+    path (FusedBatchNormV3, is_training): normalise with this call's batch mean and BIASED
+    variance over (N, H, W), eps=1e-3; the moving statistics are updated in place as the fused
+    op does with exponential_avg_factor f = 1 - momentum: moving = (1 - f) moving + f stat,
+    the variance with Bessel's correction n / (n - 1).  Gradients flow through the batch
+    statistics (FusedBatchNormGradV3)."""
+    g, be = p[prefix + "/gamma"], p[prefix + "/beta"]
+    red = tuple(range(x.dim() - 1))
+    mu = x.mean(dim=red)
+    var = ((x - mu) ** 2).mean(dim=red)
+    n = x.numel() // x.shape[-1]
+    with torch.no_grad():
+        f = 1.0 - BN_MOMENTUM
+        mm, mv = p[prefix + "/moving_mean"], p[prefix + "/moving_variance"]
+        mm.copy_((1 - f) * mm + f * mu.detach().to(mm.dtype))
+        mv.copy_((1 - f) * mv + f * (var.detach() * (n / max(n - 1, 1))).to(mv.dtype))
+    return (x - mu) / torch.sqrt(var + BN_EPS) * g + be
+
+
+def batchnorm(x, p, prefix):
+    return batchnorm_training(x, p, prefix) if BN_MODE == "training" else \
+        batchnorm_inference(x, p, prefix)
+
+
 def batchnorm_inference(x, p: Dict[str, torch.Tensor], prefix: str):
     """keras BatchNormalization called with training unset -> inference mode: moving
     statistics, eps=1e-3, no statistic update; gamma/beta trainable (P5; train.py:51)."""
@@ -155,6 +193,9 @@ def maxpool2(x):
 
 # -------------------------------------------------------------------------- encoder ----
 def _conv_bn(x, p, conv, bn, stride):
+    if BN_MODE == "training":      # batch statistics: the plain conv, then the BN (P5)
+        return batchnorm_training(conv2d_same(x, p[conv + "/kernel"], p[conv + "/bias"], stride),
+                                  p, bn)
     if CONV_PRECISION == "bf16":
         return _Bf16ConvBN.apply(x, p[conv + "/kernel"], p[conv + "/bias"], p[bn + "/gamma"],
                                  p[bn + "/beta"], p[bn + "/moving_mean"],
@@ -175,7 +216,7 @@ def resnet_block(x, p, prefix, stride, proj):
 def encoder(x, p, blocks):
     """reset18_encoder (model.py:10-26) -> [H/2 x64, H/4 x64, H/8 x128, H/16 x256]."""
     x = conv2d_same(x, p["ResNet18/conv1/kernel"], p["ResNet18/conv1/bias"], 2)
-    x = torch.relu(batchnorm_inference(x, p, "ResNet18/layer1_bn"))
+    x = torch.relu(batchnorm(x, p, "ResNet18/layer1_bn"))
     outs = [x]
     x = maxpool2(x)
     for i, (prefix, cin, cout, stride, proj) in enumerate(blocks):

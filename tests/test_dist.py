@@ -157,3 +157,116 @@ def test_bucket_allreduce_on_collective_stream(monkeypatch):
         k = calls.index(("comm_stream", ar[i][1]))
         assert calls[k + 1] == ar[i]
     assert held in red.buckets[-1]
+
+
+# ---------------------------------------------------------------------------------------------
+# N > 1 communicator set-up without hardware: the joint fallback vote and the
+# deadlines, with the RCCL communicator replaced by fakes (an RCCL communicator needs one GPU
+# per rank; these paths are host logic).
+class _FakeRccl:
+    kind = "rccl"
+
+    def __init__(self, rank, world, timeout=None, **kw):
+        if rank == 1:
+            raise RuntimeError("simulated of_comm_init failure on rank 1")
+        self.rank, self.world, self.closed = rank, world, None
+
+    def close(self, abort=False):
+        self.closed = abort
+
+
+def _vote_worker(rank, world, port, q, mode):
+    try:
+        _init(rank, world, port)
+        from optical_flow_amd import comm as CM
+        CM.RcclComm = _FakeRccl
+        CM.selftest = lambda c, r, w: True
+        if mode == "fallback":
+            c = CM.make_comm("rccl", rank, world, fallback="torch", timeout=30)
+            t = torch.full((4,), float(rank + 1))
+            c.allreduce_(t)
+            c.wait()
+            q.put((rank, c.kind, float(t[0])))
+        else:                              # "timeout": rank 1 never votes
+            if rank == 0:
+                try:
+                    CM.make_comm("rccl", rank, world, fallback="torch", timeout=2)
+                    q.put((rank, "no error", None))
+                except CM.CommError as e:
+                    q.put((rank, "CommError", str(e)[:80]))
+            else:
+                q.put((rank, "skipped", None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None))
+
+
+def _run2(target, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=target, args=(r, 2, port, q) + args) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    return res
+
+
+def test_make_comm_joint_fallback():
+    """comm.make_comm's vote (through the rendezvous store, not a collective): the RCCL
+    communicator fails on rank 1 only, and BOTH ranks must end on the same fallback -- whose
+    all-reduce then works (1 + 2 = 3)."""
+    res = _run2(_vote_worker, "fallback")
+    assert res == [(0, "torch", 3.0), (1, "torch", 3.0)], res
+
+
+def test_make_comm_vote_deadline():
+    """A rank that never reaches the vote makes the other one raise CommError after the
+    deadline instead of blocking forever."""
+    res = _run2(_vote_worker, "timeout")
+    assert res[0][:2] == (0, "CommError"), res
+    assert res[1][:2] == (1, "skipped"), res
+
+
+def test_comm_watchdog():
+    """comm.CommWatchdog: a completion predicate that never turns true expires after the
+    timeout (on_expire is called once, check() raises CommError in the caller's thread); one
+    that completes is dropped; an asynchronous communicator error fails at once."""
+    import time
+    from optical_flow_amd.comm import CommError, CommWatchdog
+    seen = []
+    w = CommWatchdog(0.3, seen.append, poll_s=0.005)
+    w.watch(lambda: True)
+    t0 = time.monotonic()
+    while w.pending() and time.monotonic() - t0 < 5:
+        time.sleep(0.01)
+    assert w.pending() == 0 and w.failed is None
+    w.check()
+    w.watch(lambda: False)
+    while w.failed is None and time.monotonic() - t0 < 5:
+        time.sleep(0.01)
+    assert len(seen) == 1 and "did not complete" in seen[0]
+    with pytest.raises(CommError):
+        w.check()
+    w.close()
+    seen2 = []
+    w2 = CommWatchdog(60, seen2.append, poll_s=0.005, error_probe=lambda: "RCCL failed: x")
+    w2.watch(lambda: False)
+    t0 = time.monotonic()
+    while w2.failed is None and time.monotonic() - t0 < 5:
+        time.sleep(0.01)
+    assert seen2 == ["RCCL failed: x"]
+    w2.close()
+
+
+def test_vote_single_process_store():
+    """comm.vote over a store: all ok -> True, one not ok -> False (a HashStore, world 1 and
+    a pre-set second vote)."""
+    from optical_flow_amd.comm import vote
+    st = dist.HashStore()
+    assert vote(st, "t1", 0, 1, True, timeout=2) is True
+    st.set("t2/1", b"0")
+    assert vote(st, "t2", 0, 2, True, timeout=2) is False

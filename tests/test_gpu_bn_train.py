@@ -1,0 +1,183 @@
+"""BatchNormalization in training mode (bn_mode="training"): the legacy loop's
+model(images, training=True) (old/train.py:59) -- batch statistics per encoder call, moving
+statistics updated -- against the oracle's batchnorm_training (oracle/ref_flow.py), kernel by
+kernel (of_bn_train_*) and for the whole flow net's train step at 64x128.  The reference's own
+train.py:51 runs inference mode, the build default (every other test)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import REL_TOL, dev, rel_inf, rel_l2
+from oracle import ref_flow as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _bn_ref(z, gamma, beta, res, act, groups, mm, mv):
+    """Oracle forward per group (each group one encoder call) + the moving-stat updates."""
+    outs = []
+    p = {"L/gamma": gamma, "L/beta": beta, "L/moving_mean": mm, "L/moving_variance": mv}
+    R.set_bn_mode("training")
+    try:
+        for zg in z.chunk(groups, 0):
+            outs.append(R.batchnorm_training(zg, p, "L"))
+    finally:
+        R.set_bn_mode("inference")
+    u = torch.cat(outs, 0)
+    if res is not None:
+        u = u + res
+    return torch.relu(u) if act == 1 else u
+
+
+@pytest.mark.parametrize("groups,act,with_res,c", [(1, 0, False, 64), (2, 1, True, 128),
+                                                   (2, 1, False, 256), (1, 1, True, 64)])
+def test_bn_train_kernels(groups, act, with_res, c):
+    """of_bn_train_stats / _apply / _bwd against the oracle in float64: output, moving statistics,
+    dz, the residual's gradient t, dgamma and dbeta within 1e-3 (rows of 2 x 3 x 37 x 41 pixels:
+    not a multiple of the kernels' row blocks)."""
+    from optical_flow_amd import _lib, ops
+    from optical_flow_amd._lib import call
+    g = torch.Generator().manual_seed(c + groups)
+    n, h, w = 2 * groups, 37, 41
+    z0 = torch.randn(n, h, w, c, generator=g, dtype=torch.float64) * 3 + 1.5
+    gamma0 = torch.rand(c, generator=g, dtype=torch.float64) + 0.5
+    beta0 = torch.randn(c, generator=g, dtype=torch.float64)
+    res0 = torch.randn(n, h, w, c, generator=g, dtype=torch.float64) if with_res else None
+    mm0 = torch.randn(c, generator=g, dtype=torch.float64) * 0.1
+    mv0 = torch.rand(c, generator=g, dtype=torch.float64) + 0.5
+    dy0 = torch.randn(n, h, w, c, generator=g, dtype=torch.float64)
+    # oracle (float64 autograd through the batch statistics)
+    zr = z0.float().double().requires_grad_(True)
+    gr = gamma0.float().double().requires_grad_(True)
+    br = beta0.float().double().requires_grad_(True)
+    rr = res0.float().double().requires_grad_(True) if with_res else None
+    mmr, mvr = mm0.float().double().clone(), mv0.float().double().clone()
+    yr = _bn_ref(zr, gr, br, rr, act, groups, mmr, mvr)
+    yr.backward(dy0.float().double())
+    # HIP
+    npix = n * h * w
+    z, gamma, beta = dev(z0.float()), dev(gamma0.float()), dev(beta0.float())
+    res = dev(res0.float()) if with_res else None
+    mm, mv = dev(mm0.float()), dev(mv0.float())
+    mean = torch.empty(groups, c, device="cuda")
+    invstd = torch.empty(groups, c, device="cuda")
+    ws = torch.empty(_lib.lib().of_bn_train_workspace(npix, c, groups) // 4 + 1, device="cuda")
+    P = ops._ptr
+    s = ops._stream()
+    call("of_bn_train_stats", npix, c, groups, P(z), R.BN_EPS, R.BN_MOMENTUM, P(mean), P(invstd),
+         P(mm), P(mv), P(ws), s)
+    y = torch.empty_like(z)
+    call("of_bn_train_apply", npix, c, groups, P(z), P(mean), P(invstd), P(gamma), P(beta), P(res),
+         act, P(y), s)
+    dy = dev(dy0.float())
+    dz = torch.empty_like(z)
+    t = torch.empty_like(z)
+    dg = torch.zeros(c, device="cuda")
+    db = torch.zeros(c, device="cuda")
+    call("of_bn_train_bwd", npix, c, groups, act, P(dy), P(y), P(z), P(mean), P(invstd), P(gamma),
+         P(dz), P(t), P(dg), P(db), 1, P(ws), s)
+    torch.cuda.synchronize()
+    errs = {"y": rel_inf(y, yr), "moving_mean": rel_inf(mm, mmr), "moving_var": rel_inf(mv, mvr),
+            "dz": rel_l2(dz, zr.grad), "dgamma": rel_l2(dg, gr.grad), "dbeta": rel_l2(db, br.grad)}
+    if with_res:
+        errs["t"] = rel_l2(t, rr.grad)
+    print(groups, act, with_res, c, {k: "%.2e" % v for k, v in errs.items()})
+    bad = {k: v for k, v in errs.items() if not v < REL_TOL}
+    assert not bad, bad
+    # bitwise reproducible (fixed-order reductions)
+    dz2 = torch.empty_like(z)
+    call("of_bn_train_bwd", npix, c, groups, act, P(dy), P(y), P(z), P(mean), P(invstd), P(gamma),
+         P(dz2), None, None, None, 0, P(ws), s)
+    torch.cuda.synchronize()
+    assert torch.equal(dz, dz2)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_flow_net_bn_training(precision):
+    """The whole flow net with bn_mode="training" at 64x128, B=2: flows, loss and all 108 weight
+    gradients against the oracle's train step in training mode (float64; bf16: the oracle with
+    the bf16 operand rounding, at the whole-net bf16 bounds of test_flow_net_bf16), and the
+    moving statistics of every BN layer after the step (updated once per encoder call, image1s
+    then image2s) within 1e-5 of the oracle's."""
+    from optical_flow_amd.data import synthetic_batch
+    from optical_flow_amd.loss import LossLayer
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params, perturb_params
+    H, W, B = 64, 128, 2
+    vals = perturb_params(init_params(flow_net_spec(), 21), 22)
+    batch = synthetic_batch(B, H, W, seed=4321)
+    net = FlowNet(H, W, values=vals, precision=precision, bn_mode="training")
+    p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+    R.set_bn_mode("training")
+    R.set_conv_precision(precision)
+    try:
+        loss_o, flows_o, grads_o = R.train_step(torch.tensor(batch, dtype=torch.float64), p,
+                                                list(encoder_blocks()), None)
+    finally:
+        R.set_bn_mode("inference")
+        R.set_conv_precision("fp32")
+    net.store.zero_grad()
+    bd = dev(torch.from_numpy(batch))
+    flows = net(bd)
+    loss = LossLayer()(bd, flows)
+    loss.backward()
+    torch.cuda.synchronize()
+    lrel = abs(float(loss) - loss_o.item()) / abs(loss_o.item())
+    frel = [rel_inf(flows[k], flows_o[k]) for k in range(4)]
+    print("%s loss rel %.2e, flows rel_inf %s" % (precision, lrel, ["%.1e" % e for e in frel]))
+    errs = {n: rel_l2(g, grads_o[n]) for n, g in net.store.grads().items()}
+    worst = max(errs.items(), key=lambda kv: kv[1])
+    med = float(np.median(list(errs.values())))
+    print("grads: median %.2e, worst %.2e (%s)" % (med, worst[1], worst[0]))
+    mstat = max(rel_inf(net.store.params[n], p[n]) for n in p
+                if n.endswith(("moving_mean", "moving_variance")))
+    print("moving statistics: worst rel_inf %.2e" % mstat)
+    assert mstat < 1e-5
+    assert all(torch.isfinite(g).all() for g in net.store.grads().values())
+    if precision == "fp32":
+        assert lrel < REL_TOL
+        assert max(frel) < REL_TOL, frel
+        assert worst[1] < REL_TOL, worst
+    else:   # test_flow_net_bf16's statistical bounds
+        assert lrel < 3e-2
+        assert max(frel) < 3e-2, frel
+        assert med < 8e-2 and worst[1] < 2.5e-1, (med, worst)
+
+
+def test_bn_mode_switch_and_graph():
+    """FlowNet.set_bn_mode switches both ways (inference results unchanged after a training
+    step's moving-statistics update is undone), and a training-mode train step replays from a
+    captured graph like the eager step (deterministic warp backward: bitwise)."""
+    from optical_flow_amd import ops
+    from optical_flow_amd.data import synthetic_batch
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import flow_net_spec, init_params, perturb_params
+    from optical_flow_amd.train import KerasAdam, Trainer
+    H, W, B = 64, 128, 2
+    vals = perturb_params(init_params(flow_net_spec(), 5), 6)
+    b = [dev(torch.from_numpy(synthetic_batch(B, H, W, seed=70 + i))) for i in range(3)]
+    with ops.deterministic(True):
+        ga = Trainer(FlowNet(H, W, values=vals, bn_mode="training"), None)
+        ea = Trainer(FlowNet(H, W, values=vals, bn_mode="training"), None)
+        step = ga.graphed(b[0].clone(), warmup=1)
+        ea.train_step(b[0])                              # same state: one step each
+        for k in (1, 2):
+            le, _ = ea.train_step(b[k])
+            lg, _ = step(b[k])
+            torch.cuda.synchronize()
+            assert float(le) == float(lg)
+            assert torch.equal(ea.flow_net.store.grad_arena, ga.flow_net.store.grad_arena)
+            assert torch.equal(ea.flow_net.store.buffers, ga.flow_net.store.buffers)
+    net = FlowNet(H, W, values=vals)
+    with torch.no_grad():
+        f0 = [f.clone() for f in net(b[0])]
+        net.set_bn_mode("training")
+        net(b[0])
+        assert net.bn_mode == "training"
+        net.set_bn_mode("inference")
+        net.store.load(vals)                             # moving statistics back
+        f1 = net(b[0])
+    for a, c in zip(f0, f1):
+        assert torch.equal(a, c)

@@ -152,5 +152,9 @@ def test_rccl_dp_step_world1(precision, H, W, B, det):
     if det:
         assert torch.equal(got, ref), err
     else:
-        assert err < 1e-5, err
+        # the atomic warp backward's add order differs between the two steps; in bf16 one
+        # fp32-ulp difference can flip the bf16 rounding of a gradient the next conv reads, a
+        # 2^-8 step (measured up to 1.6e-4 rel_l2, test_gpu_graph.py): the bound is per
+        # precision, the det case above is the exact check
+        assert err < (1e-5 if precision == "fp32" else 3e-4), err
     comm.close()

@@ -112,3 +112,44 @@ def _graph_vs_eager(precision, comm, det):
     assert gt.optimizer.iterations == 5
     if c is not None:
         c.close()
+
+
+def test_graph_bn_guard_recapture():
+    """The BN gamma guard in graphed training: the captured step bakes in which BN
+    layers store z (ops.BNZGuard), so GraphedStep drives the guard itself -- a min |gamma|
+    check every BNZGuard.EVERY replays, read back asynchronously -- and captures the step again
+    once a check flags a new layer.  A gamma set to 0 between replays must be flagged within
+    EVERY + LAG_MAX replays, the step re-captured, and the next replay must then equal an eager
+    step from the same state bitwise (deterministic warp backward), with finite gradients.
+    (The gamma is set to 3e-3, under the guard's 1e-2 threshold: the guard exists to switch a
+    layer while its gamma drifts towards 0 by Adam steps of ~lr, before the recovery divides by
+    0.)"""
+    from optical_flow_amd import ops
+    from optical_flow_amd.data import synthetic_batch
+    H, W, B = 64, 128, 2
+    batches = [dev(torch.from_numpy(synthetic_batch(B, H, W, seed=90 + i))) for i in range(3)]
+    with ops.deterministic(True):
+        gt, _ = _trainer(H, W)
+        step = gt.graphed(batches[0].clone(), warmup=1)
+        assert step.captures == 1
+        store = gt.flow_net.store
+        assert "ResNet18/res3_0/conv_b" not in store.bn_guard.flagged
+        with torch.no_grad():
+            store.params["ResNet18/res3_0/bn_b/gamma"].fill_(3e-3)
+        for k in range(2 * ops.BNZGuard.EVERY + ops.BNZGuard.LAG_MAX + 2):
+            step(batches[1])
+            if step.captures > 1:
+                break
+        torch.cuda.synchronize()
+        assert step.captures == 2, step.captures
+        assert "ResNet18/res3_0/conv_b" in store.bn_guard.flagged
+        eager, _ = _trainer(H, W)
+        _sync_state(eager, gt)
+        le, _ = eager.train_step(batches[2])
+        assert "ResNet18/res3_0/conv_b" in eager.flow_net.store.bn_guard.flagged
+        lg, _ = step(batches[2])
+        torch.cuda.synchronize()
+        assert torch.isfinite(store.grad_arena).all()
+        assert float(lg) == float(le)
+        assert torch.equal(store.grad_arena, eager.flow_net.store.grad_arena), rel_l2(
+            store.grad_arena, eager.flow_net.store.grad_arena)

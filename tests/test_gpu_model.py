@@ -235,13 +235,16 @@ def test_resnet_layer_simple(idx, nblocks, down, cin):
         assert e < REL_TOL, "grad %s rel_l2 %.3e" % (name, e)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("case", ["gamma0", "gamma1e-4", "large_residual"])
-def test_resnet_block_bn_guard(case):
+def test_resnet_block_bn_guard(case, precision):
     """One projected residual block (resnet_layer_simple, model.py:20) whose BN gammas are 0 or
     1e-4, or whose conv_b output is added to a large residual (beta 40 on the projection's BN,
     |res + beta| >> |gamma zhat|): where recovering zhat from y would divide by ~0 or cancel
     (ADVICE r3), ops.BNZGuard keeps z for the layer; output, input gradient and every weight
-    gradient against the float64 oracle at 1e-3."""
+    gradient against the float64 oracle at 1e-3 (fp32), or -- bf16, the block's input given
+    (teacher forcing, as test_res_block_bf16_teacher_forced) -- against the oracle with the same
+    bf16 operand rounding at the module tests' 1e-2."""
     from optical_flow_amd.model import ParamStore, resnet_layer_simple
     from optical_flow_amd.params import blocks_spec, init_params, perturb_params, stage_blocks
     blocks = stage_blocks(3, 64, 1, True)
@@ -262,7 +265,7 @@ def test_resnet_block_bn_guard(case):
     x0 = torch.randn(2, 32, 48, 64, generator=g, dtype=torch.float64)
     x = dev(x0.float()).requires_grad_(True)
     store.zero_grad()
-    y = resnet_layer_simple(x, 1, True, 3, store=store)
+    y = resnet_layer_simple(x, 1, True, 3, store=store, precision=precision)
     dy0 = torch.randn(tuple(y.shape), generator=g, dtype=torch.float64)
     y.backward(dev(dy0.float()))
     torch.cuda.synchronize()
@@ -270,15 +273,24 @@ def test_resnet_block_bn_guard(case):
             "large_residual": {pre + "/conv_b"}}[case]
     assert store.bn_guard.flagged == want, store.bn_guard.flagged
     p = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in vals.items()}
-    xo = x0.clone().requires_grad_(True)
-    yo = R.resnet_block(xo, p, pre, 2, True)
-    yo.backward(dy0)
-    assert rel_inf(y, yo) < REL_TOL
-    assert rel_l2(x.grad, xo.grad) < REL_TOL
+    xo = x0.float().double().requires_grad_(True)
+    R.set_conv_precision(precision)
+    try:
+        yo = R.resnet_block(xo, p, pre, 2, True)
+        yo.backward(dy0)
+    finally:
+        R.set_conv_precision("fp32")
+    tol = REL_TOL if precision == "fp32" else 1e-2
+    errs = [("out", rel_l2(y, yo)), ("dx", rel_l2(x.grad, xo.grad))]
     for name, gr in store.grads().items():
         assert torch.isfinite(gr).all(), name
-        e = rel_l2(gr, p[name].grad)
-        assert e < REL_TOL, "grad %s rel_l2 %.3e" % (name, e)
+        errs.append((name, rel_l2(gr, p[name].grad)))
+    for name, e in errs:
+        print("%s %-36s rel_l2 %.3e" % (precision, name, e))
+    if precision == "fp32":
+        assert rel_inf(y, yo) < REL_TOL
+    bad = [(n, e) for n, e in errs if not e < tol]
+    assert not bad, bad
 
 
 def test_resnet_layer_simple_fresh_layers():

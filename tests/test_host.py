@@ -147,3 +147,31 @@ def test_draw_all_arrows_geometry():
         np.testing.assert_array_equal(pic[ty, tx], ARROW_COLOR)
     untouched = pic[(pic != np.array(ARROW_COLOR, np.float32)).any(-1)]
     np.testing.assert_allclose(untouched, 0.4, rtol=1e-6)
+
+
+def test_flowgrad_release_deferred_to_join():
+    """inside a backward that forked side streams, a flow head's loss-gradient
+    buffer may still be read there by the head's weight gradient; FlowGrad.release then
+    pools it only at the end-of-backward join (ops._side_join), after the current stream has
+    been ordered behind the side streams, so the next FlowGrad cannot pop and overwrite it
+    first.  Without side streams armed it is pooled at once."""
+    from optical_flow_amd import ops
+    key_shape = (1, 3, 5, 2)
+    ops.FlowGrad._pool.pop(("cpu", key_shape), None)
+    fg = ops.FlowGrad(key_shape, "cpu")
+    buf = fg.buffer()
+    prev = ops._side_armed
+    try:
+        ops._side_armed = True
+        fg.release()
+        assert not ops.FlowGrad._pool.get(("cpu", key_shape))
+        other = ops.FlowGrad(key_shape, "cpu")
+        assert other.buffer() is not buf          # not handed out before the join
+        ops._side_join()
+        assert ops.FlowGrad._pool[("cpu", key_shape)][-1] is buf
+        ops._side_armed = False
+        other.release()
+        assert len(ops.FlowGrad._pool[("cpu", key_shape)]) == 2     # pooled at once
+    finally:
+        ops._side_armed = prev
+        ops.FlowGrad._pool.pop(("cpu", key_shape), None)

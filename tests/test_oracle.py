@@ -136,6 +136,36 @@ def test_bn_inference_uses_moving_stats():
     assert y.item() == pytest.approx((3.0 - 1.0) * 2.0 / 2.0 + 0.5)
 
 
+def test_bn_training_batch_stats_and_moving_update():
+    """batchnorm_training (P5, old/train.py:59): a hand-computed case.  One channel, values
+    1, 2, 3, 6: mean 3, biased variance 3.5 (normalisation), unbiased 14/3 (moving variance);
+    moving = 0.99 moving + 0.01 stat (Keras momentum 0.99)."""
+    p = {"b/gamma": torch.tensor([2.0], dtype=torch.float64),
+         "b/beta": torch.tensor([0.5], dtype=torch.float64),
+         "b/moving_mean": torch.tensor([1.0], dtype=torch.float64),
+         "b/moving_variance": torch.tensor([2.0], dtype=torch.float64)}
+    x = torch.tensor([1.0, 2.0, 3.0, 6.0], dtype=torch.float64).view(1, 2, 2, 1)
+    y = R.batchnorm_training(x, p, "b")
+    want = (x - 3.0) / np.sqrt(3.5 + R.BN_EPS) * 2.0 + 0.5
+    assert torch.allclose(y, want, rtol=1e-14, atol=1e-14)
+    assert p["b/moving_mean"].item() == pytest.approx(0.99 * 1.0 + 0.01 * 3.0, rel=1e-14)
+    assert p["b/moving_variance"].item() == pytest.approx(0.99 * 2.0 + 0.01 * 14.0 / 3.0,
+                                                          rel=1e-14)
+    # FusedBatchNormGradV3: gradients through the batch statistics (gradcheck, fresh stats)
+    xg = torch.tensor(np.random.default_rng(9).standard_normal((2, 3, 3, 2)),
+                      requires_grad=True)
+    gg = torch.tensor([1.3, -0.7], dtype=torch.float64, requires_grad=True)
+    q = {"b/gamma": gg, "b/beta": torch.tensor([0.1, 0.2], dtype=torch.float64),
+         "b/moving_mean": torch.zeros(2, dtype=torch.float64),
+         "b/moving_variance": torch.ones(2, dtype=torch.float64)}
+    assert torch.autograd.gradcheck(lambda a, g_: R.batchnorm_training(a, dict(q, **{"b/gamma": g_}),
+                                                                      "b"), (xg, gg))
+    # dL/dz sums to 0 per channel (the mean is subtracted), so the conv bias gets ~0
+    xg.grad = None
+    R.batchnorm_training(xg, q, "b").pow(3).sum().backward()
+    assert xg.grad.sum(dim=(0, 1, 2)).abs().max().item() < 1e-12
+
+
 def test_photometric_loss_zero_for_identity_pairs():
     # image2 == transposed image1 and zero flows give the reference warp (transpose) ...
     # so use square images where the transpose of a symmetric image is itself
