@@ -108,9 +108,9 @@ def conv_math(precision):
         return ("fp32: every conv with >= 16 input channels (3x3 stride-1 halo tiles; stride-2 "
                 "and 1x1 implicit GEMMs) fwd/dgrad/wgrad on bf16 MFMA with an exact 3-term "
                 "operand split (6 products, fp32 accumulation; error vs fp64 at fp32-MFMA level, "
-                "test_conv_x3_accuracy / test_conv_gemm_x3_accuracy); the 3-channel stem forward on "
-                "its own split-bf16 kernel and its weight gradient on fp32 MFMA, the Cout<=4 flow "
-                "convs on fp32 VALU")
+                "test_conv_x3_accuracy / test_conv_gemm_x3_accuracy); the 3-channel stem's "
+                "forward and weight gradient on their own split-bf16 kernels (conv_stem_x3, "
+                "conv_wgrad_stem_x3), the Cout<=4 flow convs on fp32 VALU")
     return "fp32 MFMA (flow convs cout<=4: fp32 VALU)"
 
 

@@ -400,7 +400,9 @@ int of_timing_enable(int on);
  * in flight during the epilogue (1; 2: on 8 workgroups, for tests) or one tile per workgroup
  * (0, default: the persistent form measured even);
  * keys 25 / 26 = the K-split cost models' slab-pass term (tenths of a chunk per slice and tile
- * round; default 5) of the fp32 halo-tile kernels and of the split implicit GEMMs. */
+ * round; default 5) of the fp32 halo-tile kernels and of the split implicit GEMMs;
+ * key 27 = fp32 split 3x3 layers whose BN = 128 grid has fewer than this many workgroups run
+ * BN = 64 tiles, two workgroups per CU (0 = never). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 
@@ -563,6 +565,22 @@ int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const f
                            const float* y, const float* gamma, const float* beta,
                            const float* var, float eps, float* dz, float* dgamma, float* dbeta,
                            float* dbias, int accumulate, void* workspace, void* stream);
+
+/* The stem's whole backward in one conv kernel (model.py:12-17, reset18_encoder's conv1 ->
+ * layer1_bn -> ReLU -> {out0, MaxPool2D}): dz = relu'(y) (g + the max-pool gradient dyp at the
+ * first maximum of each 2x2 window) * gamma / sqrt(var + eps) is formed while the weight
+ * gradient stages it (of_maxpool_bn_relu_bwd's math, dz never stored), with dw (HWIO, 7x7x3x64),
+ * dbias = s sum t, dgamma = sum t zhat (zhat = (y - beta) / gamma), dbeta = sum t (accumulate
+ * != 0 adds into them).  y: the stem output (n, ho, wo, 64), g: its other consumer's gradient or
+ * NULL, dyp: the pooled gradient (n, ho/2, wo/2, 64).  precision 2 (the fp32 split) or 1 (bf16);
+ * OF_EUNSUPPORTED for other shapes (then of_maxpool_bn_relu_bwd + of_conv2d_wgrad*).
+ * Workspace: of_stem_bwd_fused_workspace(d, precision) bytes (0: unsupported). */
+size_t of_stem_bwd_fused_workspace(const of_conv_desc* d, int precision);
+int of_stem_bwd_fused(const of_conv_desc* d, int precision, const float* x, int ldx,
+                      const float* dyp, const float* g, const float* y, const float* gamma,
+                      const float* beta, const float* var, float eps, float* dw, float* dbias,
+                      float* dgamma, float* dbeta, int accumulate, void* workspace,
+                      size_t ws_bytes, void* stream);
 
 /* ==== SURVEY.md §8 P5: BatchNormalization in training mode (bn_mode = "training") ========= */
 /* keras BatchNormalization called with training=True (old/train.py:59; the reference's

@@ -58,6 +58,10 @@ struct GemmArgs {
   int tiles_total;        // sum over groups of m_tiles * n_tiles
   int colsum;             // wgrad: column sums of B (bias grad) into slab row M
   int bm;                 // M tile of the launched configuration
+  int bn_tile;            // conv_tile_x3: N tile when not pick_bn(N) (0: pick_bn)
+  // conv_wgrad_stem_x3<NP, true>: dz formed on load from the stem's max-pool / BN / ReLU
+  // backward inputs (pooled gradient, the out0 gradient or NULL, the stem output y)
+  const float* st_dyp; const float* st_g; const float* st_y;
   int ngroups;
   int vec_ep;             // tile kernels: 4-column epilogue (N, every ld a multiple of 4,
                           // every row pointer 16-byte aligned)

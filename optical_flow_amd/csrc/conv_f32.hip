@@ -2556,7 +2556,14 @@ constexpr int SW_NW = 5, SW_NT = 64 * SW_NW;
 constexpr int SW_HQ = (SW_HH * SW_HX + SW_NT - 1) / SW_NT; // halo pixels per thread
 constexpr int SW_WGS_PER_CU = 3;
 
-template <int NP>
+// FUSED (round 5): the stem's backward in one kernel.  conv1 -> layer1_bn -> ReLU feeds out0 and
+// the max-pool (model.py:12-17); dz = t * s with t = relu'(y) (g + the pooled gradient at the
+// first maximum of each 2 x 2 window) and s = gamma / sqrt(var + eps) -- misc.hip's
+// maxpool_bn_act_bwd_partial math -- is formed while each dz chunk is staged, from y (this row
+// and its window partner row), g and the pooled gradient, so dz (the encoder's largest tensor)
+// is never written and read back.  The BN sums ride along: slab rows 196 (sum t) and 197
+// (sum t zhat, zhat = (y - beta) / gamma where y > 0) instead of the bias column sums.
+template <int NP, bool FUSED = false>
 __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
   constexpr int NT = SW_NT;
   static_assert(NP == 3 || NP == 1, "three split planes (fp32) or one (bf16)");
@@ -2585,14 +2592,73 @@ __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
   const bool d_on = tid < 256 && d_co < a.N;
   const uint32_t d_step = (uint32_t)a.ldb * 4;        // bytes between consecutive pixels
   float dv[2][8], csum = 0.f;
-  auto load_dz = [&](int c, float* v) {
+  // FUSED: raw inputs of two chunks in flight (y of the row and of its window partner, g, the
+  // four pooled gradients of the octet), the BN scale / shift of this lane's channel, sums
+  float fy[FUSED ? 2 : 1][8], fp[FUSED ? 2 : 1][8], fg[FUSED ? 2 : 1][8], fd[FUSED ? 2 : 1][4];
+  float f_sc = 0.f, f_bt = 0.f, f_ig = 0.f, f_st = 0.f, f_stz = 0.f;
+  const rsrc_t ry = make_rsrc(FUSED ? a.st_y : a.B, FUSED ? a.b_bytes : 0);
+  const rsrc_t rg = make_rsrc(FUSED && a.st_g ? a.st_g : a.B, FUSED && a.st_g ? a.b_bytes : 0);
+  const rsrc_t rp = make_rsrc(FUSED ? a.st_dyp : a.B, FUSED ? a.b_bytes / 4 : 0);
+  if constexpr (FUSED) {
+    if (d_on) {
+      const float gm = a.bn_g[d_co];
+      f_sc = gm * rsqrtf(a.bn_v[d_co] + a.bn_eps);
+      f_bt = a.bn_b[d_co];
+      f_ig = 1.f / gm;
+    }
+  }
+  auto load_dz = [&](int c, float* v, int set) {
     int b, oy0, ox0;
     tile_of(t_begin + c / SW_TH, b, oy0, ox0);
     const int oy = oy0 + c % SW_TH, px0 = ox0 + 8 * d_kg;
     const int lim = d_on && oy < a.ho ? a.wo - px0 : 0;   // pixels of this octet in the row
     const uint32_t base = (uint32_t)((((int64_t)b * a.ho + oy) * a.wo + px0) * a.ldb + d_co) * 4;
+    if constexpr (FUSED) {
+      // (even ho, wo and 4 x 32 tiles: the partner row oy ^ 1 and the octet's 4 windows are
+      // inside the image whenever the row is)
+      const uint32_t pbase = (uint32_t)((((int64_t)b * a.ho + (oy ^ 1)) * a.wo + px0) * a.ldb + d_co) * 4;
+      const int pw = a.wo / 2;
+      const uint32_t dbase =
+          (uint32_t)((((int64_t)b * (a.ho / 2) + (oy >> 1)) * pw + (px0 >> 1)) * a.ldb + d_co) * 4;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        fy[set][e] = bload1(ry, e < lim ? base + e * d_step : kOOB);
+        fp[set][e] = bload1(ry, e < lim ? pbase + e * d_step : kOOB);
+        fg[set][e] = bload1(rg, e < lim ? base + e * d_step : kOOB);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) fd[set][e] = bload1(rp, 2 * e < lim ? dbase + e * d_step : kOOB);
+      (void)v;
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = bload1(rd, e < lim ? base + e * d_step : kOOB);
+  };
+  // FUSED: dz of the chunk from its raw inputs; `odd`: the row is the odd row of its windows
+  auto form_dz = [&](int set, bool odd, float* v) {
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      // window corners k = 2 (row parity) + (column parity), first maximum, strict >
+      float wy[4];
+      wy[odd ? 2 : 0] = fy[set][2 * e2];
+      wy[odd ? 3 : 1] = fy[set][2 * e2 + 1];
+      wy[odd ? 0 : 2] = fp[set][2 * e2];
+      wy[odd ? 1 : 3] = fp[set][2 * e2 + 1];
+      int bk = 0;
+      float mx = wy[0];
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+        if (wy[k] > mx) bk = k, mx = wy[k];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = (odd ? 2 : 0) + u;
+        const float yk = fy[set][2 * e2 + u];
+        const float t = yk > 0.f ? fg[set][2 * e2 + u] + (k == bk ? fd[set][e2] : 0.f) : 0.f;
+        v[2 * e2 + u] = t * f_sc;
+        f_st += t;
+        f_stz += t * ((yk - f_bt) * f_ig);
+      }
+    }
   };
   auto store_dz = [&](int buf, const float* v) {
     if (tid >= 256) return;
@@ -2657,20 +2723,23 @@ __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
 
   if (nchunks > 0) {
     load_halo(t_begin);
-    load_dz(0, dv[0]);
-    if (nchunks > 1) load_dz(1, dv[1]);
+    load_dz(0, dv[0], 0);
+    if (nchunks > 1) load_dz(1, dv[1], 1);
     store_halo(0);
   }
   // chunk c uses dz register set c & 1 (static: the body is instantiated for both sets)
-  auto chunk = [&](int c, float* dvc) {
+  auto chunk = [&](int c, float* dvc, int set) {
     const int j = c % SW_TH, tl = c / SW_TH;
     const int buf = c & 1;
     // The halo of tile tl + 1 is stored into the other buffer at j = 1: every wave passed this
     // chunk's barrier, so none still reads that buffer (tile tl - 1, last read at chunk c - 2).
     if (j == 0 && tl + 1 < ntiles) load_halo(t_begin + tl + 1);
+    if constexpr (FUSED) {
+      if (tid < 256) form_dz(set, (j & 1) != 0, dvc);   // tiles start at even rows
+    }
     store_dz(buf, dvc);
     __syncthreads();                               // this chunk's dz (and its tile's halo)
-    if (c + 2 < nchunks) load_dz(c + 2, dvc);      // two chunks in flight
+    if (c + 2 < nchunks) load_dz(c + 2, dvc, set); // two chunks in flight
     if (j == 1 && tl + 1 < ntiles) store_halo((tl + 1) & 1);
     const float* hrow = Hs[tl & 1] + 2 * j * 8 * SW_HC;
     bf16x8 av[2][NP];
@@ -2706,8 +2775,8 @@ __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
     }
   };
   for (int c = 0; c < nchunks; c += 2) {
-    chunk(c, dv[0]);
-    if (c + 1 < nchunks) chunk(c + 1, dv[1]);
+    chunk(c, dv[0], 0);
+    if (c + 1 < nchunks) chunk(c + 1, dv[1], 1);
   }
 
   // ---- this workgroup's slab: lane's value rr of (mt, nt) is row m = 16 (2 wave + mt) +
@@ -2726,7 +2795,20 @@ __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
         if (co < a.N) slab[(int64_t)(tap * 4 + ci) * a.slab_ld + co] = acc[mt][nt][rr];
       }
     }
-  if (a.colsum) {                                  // bias: column sums of dz, fixed order
+  if (FUSED) {                                     // BN sums (rows 196, 197), fixed order
+    float* Cs = reinterpret_cast<float*>(&Ds[0][0]);
+    __syncthreads();                               // every wave is done with Ds
+    if (tid < 256) {
+      Cs[d_kg * 64 + d_co] = f_st;
+      Cs[256 + d_kg * 64 + d_co] = f_stz;
+    }
+    __syncthreads();
+    if (tid < 128 && (tid & 63) < a.N) {
+      const int o = (tid >> 6) * 256, cc = tid & 63;
+      slab[(int64_t)(196 + (tid >> 6)) * a.slab_ld + cc] =
+          (Cs[o + cc] + Cs[o + 64 + cc]) + (Cs[o + 128 + cc] + Cs[o + 192 + cc]);
+    }
+  } else if (a.colsum) {                           // bias: column sums of dz, fixed order
     float* Cs = reinterpret_cast<float*>(&Ds[0][0]);
     __syncthreads();                               // every wave is done with Ds
     if (tid < 256) Cs[d_kg * 64 + d_co] = csum;
@@ -2734,6 +2816,38 @@ __global__ __launch_bounds__(SW_NT, 3) void conv_wgrad_stem_x3(GemmArgs a) {
     if (tid < 64 && tid < a.N)
       slab[(int64_t)196 * a.slab_ld + tid] = (Cs[tid] + Cs[64 + tid]) + (Cs[128 + tid] + Cs[192 + tid]);
   }
+}
+
+// The fused stem backward's BN parameter gradients: per channel the slab rows 196 (sum t) and
+// 197 (sum t zhat) of every split, in split order (four lane groups over contiguous quarters,
+// then the quarters in order): dbeta (+)= sum t, dgamma (+)= sum t zhat, dbias (+)= s sum t.
+__global__ __launch_bounds__(256) void stem_bn_final(const float* __restrict__ slab, int splits,
+                                                     int64_t split_stride, int ld, int c,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ var, float eps,
+                                                     float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta,
+                                                     float* __restrict__ dbias, int accum) {
+  __shared__ float red[2][4][64];
+  const int co = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int s0 = (int)((int64_t)g * splits / 4), s1 = (int)((int64_t)(g + 1) * splits / 4);
+  float st = 0.f, stz = 0.f;
+  if (co < c) {
+    for (int sp = s0; sp < s1; ++sp) {
+      st += slab[sp * split_stride + 196 * (int64_t)ld + co];
+      stz += slab[sp * split_stride + 197 * (int64_t)ld + co];
+    }
+  }
+  red[0][g][co] = st;
+  red[1][g][co] = stz;
+  __syncthreads();
+  if (g != 0 || co >= c) return;
+  st = (red[0][0][co] + red[0][1][co]) + (red[0][2][co] + red[0][3][co]);
+  stz = (red[1][0][co] + red[1][1][co]) + (red[1][2][co] + red[1][3][co]);
+  const float db = st * gamma[co] * rsqrtf(var[co] + eps);
+  if (dbeta) dbeta[co] = accum ? dbeta[co] + st : st;
+  if (dgamma) dgamma[co] = accum ? dgamma[co] + stz : stz;
+  if (dbias) dbias[co] = accum ? dbias[co] + db : db;
 }
 
 template <int WAVES_CI, int WAVES_CO, int WAVES_R, int XH>
@@ -4343,7 +4457,7 @@ bool x3_tall(int n, int oh, int ow, int N) {
 // plan is also unsplit (x3_nb1).
 constexpr int X3_NB1_MIN = 384;
 bool x3_nb1_candidate(const GemmArgs& a, bool tall) {
-  return !tall && pick_bn(a.N) == 128 && a.tiles_total >= X3_NB1_MIN;
+  return !tall && a.bn_tile == 0 && pick_bn(a.N) == 128 && a.tiles_total >= X3_NB1_MIN;
 }
 bool x3_nb1(const GemmArgs& a) {
   return a.bm != X3_TH0 * TF_W && a.splits == 1 && x3_nb1_candidate(a, false);
@@ -4361,6 +4475,7 @@ bool ws_ok(const of_conv_desc* d, int mode) {
 // slice and tile round, of the halo-tile kernels (tile_args) and of conv_gemm_x3 (gemm_x3_plan).
 static int g_x3t_ep = 5;
 static int g_x3g_ep = 5;
+static int g_x3_small_bn = 0;
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false,
                    bool b16 = false, bool ws = false) {
   GemmArgs a = base_args(d);
@@ -4370,8 +4485,15 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   a.nb = fwd ? d->cout : g.nd;
   a.ldb = fwd ? g.kf16 : (int)g.kd16;
   const int OH = fwd ? d->ho : d->h, OW = fwd ? d->wo : d->w;
+  // of_set_tuning key 27: fp32 split layers whose BN = 128 grid of 4 x 32 tiles has fewer than
+  // g_x3_small_bn workgroups run BN = 64 tiles instead (conv_tile_x3<64, ...>: 64 KB of LDS, two
+  // workgroups per CU, twice the N tiles): the coarse levels' grids (enc.l4, dec0 / dec1 heads)
+  // leave CUs idle at BN = 128 with one workgroup per CU.
+  if (x3 && !b16 && !ws && g_x3_small_bn > 0 && pick_bn(a.N) == 128 &&
+      (int64_t)d->n * cdiv(OH, TF_H) * cdiv(OW, TF_W) * cdiv(a.N, 128) < g_x3_small_bn)
+    a.bn_tile = 64;
   // bf16: fwd only (8 x 32 tiles measured +5 % on dec3 fwd, -2 % on dgrad); conv_tile_ws: always
-  const bool tall = ws ? true
+  const bool tall = a.bn_tile ? false : ws ? true
                   : x3 || b16 ? x3_tall(d->n, OH, OW, a.N)
                              : (fwd || g_tall16_dgrad) && pick_bn(a.N) == 128 &&
                                    x3_tall(d->n, OH, OW, a.N);
@@ -4386,7 +4508,7 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   G.ns = 3;
   G.ntaps = 9;
   a.M = G.M;
-  a.n_tiles = (int)cdiv(a.N, pick_bn(a.N));
+  a.n_tiles = (int)cdiv(a.N, a.bn_tile ? a.bn_tile : pick_bn(a.N));
   a.tiles_total = m_tiles * a.n_tiles;
   a.K = (int)cdiv(a.kc, 32);                       // channel chunks
   G.K = a.K;
@@ -4399,8 +4521,8 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
     // (Measured: enc.l3 384 tiles unsplit, dec1 192 tiles unsplit, enc.l4 96 tiles in 2.)
     // (The single-buffered BN = 128 4 x 32 configuration, used from X3_NB1_MIN tiles, runs
     // two workgroups per CU.)
-    const int slots = !ws && ((b16 && !tall) || x3_nb1_candidate(a, tall)) ? 2 * device_cus()
-                                                                            : device_cus();
+    const int slots = !ws && ((b16 && !tall) || x3_nb1_candidate(a, tall) || a.bn_tile == 64)
+                          ? 2 * device_cus() : device_cus();
     int best = 1;
     double best_cost = 1e30;
     for (int sp = 1; sp <= std::min(8, a.K); ++sp) {
@@ -4457,7 +4579,7 @@ struct WgradPlan {
 // fp32 3x3 stride-1 fwd / dgrad on the split-bf16 kernel: timing kinds 128 + mode * 8 + cfg.
 template <int MODE>
 int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
-  const int bn = pick_bn(a.N);
+  const int bn = a.bn_tile ? a.bn_tile : pick_bn(a.N);
   dim3 grid(a.tiles_total * a.splits), block(256);
   const bool tall = a.bm == X3_TH0 * TF_W;
   const int cfg = bn == 128 ? (tall ? 0 : x3_nb1(a) ? 4 : 6)
@@ -4810,6 +4932,7 @@ int of_set_tuning(int key, int value) {
   if (key == 24 && value >= 0 && value <= 2) { g_b16i_persist = value; return OF_OK; }
   if (key == 25 && value >= 0 && value <= 1000) { g_x3t_ep = value; return OF_OK; }
   if (key == 26 && value >= 0 && value <= 1000) { g_x3g_ep = value; return OF_OK; }
+  if (key == 27 && value >= 0 && value <= 100000) { g_x3_small_bn = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -5356,6 +5479,81 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
                      static_cast<const float*>(workspace), p.splits, p.split_stride, g.taps,
                      g.cin_p, d->cin, d->cout, p.ldc, dw, db, accumulate, bn_g, bn_v, bn_eps);
   return check_launch("wgrad_reduce");
+}
+
+// ---- the stem's whole backward in one conv kernel (conv_wgrad_stem_x3<NP, true>) -----------
+static bool stem_fused_ok(const of_conv_desc* d, int prec) {
+  return (prec == 2 || (prec == 1 && g_stem_bf16)) && stem_wg_ok(d) && d->ho % 2 == 0 &&
+         d->wo % 2 == 0 && d->cout == 64;
+}
+
+size_t of_stem_bwd_fused_workspace(const of_conv_desc* d, int precision) {
+  if (validate(d) != OF_OK || !stem_fused_ok(d, precision)) return 0;
+  WgradPlan p = wgrad_plan(d, precision == 1, true);
+  return (size_t)p.splits * (p.M + 2) * p.ldc * sizeof(float);
+}
+
+int of_stem_bwd_fused(const of_conv_desc* d, int precision, const float* x, int ldx,
+                      const float* dyp, const float* g, const float* y, const float* gamma,
+                      const float* beta, const float* var, float eps, float* dw, float* dbias,
+                      float* dgamma, float* dbeta, int accumulate, void* workspace,
+                      size_t ws_bytes, void* stream) {
+  int st = validate(d);
+  if (st) return st;
+  if (!stem_fused_ok(d, precision))
+    return fail(OF_EUNSUPPORTED, "stem bwd fused: not the 7x7/2 3->64 stem on the split / bf16 "
+                                 "kernels with an even output");
+  OF_CHECK_ARG(x && dyp && y && gamma && beta && var && dw && workspace, "stem bwd fused: NULL");
+  OF_CHECK_ARG(ldx >= d->cin_p && ldx % 4 == 0, "stem bwd fused: ldx");
+  WgradPlan p = wgrad_plan(d, precision == 1, true);
+  const int64_t stride = (int64_t)(p.M + 2) * p.ldc;
+  OF_CHECK_ARG(ws_bytes >= (size_t)p.splits * stride * sizeof(float),
+               "stem bwd fused: workspace too small");
+  GemmArgs a = base_args(d);
+  a.kc = d->cin_p;
+  a.N = d->cout;
+  a.M = p.M;
+  a.A = x;
+  a.lda = ldx;
+  a.a_bytes = (int64_t)d->n * d->h * d->w * ldx * 4;
+  a.B = y;                                     // (only sizes the FUSED resources)
+  a.ldb = 64;
+  a.b_bytes = (int64_t)d->n * d->ho * d->wo * 64 * 4;
+  OF_CHECK_ARG(a.a_bytes < INT32_MAX && a.b_bytes < INT32_MAX, "stem bwd fused: < 2 GiB tensors");
+  a.nb = 64;
+  a.slab = static_cast<float*>(workspace);
+  a.slab_ld = p.ldc;
+  a.splits = p.splits;
+  a.k_per_split = p.k_per_split;
+  a.split_stride = stride;
+  a.colsum = 0;
+  a.K = stem_wg_tiles(d);
+  a.bn_g = gamma;
+  a.bn_b = beta;
+  a.bn_v = var;
+  a.bn_eps = eps;
+  a.st_dyp = dyp;
+  a.st_g = g;
+  a.st_y = y;
+  hipStream_t s = as_stream(stream);
+  const double flops = 2.0 * (double)d->n * d->ho * d->wo * d->cout * 49 * d->cin;
+  if (timing_on()) timing_begin(s);
+  if (precision == 1) hipLaunchKernelGGL((conv_wgrad_stem_x3<1, true>), dim3(a.splits), dim3(SW_NT), 0, s, a);
+  else hipLaunchKernelGGL((conv_wgrad_stem_x3<3, true>), dim3(a.splits), dim3(SW_NT), 0, s, a);
+  if (timing_on()) timing_end(s, precision == 1 ? 187 : 185, flops);   // bench.py KIND_STEM_*
+  st = check_launch("conv_wgrad_stem_x3 fused");
+  if (st) return st;
+  Geo gg = geo(d);
+  const int64_t items = (int64_t)gg.taps * d->cin * cdiv(d->cout, 4);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
+                     static_cast<const float*>(workspace), p.splits, stride, gg.taps, gg.cin_p,
+                     d->cin, d->cout, p.ldc, dw, nullptr, accumulate, nullptr, nullptr, 0.f);
+  st = check_launch("wgrad_reduce");
+  if (st) return st;
+  hipLaunchKernelGGL(stem_bn_final, dim3(1), dim3(256), 0, s, static_cast<const float*>(workspace),
+                     p.splits, stride, p.ldc, d->cout, gamma, var, eps, dgamma, dbeta, dbias,
+                     accumulate);
+  return check_launch("stem_bn_final");
 }
 
 int of_conv2d_wgrad(const of_conv_desc* d, const float* x, int ldx, const float* dy, int lddy,

@@ -1,30 +1,29 @@
 // Deterministic feature-warp backward ("a deterministic-mode flag (no atomics in
-// the warp bwd)").
+// the warp bwd)"), the default since round 5 (ops.DETERMINISTIC).
 //
 // The reference samples with four gather_nd taps (transformations.py:98-129, reached from
 // warp_features, model.py:55-73); TF's gradient of a gather is a scatter-add into the feature
-// map, whose adds land in whatever order the hardware retires them.  The default HIP backward
+// map, whose adds land in whatever order the hardware retires them.  The atomic HIP backward
 // (flow_ops.hip warp_bwd_gather) keeps that shape: per-tile sums added with float atomics, so
 // two identical steps can differ in the last bit of d(features).  Here the scatter becomes a
-// gather with a fixed summation order:
+// gather with a fixed summation order, all hand-written (a counting sort by destination):
 //
-//   1. entries : every (source pixel p, corner k) -> key = destination pixel, value = (p, w_k)
-//                (the clipped corners and weights of P2, computed exactly as the forward does);
-//   2. sort    : a stable LSD radix sort of the 4·n·h·w entries by key (rocPRIM's device radix
-//                sort): equal keys keep entry order p·4 + k;
-//   3. bounds  : [begin, end) of each destination's run in the sorted array;
-//   4. gather  : one thread per (destination pixel, channel quad) sums w · dout[p] over its run
-//                in that order and STORES d(features) -- every element written once, so no
-//                zero-fill pass and no atomics;
-//   5. d(flow) : per source pixel over all channels in a fixed order (16 lanes x channel quads,
+//   1. count   : every (source pixel p, corner k) adds 1 to its destination's counter
+//                (integer adds: exact in any order);
+//   2. scan    : exclusive prefix sums of the counts -> each destination's segment;
+//   3. fill    : each entry's code 4 p + k into a slot of its segment (slot order free);
+//   4. gather  : per destination, the segment's codes ranked (16 lanes, codes distinct) and
+//                w_k * dout[p] summed in ascending code order, STORED -- every row written
+//                once, so no zero-fill pass and no float atomics;
+//   5. big     : segments of more than 16 entries (a field clipped onto the border) through an
+//                LDS bitmap over the code range, visited in code order;
+//   6. d(flow) : per source pixel over all channels in a fixed order (16 lanes x channel quads,
 //                then a fixed DPP row reduction), plus the optional addend of of_warp_bwd_add.
 //
-// Bitwise reproducible run to run, in eager mode and inside a captured graph alike.  Bounded
-// by HBM/L2 (the entries: 24 B per (pixel, corner) through the sort passes; the gather reads
-// the dout rows of its run, mostly L2 hits for smooth flows), O(n·h·w) for any flow field --
-// a field clipped onto the border only makes the runs of the border pixels long.
-#include <rocprim/device/device_radix_sort.hpp>
-
+// Bitwise reproducible run to run, in eager mode and inside a captured graph alike.  HBM / L2
+// bound: 8 B of flow and 12 B of counters per (pixel, corner) through steps 1-3, the gather
+// reads each destination's source rows (mostly L2 hits for smooth flows) and writes d(features)
+// once; O(n h w) for any flow field.
 #include "common.h"
 
 namespace oflow {
@@ -62,11 +61,10 @@ __device__ __forceinline__ float det_row16_sum(float v) {   // over the 16 lanes
   return v;
 }
 
-// 1. one thread per source pixel: its four (destination, (p, weight)) entries.
-__global__ __launch_bounds__(256) void det_entries(const float* __restrict__ flow, int n, int h,
-                                                   int w, int absolute,
-                                                   uint32_t* __restrict__ keys,
-                                                   uint64_t* __restrict__ vals) {
+// 1. count: one thread per source pixel, one integer add per (pixel, corner) on its
+// destination's counter (integer adds commute: the counts are exact whatever the order).
+__global__ __launch_bounds__(256) void own_count(const float* __restrict__ flow, int n, int h,
+                                                 int w, int absolute, int* __restrict__ cnt) {
   const int64_t npix = (int64_t)n * h * w;
   const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (p >= npix) return;
@@ -76,73 +74,273 @@ __global__ __launch_bounds__(256) void det_entries(const float* __restrict__ flo
   const int64_t img = (t2 / h) * h * w;
   const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
   const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
-  uint4 k4;
-  uint32_t* kk = reinterpret_cast<uint32_t*>(&k4);
-  uint64_t v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) atomicAdd(cnt + img + (int64_t)t.y[k] * w + t.x[k], 1);
+}
+
+// 2. exclusive scan of the counts (three launches: per-block sums, the block sums in one
+// workgroup, per-block scan + block offset).  OWN_SB elements per block.
+constexpr int OWN_SB = 2048;
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void own_block_sums(const int* __restrict__ cnt, int64_t total,
+                                                      int* __restrict__ bsum) {
+  __shared__ int red[4];
+  const int64_t base = blockIdx.x * (int64_t)OWN_SB;
+  int s = 0;
+  for (int k = threadIdx.x; k < OWN_SB; k += 256) {
+    const int64_t e = base + k;
+    s += e < total ? cnt[e] : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// one workgroup: bsum -> exclusive offsets, in place (nb block sums, any count)
+__global__ __launch_bounds__(1024) void own_scan_sums(int* __restrict__ bsum, int nb) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < nb; b0 += 1024) {
+    const int v = b0 + tid < nb ? bsum[b0 + tid] : 0;
+    const int inc = wave_incl_scan(v, lane);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    int before = carry;
+    for (int k = 0; k < wv; ++k) before += wsum[k];
+    if (b0 + tid < nb) bsum[b0 + tid] = before + inc - v;
+    __syncthreads();
+    if (tid == 1023) carry = before + inc;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void own_block_scan(const int* __restrict__ cnt, int64_t total,
+                                                      const int* __restrict__ boff,
+                                                      int* __restrict__ off) {
+  __shared__ int wsum[4];
+  __shared__ int carry;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t base = blockIdx.x * (int64_t)OWN_SB;
+  if (tid == 0) carry = boff[blockIdx.x];
+  __syncthreads();
+  for (int k0 = 0; k0 < OWN_SB; k0 += 256) {
+    const int64_t e = base + k0 + tid;
+    const int v = e < total ? cnt[e] : 0;
+    const int inc = wave_incl_scan(v, lane);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    int before = carry;
+    for (int k = 0; k < wv; ++k) before += wsum[k];
+    if (e < total) off[e] = before + inc - v;
+    __syncthreads();
+    if (tid == 255) carry = before + inc;
+    __syncthreads();
+  }
+}
+
+// 3. fill: each (pixel, corner) entry goes to a slot of its destination's segment.  The slot
+// order inside a segment depends on the order of the integer adds; the gather below orders
+// every segment itself, so nothing downstream depends on it.  Entry code = 4 p + k (p the
+// pixel within its image, k the corner: bit 0 -> row y1, bit 1 -> column x1).
+__global__ __launch_bounds__(256) void own_fill(const float* __restrict__ flow, int n, int h,
+                                                int w, int absolute, const int* __restrict__ off,
+                                                int* __restrict__ cursor,
+                                                uint32_t* __restrict__ list) {
+  const int64_t npix = (int64_t)n * h * w;
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const int j = (int)(p % w);
+  const int64_t t2 = p / w;
+  const int i = (int)(t2 % h);
+  const int64_t img = (t2 / h) * h * w;
+  const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
+  const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    kk[k] = (uint32_t)(img + (int64_t)t.y[k] * w + t.x[k]);
-    const float wt = ((k & 2) ? 1.f - t.a : t.a) * ((k & 1) ? 1.f - t.b : t.b);
-    v[k] = (uint64_t)(uint32_t)p | ((uint64_t)__float_as_uint(wt) << 32);
+    const int64_t d = img + (int64_t)t.y[k] * w + t.x[k];
+    list[off[d] + atomicAdd(cursor + d, 1)] = (uint32_t)(4 * (p - img) + k);
   }
-  *reinterpret_cast<uint4*>(keys + 4 * p) = k4;
-  *reinterpret_cast<ulonglong2*>(vals + 4 * p) = make_ulonglong2(v[0], v[1]);
-  *reinterpret_cast<ulonglong2*>(vals + 4 * p + 2) = make_ulonglong2(v[2], v[3]);
 }
 
-// 3. run bounds of every destination present in the sorted keys (absent ones stay [0, 0)).
-__global__ __launch_bounds__(256) void det_bounds(const uint32_t* __restrict__ keys, int64_t ne,
-                                                  int2* __restrict__ runs) {
-  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (e >= ne) return;
-  const uint32_t k = keys[e];
-  if (e == 0 || keys[e - 1] != k) runs[k].x = (int)e;
-  if (e == ne - 1 || keys[e + 1] != k) runs[k].y = (int)(e + 1);
+// the weight of entry `code` of image `img` (the forward's bilinear weights, P2)
+__device__ __forceinline__ float own_weight(const float* __restrict__ flow, int64_t img, int h,
+                                            int w, int absolute, uint32_t code) {
+  const int64_t pi = code >> 2;
+  const int k = code & 3;
+  const float2 f = *reinterpret_cast<const float2*>(flow + 2 * (img + pi));
+  const DetCorners t = det_corners((int)(pi / w), (int)(pi % w), f.x, f.y, h, w, absolute != 0);
+  return ((k & 2) ? 1.f - t.a : t.a) * ((k & 1) ? 1.f - t.b : t.b);
 }
 
-// 4. d(features): one thread per (destination pixel, channel quad), the run summed in entry
-// order (c % 4 == 0, 16-byte rows) ...
-__global__ __launch_bounds__(256) void det_gather_vec(const float* __restrict__ dout, int64_t npix,
-                                                      int c, const int2* __restrict__ runs,
-                                                      const uint64_t* __restrict__ vals,
+// 4. gather, destinations with at most 16 entries: 16 lanes per destination (channel quads),
+// four destinations per wave.  Lane j < n holds entry j; its rank (the number of smaller codes
+// in the segment) orders the sum: sum over codes ascending of w * dout[p] -- the same order
+// whatever slots the fill gave them.  A segment of more than 16 entries is listed for step 5.
+// Every destination row is written (0 when no entry lands on it): no zero-fill pass.
+constexpr int OWN_SMALL = 16;
+// VEC: rows of float4 quads (c % 4 == 0, 16-byte aligned); else one channel per lane.
+template <bool VEC>
+__device__ __forceinline__ void own_acc(float4& acc, float wr, const float* __restrict__ row,
+                                        int k) {
+  if (VEC) {
+    const float4 g = *reinterpret_cast<const float4*>(row + 4 * k);
+    acc.x += wr * g.x;
+    acc.y += wr * g.y;
+    acc.z += wr * g.z;
+    acc.w += wr * g.w;
+  } else {
+    acc.x += wr * row[k];
+  }
+}
+
+template <bool VEC>
+__device__ __forceinline__ void own_store(float* __restrict__ row, int k, const float4& v) {
+  if (VEC) *reinterpret_cast<float4*>(row + 4 * k) = v;
+  else row[k] = v.x;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void own_gather(const float* __restrict__ dout,
+                                                  const float* __restrict__ flow, int n, int h,
+                                                  int w, int c, int absolute,
+                                                  const int* __restrict__ cnt,
+                                                  const int* __restrict__ off,
+                                                  const uint32_t* __restrict__ list,
+                                                  float* __restrict__ dinp,
+                                                  int* __restrict__ big_n, int* __restrict__ big) {
+  const int64_t npix = (int64_t)n * h * w;
+  const int lane = threadIdx.x & 63, g16 = lane >> 4, q = lane & 15;
+  const int64_t d = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4;
+  const bool live = d < npix;
+  const int64_t dd = live ? d : npix - 1;
+  const int ne = live ? cnt[dd] : 0;
+  const int64_t img = dd / ((int64_t)h * w) * h * w;
+  const bool small = ne <= OWN_SMALL;
+  if (live && !small && q == 0) big[atomicAdd(big_n, 1)] = (int)dd;
+  const uint32_t code = small && q < ne ? list[off[dd] + q] : 0xffffffffu;
+  // rank among the segment's codes (codes are distinct)
+  int rank = 0;
+  const int src0 = lane & 48;
+#pragma unroll
+  for (int k = 0; k < OWN_SMALL; ++k) {
+    const uint32_t o = (uint32_t)__shfl((int)code, src0 + k, 64);
+    rank += o < code ? 1 : 0;
+  }
+  const float wt = small && q < ne ? own_weight(flow, img, h, w, absolute, code) : 0.f;
+  // max entries over the four destinations of the wave: the loop bound
+  int nmax = small ? ne : 0;
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
+  const int nq = VEC ? c >> 2 : c;                     // quads, or channels
+  for (int cb = 0; cb < nq; cb += 16) {                // every lane runs every iteration
+    const int cq = cb + q;
+    const bool cok = cq < nq;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < nmax; ++r) {
+      // the lane of this group holding rank r (none when this group's segment is shorter)
+      const uint64_t bal = __ballot(small && q < ne && rank == r);
+      const int sl = (int)((bal >> (16 * g16)) & 0xffffull);
+      const bool has = sl != 0;
+      const int src = src0 + (has ? __builtin_ctz(sl) : 0);
+      const uint32_t cd = (uint32_t)__shfl((int)code, src, 64);
+      const float wr = __shfl(wt, src, 64);
+      if (has && cok) own_acc<VEC>(acc, wr, dout + (img + (cd >> 2)) * c, cq);
+    }
+    if (live && small && cok) own_store<VEC>(dinp + dd * c, cq, acc);
+  }
+}
+
+// 5. gather, destinations with more than 16 entries (a clipped flow field piles samples onto
+// the border): one workgroup per listed destination.  The segment's codes are marked in an
+// LDS bitmap over a window of the image's code range (all of it when 4 h w <= OWN_WBITS), the
+// four waves each sum a contiguous quarter of the window in code order, and the quarters are
+// added in order: a fixed order for any n.
+constexpr int OWN_WBITS = 1 << 20;    // 128 KB of bitmap
+template <bool VEC>
+__global__ __launch_bounds__(256) void own_gather_big(const float* __restrict__ dout,
+                                                      const float* __restrict__ flow, int h,
+                                                      int w, int c, int absolute,
+                                                      const int* __restrict__ cnt,
+                                                      const int* __restrict__ off,
+                                                      const uint32_t* __restrict__ list,
+                                                      const int* __restrict__ big_n,
+                                                      const int* __restrict__ big,
                                                       float* __restrict__ dinp) {
-  const int nq = c >> 2;
-  const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (idx >= npix * nq) return;
-  const int64_t d = idx / nq;
-  const int q = (int)(idx - d * nq);
-  const int2 r = runs[d];
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int e = r.x; e < r.y; ++e) {
-    const uint64_t v = vals[e];
-    const int64_t p = (int64_t)(uint32_t)v;
-    const float wt = __uint_as_float((uint32_t)(v >> 32));
-    const float4 g = *reinterpret_cast<const float4*>(dout + p * c + 4 * q);
-    acc.x += wt * g.x;
-    acc.y += wt * g.y;
-    acc.z += wt * g.z;
-    acc.w += wt * g.w;
+  extern __shared__ uint32_t bm[];
+  __shared__ float4 part[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t codes = 4 * (int64_t)h * w;
+  const int64_t wbits = codes < OWN_WBITS ? (codes + 31) / 32 * 32 : OWN_WBITS;
+  const int nwords = (int)(wbits / 32);
+  const int nb = *big_n;
+  for (int bi = blockIdx.x; bi < nb; bi += gridDim.x) {
+    const int64_t d = big[bi];
+    const int64_t img = d / ((int64_t)h * w) * h * w;
+    const int ne = cnt[d];
+    const int64_t o0 = off[d];
+    const int nq = VEC ? c >> 2 : c;
+    for (int qb = 0; qb < nq; qb += 64) {                // 64 channel quads (channels) a sweep
+      const int cq = qb + lane;
+      const bool cok = cq < nq;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int64_t w0 = 0; w0 < codes; w0 += wbits) {   // code windows
+        for (int k = tid; k < nwords; k += 256) bm[k] = 0u;
+        __syncthreads();
+        for (int e = tid; e < ne; e += 256) {
+          const int64_t cd = (int64_t)list[o0 + e] - w0;
+          if (cd >= 0 && cd < wbits) atomicOr(&bm[cd >> 5], 1u << (cd & 31));
+        }
+        __syncthreads();
+        // wave wv: words [wv * nwords / 4, (wv + 1) * nwords / 4), in order; 64 words per
+        // step, the nonzero ones visited in lane order
+        const int k0 = (int)((int64_t)wv * nwords / 4), k1 = (int)((int64_t)(wv + 1) * nwords / 4);
+        for (int kb = k0; kb < k1; kb += 64) {
+          const uint32_t myw = kb + lane < k1 ? bm[kb + lane] : 0u;
+          uint64_t nzm = __ballot(myw != 0u);
+          while (nzm) {
+            const int l = __builtin_ctzll(nzm);
+            nzm &= nzm - 1;
+            uint32_t word = (uint32_t)__shfl((int)myw, l, 64);
+            while (word) {
+              const int bit = __builtin_ctz(word);
+              word &= word - 1;
+              const uint32_t cd = (uint32_t)(w0 + 32 * (int64_t)(kb + l) + bit);
+              const float wr = own_weight(flow, img, h, w, absolute, cd);
+              if (cok) own_acc<VEC>(acc, wr, dout + (img + (cd >> 2)) * c, cq);
+            }
+          }
+        }
+        __syncthreads();                                // the bitmap is reused
+      }
+      part[wv][lane] = acc;
+      __syncthreads();
+      if (wv == 0 && cok) {
+        float4 s = part[0][lane];
+#pragma unroll
+        for (int u = 1; u < 4; ++u) {
+          s.x += part[u][lane].x;
+          s.y += part[u][lane].y;
+          s.z += part[u][lane].z;
+          s.w += part[u][lane].w;
+        }
+        own_store<VEC>(dinp + d * c, cq, s);
+      }
+      __syncthreads();
+    }
   }
-  *reinterpret_cast<float4*>(dinp + d * c + 4 * q) = acc;
-}
-
-// ... or per (destination pixel, channel) for any c.
-__global__ __launch_bounds__(256) void det_gather_scalar(const float* __restrict__ dout,
-                                                         int64_t npix, int c,
-                                                         const int2* __restrict__ runs,
-                                                         const uint64_t* __restrict__ vals,
-                                                         float* __restrict__ dinp) {
-  const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (idx >= npix * c) return;
-  const int64_t d = idx / c;
-  const int ch = (int)(idx - d * c);
-  const int2 r = runs[d];
-  float acc = 0.f;
-  for (int e = r.x; e < r.y; ++e) {
-    const uint64_t v = vals[e];
-    acc += __uint_as_float((uint32_t)(v >> 32)) * dout[(int64_t)(uint32_t)v * c + ch];
-  }
-  dinp[d * c + ch] = acc;
 }
 
 // 5. d(flow) (c % 4 == 0): 16 lanes per source pixel, lane q sums channel quads q, q + 16, ...
@@ -221,37 +419,26 @@ __global__ __launch_bounds__(256) void det_dflow_scalar(const float* __restrict_
   dflow[2 * p + 1] = dfa ? dfa[p * ldfa + 1] + gy : gy;
 }
 
-// Workspace layout (256-byte aligned pieces): keys in/out (4 B per entry), values in/out
-// (8 B per entry), runs (8 B per destination pixel), the sort's own scratch.
+// Workspace layout (256-byte aligned pieces): per destination pixel a count, a segment
+// offset and a fill cursor (4 B each), the entry list (4 B per (pixel, corner)), the block
+// sums of the scan, and the list of destinations with long segments + its length.
 struct DetWs {
-  size_t keys_in, keys_out, vals_in, vals_out, runs, sort, total, sort_bytes;
+  size_t cnt, off, cursor, list, bsum, big, big_n, total;
+  int nblk;
 };
 
-unsigned key_bits(int64_t npix) {
-  unsigned b = 1;
-  while (b < 32 && ((int64_t)1 << b) < npix) ++b;
-  return b;
-}
-
-int det_layout(int64_t npix, DetWs& L) {
-  const int64_t ne = 4 * npix;
-  size_t sort_bytes = 0;
-  const hipError_t e = rocprim::radix_sort_pairs(
-      nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint64_t*)nullptr,
-      (uint64_t*)nullptr, (size_t)ne, 0u, key_bits(npix), (hipStream_t)0, false);
-  if (e != hipSuccess) return fail(OF_EHIP, std::string("warp bwd det: sort size query: ") +
-                                                hipGetErrorString(e));
+void det_layout(int64_t npix, DetWs& L) {
   auto al = [](size_t v) { return (v + 255) / 256 * 256; };
+  L.nblk = (int)cdiv(npix, OWN_SB);
   size_t o = 0;
-  L.keys_in = o, o += al(ne * 4);
-  L.keys_out = o, o += al(ne * 4);
-  L.vals_in = o, o += al(ne * 8);
-  L.vals_out = o, o += al(ne * 8);
-  L.runs = o, o += al(npix * 8);
-  L.sort = o, o += al(sort_bytes);
+  L.cnt = o, o += al(npix * 4);
+  L.cursor = o, o += al(npix * 4);     // (cnt and cursor adjacent: one memset)
+  L.off = o, o += al(npix * 4);
+  L.list = o, o += al(4 * npix * 4);
+  L.bsum = o, o += al((size_t)L.nblk * 4);
+  L.big = o, o += al(npix * 4);
+  L.big_n = o, o += 256;
   L.total = o;
-  L.sort_bytes = sort_bytes;
-  return OF_OK;
 }
 
 }  // namespace
@@ -262,7 +449,7 @@ size_t of_warp_bwd_det_workspace(int n, int h, int w, int c) {
   (void)c;
   if (n <= 0 || h <= 0 || w <= 0) return 0;
   DetWs L;
-  if (det_layout((int64_t)n * h * w, L)) return 0;
+  det_layout((int64_t)n * h * w, L);
   return L.total;
 }
 
@@ -279,34 +466,52 @@ int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, in
                    (!dinp || ((uintptr_t)dinp & 15) == 0);
   if (dinp) {
     DetWs L;
-    if (int st = det_layout(npix, L)) return st;
+    det_layout(npix, L);
     OF_CHECK_ARG(ws && ws_bytes >= L.total, "warp bwd det: workspace too small");
     char* base = static_cast<char*>(ws);
-    uint32_t* kin = reinterpret_cast<uint32_t*>(base + L.keys_in);
-    uint32_t* kout = reinterpret_cast<uint32_t*>(base + L.keys_out);
-    uint64_t* vin = reinterpret_cast<uint64_t*>(base + L.vals_in);
-    uint64_t* vout = reinterpret_cast<uint64_t*>(base + L.vals_out);
-    int2* runs = reinterpret_cast<int2*>(base + L.runs);
-    const int64_t ne = 4 * npix;
-    hipLaunchKernelGGL(det_entries, dim3((unsigned)cdiv(npix, 256)), dim3(256), 0, s, flow, n, h,
-                       w, absolute, kin, vin);
-    if (int st = check_launch("warp_bwd_det: entries")) return st;
-    size_t sb = L.sort_bytes;
-    const hipError_t e = rocprim::radix_sort_pairs(base + L.sort, sb, kin, kout, vin, vout,
-                                                   (size_t)ne, 0u, key_bits(npix), s, false);
-    if (e != hipSuccess)
-      return fail(OF_EHIP, std::string("warp bwd det: sort: ") + hipGetErrorString(e));
-    if (hipMemsetAsync(runs, 0, (size_t)npix * sizeof(int2), s) != hipSuccess)
-      return check_launch("warp_bwd_det: runs memset");
-    hipLaunchKernelGGL(det_bounds, dim3((unsigned)cdiv(ne, 256)), dim3(256), 0, s, kout, ne, runs);
-    if (int st = check_launch("warp_bwd_det: bounds")) return st;
-    if (vec) {
-      hipLaunchKernelGGL(det_gather_vec, dim3((unsigned)cdiv(npix * (c / 4), 256)), dim3(256), 0,
-                         s, dout, npix, c, runs, vout, dinp);
-    } else {
-      hipLaunchKernelGGL(det_gather_scalar, dim3((unsigned)cdiv(npix * c, 256)), dim3(256), 0, s,
-                         dout, npix, c, runs, vout, dinp);
+    int* cnt = reinterpret_cast<int*>(base + L.cnt);
+    int* cursor = reinterpret_cast<int*>(base + L.cursor);
+    int* off = reinterpret_cast<int*>(base + L.off);
+    uint32_t* list = reinterpret_cast<uint32_t*>(base + L.list);
+    int* bsum = reinterpret_cast<int*>(base + L.bsum);
+    int* big = reinterpret_cast<int*>(base + L.big);
+    int* big_n = reinterpret_cast<int*>(base + L.big_n);
+    if (hipMemsetAsync(cnt, 0, L.off - L.cnt, s) != hipSuccess ||
+        hipMemsetAsync(big_n, 0, sizeof(int), s) != hipSuccess)
+      return check_launch("warp_bwd_det: memset");
+    const dim3 gp((unsigned)cdiv(npix, 256));
+    hipLaunchKernelGGL(own_count, gp, dim3(256), 0, s, flow, n, h, w, absolute, cnt);
+    hipLaunchKernelGGL(own_block_sums, dim3(L.nblk), dim3(256), 0, s, cnt, npix, bsum);
+    hipLaunchKernelGGL(own_scan_sums, dim3(1), dim3(1024), 0, s, bsum, L.nblk);
+    hipLaunchKernelGGL(own_block_scan, dim3(L.nblk), dim3(256), 0, s, cnt, npix, bsum, off);
+    hipLaunchKernelGGL(own_fill, gp, dim3(256), 0, s, flow, n, h, w, absolute, off, cursor, list);
+    if (int st = check_launch("warp_bwd_det: sort")) return st;
+    if (vec)
+      hipLaunchKernelGGL(own_gather<true>, dim3((unsigned)cdiv(npix * 16, 256)), dim3(256), 0, s,
+                         dout, flow, n, h, w, c, absolute, cnt, off, list, dinp, big_n, big);
+    else
+      hipLaunchKernelGGL(own_gather<false>, dim3((unsigned)cdiv(npix * 16, 256)), dim3(256), 0, s,
+                         dout, flow, n, h, w, c, absolute, cnt, off, list, dinp, big_n, big);
+    const int64_t codes = 4 * (int64_t)h * w;
+    const size_t bm_bytes =
+        (size_t)(codes < OWN_WBITS ? (codes + 31) / 32 * 32 : OWN_WBITS) / 8;
+    static bool attr = false;
+    if (!attr) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(own_gather_big<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              OWN_WBITS / 8) != hipSuccess ||
+          hipFuncSetAttribute(reinterpret_cast<const void*>(own_gather_big<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              OWN_WBITS / 8) != hipSuccess)
+        return check_launch("warp_bwd_det: LDS attribute");
+      attr = true;
     }
+    if (vec)
+      hipLaunchKernelGGL(own_gather_big<true>, dim3(2 * device_cus()), dim3(256), bm_bytes, s,
+                         dout, flow, h, w, c, absolute, cnt, off, list, big_n, big, dinp);
+    else
+      hipLaunchKernelGGL(own_gather_big<false>, dim3(2 * device_cus()), dim3(256), bm_bytes, s,
+                         dout, flow, h, w, c, absolute, cnt, off, list, big_n, big, dinp);
     if (int st = check_launch("warp_bwd_det: gather")) return st;
   }
   if (vec) {

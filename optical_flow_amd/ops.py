@@ -987,6 +987,23 @@ class _EncoderFn(torch.autograd.Function):
         tbias = grad_target(conv1.bias) if nbias else (None, 0, None)
         acc = tg[1] if ng else (tb[1] if nbe else tbias[1])
         assert all(t[0] is None or t[1] == acc for t in (tg, tb, tbias))
+        d1 = conv1.desc(*x4.shape[:3])
+        m1 = conv1.mode(d1)
+        tk = grad_target(conv1.kernel) if nk else (None, 0, None)
+        if (STEM_FUSED and z0 is None and m1 in (1, 2) and nk and nbias and ng and nbe and
+                tk[1] == acc):
+            fws = _lib.lib().of_stem_bwd_fused_workspace(C.byref(d1), m1)
+            if fws > 0:
+                # the whole stem backward in the weight-gradient kernel: dz never stored
+                wsf = torch.empty(fws // 4 + 1, device=y0.device)
+                _tag(conv1, 2)
+                call("of_stem_bwd_fused", C.byref(d1), m1, _ptr(x4), x4.shape[-1],
+                     _ptr(dy.contiguous()), _ptr(gouts[0]), _ptr(y0), _ptr(gamma), _ptr(beta),
+                     _ptr(var), BN_EPS, _ptr(tk[0]), _ptr(tbias[0]), _ptr(tg[0]), _ptr(tb[0]),
+                     acc, _ptr(wsf), fws, _stream())
+                _grad_ready(conv1.kernel, conv1.bias, gamma, beta)
+                stem = [tk[2], tbias[2], tg[2], tb[2]]
+                return (None, *stem, *grads, None)
         dz0 = torch.empty_like(y0)
         ws = torch.empty(_lib.lib().of_maxpool_bn_act_bwd_workspace(n, h, w, c) // 4 + 1,
                          device=y0.device)
@@ -1117,6 +1134,12 @@ def encoder_forward_train(x4, conv1: ConvLayer, blocks, groups: int = 2):
         if i % 2 == 1:
             outs.append(x)
     return outs
+
+
+# The stem's backward (max-pool + out0 gradient + BN + ReLU, then the 7x7 weight gradient) in
+# the weight-gradient kernel itself (of_stem_bwd_fused): dz0, the encoder's largest tensor, is
+# never written and read back.  OFLOW_STEM_FUSED=0 keeps of_maxpool_bn_relu_bwd + the wgrad.
+STEM_FUSED = os.environ.get("OFLOW_STEM_FUSED", "1") == "1"
 
 
 def encoder_forward(x4, conv1: ConvLayer, blocks):

@@ -380,3 +380,43 @@ def test_two_forwards_one_backward():
     err = rel_l2(net.store.grad_arena, sep[0] + sep[1])
     print("two forwards, one backward: grad rel_l2 %.2e" % err)
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_stem_backward_fused(precision):
+    """The stem's backward in the weight-gradient kernel (ops.STEM_FUSED, of_stem_bwd_fused:
+    max-pool + out0 gradient + BN + ReLU backward formed while dz is staged, model.py:12-17)
+    against the two-kernel form (of_maxpool_bn_relu_bwd + the stem weight gradient) on the same
+    step: the stem's kernel, bias, gamma and beta gradients within 1e-5 relative L2 (the same
+    math, summed in another order), every other gradient bitwise equal; and the fused fp32
+    gradients against the float64 oracle at 1e-3."""
+    from optical_flow_amd import ops
+    from optical_flow_amd.loss import LossLayer
+    net, vals, batch, blocks = _setup(64, 128, 2, seed=11)
+    net.set_precision(precision)
+    bd = dev(torch.from_numpy(batch))
+    res = {}
+    with ops.deterministic(True):
+        for fused in (False, True):
+            prev, ops.STEM_FUSED = ops.STEM_FUSED, fused
+            try:
+                net.store.zero_grad()
+                LossLayer()(bd, net(bd)).backward()
+                torch.cuda.synchronize()
+            finally:
+                ops.STEM_FUSED = prev
+            res[fused] = {k: v.clone() for k, v in net.store.grads().items()}
+    stem = {"ResNet18/conv1/kernel", "ResNet18/conv1/bias", "ResNet18/layer1_bn/gamma",
+            "ResNet18/layer1_bn/beta"}
+    for k in res[True]:
+        if k in stem:
+            e = rel_l2(res[True][k], res[False][k])
+            print("%s %-28s fused vs two-kernel rel_l2 %.2e" % (precision, k, e))
+            assert e < 1e-5, (k, e)
+        else:
+            assert torch.equal(res[True][k], res[False][k]), k
+    if precision == "fp32":
+        p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+        _, _, go = R.train_step(torch.tensor(batch, dtype=torch.float64), p, blocks, None)
+        for k in stem:
+            assert rel_l2(res[True][k], go[k]) < REL_TOL, k
