@@ -566,6 +566,15 @@ int of_maxpool_bn_relu_bwd(int n, int h, int w, int c, const float* dyp, const f
                            const float* var, float eps, float* dz, float* dgamma, float* dbeta,
                            float* dbias, int accumulate, void* workspace, void* stream);
 
+/* The stem forward (conv1 + layer1_bn + ReLU, model.py:12-15) with the following MaxPool2D
+ * (model.py:17) in its epilogue: y as of_conv2d_fwd_x3 / _bf16 (precision 2 / 1) writes it, and
+ * pool (n, ho/2, wo/2, cout) = the 2x2 / stride-2 max of y, bit-identical to of_maxpool2_fwd.
+ * OF_EUNSUPPORTED unless the stem kernel takes the layer with an even output. */
+int of_conv2d_fwd_pool(const of_conv_desc* d, int precision, const float* x, int ldx,
+                       const void* w_fwd, const float* bias, const float* bn_gamma,
+                       const float* bn_beta, const float* bn_mean, const float* bn_var,
+                       float bn_eps, int act, float alpha, float* z, int ldz, float* y, int ldy,
+                       float* pool, void* workspace, size_t ws_bytes, void* stream);
 /* The stem's whole backward in one conv kernel (model.py:12-17, reset18_encoder's conv1 ->
  * layer1_bn -> ReLU -> {out0, MaxPool2D}): dz = relu'(y) (g + the max-pool gradient dyp at the
  * first maximum of each 2x2 window) * gamma / sqrt(var + eps) is formed while the weight

@@ -154,6 +154,7 @@ PROTOTYPES = {
     "of_conv2d_dgrad_add_act": (I, [PD, I, P, I, P, P, I, P, I, I, F, P, I, P, SZ, P]),
     "of_bn_bwd_reduce": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     "of_maxpool_bn_relu_bwd": (I, [I, I, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
+    "of_conv2d_fwd_pool": (I, [PD, I, P, I, P, P, P, P, P, P, F, I, F, P, I, P, I, P, P, SZ, P]),
     "of_stem_bwd_fused_workspace": (SZ, [PD, I]),
     "of_stem_bwd_fused": (I, [PD, I, P, I, P, P, P, P, P, P, F, P, P, P, P, I, P, SZ, P]),
     # BatchNormalization in training mode (bn_mode="training")

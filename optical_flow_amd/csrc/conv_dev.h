@@ -62,6 +62,7 @@ struct GemmArgs {
   // conv_wgrad_stem_x3<NP, true>: dz formed on load from the stem's max-pool / BN / ReLU
   // backward inputs (pooled gradient, the out0 gradient or NULL, the stem output y)
   const float* st_dyp; const float* st_g; const float* st_y;
+  float* pool_out;        // conv_stem_x3: also the 2x2 / stride-2 max-pool of the output (ld N)
   int ngroups;
   int vec_ep;             // tile kernels: 4-column epilogue (N, every ld a multiple of 4,
                           // every row pointer 16-byte aligned)

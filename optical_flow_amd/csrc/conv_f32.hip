@@ -1689,6 +1689,42 @@ __global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : NP == 1 ? 4 : 2) void conv_s
     if (oy < a.ho && ox < a.wo && n < a.N)
       epilogue_store4<MODE_FWD>(a, 0, img + (int64_t)oy * a.wo + ox, n, v);
   }
+  if (a.pool_out) {
+    // MaxPool2D (model.py:17) of the two output rows this wave owns (even rows: the 2 x 2
+    // windows never straddle waves or tiles): the epilogue's value of each of the four pixels
+    // (bias, BN, ReLU as epilogue_store4 computes it) and the max in maxpool2_fwd_kernel's order,
+    // so the pooled tensor is the separate pass's bit for bit, without re-reading the output.
+    const int pho = a.ho / 2, pwo = a.wo / 2;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = lane + 64 * u;                 // 16 pooled columns x 8 channel quads
+      const int pc = it >> 3, qq = it & 7;
+      const int nn = co0 + wn * WN + 4 * qq;
+      const int py = (oy0 + 2 * wm) / 2, px = ox0 / 2 + pc;
+      if (py >= pho || px >= pwo || nn >= a.N) continue;
+      float bias[4], scale[4], shift[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) column_params<MODE_FWD>(a, nn + e, bias[e], scale[e], shift[e]);
+      float r[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {                 // (0,0), (0,1), (1,0), (1,1)
+        const int m = (k >> 1) * 32 + 2 * pc + (k & 1);
+        const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * qq]);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = vv[e] + bias[e];
+          if (a.bn_g) x = x * scale[e] + shift[e];
+          r[k][e] = act_fwd(x, a.act, a.alpha);
+        }
+      }
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = fmaxf(fmaxf(r[0][e], r[1][e]), fmaxf(r[2][e], r[3][e]));
+      *reinterpret_cast<float4*>(&a.pool_out[(((int64_t)b * pho + py) * pwo + px) * a.N + nn]) =
+          make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
 }
 
 // of_set_tuning key 8: the stem on conv_stem_x3 (1: two 32-channel workgroups per CU,
@@ -5028,7 +5064,7 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
                          const float* bn_beta, const float* bn_mean, const float* bn_var,
                          float bn_eps, const float* residual, int ldr, int act, float alpha,
                          float* z, int ldz, float* y, int ldy, void* workspace, size_t ws_bytes,
-                         void* stream) {
+                         void* stream, float* pool = nullptr) {
   int st = validate(d);
   if (st) return st;
   const bool bf16 = prec == 1, x3 = prec == 2;
@@ -5097,6 +5133,12 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
   // split 3x3 forward, one K slice, fp32 output only: the direct epilogue (conv_dev.h)
   a.direct16 = x3 && tile && (g_x3_direct & 1) && a.splits == 1 && a.vec_ep && !residual && !z &&
                d->cout % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)y & 15) == 0;
+  if (pool) {
+    if (!stem || d->ho % 2 || d->wo % 2 || d->cout % 4)
+      return fail(OF_EUNSUPPORTED, "conv fwd pool: only the stem kernel with an even output");
+    OF_CHECK_ARG(((uintptr_t)pool & 15) == 0, "conv fwd pool: 16-byte alignment");
+    a.pool_out = pool;
+  }
   if (stem) {
     const int64_t tiles = (int64_t)d->n * cdiv(d->ho, ST_TH) * cdiv(d->wo, ST_TW);
     OF_CHECK_ARG(tiles < INT32_MAX, "conv stem: too many tiles");
@@ -5128,6 +5170,17 @@ int of_conv2d_fwd(const of_conv_desc* d, const float* x, int ldx, const float* w
   return conv_fwd_impl(0, d, x, ldx, w_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
                        bn_eps, residual, ldr, act, alpha, z, ldz, y, ldy, workspace, ws_bytes,
                        stream);
+}
+
+int of_conv2d_fwd_pool(const of_conv_desc* d, int precision, const float* x, int ldx,
+                       const void* w_fwd, const float* bias, const float* bn_gamma,
+                       const float* bn_beta, const float* bn_mean, const float* bn_var,
+                       float bn_eps, int act, float alpha, float* z, int ldz, float* y, int ldy,
+                       float* pool, void* workspace, size_t ws_bytes, void* stream) {
+  OF_CHECK_ARG(pool && (precision == 1 || precision == 2), "conv fwd pool: args");
+  return conv_fwd_impl(precision, d, x, ldx, w_fwd, bias, bn_gamma, bn_beta, bn_mean, bn_var,
+                       bn_eps, nullptr, 0, act, alpha, z, ldz, y, ldy, workspace, ws_bytes,
+                       stream, pool);
 }
 
 int of_conv2d_fwd_bf16(const of_conv_desc* d, const float* x, int ldx, const void* w16_fwd,

@@ -935,10 +935,8 @@ class _EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x4, *args):
         conv1, blocks = args[-1]
-        y0, z0 = _conv_forward(conv1, x4.contiguous())
-        n, h, w, c = y0.shape
-        xp = torch.empty((n, h // 2, w // 2, c), device=y0.device)
-        call("of_maxpool2_fwd", _ptr(y0), n, h, w, c, _ptr(xp), _stream())
+        x4 = x4.contiguous()
+        y0, z0, xp = _stem_forward_pool(conv1, x4)
         x = xp
         saved = [x4, y0, z0]
         outs = [y0]
@@ -1140,6 +1138,42 @@ def encoder_forward_train(x4, conv1: ConvLayer, blocks, groups: int = 2):
 # the weight-gradient kernel itself (of_stem_bwd_fused): dz0, the encoder's largest tensor, is
 # never written and read back.  OFLOW_STEM_FUSED=0 keeps of_maxpool_bn_relu_bwd + the wgrad.
 STEM_FUSED = os.environ.get("OFLOW_STEM_FUSED", "1") == "1"
+
+
+# The stem forward writes the max-pooled tensor too (of_conv2d_fwd_pool: MaxPool2D,
+# model.py:17, in the stem kernel's epilogue), so the pool does not re-read the encoder's
+# largest activation.  OFLOW_STEM_POOL=0 keeps the separate of_maxpool2_fwd pass.
+STEM_POOL = os.environ.get("OFLOW_STEM_POOL", "1") == "1"
+
+
+def _stem_forward_pool(conv1: ConvLayer, x4):
+    """conv1 + BN + ReLU -> (y0, z0, max-pool of y0)."""
+    n, h, w, cx = x4.shape
+    d = conv1.desc(n, h, w)
+    m = conv1.mode(d)
+    if STEM_POOL and m in (1, 2) and not conv1.store_z and d.ho % 2 == 0 and d.wo % 2 == 0:
+        wf, _ = conv1.packed(d)
+        y0 = torch.empty((n, d.ho, d.wo, conv1.cout), device=x4.device)
+        xp = torch.empty((n, d.ho // 2, d.wo // 2, conv1.cout), device=x4.device)
+        entry, wsz = conv1.fwd_entry(d)
+        wsk, wsp, wsb = _workspace(wsz, x4.device)
+        bn = conv1.bn
+        _tag(conv1, 0)
+        st = _lib.lib().of_conv2d_fwd_pool(
+            C.byref(d), m, _ptr(x4), cx, _ptr(wf), _ptr(conv1.bias), _ptr(bn[0]), _ptr(bn[1]),
+            _ptr(bn[2]), _ptr(bn[3]), BN_EPS, conv1.act, conv1.alpha, None, conv1.cout, _ptr(y0),
+            conv1.cout, _ptr(xp), wsp, wsb, _stream())
+        if st == _lib.OF_OK:
+            return y0, None, xp
+        if st != _lib.OF_EUNSUPPORTED:
+            _lib.check(st, "of_conv2d_fwd_pool")
+        if TIMING_TAGS and TIMING_TAGS[-1] == (conv1.name, 0):
+            TIMING_TAGS.pop()                # nothing was launched: the tag is re-added below
+    y0, z0 = _conv_forward(conv1, x4)
+    n, h, w, c = y0.shape
+    xp = torch.empty((n, h // 2, w // 2, c), device=y0.device)
+    call("of_maxpool2_fwd", _ptr(y0), n, h, w, c, _ptr(xp), _stream())
+    return y0, z0, xp
 
 
 def encoder_forward(x4, conv1: ConvLayer, blocks):

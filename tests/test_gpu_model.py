@@ -310,8 +310,16 @@ def test_bn_gamma_near_zero(precision):
     """Inference BN (model.py:14, the resnet blocks) with gammas at 0 and 1e-4 and a large
     beta / residual: the backward's zhat = (y - res - beta) / gamma is undefined or
     imprecise there, so ops.BNZGuard keeps z for those layers and the BN backward reads it.
-    Every gradient against the oracle (float64; bf16: the bf16-rounded oracle at the module
-    test's 1e-2), no NaN, and the guard picked exactly the layers with small gammas."""
+    No NaN, the guard picks exactly the layers with small gammas, and every gradient matches the
+    oracle: fp32 through the train step's loss against the float64 oracle at 1e-3.
+
+    bf16 is checked through a smooth objective, sum_k <flow_k, G_k> with fixed random G_k,
+    against the bf16-rounded oracle: the median encoder-gradient error at the whole-net bf16
+    bound (8e-2, test_flow_net_bf16), the worst at 0.25.  (Through the photometric loss the
+    bf16 median measured 0.104 in round 4: the loss's |.| and the warp's floor() turn the bf16
+    rounding differences of the flows (~1e-2) into flipped per-pixel gradient contributions
+    that every encoder gradient inherits -- the end-to-end statistics of DESIGN.md §1, not the
+    BN guard; the smooth objective leaves only the network's own LeakyReLU / ReLU kinks.)"""
     from optical_flow_amd.loss import LossLayer
     from optical_flow_amd.data import synthetic_batch
     from optical_flow_amd.model import FlowNet
@@ -327,35 +335,52 @@ def test_bn_gamma_near_zero(precision):
     net = FlowNet(H, W, values=vals, precision=precision)
     batch = synthetic_batch(B, H, W, seed=77)
     p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+    blocks = list(encoder_blocks())
+    smooth = precision == "bf16"
+    gs = None
+    if smooth:
+        rng = np.random.default_rng(78)
+        gs = [torch.tensor(rng.standard_normal((B, H >> (k + 1), W >> (k + 1), 2)))
+              for k in range(4)]
     R.set_conv_precision(precision)
     try:
-        loss_o, flows_o, grads_o = R.train_step(torch.tensor(batch, dtype=torch.float64), p,
-                                                list(encoder_blocks()), None)
+        if smooth:
+            tr = {k: v.clone().requires_grad_(True) for k, v in p.items()
+                  if not k.endswith(("moving_mean", "moving_variance"))}
+            pp = dict(p, **tr)
+            fo = R.flow_net(torch.tensor(batch, dtype=torch.float64), pp, blocks)
+            obj = sum((f * gk).sum() for f, gk in zip(fo, gs))
+            grads_o = dict(zip(tr, torch.autograd.grad(obj, list(tr.values()), allow_unused=True)))
+        else:
+            _, _, grads_o = R.train_step(torch.tensor(batch, dtype=torch.float64), p, blocks, None)
     finally:
         R.set_conv_precision("fp32")
     net.store.zero_grad()
     bd = dev(torch.from_numpy(batch))
     flows = net(bd)
-    LossLayer()(bd, flows).backward()
+    if smooth:
+        sum((f * dev(gk.float())).sum() for f, gk in zip(flows, gs)).backward()
+    else:
+        LossLayer()(bd, flows).backward()
     torch.cuda.synchronize()
     assert sorted(net.store.bn_guard.stored()) == sorted(
         ["conv1", "ResNet18/res2_0/conv_a", "ResNet18/res3_0/conv_b",
          "ResNet18/res4_0/proj"]), net.store.bn_guard.stored()
-    # bf16: the whole net against the bf16-rounded oracle carries the flow heads' rounding
-    # sensitivity (no teacher forcing here), so the bound is the full-size tests' (worst 0.25,
-    # test_gpu_fullsize.py), the module-level 1e-2 being test_gpu_bf16_modules'.
-    tol = REL_TOL if precision == "fp32" else 0.25
     bad, errs = [], []
     for name, gr in net.store.grads().items():
         assert torch.isfinite(gr).all(), name
-        e = rel_l2(gr, grads_o[name])
+        ref = grads_o[name] if grads_o[name] is not None else torch.zeros_like(gr.double().cpu())
+        e = rel_l2(gr, ref)
         print("%-40s rel_l2 %.3e" % (name, e))
         if name.startswith("ResNet18"):
             errs.append(e)
-            if e >= tol:
+            if e >= (REL_TOL if precision == "fp32" else 0.25):
                 bad.append((name, e))
-    print("median ResNet18 grad rel_l2 %.3e" % float(np.median(errs)))
+    med = float(np.median(errs))
+    print("%s: median ResNet18 grad rel_l2 %.3e, worst %.3e" % (precision, med, max(errs)))
     assert not bad, bad
+    if precision == "bf16":
+        assert med < 8e-2, med
 
 
 def test_two_forwards_one_backward():
@@ -420,3 +445,24 @@ def test_stem_backward_fused(precision):
         _, _, go = R.train_step(torch.tensor(batch, dtype=torch.float64), p, blocks, None)
         for k in stem:
             assert rel_l2(res[True][k], go[k]) < REL_TOL, k
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_stem_forward_pool(precision):
+    """The stem forward with the max-pool in its epilogue (ops.STEM_POOL, of_conv2d_fwd_pool,
+    model.py:12-17): the encoder's outputs -- out0 and everything after the pool -- are
+    bitwise those of the separate of_maxpool2_fwd pass."""
+    from optical_flow_amd import ops
+    net, vals, batch, blocks = _setup(64, 128, 2, seed=12)
+    net.set_precision(precision)
+    x4 = ops.split_pair(dev(torch.from_numpy(batch)))
+    outs = {}
+    with torch.no_grad():
+        for on in (False, True):
+            prev, ops.STEM_POOL = ops.STEM_POOL, on
+            try:
+                outs[on] = [t.clone() for t in net.encoder.forward4(x4)]
+            finally:
+                ops.STEM_POOL = prev
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
