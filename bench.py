@@ -342,9 +342,10 @@ def main():
                     help="1: run the step on a high-priority HIP stream, so the hardware "
                          "dispatches its workgroups ahead of the side streams' (weight "
                          "gradients, the cost volume's df1) when both have work queued")
-    ap.add_argument("--deterministic", type=int, choices=[0, 1], default=0,
-                    help="1: the deterministic (sort + fixed-order gather) warp backward "
-                         "(ops.DETERMINISTIC)")
+    ap.add_argument("--deterministic", type=int, choices=[0, 1],
+                    default=int(os.environ.get("OFLOW_DETERMINISTIC", "1")),
+                    help="1 (default): the deterministic warp backward (window gather / int64 "
+                         "fixed point, ops.DETERMINISTIC); 0: the float-atomic warp_bwd_gather")
     args = ap.parse_args()
 
     from optical_flow_amd import _lib, ops

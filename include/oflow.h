@@ -278,13 +278,20 @@ int of_bilinear_fwd(const float* inp, int n, int h, int w, int c, const float* p
 int of_bilinear_bwd(const float* dout, const float* inp, int n, int h, int w, int c,
                     const float* pts, float* dinp, float* dpts, void* stream);
 /* Deterministic mode of the three backward entry points above (no atomics in the
- * warp backward; the gradient of the gathers of transformations.py:110-113,128): the scatter
- * into dinp becomes a stable sort of the (source pixel, corner) entries by destination and a
- * fixed-order gather, so the result is bitwise reproducible.  dinp is WRITTEN (not accumulated;
- * NULL skips it), dflow = d/d(flow) (+ dflow_add with row stride ld_add if non-NULL);
- * absolute != 0: flow holds absolute (x, y) sampling points (of_bilinear_bwd).  Workspace:
- * of_warp_bwd_det_workspace(n, h, w, c) bytes. */
+ * warp backward; the gradient of the gathers of transformations.py:110-113,128): the float
+ * scatter into dinp becomes either a fixed-order gather -- every destination sums its (source
+ * pixel, corner) entries in ascending source order, found by a window scan around the source
+ * position (relative flows) -- or, for absolute points and flows the window cannot cover, an
+ * exact int64 fixed-point sum (scale from max |dout|: each term exact to max|dout| 2^(L-61),
+ * 4 n h w <= 2^L; integer adds, so in any order the same).  Bitwise reproducible either way.
+ * dinp is WRITTEN (not accumulated; NULL skips it), dflow = d/d(flow) (+ dflow_add with row
+ * stride ld_add if non-NULL); absolute != 0: flow holds absolute (x, y) sampling points
+ * (of_bilinear_bwd).  Workspace: of_warp_bwd_det_workspace(n, h, w, c) bytes; its int header
+ * at byte of_warp_bwd_det_header(n, h, w, c) holds after a call [1] = R = floor(max |flow|) +
+ * 2 (the window is mode A when R <= of_set_tuning key 28, else mode B) and at ints 64 (1 + s),
+ * s < 32, the hits mode B found (their sum is 4 n h w when its window served). */
 size_t of_warp_bwd_det_workspace(int n, int h, int w, int c);
+size_t of_warp_bwd_det_header(int n, int h, int w, int c);
 int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, int c,
                     const float* flow, int absolute, float* dinp, float* dflow,
                     const float* dflow_add, int ld_add, void* workspace, size_t ws_bytes,
@@ -322,6 +329,17 @@ int of_photo_l1_bwd(const float* img6, const float* flow, int n, int h, int w, f
 int of_photo_l1_bwd_ld(const float* img6, const float* flow, int n, int h, int w, float coef,
                        const float* dloss, float* dflow, int lddf, void* stream);
 /* out[0] = sum_i coef_j * partials_j[i] over `count` groups (deterministic). */
+/* Every scale of the loss in one launch (levels <= 8; level l at hs[l] x ws[l]): the forward's
+ * partials concatenated in level order (sum over l of of_photo_l1_partials(n, hs[l], ws[l])
+ * floats; level l's are the ones of_photo_l1_fwd would write), the backward's d(flow) of level
+ * l times coefs[l] (* dloss[0] if dloss) at row stride lds[l]. */
+int of_photo_l1_fwd_multi(const float* const* img6s, const float* const* flows, int n,
+                          const int* hs, const int* ws, int levels, float* partials,
+                          void* stream);
+int of_photo_l1_bwd_multi(const float* const* img6s, const float* const* flows, int n,
+                          const int* hs, const int* ws, int levels, const float* coefs,
+                          const float* dloss, float* const* dflows, const int* lds,
+                          void* stream);
 int of_sum_partials(const float* const* parts, const int* counts, const float* coefs,
                     int ngroups, float* out, void* stream);
 
@@ -402,7 +420,10 @@ int of_timing_enable(int on);
  * keys 25 / 26 = the K-split cost models' slab-pass term (tenths of a chunk per slice and tile
  * round; default 5) of the fp32 halo-tile kernels and of the split implicit GEMMs;
  * key 27 = fp32 split 3x3 layers whose BN = 128 grid has fewer than this many workgroups run
- * BN = 64 tiles, two workgroups per CU (0 = never). */
+ * BN = 64 tiles, two workgroups per CU (default 256; 0 = never);
+ * key 28 = of_warp_bwd_det's window gather: mode A (a window of radius R around the
+ * transposed position) when R = floor(max |flow|) + 2 <= this, else mode B (default 8; 0 =
+ * no window, always the fixed-point path; 1 = always mode B). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -109,6 +109,7 @@ PROTOTYPES = {
     "of_conv2d_wgrad_b16i_workspace": (SZ, [PD]),
     "of_conv2d_wgrad_b16i": (I, [PD, P, I, P, I, P, I, P, P, F, P, SZ, P]),
     "of_warp_bwd_det_workspace": (SZ, [I, I, I, I]),
+    "of_warp_bwd_det_header": (SZ, [I, I, I, I]),
     "of_warp_bwd_det": (I, [P, P, I, I, I, I, P, I, P, P, P, I, P, SZ, P]),
     "of_upscale2x_fwd": (I, [P, I, I, I, I, F, P, I, P]),
     "of_upscale2x_bwd": (I, [P, I, I, I, I, I, F, P, I, P]),
@@ -155,6 +156,10 @@ PROTOTYPES = {
     "of_bn_bwd_reduce": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     "of_maxpool_bn_relu_bwd": (I, [I, I, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     "of_conv2d_fwd_pool": (I, [PD, I, P, I, P, P, P, P, P, P, F, I, F, P, I, P, I, P, P, SZ, P]),
+    "of_photo_l1_fwd_multi": (I, [C.POINTER(P), C.POINTER(P), I, C.POINTER(I), C.POINTER(I), I, P,
+                                  P]),
+    "of_photo_l1_bwd_multi": (I, [C.POINTER(P), C.POINTER(P), I, C.POINTER(I), C.POINTER(I), I,
+                                  C.POINTER(F), P, C.POINTER(P), C.POINTER(I), P]),
     "of_stem_bwd_fused_workspace": (SZ, [PD, I]),
     "of_stem_bwd_fused": (I, [PD, I, P, I, P, P, P, P, P, P, F, P, P, P, P, I, P, SZ, P]),
     # BatchNormalization in training mode (bn_mode="training")

@@ -59,7 +59,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
             list(ex.map(run, jobs))
     if jobs or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o)
                                                                         for o in objs):
-        run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lz", "-lpthread", "-ldl"])
+        # link to a temporary name, then rename: a reader (or a snapshot of the tree) never
+        # sees a half-written library
+        tmp = LIB + ".tmp%d" % os.getpid()
+        run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs + ["-lz", "-lpthread", "-ldl"])
+        os.replace(tmp, LIB)
     return LIB
 
 

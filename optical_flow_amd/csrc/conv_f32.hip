@@ -4131,7 +4131,12 @@ __global__ void pack_one_kernel(PackEntry E, int64_t total) {
 }
 
 // dw[tap][ci][co] (HWIO) = sum_z slab[z][tap*kc + ci][co]; optional db[co] = sum_z slab[z][M][co].
-// Workgroup = 32 items x 8 split lanes, item = (output row, 4 columns); fixed-order reduction.
+// Workgroup = 256 / LANES items x LANES split lanes, item = (output row, 4 columns); each lane
+// sums every LANES-th slab with eight loads in flight, then a fixed-order LDS reduction over
+// the lanes.  LANES = 32 for many slabs (the 9-tap weight gradients write one slab per
+// workgroup: 256 of them for the encoder's 64-channel layers): more workgroups and fewer
+// serial loads per lane, so the pass keeps its bandwidth when it shares the chip.
+template <int LANES>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws,
                                                            int splits, int64_t split_stride,
                                                            int taps, int kc, int cin, int cout,
@@ -4140,11 +4145,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
                                                            const float* __restrict__ bn_g,
                                                            const float* __restrict__ bn_v,
                                                            float bn_eps) {
-  __shared__ float4 red[EP_LANES][EP_ITEMS];
-  const int it = threadIdx.x % EP_ITEMS, sl = threadIdx.x / EP_ITEMS;
+  constexpr int ITEMS = 256 / LANES;
+  __shared__ float4 red[LANES][ITEMS];
+  const int it = threadIdx.x % ITEMS, sl = threadIdx.x / ITEMS;
   const int cq = (cout + 3) / 4;
   const int rows = taps * cin + (db ? 1 : 0);
-  const int64_t item = (int64_t)blockIdx.x * EP_ITEMS + it;
+  const int64_t item = (int64_t)blockIdx.x * ITEMS + it;
   const bool live = item < (int64_t)rows * cq;
   const int q = live ? (int)(item % cq) : 0;
   const int row = live ? (int)(item / cq) : 0;
@@ -4158,18 +4164,42 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (live) {
-    acc = strided_sum4(ws + m * ldc + 4 * q, sl, splits, split_stride);
+    const float* src = ws + m * ldc + 4 * q;
+    int z = sl;
+    for (; z + 7 * LANES < splits; z += 8 * LANES) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = *reinterpret_cast<const float4*>(src + (int64_t)(z + u * LANES) * split_stride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) add4(acc, v[u]);
+    }
+    for (; z < splits; z += LANES)
+      add4(acc, *reinterpret_cast<const float4*>(src + (int64_t)z * split_stride));
   }
   red[sl][it] = acc;
   __syncthreads();
   if (sl != 0 || !live) return;
-  for (int k = 1; k < EP_LANES; ++k) add4(acc, red[k][it]);
+  for (int k = 1; k < LANES; ++k) add4(acc, red[k][it]);
   float v[4] = {acc.x, acc.y, acc.z, acc.w};
   float* dst = is_bias ? db + 4 * q : dw + (int64_t)row * cout + 4 * q;
   const int nv = min(4, cout - 4 * q);
   if (bn_g)                       // dL/dz = t * gamma / sqrt(var + eps), folded per column
     for (int e = 0; e < nv; ++e) v[e] *= bn_g[4 * q + e] * rsqrtf(bn_v[4 * q + e] + bn_eps);
   for (int e = 0; e < nv; ++e) dst[e] = accum ? dst[e] + v[e] : v[e];
+}
+
+// launch with the lane count by the number of slabs
+void launch_wgrad_reduce(hipStream_t s, const float* ws, int splits, int64_t split_stride,
+                         int taps, int kc, int cin, int cout, int ldc, float* dw, float* db,
+                         int accum, const float* bn_g, const float* bn_v, float bn_eps) {
+  const int64_t items = ((int64_t)taps * cin + (db ? 1 : 0)) * cdiv(cout, 4);
+  if (splits >= 64)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<32>, dim3(cdiv(items, 8)), dim3(256), 0, s, ws, splits,
+                       split_stride, taps, kc, cin, cout, ldc, dw, db, accum, bn_g, bn_v, bn_eps);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(cdiv(items, 32)), dim3(256), 0, s, ws, splits,
+                       split_stride, taps, kc, cin, cout, ldc, dw, db, accum, bn_g, bn_v, bn_eps);
 }
 
 // ------------------------------------------------------------------------------ dispatch --
@@ -4511,7 +4541,7 @@ bool ws_ok(const of_conv_desc* d, int mode) {
 // slice and tile round, of the halo-tile kernels (tile_args) and of conv_gemm_x3 (gemm_x3_plan).
 static int g_x3t_ep = 5;
 static int g_x3g_ep = 5;
-static int g_x3_small_bn = 0;
+static int g_x3_small_bn = 256;
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false,
                    bool b16 = false, bool ws = false) {
   GemmArgs a = base_args(d);
@@ -4969,6 +4999,7 @@ int of_set_tuning(int key, int value) {
   if (key == 25 && value >= 0 && value <= 1000) { g_x3t_ep = value; return OF_OK; }
   if (key == 26 && value >= 0 && value <= 1000) { g_x3g_ep = value; return OF_OK; }
   if (key == 27 && value >= 0 && value <= 100000) { g_x3_small_bn = value; return OF_OK; }
+  if (key == 28 && value >= 0 && value <= 64) { g_det_rmax = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -5527,10 +5558,8 @@ static int conv_wgrad_impl(int prec, const of_conv_desc* d, const float* x, int 
     st = launch_gemm<MODE_WGRAD>(a, s, flops);
   }
   if (st) return st;
-  const int64_t items = ((int64_t)g.taps * d->cin + (db ? 1 : 0)) * cdiv(d->cout, 4);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
-                     static_cast<const float*>(workspace), p.splits, p.split_stride, g.taps,
-                     g.cin_p, d->cin, d->cout, p.ldc, dw, db, accumulate, bn_g, bn_v, bn_eps);
+  launch_wgrad_reduce(s, static_cast<const float*>(workspace), p.splits, p.split_stride, g.taps,
+                      g.cin_p, d->cin, d->cout, p.ldc, dw, db, accumulate, bn_g, bn_v, bn_eps);
   return check_launch("wgrad_reduce");
 }
 
@@ -5597,10 +5626,9 @@ int of_stem_bwd_fused(const of_conv_desc* d, int precision, const float* x, int 
   st = check_launch("conv_wgrad_stem_x3 fused");
   if (st) return st;
   Geo gg = geo(d);
-  const int64_t items = (int64_t)gg.taps * d->cin * cdiv(d->cout, 4);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(items, EP_ITEMS)), dim3(256), 0, s,
-                     static_cast<const float*>(workspace), p.splits, stride, gg.taps, gg.cin_p,
-                     d->cin, d->cout, p.ldc, dw, nullptr, accumulate, nullptr, nullptr, 0.f);
+  launch_wgrad_reduce(s, static_cast<const float*>(workspace), p.splits, stride, gg.taps,
+                      gg.cin_p, d->cin, d->cout, p.ldc, dw, nullptr, accumulate, nullptr, nullptr,
+                      0.f);
   st = check_launch("wgrad_reduce");
   if (st) return st;
   hipLaunchKernelGGL(stem_bn_final, dim3(1), dim3(256), 0, s, static_cast<const float*>(workspace),

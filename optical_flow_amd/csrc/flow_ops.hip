@@ -1633,6 +1633,41 @@ __global__ __launch_bounds__(256) void pyramid6_kernel(const float* __restrict__
   }
 }
 
+// All levels in one launch (the per-level launches were ~5 us each, latency-bound): element
+// idx of the concatenation of the levels' outputs; level l + 1 starts at begin[l].
+struct PyrArgs {
+  float* out[8];
+  int64_t begin[9];
+  int levels;
+};
+__global__ __launch_bounds__(256) void pyramid6_multi(const float* __restrict__ in, int n, int H,
+                                                      int W, PyrArgs pa) {
+  const int64_t total = pa.begin[pa.levels];
+  for (int64_t gi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gi < total;
+       gi += (int64_t)gridDim.x * blockDim.x) {
+    int l = 0;
+    while (l + 1 < pa.levels && gi >= pa.begin[l + 1]) ++l;
+    const int64_t idx = gi - pa.begin[l];
+    const int f = 2 << l;
+    const int h = H / f, w = W / f;
+    const int e = (int)(idx % 6);
+    const int64_t p = idx / 6;
+    const int x = (int)(p % w);
+    const int64_t t2 = p / w;
+    const int y = (int)(t2 % h);
+    const int64_t b = t2 / h;
+    const int y0 = f * y + f / 2 - 1, x0 = f * x + f / 2 - 1;
+    const float* base = in + (b * H * W) * 6 + e;
+    const float v00 = base[((int64_t)y0 * W + x0) * 6];
+    const float v01 = base[((int64_t)y0 * W + x0 + 1) * 6];
+    const float v10 = base[((int64_t)(y0 + 1) * W + x0) * 6];
+    const float v11 = base[((int64_t)(y0 + 1) * W + x0 + 1) * 6];
+    const float top = v00 + (v01 - v00) * 0.5f;
+    const float bot = v10 + (v11 - v10) * 0.5f;
+    pa.out[l][idx] = top + (bot - top) * 0.5f;
+  }
+}
+
 // Siamese split (model.py:122-123,131-132): (B,H,W,6) -> (2B,H,W,4), channel 3 zero.
 __global__ __launch_bounds__(256) void split_pair_kernel(const float* __restrict__ in, int n,
                                                          int h, int w, float* __restrict__ out) {
@@ -1696,6 +1731,85 @@ __global__ __launch_bounds__(PL_THREADS) void photo_l1_fwd_kernel(const float* _
     float t = 0.f;
     for (int k = 0; k < PL_THREADS / 64; ++k) t += red[k];
     partials[blockIdx.x] = t;
+  }
+}
+
+// The photometric loss of every scale in one launch: level l's blocks are [bbeg[l], bbeg[l+1])
+// (forward: one partial per block, the partial arrays concatenated in level order) or its
+// pixels [pbeg[l], pbeg[l+1]) (backward: d(flow) of level l at row stride ld[l]).
+struct PhotoMulti {
+  const float* img6[8];
+  const float* flow[8];
+  float* dflow[8];
+  int ld[8];
+  float coef[8];
+  int h[8], w[8];
+  int64_t beg[9];
+  int levels;
+};
+__global__ __launch_bounds__(PL_THREADS) void photo_l1_fwd_multi(int n, PhotoMulti m,
+                                                                 float* __restrict__ partials) {
+  int l = 0;
+  while (l + 1 < m.levels && (int64_t)blockIdx.x >= m.beg[l + 1]) ++l;
+  const int h = m.h[l], w = m.w[l];
+  const float* img6 = m.img6[l];
+  const float* flow = m.flow[l];
+  const int64_t npix = (int64_t)n * h * w;
+  const int64_t p0 = ((int64_t)blockIdx.x - m.beg[l]) * PL_PIX_PER_BLOCK;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < PL_PIX_PER_BLOCK; k += PL_THREADS) {
+    const int64_t p = p0 + k;
+    if (p >= npix) break;
+    const int j = (int)(p % w);
+    const int64_t t2 = p / w;
+    const int i = (int)(t2 % h);
+    const int64_t img = (t2 / h) * h * w;
+    float diff[3], v[4][3];
+    WarpTap t;
+    photo_sample(img6, p, i, j, flow[2 * p], flow[2 * p + 1], h, w, img, diff, t, v);
+    s += fabsf(diff[0]) + fabsf(diff[1]) + fabsf(diff[2]);
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  __shared__ float red[PL_THREADS / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < PL_THREADS / 64; ++k) t += red[k];
+    partials[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void photo_l1_bwd_multi(int n, PhotoMulti m,
+                                                          const float* __restrict__ dloss) {
+  const int64_t total = m.beg[m.levels];
+  const float dl = dloss ? dloss[0] : 1.f;
+  for (int64_t gp = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gp < total;
+       gp += (int64_t)gridDim.x * blockDim.x) {
+    int l = 0;
+    while (l + 1 < m.levels && gp >= m.beg[l + 1]) ++l;
+    const int h = m.h[l], w = m.w[l];
+    const float* img6 = m.img6[l];
+    const float* flow = m.flow[l];
+    const int64_t p = gp - m.beg[l];
+    const int j = (int)(p % w);
+    const int64_t t2 = p / w;
+    const int i = (int)(t2 % h);
+    const int64_t img = (t2 / h) * h * w;
+    float diff[3], v[4][3];
+    WarpTap t;
+    photo_sample(img6, p, i, j, flow[2 * p], flow[2 * p + 1], h, w, img, diff, t, v);
+    const float a = t.a, b = t.b, coef = m.coef[l] * dl;
+    float gx = 0.f, gy = 0.f;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const float sg = diff[e] > 0.f ? 1.f : (diff[e] < 0.f ? -1.f : 0.f);
+      const float g = -coef * sg;
+      gx -= g * (b * (v[0][e] - v[2][e]) + (1.f - b) * (v[1][e] - v[3][e]));
+      gy -= g * (a * (v[0][e] - v[1][e]) + (1.f - a) * (v[2][e] - v[3][e]));
+    }
+    m.dflow[l][m.ld[l] * p] = gx;
+    m.dflow[l][m.ld[l] * p + 1] = gy;
   }
 }
 
@@ -2149,14 +2263,63 @@ int of_pyramid6(const float* batch, int n, int h, int w, int levels, float* cons
   OF_CHECK_ARG(h % (1 << levels) == 0 && w % (1 << levels) == 0,
                "pyramid: H and W must be divisible by 2^levels (P17)");
   hipStream_t s = as_stream(stream);
+  PyrArgs pa{};
+  pa.levels = levels;
+  pa.begin[0] = 0;
   for (int l = 1; l <= levels; ++l) {
-    const int64_t total = (int64_t)n * (h >> l) * (w >> l) * 6;
-    hipLaunchKernelGGL(pyramid6_kernel, dim3(grid_for(total)), dim3(256), 0, s, batch, n, h, w, l,
-                       outs[l - 1]);
-    int st = check_launch("pyramid6");
-    if (st) return st;
+    OF_CHECK_ARG(outs[l - 1], "pyramid: NULL output");
+    pa.out[l - 1] = outs[l - 1];
+    pa.begin[l] = pa.begin[l - 1] + (int64_t)n * (h >> l) * (w >> l) * 6;
   }
-  return OF_OK;
+  hipLaunchKernelGGL(pyramid6_multi, dim3(grid_for(pa.begin[levels])), dim3(256), 0, s, batch, n,
+                     h, w, pa);
+  return check_launch("pyramid6");
+}
+
+int of_photo_l1_fwd_multi(const float* const* img6s, const float* const* flows, int n,
+                          const int* hs, const int* ws, int levels, float* partials,
+                          void* stream) {
+  OF_CHECK_ARG(img6s && flows && hs && ws && partials && levels >= 1 && levels <= 8,
+               "photo l1 fwd multi: args");
+  PhotoMulti m{};
+  m.levels = levels;
+  m.beg[0] = 0;
+  for (int l = 0; l < levels; ++l) {
+    OF_CHECK_ARG(img6s[l] && flows[l], "photo l1 fwd multi: NULL level");
+    m.img6[l] = img6s[l];
+    m.flow[l] = flows[l];
+    m.h[l] = hs[l];
+    m.w[l] = ws[l];
+    m.beg[l + 1] = m.beg[l] + of_photo_l1_partials(n, hs[l], ws[l]);
+  }
+  hipLaunchKernelGGL(photo_l1_fwd_multi, dim3((unsigned)m.beg[levels]), dim3(PL_THREADS), 0,
+                     as_stream(stream), n, m, partials);
+  return check_launch("photo_l1_fwd_multi");
+}
+
+int of_photo_l1_bwd_multi(const float* const* img6s, const float* const* flows, int n,
+                          const int* hs, const int* ws, int levels, const float* coefs,
+                          const float* dloss, float* const* dflows, const int* lds,
+                          void* stream) {
+  OF_CHECK_ARG(img6s && flows && hs && ws && coefs && dflows && lds && levels >= 1 && levels <= 8,
+               "photo l1 bwd multi: args");
+  PhotoMulti m{};
+  m.levels = levels;
+  m.beg[0] = 0;
+  for (int l = 0; l < levels; ++l) {
+    OF_CHECK_ARG(img6s[l] && flows[l] && dflows[l] && lds[l] >= 2, "photo l1 bwd multi: level");
+    m.img6[l] = img6s[l];
+    m.flow[l] = flows[l];
+    m.dflow[l] = dflows[l];
+    m.ld[l] = lds[l];
+    m.coef[l] = coefs[l];
+    m.h[l] = hs[l];
+    m.w[l] = ws[l];
+    m.beg[l + 1] = m.beg[l] + (int64_t)n * hs[l] * ws[l];
+  }
+  hipLaunchKernelGGL(photo_l1_bwd_multi, dim3(grid_for(m.beg[levels])), dim3(256), 0,
+                     as_stream(stream), n, m, dloss);
+  return check_launch("photo_l1_bwd_multi");
 }
 
 int of_split_pair(const float* batch, int n, int h, int w, float* out, void* stream) {

@@ -6,24 +6,32 @@
 // map, whose adds land in whatever order the hardware retires them.  The atomic HIP backward
 // (flow_ops.hip warp_bwd_gather) keeps that shape: per-tile sums added with float atomics, so
 // two identical steps can differ in the last bit of d(features).  Here the scatter becomes a
-// gather with a fixed summation order, all hand-written (a counting sort by destination):
+// gather with a fixed summation order: every destination row sums w_k * dout[p] over its
+// (source p, corner k) entries in ascending code 4 p + k, and is STORED once (no zero-fill,
+// no float atomics).  Two ways to find a destination's entries:
 //
-//   1. count   : every (source pixel p, corner k) adds 1 to its destination's counter
-//                (integer adds: exact in any order);
-//   2. scan    : exclusive prefix sums of the counts -> each destination's segment;
-//   3. fill    : each entry's code 4 p + k into a slot of its segment (slot order free);
-//   4. gather  : per destination, the segment's codes ranked (16 lanes, codes distinct) and
-//                w_k * dout[p] summed in ascending code order, STORED -- every row written
-//                once, so no zero-fill pass and no float atomics;
-//   5. big     : segments of more than 16 entries (a field clipped onto the border) through an
-//                LDS bitmap over the code range, visited in code order;
-//   6. d(flow) : per source pixel over all channels in a fixed order (16 lanes x channel quads,
-//                then a fixed DPP row reduction), plus the optional addend of of_warp_bwd_add.
+//   window (own_window, relative flows): every destination scans a window of candidate
+//     sources in ascending order, 16 candidates a step over 16 lanes, and sums its hits.
+//     Mode A (R <= of_set_tuning key 28, R = floor(max |flow|) + 2 from own_radius): a
+//     sample lands within R of its source's transposed position (P1's grid), so the window is
+//     (2R+1)^2 around it -- complete by construction.  Mode B (larger flows): the window is
+//     (2 WIN_RB + 1)^2 around a source position found by two fixed-point steps on the flow
+//     (smooth fields: complete); destinations on the image border scan the whole clipped
+//     range.  Mode B counts the hits it found; complete iff the count is 4 n h w (each
+//     entry lands on exactly one destination, and no window yields a false hit).
+//     Destinations on a pile (the last row when w - h > WIN_PILE in mode A: P1 clips every
+//     source beyond h onto it; every border pixel in mode B) get a workgroup each.
+//   fixed point (absolute points, key 28 = 0, or a mode-B count short of 4 n h w): every
+//     contribution rounded to an int64 at a scale set by max |dout| and added with integer
+//     atomics (exact, so in any order the same), tile-aggregated in LDS so that samples piled
+//     onto the border add once per workgroup; then scaled back (fix_prep / fix_scatter /
+//     fix_convert below).  Its kernels return at once when the window served (~5 us a launch).
+//   6. d(flow): per source pixel over all channels in a fixed order (16 lanes x channel quads,
+//      then a fixed DPP row reduction), plus the optional addend of of_warp_bwd_add -- in
+//      own_window (its loads issued before the window's), or its own kernel.
 //
-// Bitwise reproducible run to run, in eager mode and inside a captured graph alike.  HBM / L2
-// bound: 8 B of flow and 12 B of counters per (pixel, corner) through steps 1-3, the gather
-// reads each destination's source rows (mostly L2 hits for smooth flows) and writes d(features)
-// once; O(n h w) for any flow field.
+// Bitwise reproducible run to run, in eager mode and inside a captured graph alike (the mode,
+// the windows and the path are functions of the flow and dout).
 #include "common.h"
 
 namespace oflow {
@@ -61,148 +69,80 @@ __device__ __forceinline__ float det_row16_sum(float v) {   // over the 16 lanes
   return v;
 }
 
-// 1. count: one thread per source pixel, one integer add per (pixel, corner) on its
-// destination's counter (integer adds commute: the counts are exact whatever the order).
-__global__ __launch_bounds__(256) void own_count(const float* __restrict__ flow, int n, int h,
-                                                 int w, int absolute, int* __restrict__ cnt) {
-  const int64_t npix = (int64_t)n * h * w;
-  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (p >= npix) return;
-  const int j = (int)(p % w);
-  const int64_t t2 = p / w;
-  const int i = (int)(t2 % h);
-  const int64_t img = (t2 / h) * h * w;
-  const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
-  const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) atomicAdd(cnt + img + (int64_t)t.y[k] * w + t.x[k], 1);
+
+// Workspace header (ints, zeroed per call): [0] max |dout| (float bits, fixed-point path),
+// [1] R, [2] V (own_radius), and DET_SLOTS counters of the hits mode B found, 256 B apart (spread atomics).
+constexpr int DET_SLOTS = 32;
+constexpr int DET_HDR_INTS = 64 * (1 + DET_SLOTS);
+__device__ __forceinline__ int* det_slot(int* hdr, int s) { return hdr + 64 * (1 + s); }
+
+// The fixed-point path runs unless a window served: mode A (R <= rmax), or mode B with all
+// 4 n h w entries found.  rmax < 0: no window was launched.
+__device__ __forceinline__ bool own_fallback(const int* __restrict__ hdr, int rmax,
+                                             int64_t npix) {
+  if (rmax < 0) return true;
+  if (hdr[1] <= rmax) return false;
+  int64_t s = 0;
+#pragma unroll 8
+  for (int k = 0; k < DET_SLOTS; ++k) s += hdr[64 * (1 + k)];
+  return s != 4 * npix;
 }
 
-// 2. exclusive scan of the counts (three launches: per-block sums, the block sums in one
-// workgroup, per-block scan + block offset).  OWN_SB elements per block.
-constexpr int OWN_SB = 2048;
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
+// 0. R = floor(max |flow| + 0.01) + 2 over the batch (INT_MAX for a component that is not
+// finite or above DET_HUGE); the margin covers the rounding of (float)j + f near an integer
+// for coordinates below 2^16 (the host checks h, w).  And the roughness V = the largest
+// change of a flow component between horizontal / vertical neighbours (in 1/1024 px,
+// hdr[2]): mode B is tried only on fields smooth enough for its source estimate.
+constexpr float DET_HUGE = 1048576.f;
+__global__ __launch_bounds__(256) void own_radius(const float* __restrict__ flow, int64_t npix,
+                                                  int h, int w, int* __restrict__ hdr) {
+  __shared__ int red[2][4];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int r = 0, v = 0;
+  for (int64_t p = t0; p < npix; p += stride) {
+    const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
+    const float ax = fabsf(f.x), ay = fabsf(f.y);
+    const bool ok = ax <= DET_HUGE && ay <= DET_HUGE;       // false for NaN
+    r = max(r, ok ? (int)(fmaxf(ax, ay) + 0.01f) + 2 : INT_MAX);
+    const int j = (int)(p % w), i = (int)((p / w) % h);
+    float dv = 0.f;
+    if (j + 1 < w) {
+      const float2 g = *reinterpret_cast<const float2*>(flow + 2 * (p + 1));
+      dv = fmaxf(dv, fmaxf(fabsf(g.x - f.x), fabsf(g.y - f.y)));
+    }
+    if (i + 1 < h) {
+      const float2 g = *reinterpret_cast<const float2*>(flow + 2 * (p + w));
+      dv = fmaxf(dv, fmaxf(fabsf(g.x - f.x), fabsf(g.y - f.y)));
+    }
+    v = max(v, dv <= 1.0e6f ? (int)(dv * 1024.f) : INT_MAX);  // (NaN: INT_MAX)
   }
-  return v;
-}
-
-__global__ __launch_bounds__(256) void own_block_sums(const int* __restrict__ cnt, int64_t total,
-                                                      int* __restrict__ bsum) {
-  __shared__ int red[4];
-  const int64_t base = blockIdx.x * (int64_t)OWN_SB;
-  int s = 0;
-  for (int k = threadIdx.x; k < OWN_SB; k += 256) {
-    const int64_t e = base + k;
-    s += e < total ? cnt[e] : 0;
-  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  for (int o = 32; o > 0; o >>= 1) {
+    r = max(r, __shfl_xor(r, o, 64));
+    v = max(v, __shfl_xor(v, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = r, red[1][threadIdx.x >> 6] = v;
   __syncthreads();
-  if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-
-// one workgroup: bsum -> exclusive offsets, in place (nb block sums, any count)
-__global__ __launch_bounds__(1024) void own_scan_sums(int* __restrict__ bsum, int nb) {
-  __shared__ int wsum[16];
-  __shared__ int carry;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) carry = 0;
-  __syncthreads();
-  for (int b0 = 0; b0 < nb; b0 += 1024) {
-    const int v = b0 + tid < nb ? bsum[b0 + tid] : 0;
-    const int inc = wave_incl_scan(v, lane);
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    int before = carry;
-    for (int k = 0; k < wv; ++k) before += wsum[k];
-    if (b0 + tid < nb) bsum[b0 + tid] = before + inc - v;
-    __syncthreads();
-    if (tid == 1023) carry = before + inc;
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicMax(hdr + 1, max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3])));
+    atomicMax(hdr + 2, max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3])));
   }
 }
 
-__global__ __launch_bounds__(256) void own_block_scan(const int* __restrict__ cnt, int64_t total,
-                                                      const int* __restrict__ boff,
-                                                      int* __restrict__ off) {
-  __shared__ int wsum[4];
-  __shared__ int carry;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t base = blockIdx.x * (int64_t)OWN_SB;
-  if (tid == 0) carry = boff[blockIdx.x];
-  __syncthreads();
-  for (int k0 = 0; k0 < OWN_SB; k0 += 256) {
-    const int64_t e = base + k0 + tid;
-    const int v = e < total ? cnt[e] : 0;
-    const int inc = wave_incl_scan(v, lane);
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    int before = carry;
-    for (int k = 0; k < wv; ++k) before += wsum[k];
-    if (e < total) off[e] = before + inc - v;
-    __syncthreads();
-    if (tid == 255) carry = before + inc;
-    __syncthreads();
-  }
-}
-
-// 3. fill: each (pixel, corner) entry goes to a slot of its destination's segment.  The slot
-// order inside a segment depends on the order of the integer adds; the gather below orders
-// every segment itself, so nothing downstream depends on it.  Entry code = 4 p + k (p the
-// pixel within its image, k the corner: bit 0 -> row y1, bit 1 -> column x1).
-__global__ __launch_bounds__(256) void own_fill(const float* __restrict__ flow, int n, int h,
-                                                int w, int absolute, const int* __restrict__ off,
-                                                int* __restrict__ cursor,
-                                                uint32_t* __restrict__ list) {
-  const int64_t npix = (int64_t)n * h * w;
-  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (p >= npix) return;
-  const int j = (int)(p % w);
-  const int64_t t2 = p / w;
-  const int i = (int)(t2 % h);
-  const int64_t img = (t2 / h) * h * w;
-  const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
-  const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t d = img + (int64_t)t.y[k] * w + t.x[k];
-    list[off[d] + atomicAdd(cursor + d, 1)] = (uint32_t)(4 * (p - img) + k);
-  }
-}
-
-// the weight of entry `code` of image `img` (the forward's bilinear weights, P2)
-__device__ __forceinline__ float own_weight(const float* __restrict__ flow, int64_t img, int h,
-                                            int w, int absolute, uint32_t code) {
-  const int64_t pi = code >> 2;
-  const int k = code & 3;
-  const float2 f = *reinterpret_cast<const float2*>(flow + 2 * (img + pi));
-  const DetCorners t = det_corners((int)(pi / w), (int)(pi % w), f.x, f.y, h, w, absolute != 0);
-  return ((k & 2) ? 1.f - t.a : t.a) * ((k & 1) ? 1.f - t.b : t.b);
-}
-
-// 4. gather, destinations with at most 16 entries: 16 lanes per destination (channel quads),
-// four destinations per wave.  Lane j < n holds entry j; its rank (the number of smaller codes
-// in the segment) orders the sum: sum over codes ascending of w * dout[p] -- the same order
-// whatever slots the fill gave them.  A segment of more than 16 entries is listed for step 5.
-// Every destination row is written (0 when no entry lands on it): no zero-fill pass.
-constexpr int OWN_SMALL = 16;
-// VEC: rows of float4 quads (c % 4 == 0, 16-byte aligned); else one channel per lane.
+// VEC: rows of float4 quads (c % 4 == 0, 16-byte aligned); else one channel per lane.  Every
+// add is an explicit fma, so no path's sums depend on how the compiler packs them.
 template <bool VEC>
 __device__ __forceinline__ void own_acc(float4& acc, float wr, const float* __restrict__ row,
                                         int k) {
   if (VEC) {
     const float4 g = *reinterpret_cast<const float4*>(row + 4 * k);
-    acc.x += wr * g.x;
-    acc.y += wr * g.y;
-    acc.z += wr * g.z;
-    acc.w += wr * g.w;
+    acc.x = fmaf(wr, g.x, acc.x);
+    acc.y = fmaf(wr, g.y, acc.y);
+    acc.z = fmaf(wr, g.z, acc.z);
+    acc.w = fmaf(wr, g.w, acc.w);
   } else {
-    acc.x += wr * row[k];
+    acc.x = fmaf(wr, row[k], acc.x);
   }
 }
 
@@ -212,173 +152,135 @@ __device__ __forceinline__ void own_store(float* __restrict__ row, int k, const 
   else row[k] = v.x;
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(256) void own_gather(const float* __restrict__ dout,
-                                                  const float* __restrict__ flow, int n, int h,
-                                                  int w, int c, int absolute,
-                                                  const int* __restrict__ cnt,
-                                                  const int* __restrict__ off,
-                                                  const uint32_t* __restrict__ list,
-                                                  float* __restrict__ dinp,
-                                                  int* __restrict__ big_n, int* __restrict__ big) {
+// The fixed-point fallback (absolute points, key 28 = 0, or a window that did not serve):
+// every (pixel, corner) contribution w_k * dout[p] (fp32, as the windows form it) is scaled by
+// 2^S and rounded to an int64, and the int64s are added -- integer adds commute, so the sums
+// are exact and the same in any order: bitwise reproducible with atomics.  S = 61 - E - L for
+// max |dout| <= 2^E and 4 n h w <= 2^L keeps every sum below 2^61 in magnitude; a
+// contribution is exact to 2^-S = max|dout| 2^(L - 61) (2^-40 of it at 192 x 256 x 8).
+//   fix_prep   : zeroes the accumulator, reduces max |dout| (float bits, atomicMax).
+//   fix_scatter: one 8 x 8 source tile and 64 channels per workgroup, one wave per pixel
+//                (lanes = channels); corners go through a 128-slot direct-mapped LDS cache of
+//                destination rows (int64 LDS adds), a slot collision straight to global int64
+//                atomics, and the cache leaves as one 512-B atomic wave-instruction per
+//                destination: a tile's samples piled onto the border add once per destination.
+//   fix_convert: dinp = acc * 2^-S (NaN everywhere if dout holds a non-finite value).
+constexpr int FX_T = 8, FX_SLOTS = 128, FX_WAVES = 8;
+
+__global__ __launch_bounds__(256) void fix_prep(const float* __restrict__ dout, int64_t nel,
+                                                int4* __restrict__ acc4, int64_t nacc4,
+                                                int* __restrict__ hdr, int rmax, int64_t npix) {
+  if (!own_fallback(hdr, rmax, npix)) return;
+  __shared__ unsigned red[4];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  unsigned m = 0;
+  for (int64_t e = t0; e < nel; e += stride)
+    m = max(m, __float_as_uint(dout[e]) & 0x7fffffffu);   // NaN > inf > finite as bits
+  for (int64_t k = t0; k < nacc4; k += stride) acc4[k] = make_int4(0, 0, 0, 0);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned*>(hdr), max(max(red[0], red[1]), max(red[2], red[3])));
+}
+
+// S from max |dout| (0 when it is not finite: fix_convert writes NaN then)
+__device__ __forceinline__ int fix_shift(const int* __restrict__ hdr, int lg4n) {
+  const float m = __uint_as_float((unsigned)hdr[0]);
+  if (!(m <= 3.0e38f)) return 0;
+  int e = 0;
+  frexpf(m, &e);                                       // m < 2^e
+  return 61 - e - lg4n;
+}
+
+__global__ __launch_bounds__(64 * FX_WAVES) void fix_scatter(const float* __restrict__ dout,
+                                                             const float* __restrict__ flow,
+                                                             int n, int h, int w, int c,
+                                                             int absolute,
+                                                             const int* __restrict__ hdr,
+                                                             int rmax, int lg4n,
+                                                             unsigned long long* __restrict__ acc) {
   const int64_t npix = (int64_t)n * h * w;
-  const int lane = threadIdx.x & 63, g16 = lane >> 4, q = lane & 15;
-  const int64_t d = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4;
-  const bool live = d < npix;
-  const int64_t dd = live ? d : npix - 1;
-  const int ne = live ? cnt[dd] : 0;
-  const int64_t img = dd / ((int64_t)h * w) * h * w;
-  const bool small = ne <= OWN_SMALL;
-  if (live && !small && q == 0) big[atomicAdd(big_n, 1)] = (int)dd;
-  const uint32_t code = small && q < ne ? list[off[dd] + q] : 0xffffffffu;
-  // rank among the segment's codes (codes are distinct)
-  int rank = 0;
-  const int src0 = lane & 48;
+  if (!own_fallback(hdr, rmax, npix)) return;
+  __shared__ unsigned long long data[FX_SLOTS * 64];
+  __shared__ int tag[FX_SLOTS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_i = (h + FX_T - 1) / FX_T, tiles_j = (w + FX_T - 1) / FX_T;
+  const int passes = (c + 63) / 64;
+  const int cc = (blockIdx.x % passes) * 64;
+  const int tile = blockIdx.x / passes;
+  const int b = tile / (tiles_i * tiles_j);
+  const int rem = tile - b * tiles_i * tiles_j;
+  const int i0 = (rem / tiles_j) * FX_T, j0 = (rem % tiles_j) * FX_T;
+  const int64_t img = (int64_t)b * h * w;
+  const int S = fix_shift(hdr, lg4n);
+  const int e = cc + lane;
+  const bool eok = e < c;
+  for (int k = tid; k < FX_SLOTS * 64; k += 64 * FX_WAVES) data[k] = 0ull;
+  if (tid < FX_SLOTS) tag[tid] = -1;
+  __syncthreads();
+  for (int pr = wave; pr < FX_T * FX_T; pr += FX_WAVES) {
+    const int i = i0 + pr / FX_T, j = j0 + pr % FX_T;
+    if (i >= h || j >= w) continue;                    // wave-uniform
+    const int64_t p = img + (int64_t)i * w + j;
+    const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
+    const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
+    const float g = eok ? dout[p * c + e] : 0.f;
 #pragma unroll
-  for (int k = 0; k < OWN_SMALL; ++k) {
-    const uint32_t o = (uint32_t)__shfl((int)code, src0 + k, 64);
-    rank += o < code ? 1 : 0;
-  }
-  const float wt = small && q < ne ? own_weight(flow, img, h, w, absolute, code) : 0.f;
-  // max entries over the four destinations of the wave: the loop bound
-  int nmax = small ? ne : 0;
-#pragma unroll
-  for (int o = 16; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
-  const int nq = VEC ? c >> 2 : c;                     // quads, or channels
-  for (int cb = 0; cb < nq; cb += 16) {                // every lane runs every iteration
-    const int cq = cb + q;
-    const bool cok = cq < nq;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r = 0; r < nmax; ++r) {
-      // the lane of this group holding rank r (none when this group's segment is shorter)
-      const uint64_t bal = __ballot(small && q < ne && rank == r);
-      const int sl = (int)((bal >> (16 * g16)) & 0xffffull);
-      const bool has = sl != 0;
-      const int src = src0 + (has ? __builtin_ctz(sl) : 0);
-      const uint32_t cd = (uint32_t)__shfl((int)code, src, 64);
-      const float wr = __shfl(wt, src, 64);
-      if (has && cok) own_acc<VEC>(acc, wr, dout + (img + (cd >> 2)) * c, cq);
+    for (int k = 0; k < 4; ++k) {
+      const float wk = ((k & 2) ? 1.f - t.a : t.a) * ((k & 1) ? 1.f - t.b : t.b);
+      const unsigned long long v = (unsigned long long)llrint(ldexp((double)(wk * g), S));
+      const int d = t.y[k] * w + t.x[k];
+      const int sl = ((t.y[k] & 7) << 4) | (t.x[k] & 15);
+      int tg = 0;
+      if (lane == 0) tg = atomicCAS(&tag[sl], -1, d);
+      tg = __builtin_amdgcn_readfirstlane(tg);
+      if (tg == -1 || tg == d)
+        atomicAdd(&data[sl * 64 + lane], v);
+      else if (eok)
+        atomicAdd(acc + (img + d) * c + e, v);
     }
-    if (live && small && cok) own_store<VEC>(dinp + dd * c, cq, acc);
+  }
+  __syncthreads();
+  for (int sl = wave; sl < FX_SLOTS; sl += FX_WAVES) {
+    const int d = tag[sl];
+    if (d >= 0 && eok) atomicAdd(acc + (img + d) * c + e, data[sl * 64 + lane]);
   }
 }
 
-// 5. gather, destinations with more than 16 entries (a clipped flow field piles samples onto
-// the border): one workgroup per listed destination.  The segment's codes are marked in an
-// LDS bitmap over a window of the image's code range (all of it when 4 h w <= OWN_WBITS), the
-// four waves each sum a contiguous quarter of the window in code order, and the quarters are
-// added in order: a fixed order for any n.
-constexpr int OWN_WBITS = 1 << 20;    // 128 KB of bitmap
-template <bool VEC>
-__global__ __launch_bounds__(256) void own_gather_big(const float* __restrict__ dout,
-                                                      const float* __restrict__ flow, int h,
-                                                      int w, int c, int absolute,
-                                                      const int* __restrict__ cnt,
-                                                      const int* __restrict__ off,
-                                                      const uint32_t* __restrict__ list,
-                                                      const int* __restrict__ big_n,
-                                                      const int* __restrict__ big,
-                                                      float* __restrict__ dinp) {
-  extern __shared__ uint32_t bm[];
-  __shared__ float4 part[4][64];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t codes = 4 * (int64_t)h * w;
-  const int64_t wbits = codes < OWN_WBITS ? (codes + 31) / 32 * 32 : OWN_WBITS;
-  const int nwords = (int)(wbits / 32);
-  const int nb = *big_n;
-  for (int bi = blockIdx.x; bi < nb; bi += gridDim.x) {
-    const int64_t d = big[bi];
-    const int64_t img = d / ((int64_t)h * w) * h * w;
-    const int ne = cnt[d];
-    const int64_t o0 = off[d];
-    const int nq = VEC ? c >> 2 : c;
-    for (int qb = 0; qb < nq; qb += 64) {                // 64 channel quads (channels) a sweep
-      const int cq = qb + lane;
-      const bool cok = cq < nq;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int64_t w0 = 0; w0 < codes; w0 += wbits) {   // code windows
-        for (int k = tid; k < nwords; k += 256) bm[k] = 0u;
-        __syncthreads();
-        for (int e = tid; e < ne; e += 256) {
-          const int64_t cd = (int64_t)list[o0 + e] - w0;
-          if (cd >= 0 && cd < wbits) atomicOr(&bm[cd >> 5], 1u << (cd & 31));
-        }
-        __syncthreads();
-        // wave wv: words [wv * nwords / 4, (wv + 1) * nwords / 4), in order; 64 words per
-        // step, the nonzero ones visited in lane order
-        const int k0 = (int)((int64_t)wv * nwords / 4), k1 = (int)((int64_t)(wv + 1) * nwords / 4);
-        for (int kb = k0; kb < k1; kb += 64) {
-          const uint32_t myw = kb + lane < k1 ? bm[kb + lane] : 0u;
-          uint64_t nzm = __ballot(myw != 0u);
-          while (nzm) {
-            const int l = __builtin_ctzll(nzm);
-            nzm &= nzm - 1;
-            uint32_t word = (uint32_t)__shfl((int)myw, l, 64);
-            while (word) {
-              const int bit = __builtin_ctz(word);
-              word &= word - 1;
-              const uint32_t cd = (uint32_t)(w0 + 32 * (int64_t)(kb + l) + bit);
-              const float wr = own_weight(flow, img, h, w, absolute, cd);
-              if (cok) own_acc<VEC>(acc, wr, dout + (img + (cd >> 2)) * c, cq);
-            }
-          }
-        }
-        __syncthreads();                                // the bitmap is reused
-      }
-      part[wv][lane] = acc;
-      __syncthreads();
-      if (wv == 0 && cok) {
-        float4 s = part[0][lane];
-#pragma unroll
-        for (int u = 1; u < 4; ++u) {
-          s.x += part[u][lane].x;
-          s.y += part[u][lane].y;
-          s.z += part[u][lane].z;
-          s.w += part[u][lane].w;
-        }
-        own_store<VEC>(dinp + d * c, cq, s);
-      }
-      __syncthreads();
-    }
-  }
+__global__ __launch_bounds__(256) void fix_convert(const long long* __restrict__ acc,
+                                                   int64_t nel, const int* __restrict__ hdr,
+                                                   int rmax, int64_t npix, int lg4n,
+                                                   float* __restrict__ dinp) {
+  if (!own_fallback(hdr, rmax, npix)) return;
+  const float m = __uint_as_float((unsigned)hdr[0]);
+  const bool fin = m <= 3.0e38f;
+  const int S = fix_shift(hdr, lg4n);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nel; k += stride)
+    dinp[k] = fin ? (float)ldexp((double)acc[k], -S) : __builtin_nanf("");
 }
 
-// 5. d(flow) (c % 4 == 0): 16 lanes per source pixel, lane q sums channel quads q, q + 16, ...
-// in order, then a fixed DPP reduction over the row -- the default kernel's per-pixel order
-// for c == 64.
-__global__ __launch_bounds__(256) void det_dflow_vec(const float* __restrict__ dout,
-                                                     const float* __restrict__ inp, int n, int h,
-                                                     int w, int c, const float* __restrict__ flow,
-                                                     int absolute, float* __restrict__ dflow,
-                                                     const float* __restrict__ dfa, int ldfa) {
-  const int64_t npix = (int64_t)n * h * w;
-  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t p = gid >> 4;
-  const int q = (int)(gid & 15);
-  const bool ok = p < npix;
-  const int64_t pp = ok ? p : npix - 1;
-  const int j = (int)(pp % w);
-  const int64_t t2 = pp / w;
-  const int i = (int)(t2 % h);
-  const int64_t img = (t2 / h) * h * w;
-  const float2 f = *reinterpret_cast<const float2*>(flow + 2 * pp);
-  const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
-  const float a = t.a, bq = t.b;
-  int64_t off[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) off[k] = (img + (int64_t)t.y[k] * w + t.x[k]) * c;
-  auto dot = [](float4 u, float4 v) { return u.x * v.x + u.y * v.y + u.z * v.z + u.w * v.w; };
-  auto sub = [](float4 u, float4 v) { return make_float4(u.x - v.x, u.y - v.y, u.z - v.z, u.w - v.w); };
-  float gx = 0.f, gy = 0.f;
-  for (int cq = 4 * q; cq < c; cq += 64) {
-    const float4 g = *reinterpret_cast<const float4*>(dout + pp * c + cq);
-    const float4 P0 = *reinterpret_cast<const float4*>(inp + off[0] + cq);
-    const float4 P1 = *reinterpret_cast<const float4*>(inp + off[1] + cq);
-    const float4 P2 = *reinterpret_cast<const float4*>(inp + off[2] + cq);
-    const float4 P3 = *reinterpret_cast<const float4*>(inp + off[3] + cq);
-    gx += -(bq * dot(g, sub(P0, P2)) + (1.f - bq) * dot(g, sub(P1, P3)));
-    gy += -(a * dot(g, sub(P0, P1)) + (1.f - a) * dot(g, sub(P2, P3)));
-  }
+// 6. d(flow) (c % 4 == 0): 16 lanes per source pixel, lane q sums channel quads q, q + 16, ...
+// in order, then a fixed DPP reduction over the row.  dflow_quad: one quad's terms, explicit
+// fmas (the same arithmetic wherever it is inlined).
+__device__ __forceinline__ float det_dot_diff(float4 g, float4 u, float4 v) {
+  float s = g.x * (u.x - v.x);
+  s = fmaf(g.y, u.y - v.y, s);
+  s = fmaf(g.z, u.z - v.z, s);
+  return fmaf(g.w, u.w - v.w, s);
+}
+__device__ __forceinline__ void dflow_quad(float& gx, float& gy, float a, float bq, float4 g,
+                                           float4 P0, float4 P1, float4 P2, float4 P3) {
+  gx -= fmaf(bq, det_dot_diff(g, P0, P2), (1.f - bq) * det_dot_diff(g, P1, P3));
+  gy -= fmaf(a, det_dot_diff(g, P0, P1), (1.f - a) * det_dot_diff(g, P2, P3));
+}
+__device__ __forceinline__ void dflow_store(float gx, float gy, int64_t p, bool ok, int q,
+                                            float* __restrict__ dflow,
+                                            const float* __restrict__ dfa, int ldfa) {
   gx = det_row16_sum(gx);
   gy = det_row16_sum(gy);
   if (q == 0 && ok) {
@@ -387,6 +289,386 @@ __global__ __launch_bounds__(256) void det_dflow_vec(const float* __restrict__ d
       gy = dfa[p * ldfa + 1] + gy;
     }
     *reinterpret_cast<float2*>(dflow + 2 * p) = make_float2(gx, gy);
+  }
+}
+
+// the four corner rows of pixel p's sample (offsets in floats) and its weights
+struct DetTaps {
+  int64_t off[4];
+  float a, bq;
+};
+__device__ __forceinline__ DetTaps det_taps(const float* __restrict__ flow, int64_t pp, int h,
+                                            int w, int c, int absolute) {
+  const int j = (int)(pp % w);
+  const int64_t t2 = pp / w;
+  const int i = (int)(t2 % h);
+  const int64_t img = (t2 / h) * h * w;
+  const float2 f = *reinterpret_cast<const float2*>(flow + 2 * pp);
+  const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
+  DetTaps T;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) T.off[k] = (img + (int64_t)t.y[k] * w + t.x[k]) * c;
+  T.a = t.a;
+  T.bq = t.b;
+  return T;
+}
+
+// Every lane of the wave calls it (the row reduction reads all 16 lanes).
+__device__ __forceinline__ void det_dflow_quads(const float* __restrict__ dout,
+                                                const float* __restrict__ inp, int64_t npix,
+                                                int h, int w, int c,
+                                                const float* __restrict__ flow, int absolute,
+                                                float* __restrict__ dflow,
+                                                const float* __restrict__ dfa, int ldfa,
+                                                int64_t p, int q) {
+  const bool ok = p < npix;
+  const int64_t pp = ok ? p : npix - 1;
+  const DetTaps T = det_taps(flow, pp, h, w, c, absolute);
+  float gx = 0.f, gy = 0.f;
+  for (int cq = 4 * q; cq < c; cq += 64) {
+    const float4 g = *reinterpret_cast<const float4*>(dout + pp * c + cq);
+    const float4 P0 = *reinterpret_cast<const float4*>(inp + T.off[0] + cq);
+    const float4 P1 = *reinterpret_cast<const float4*>(inp + T.off[1] + cq);
+    const float4 P2 = *reinterpret_cast<const float4*>(inp + T.off[2] + cq);
+    const float4 P3 = *reinterpret_cast<const float4*>(inp + T.off[3] + cq);
+    dflow_quad(gx, gy, T.a, T.bq, g, P0, P1, P2, P3);
+  }
+  dflow_store(gx, gy, p, ok, q, dflow, dfa, ldfa);
+}
+
+__global__ __launch_bounds__(256) void det_dflow_vec(const float* __restrict__ dout,
+                                                     const float* __restrict__ inp, int n, int h,
+                                                     int w, int c, const float* __restrict__ flow,
+                                                     int absolute, float* __restrict__ dflow,
+                                                     const float* __restrict__ dfa, int ldfa) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  det_dflow_quads(dout, inp, (int64_t)n * h * w, h, w, c, flow, absolute, dflow, dfa, ldfa,
+                  gid >> 4, (int)(gid & 15));
+}
+
+// The window gather.  win_accumulate sums a contiguous range of a destination's candidates,
+// flattened i-major (ascending source index), over the group's 16 lanes: 4 x 16 candidates per
+// batch with their flows loaded together; a candidate's corners landing on (r, x) are its hits,
+// appended in (candidate, corner) order -- ascending code 4 p + k -- to
+// the group's LDS list (row offset, weight) by a 16-lane prefix sum; the list is summed (flush)
+// four rows in flight at a time, in list order, whenever it could overflow and at the end.
+// NCB channel blocks of 16 quads (channels when !VEC) per lane; `found` += the hits.  Every
+// lane of the wave calls it (wave-wide shuffles); a group with an empty range idles.
+constexpr int WIN_CAP = 128;    // list entries per group; flushed above WIN_CAP - 64
+constexpr int WIN_PILE = 16;    // mode A: |w - h| above this, the pile row / column
+constexpr int WIN_RB = 3;       // mode B window radius around the estimated source
+constexpr int WIN_VMAX = 512;   // mode B only for V <= 0.5 px (or rmax == 1: always, tests)
+
+struct WinDest {
+  int r, x;                     // the destination
+  int ilo, jlo, nj;             // its candidates: i = ilo + k / nj, j = jlo + k % nj
+  int k0, k1;                   // the range this group sums
+};
+
+template <bool VEC, int NCB>
+__device__ __forceinline__ void win_accumulate(float4 (&acc)[NCB], int& found, const WinDest& D,
+                                               const float* __restrict__ dimg,
+                                               const float* __restrict__ fimg, int h, int w,
+                                               int c, int cb0, int* __restrict__ l_off,
+                                               float* __restrict__ l_w, int q, int src0) {
+  const int nq = VEC ? c >> 2 : c;
+#pragma unroll
+  for (int b = 0; b < NCB; ++b) acc[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int span = max(D.k1 - D.k0, 0);
+  int pmax = (span + 15) >> 4;
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) pmax = max(pmax, __shfl_xor(pmax, o, 64));
+  int cnt = 0;                                         // the group's list length
+  auto flush = [&]() {
+    int em = cnt;
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) em = max(em, __shfl_xor(em, o, 64));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    for (int e0 = 0; e0 < em; e0 += 4) {
+      float4 g[4][NCB];
+      float wr[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = e0 + u < cnt;
+        const int64_t o = ok ? (int64_t)l_off[e0 + u] * c : 0;
+        wr[u] = ok ? l_w[e0 + u] : 0.f;
+#pragma unroll
+        for (int b = 0; b < NCB; ++b) {
+          const int cq = cb0 + 16 * b + q;
+          g[u][b] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok && cq < nq) {
+            if (VEC) g[u][b] = *reinterpret_cast<const float4*>(dimg + o + 4 * cq);
+            else g[u][b].x = dimg[o + cq];
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (e0 + u < cnt) {
+#pragma unroll
+          for (int b = 0; b < NCB; ++b) {
+            acc[b].x = fmaf(wr[u], g[u][b].x, acc[b].x);   // explicit: a packed
+            if (VEC) {                                      // mul + add would round twice
+              acc[b].y = fmaf(wr[u], g[u][b].y, acc[b].y);
+              acc[b].z = fmaf(wr[u], g[u][b].z, acc[b].z);
+              acc[b].w = fmaf(wr[u], g[u][b].w, acc[b].w);
+            }
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    cnt = 0;
+  };
+  for (int t0 = 0; t0 < pmax; t0 += 4) {
+    float2 f[4];
+    int ci[4], cj[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = (t0 + u) * 16 + q;
+      const bool in = k < span;
+      const int kk = D.k0 + k;
+      const int di = in ? kk / D.nj : 0;
+      ci[u] = in ? D.ilo + di : -1;
+      cj[u] = D.jlo + (kk - di * D.nj);
+      f[u] = make_float2(0.f, 0.f);
+      if (in) f[u] = *reinterpret_cast<const float2*>(fimg + 2 * ((int64_t)ci[u] * w + cj[u]));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (t0 + u >= pmax) break;
+      int cm = cnt;
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) cm = max(cm, __shfl_xor(cm, o, 64));
+      if (cm > WIN_CAP - 64) flush();
+      uint32_t m = 0;
+      float ca = 0.f, cbw = 0.f;
+      if (ci[u] >= 0) {
+        const DetCorners tc = det_corners(ci[u], cj[u], f[u].x, f[u].y, h, w, false);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m |= (tc.y[k] == D.r && tc.x[k] == D.x) ? 1u << k : 0u;
+        ca = tc.a;
+        cbw = tc.b;
+      }
+      const int pc = __builtin_popcount(m);
+      int incl = pc;                                   // inclusive prefix over the 16 lanes
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const int v = __shfl_up(incl, o, 16);
+        if (q >= o) incl += v;
+      }
+      int pos = cnt + incl - pc;
+      const int poff = ci[u] * w + cj[u];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (m & (1u << k)) {
+          l_off[pos] = poff;
+          l_w[pos] = ((k & 2) ? 1.f - ca : ca) * ((k & 1) ? 1.f - cbw : cbw);
+          ++pos;
+        }
+      }
+      const int tot = __shfl(incl, src0 + 15, 64);
+      cnt += tot;
+      found += tot;
+    }
+  }
+  flush();
+}
+
+// Mode A: the candidates of destination (r, x) for radius R (sources within R of the
+// transposed position; the last row / column to the far edge).
+__device__ __forceinline__ WinDest win_dest_a(int r, int x, int h, int w, int R) {
+  WinDest D;
+  D.r = r, D.x = x;
+  D.ilo = max(0, x - R);
+  const int ihi = x == w - 1 ? h - 1 : min(h - 1, x + R);
+  D.jlo = max(0, r - R);
+  const int jhi = r == h - 1 ? w - 1 : min(w - 1, r + R);
+  D.nj = jhi - D.jlo + 1;
+  D.k0 = 0;
+  D.k1 = ihi >= D.ilo && D.nj > 0 ? (ihi - D.ilo + 1) * D.nj : 0;
+  return D;
+}
+
+// Mode B: a window of radius WIN_RB around the source estimated by three fixed-point steps
+// i <- x - f0(i, j), j <- r - f1(i, j) from the transposed position; along a border the whole
+// range a clipped sample can come from (F = R bounds |flow| + 2).
+__device__ __forceinline__ WinDest win_dest_b(const float* __restrict__ fimg, int r, int x,
+                                              int h, int w, int R) {
+  const int F = min(R, 1 << 20);
+  int i = min(x, h - 1), j = min(r, w - 1);
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {
+    const float2 f = *reinterpret_cast<const float2*>(fimg + 2 * ((int64_t)i * w + j));
+    i = (int)rintf(fminf(fmaxf((float)x - f.x, 0.f), (float)(h - 1)));   // NaN -> 0
+    j = (int)rintf(fminf(fmaxf((float)r - f.y, 0.f), (float)(w - 1)));
+  }
+  WinDest D;
+  D.r = r, D.x = x;
+  int ilo, ihi, jlo, jhi;
+  if (x == 0) ilo = 0, ihi = min(h - 1, F);
+  else if (x == w - 1) ilo = max(0, w - 1 - F), ihi = h - 1;
+  else ilo = max(0, i - WIN_RB), ihi = min(h - 1, i + WIN_RB);
+  if (r == 0) jlo = 0, jhi = min(w - 1, F);
+  else if (r == h - 1) jlo = max(0, h - 1 - F), jhi = w - 1;
+  else jlo = max(0, j - WIN_RB), jhi = min(w - 1, j + WIN_RB);
+  D.ilo = ilo;
+  D.jlo = jlo;
+  D.nj = jhi - jlo + 1;
+  D.k0 = 0;
+  D.k1 = ihi >= ilo && D.nj > 0 ? (ihi - ilo + 1) * D.nj : 0;
+  return D;
+}
+
+// The pile workgroups' destinations per image: row 0 and row h - 1 (w each), then column 0
+// and column w - 1 without the corners (h - 2 each); none for an image under 2 x 2.
+__device__ __forceinline__ void win_pile_dest(int e, int h, int w, int& r, int& x) {
+  if (e < w) r = 0, x = e;
+  else if (e < 2 * w) r = h - 1, x = e - w;
+  else if (e < 2 * w + h - 2) r = e - 2 * w + 1, x = 0;
+  else r = e - (2 * w + h - 2) + 1, x = w - 1;
+}
+
+// Is (r, x) a pile destination (a workgroup of its own)?  Mode A: the last row when
+// w - h > WIN_PILE, the last column when h - w > WIN_PILE.  Mode B: every border pixel.
+__device__ __forceinline__ bool win_piled(bool mode_a, int r, int x, int h, int w) {
+  if (h < 2 || w < 2) return false;
+  if (mode_a)
+    return (w - h > WIN_PILE && r == h - 1) || (h - w > WIN_PILE && x == w - 1);
+  return r == 0 || r == h - 1 || x == 0 || x == w - 1;
+}
+
+// The window kernel (launched when rmax >= 0).  Blocks [0, n * npb): one workgroup per pile
+// destination (win_pile_dest; those that are not piles in this mode return), its 16 groups
+// summing contiguous sixteenths of the candidate range, the partials added in group order --
+// launched first, as they are the longest.  The other blocks: 16 lanes per destination, four
+// per wave, piles skipped; with VEC (c <= 64 NCB) the group also forms d(flow) of pixel d as
+// a source, its loads issued before the window's (DFQ quads per lane).  A window that does
+// not serve (mode B, a count short of 4 n h w) is overwritten by the fixed-point path; with
+// neither mode (R > rmax and V > WIN_VMAX) the kernel forms d(flow) only.
+template <bool VEC, int NCB>
+__global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout,
+                                                  const float* __restrict__ inp,
+                                                  const float* __restrict__ flow, int n, int h,
+                                                  int w, int c, int* __restrict__ hdr,
+                                                  int rmax, float* __restrict__ dinp,
+                                                  float* __restrict__ dflow,
+                                                  const float* __restrict__ dfa, int ldfa) {
+  __shared__ int l_off[16][WIN_CAP];
+  __shared__ float l_w[16][WIN_CAP];
+  __shared__ float4 part[16][16 * NCB];
+  __shared__ int fsum[16];
+  const int64_t npix = (int64_t)n * h * w;
+  const int64_t hw = (int64_t)h * w;
+  const int lane = threadIdx.x & 63, q = lane & 15, src0 = lane & 48, grp = threadIdx.x >> 4;
+  const int nq = VEC ? c >> 2 : c;
+  const int R = hdr[1];
+  const bool mode_a = R <= rmax;                       // uniform over the grid
+  const bool mode_b = !mode_a && (hdr[2] <= WIN_VMAX || rmax == 1);
+  const int npb = h >= 2 && w >= 2 ? 2 * w + 2 * (h - 2) : 0;
+  const int npile = n * npb;
+  int found = 0;
+  if ((int)blockIdx.x < npile) {
+    int r, x;
+    const int img_i = blockIdx.x / npb;
+    win_pile_dest(blockIdx.x % npb, h, w, r, x);
+    if (!(mode_a || mode_b) || !win_piled(mode_a, r, x, h, w)) return;   // (block-uniform)
+    const int64_t img = (int64_t)img_i * hw;
+    WinDest D = mode_a ? win_dest_a(r, x, h, w, R) : win_dest_b(flow + 2 * img, r, x, h, w, R);
+    const int seg = (D.k1 + 15) / 16;
+    D.k0 = min(grp * seg, D.k1);
+    D.k1 = min(D.k0 + seg, D.k1);
+    for (int cb0 = 0; cb0 < nq; cb0 += 16 * NCB) {
+      float4 acc[NCB];
+      int fnd = 0;
+      win_accumulate<VEC, NCB>(acc, fnd, D, dout + img * c, flow + 2 * img, h, w, c, cb0,
+                               l_off[grp], l_w[grp], q, src0);
+      if (cb0 == 0) found = fnd;
+#pragma unroll
+      for (int b = 0; b < NCB; ++b) part[grp][16 * b + q] = acc[b];
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int b = 0; b < NCB; ++b) {
+          float4 t = part[0][16 * b + q];
+          for (int g2 = 1; g2 < 16; ++g2) {
+            const float4 v = part[g2][16 * b + q];
+            t.x += v.x, t.y += v.y, t.z += v.z, t.w += v.w;
+          }
+          const int cq = cb0 + 16 * b + q;
+          if (cq < nq) own_store<VEC>(dinp + (img + (int64_t)r * w + x) * c, cq, t);
+        }
+      }
+      __syncthreads();
+    }
+    if (mode_b) {
+      if (q == 0) fsum[grp] = found;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        int s = 0;
+        for (int g2 = 0; g2 < 16; ++g2) s += fsum[g2];
+        atomicAdd(det_slot(hdr, blockIdx.x % DET_SLOTS), s);
+      }
+    }
+    return;
+  }
+  const int64_t d = ((blockIdx.x - npile) * (int64_t)blockDim.x + threadIdx.x) >> 4;
+  const bool live = d < npix;
+  const int64_t dd = live ? d : npix - 1;
+  // d(flow) of pixel d: its loads first (c <= 64 NCB, one quad per channel block)
+  constexpr int DFQ = NCB;
+  const bool pre = VEC && c <= 64 * DFQ;
+  float4 pg[DFQ], pP[4][DFQ];
+  DetTaps T;
+  if (pre) {
+    T = det_taps(flow, dd, h, w, c, 0);
+#pragma unroll
+    for (int b = 0; b < DFQ; ++b) {
+      const int cq = 4 * q + 64 * b;
+      const bool ok = cq < c;
+      pg[b] = ok ? *reinterpret_cast<const float4*>(dout + dd * c + cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        pP[k][b] = ok ? *reinterpret_cast<const float4*>(inp + T.off[k] + cq)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  if (mode_a || mode_b) {
+    const int64_t img = dd / hw * hw;
+    const int rem = (int)(dd - img);
+    const int r = rem / w, x = rem % w;
+    const bool skip = !live || win_piled(mode_a, r, x, h, w);
+    WinDest D = mode_a ? win_dest_a(r, x, h, w, R) : win_dest_b(flow + 2 * img, r, x, h, w, R);
+    if (skip) D.k1 = 0;
+    for (int cb0 = 0; cb0 < nq; cb0 += 16 * NCB) {     // every lane runs every iteration
+      float4 acc[NCB];
+      int fnd = 0;
+      win_accumulate<VEC, NCB>(acc, fnd, D, dout + img * c, flow + 2 * img, h, w, c, cb0,
+                               l_off[grp], l_w[grp], q, src0);
+      if (cb0 == 0) found = fnd;
+      if (!skip) {
+#pragma unroll
+        for (int b = 0; b < NCB; ++b) {
+          const int cq = cb0 + 16 * b + q;
+          if (cq < nq) own_store<VEC>(dinp + dd * c, cq, acc[b]);
+        }
+      }
+    }
+  }
+  if (mode_b) {                                        // the wave's hits, one add
+    int s = q == 0 ? found : 0;
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0 && s) atomicAdd(det_slot(hdr, (blockIdx.x * 4 + (threadIdx.x >> 6)) % DET_SLOTS), s);
+  }
+  if (pre) {
+    float gx = 0.f, gy = 0.f;
+#pragma unroll
+    for (int b = 0; b < DFQ; ++b)
+      if (4 * q + 64 * b < c) dflow_quad(gx, gy, T.a, T.bq, pg[b], pP[0][b], pP[1][b], pP[2][b], pP[3][b]);
+    dflow_store(gx, gy, d, live, q, dflow, dfa, ldfa);
+  } else if (VEC) {
+    det_dflow_quads(dout, inp, npix, h, w, c, flow, 0, dflow, dfa, ldfa, d, q);
   }
 }
 
@@ -419,38 +701,37 @@ __global__ __launch_bounds__(256) void det_dflow_scalar(const float* __restrict_
   dflow[2 * p + 1] = dfa ? dfa[p * ldfa + 1] + gy : gy;
 }
 
-// Workspace layout (256-byte aligned pieces): per destination pixel a count, a segment
-// offset and a fill cursor (4 B each), the entry list (4 B per (pixel, corner)), the block
-// sums of the scan, and the list of destinations with long segments + its length.
+
+// Workspace layout: the int64 accumulator of the fixed-point path (n h w c), then the header.
 struct DetWs {
-  size_t cnt, off, cursor, list, bsum, big, big_n, total;
-  int nblk;
+  size_t acc, hdr, total;
 };
 
-void det_layout(int64_t npix, DetWs& L) {
-  auto al = [](size_t v) { return (v + 255) / 256 * 256; };
-  L.nblk = (int)cdiv(npix, OWN_SB);
-  size_t o = 0;
-  L.cnt = o, o += al(npix * 4);
-  L.cursor = o, o += al(npix * 4);     // (cnt and cursor adjacent: one memset)
-  L.off = o, o += al(npix * 4);
-  L.list = o, o += al(4 * npix * 4);
-  L.bsum = o, o += al((size_t)L.nblk * 4);
-  L.big = o, o += al(npix * 4);
-  L.big_n = o, o += 256;
-  L.total = o;
+void det_layout(int64_t npix, int c, DetWs& L) {
+  L.acc = 0;
+  L.hdr = (size_t)npix * c * 8;
+  L.hdr = (L.hdr + 255) / 256 * 256;
+  L.total = L.hdr + DET_HDR_INTS * 4;
 }
 
 }  // namespace
 
+int g_det_rmax = 8;
+
 extern "C" {
 
 size_t of_warp_bwd_det_workspace(int n, int h, int w, int c) {
-  (void)c;
-  if (n <= 0 || h <= 0 || w <= 0) return 0;
+  if (n <= 0 || h <= 0 || w <= 0 || c <= 0) return 0;
   DetWs L;
-  det_layout((int64_t)n * h * w, L);
+  det_layout((int64_t)n * h * w, c, L);
   return L.total;
+}
+
+size_t of_warp_bwd_det_header(int n, int h, int w, int c) {
+  if (n <= 0 || h <= 0 || w <= 0 || c <= 0) return 0;
+  DetWs L;
+  det_layout((int64_t)n * h * w, c, L);
+  return L.hdr;
 }
 
 int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, int c,
@@ -464,63 +745,59 @@ int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, in
   hipStream_t s = as_stream(stream);
   const bool vec = c % 4 == 0 && ((uintptr_t)dout & 15) == 0 && ((uintptr_t)inp & 15) == 0 &&
                    (!dinp || ((uintptr_t)dinp & 15) == 0);
-  if (dinp) {
-    DetWs L;
-    det_layout(npix, L);
-    OF_CHECK_ARG(ws && ws_bytes >= L.total, "warp bwd det: workspace too small");
-    char* base = static_cast<char*>(ws);
-    int* cnt = reinterpret_cast<int*>(base + L.cnt);
-    int* cursor = reinterpret_cast<int*>(base + L.cursor);
-    int* off = reinterpret_cast<int*>(base + L.off);
-    uint32_t* list = reinterpret_cast<uint32_t*>(base + L.list);
-    int* bsum = reinterpret_cast<int*>(base + L.bsum);
-    int* big = reinterpret_cast<int*>(base + L.big);
-    int* big_n = reinterpret_cast<int*>(base + L.big_n);
-    if (hipMemsetAsync(cnt, 0, L.off - L.cnt, s) != hipSuccess ||
-        hipMemsetAsync(big_n, 0, sizeof(int), s) != hipSuccess)
-      return check_launch("warp_bwd_det: memset");
-    const dim3 gp((unsigned)cdiv(npix, 256));
-    hipLaunchKernelGGL(own_count, gp, dim3(256), 0, s, flow, n, h, w, absolute, cnt);
-    hipLaunchKernelGGL(own_block_sums, dim3(L.nblk), dim3(256), 0, s, cnt, npix, bsum);
-    hipLaunchKernelGGL(own_scan_sums, dim3(1), dim3(1024), 0, s, bsum, L.nblk);
-    hipLaunchKernelGGL(own_block_scan, dim3(L.nblk), dim3(256), 0, s, cnt, npix, bsum, off);
-    hipLaunchKernelGGL(own_fill, gp, dim3(256), 0, s, flow, n, h, w, absolute, off, cursor, list);
-    if (int st = check_launch("warp_bwd_det: sort")) return st;
+  const dim3 gq((unsigned)cdiv(npix * 16, 256));
+  const dim3 gp((unsigned)cdiv(npix, 256));
+  if (!dinp) {
     if (vec)
-      hipLaunchKernelGGL(own_gather<true>, dim3((unsigned)cdiv(npix * 16, 256)), dim3(256), 0, s,
-                         dout, flow, n, h, w, c, absolute, cnt, off, list, dinp, big_n, big);
+      hipLaunchKernelGGL(det_dflow_vec, gq, dim3(256), 0, s, dout, inp, n, h, w, c, flow,
+                         absolute, dflow, dflow_add, ld_add);
     else
-      hipLaunchKernelGGL(own_gather<false>, dim3((unsigned)cdiv(npix * 16, 256)), dim3(256), 0, s,
-                         dout, flow, n, h, w, c, absolute, cnt, off, list, dinp, big_n, big);
-    const int64_t codes = 4 * (int64_t)h * w;
-    const size_t bm_bytes =
-        (size_t)(codes < OWN_WBITS ? (codes + 31) / 32 * 32 : OWN_WBITS) / 8;
-    static bool attr = false;
-    if (!attr) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(own_gather_big<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              OWN_WBITS / 8) != hipSuccess ||
-          hipFuncSetAttribute(reinterpret_cast<const void*>(own_gather_big<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              OWN_WBITS / 8) != hipSuccess)
-        return check_launch("warp_bwd_det: LDS attribute");
-      attr = true;
-    }
-    if (vec)
-      hipLaunchKernelGGL(own_gather_big<true>, dim3(2 * device_cus()), dim3(256), bm_bytes, s,
-                         dout, flow, h, w, c, absolute, cnt, off, list, big_n, big, dinp);
-    else
-      hipLaunchKernelGGL(own_gather_big<false>, dim3(2 * device_cus()), dim3(256), bm_bytes, s,
-                         dout, flow, h, w, c, absolute, cnt, off, list, big_n, big, dinp);
-    if (int st = check_launch("warp_bwd_det: gather")) return st;
+      hipLaunchKernelGGL(det_dflow_scalar, gp, dim3(256), 0, s, dout, inp, n, h, w, c, flow,
+                         absolute, dflow, dflow_add, ld_add);
+    return check_launch("warp_bwd_det: dflow");
   }
-  if (vec) {
-    hipLaunchKernelGGL(det_dflow_vec, dim3((unsigned)cdiv(npix * 16, 256)), dim3(256), 0, s, dout,
-                       inp, n, h, w, c, flow, absolute, dflow, dflow_add, ld_add);
-  } else {
-    hipLaunchKernelGGL(det_dflow_scalar, dim3((unsigned)cdiv(npix, 256)), dim3(256), 0, s, dout,
-                       inp, n, h, w, c, flow, absolute, dflow, dflow_add, ld_add);
+  DetWs L;
+  det_layout(npix, c, L);
+  OF_CHECK_ARG(ws && ws_bytes >= L.total, "warp bwd det: workspace too small");
+  char* base = static_cast<char*>(ws);
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(base + L.acc);
+  int* hdr = reinterpret_cast<int*>(base + L.hdr);
+  // the window needs relative flows and coordinates below 2^16 (own_radius's margin)
+  const int rmax = absolute || h >= 65536 || w >= 65536 || g_det_rmax == 0 ? -1 : g_det_rmax;
+  if (hipMemsetAsync(hdr, 0, DET_HDR_INTS * 4, s) != hipSuccess)
+    return check_launch("warp_bwd_det: memset");
+  if (rmax >= 0) {
+    // R, then the window and d(flow); the fallback's kernels after it read its mode-B count
+    const unsigned gr = (unsigned)std::min<int64_t>(cdiv(npix, 256), 4 * device_cus());
+    hipLaunchKernelGGL(own_radius, dim3(gr), dim3(256), 0, s, flow, npix, h, w, hdr);
+    const int nq = vec ? c / 4 : c;
+    auto kw = vec ? (nq > 16 ? own_window<true, 2> : own_window<true, 1>)
+                  : (nq > 16 ? own_window<false, 2> : own_window<false, 1>);
+    const int64_t npile = h >= 2 && w >= 2 ? (int64_t)n * (2 * w + 2 * (h - 2)) : 0;
+    hipLaunchKernelGGL(kw, dim3((unsigned)(gq.x + npile)), dim3(256), 0, s, dout, inp, flow, n,
+                       h, w, c, hdr, rmax, dinp, dflow, dflow_add, ld_add);
+    if (int st = check_launch("warp_bwd_det: window")) return st;
   }
+  // the fixed-point fallback (each kernel returns at once when the window served)
+  int lg4n = 0;
+  while ((int64_t(1) << lg4n) < 4 * npix) ++lg4n;
+  const int64_t nel = npix * c;
+  const unsigned gs = (unsigned)std::min<int64_t>(cdiv(nel, 256), 8 * device_cus());
+  hipLaunchKernelGGL(fix_prep, dim3(gs), dim3(256), 0, s, dout, nel,
+                     reinterpret_cast<int4*>(acc), (nel + 1) / 2, hdr, rmax, npix);
+  const int64_t tiles = (int64_t)n * cdiv(h, FX_T) * cdiv(w, FX_T) * ((c + 63) / 64);
+  hipLaunchKernelGGL(fix_scatter, dim3((unsigned)tiles), dim3(64 * FX_WAVES), 0, s, dout, flow,
+                     n, h, w, c, absolute, hdr, rmax, lg4n, acc);
+  hipLaunchKernelGGL(fix_convert, dim3(gs), dim3(256), 0, s,
+                     reinterpret_cast<const long long*>(acc), nel, hdr, rmax, npix, lg4n, dinp);
+  if (int st = check_launch("warp_bwd_det: fixed point")) return st;
+  if (rmax >= 0 && vec) return OF_OK;                  // d(flow) formed by own_window
+  if (vec)
+    hipLaunchKernelGGL(det_dflow_vec, gq, dim3(256), 0, s, dout, inp, n, h, w, c, flow, absolute,
+                       dflow, dflow_add, ld_add);
+  else
+    hipLaunchKernelGGL(det_dflow_scalar, gp, dim3(256), 0, s, dout, inp, n, h, w, c, flow,
+                       absolute, dflow, dflow_add, ld_add);
   return check_launch("warp_bwd_det: dflow");
 }
 

@@ -47,11 +47,13 @@ def _tag(layer, kind):
 
 # Deterministic mode: the feature-warp backward -- the only kernel of the step
 # that adds with float atomics (the scatter-add gradient of the gathers of
-# transformations.py:110-113,128) -- runs as a stable sort + fixed-order gather
-# (of_warp_bwd_det), so a train step is bitwise reproducible run to run, eager or replayed
-# from a graph.  Every other reduction of the step is fixed-order already.  Off by default
-# (DESIGN.md §3 gives its cost); OFLOW_DETERMINISTIC=1 or set_deterministic(True) turns it on.
-DETERMINISTIC = os.environ.get("OFLOW_DETERMINISTIC", "0") == "1"
+# transformations.py:110-113,128) -- runs as a fixed-order window gather, or an exact int64
+# fixed-point sum where no window covers the field (of_warp_bwd_det), so a train step is
+# bitwise reproducible run to run, eager or replayed from a graph.  Every other reduction of
+# the step is fixed-order already.  ON by default since round 5 (DESIGN.md §3 gives its cost
+# against the float-atomic form); OFLOW_DETERMINISTIC=0 or set_deterministic(False) selects
+# the atomic warp_bwd_gather.
+DETERMINISTIC = os.environ.get("OFLOW_DETERMINISTIC", "1") == "1"
 
 
 def set_deterministic(on: bool = True) -> bool:
@@ -1136,8 +1138,10 @@ def encoder_forward_train(x4, conv1: ConvLayer, blocks, groups: int = 2):
 
 # The stem's backward (max-pool + out0 gradient + BN + ReLU, then the 7x7 weight gradient) in
 # the weight-gradient kernel itself (of_stem_bwd_fused): dz0, the encoder's largest tensor, is
-# never written and read back.  OFLOW_STEM_FUSED=0 keeps of_maxpool_bn_relu_bwd + the wgrad.
-STEM_FUSED = os.environ.get("OFLOW_STEM_FUSED", "1") == "1"
+# never written and read back.  Off by default: measured on the bench step (profiles/r5_*) the
+# fused weight gradient took 340 us + 65 us of stem_bn_final against 150 + 132 us for
+# of_maxpool_bn_relu_bwd + the plain wgrad (it re-forms dz per K slice).  OFLOW_STEM_FUSED=1.
+STEM_FUSED = os.environ.get("OFLOW_STEM_FUSED", "0") == "1"
 
 
 # The stem forward writes the max-pooled tensor too (of_conv2d_fwd_pool: MaxPool2D,
@@ -1723,7 +1727,7 @@ class _Warp(torch.autograd.Function):
             dinp = new_grad(ctx.dst, inp)
         dflow = torch.empty_like(flow)
         fa = ctx.fa
-        if DETERMINISTIC:       # sort-based fixed-order gather: dinp written, no fill
+        if DETERMINISTIC:       # fixed-order gather / exact fixed point: dinp written, no fill
             add, ld = None, 0
             if fa is not None and fa.addend is not None and ctx.needs_input_grad[1]:
                 dcat, off, ld = fa.addend
@@ -1985,20 +1989,24 @@ class _PhotoLoss(torch.autograd.Function):
         # every level is a resize of the full-resolution batch (loss.py:17-18)
         outs = (C.c_void_p * ns)(*[p.data_ptr() for p in pyr])
         call("of_pyramid6", _ptr(b), n, H, W, ns, outs, s)
-        nparts, parts, coefs = [], [], []
+        # every scale's partial sums in one launch (of_photo_l1_fwd_multi), one partial array
+        fl = [f.contiguous() for f in flows]
+        hs = [p.shape[1] for p in pyr]
+        ws_ = [p.shape[2] for p in pyr]
+        nparts = [_lib.lib().of_photo_l1_partials(n, h, w) for h, w in zip(hs, ws_)]
+        coefs = [1.0 / (ns * n * h * w * 3) for h, w in zip(hs, ws_)]
+        parts = torch.empty(sum(nparts), device=b.device)
+        call("of_photo_l1_fwd_multi", (C.c_void_p * ns)(*[p.data_ptr() for p in pyr]),
+             (C.c_void_p * ns)(*[f.data_ptr() for f in fl]), n, (C.c_int * ns)(*hs),
+             (C.c_int * ns)(*ws_), ns, _ptr(parts), s)
+        offs = [0]
         for k in range(ns):
-            h, w = pyr[k].shape[1], pyr[k].shape[2]
-            npart = _lib.lib().of_photo_l1_partials(n, h, w)
-            pt = torch.empty(npart, device=b.device)
-            call("of_photo_l1_fwd", _ptr(pyr[k]), _ptr(flows[k].contiguous()), n, h, w, _ptr(pt),
-                 s)
-            parts.append(pt)
-            nparts.append(npart)
-            coefs.append(1.0 / (ns * n * h * w * 3))
+            offs.append(offs[-1] + nparts[k])
         loss = torch.empty((), device=b.device)
-        call("of_sum_partials", (C.c_void_p * ns)(*[p.data_ptr() for p in parts]),
+        call("of_sum_partials",
+             (C.c_void_p * ns)(*[parts.data_ptr() + 4 * offs[k] for k in range(ns)]),
              (C.c_int * ns)(*nparts), (C.c_float * ns)(*coefs), ns, _ptr(loss), s)
-        ctx.save_for_backward(*pyr, *[f.contiguous() for f in flows])
+        ctx.save_for_backward(*pyr, *fl)
         ctx.ns = ns
         ctx.coefs = coefs
         return loss
@@ -2010,24 +2018,31 @@ class _PhotoLoss(torch.autograd.Function):
         pyr, flows = saved[:ns], saved[ns:]
         dloss = dloss.contiguous()
         s = _stream()
-        grads = []
+        grads, lv = [], []          # lv: (level, output, row stride) of one multi launch
         for k in range(ns):
-            n, h, w, _ = pyr[k].shape
             if not ctx.needs_input_grad[2 + k]:
                 grads.append(None)
                 continue
             fg = ctx.fgs[k]
             if fg is not None:         # into the flow head's padded gradient (FlowGrad)
                 buf = fg.buffer()
-                call("of_photo_l1_bwd_ld", _ptr(pyr[k]), _ptr(flows[k]), n, h, w, ctx.coefs[k],
-                     _ptr(dloss), _ptr(buf), 4, s)
                 fg.filled = True
                 grads.append(buf[..., :2])
+                lv.append((k, buf, 4))
                 continue
             df = torch.empty_like(flows[k])
-            call("of_photo_l1_bwd", _ptr(pyr[k]), _ptr(flows[k]), n, h, w, ctx.coefs[k],
-                 _ptr(dloss), _ptr(df), s)
             grads.append(df)
+            lv.append((k, df, 2))
+        if lv:
+            m = len(lv)
+            n = pyr[0].shape[0]
+            call("of_photo_l1_bwd_multi", (C.c_void_p * m)(*[pyr[k].data_ptr() for k, _, _ in lv]),
+                 (C.c_void_p * m)(*[flows[k].data_ptr() for k, _, _ in lv]), n,
+                 (C.c_int * m)(*[pyr[k].shape[1] for k, _, _ in lv]),
+                 (C.c_int * m)(*[pyr[k].shape[2] for k, _, _ in lv]), m,
+                 (C.c_float * m)(*[ctx.coefs[k] for k, _, _ in lv]), _ptr(dloss),
+                 (C.c_void_p * m)(*[o.data_ptr() for _, o, _ in lv]),
+                 (C.c_int * m)(*[ld for _, _, ld in lv]), s)
         return (None, None, *grads)
 
 

@@ -96,11 +96,15 @@ def test_bn_train_kernels(groups, act, with_res, c):
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_flow_net_bn_training(precision):
-    """The whole flow net with bn_mode="training" at 64x128, B=2: flows, loss and all 108 weight
-    gradients against the oracle's train step in training mode (float64; bf16: the oracle with
-    the bf16 operand rounding, at the whole-net bf16 bounds of test_flow_net_bf16), and the
-    moving statistics of every BN layer after the step (updated once per encoder call, image1s
-    then image2s) within 1e-5 of the oracle's."""
+    """The whole flow net with bn_mode="training" at 64x128, B=2, one train step against the
+    oracle's (float64; bf16: the oracle with the bf16 operand rounding): the loss, the moving
+    statistics of every BN layer after the step (updated once per encoder call, image1s then
+    image2s) and finite gradients.  The gradients themselves are checked teacher-forced,
+    test_encoder_bn_training: through the whole net this weight set's flows come within 1e-5
+    of integer sample coordinates at some pixels, where the warp's floor() (model.py:69-71)
+    and the loss's |.| turn the forward's rounding differences (fp32: 8e-4 relative at H/2)
+    into flipped per-pixel gradient contributions (measured round 5: fp32 gradients median
+    1e-1) -- the end-to-end sensitivity of DESIGN.md §1, not the BN mode."""
     from optical_flow_amd.data import synthetic_batch
     from optical_flow_amd.loss import LossLayer
     from optical_flow_amd.model import FlowNet
@@ -127,23 +131,98 @@ def test_flow_net_bn_training(precision):
     lrel = abs(float(loss) - loss_o.item()) / abs(loss_o.item())
     frel = [rel_inf(flows[k], flows_o[k]) for k in range(4)]
     print("%s loss rel %.2e, flows rel_inf %s" % (precision, lrel, ["%.1e" % e for e in frel]))
-    errs = {n: rel_l2(g, grads_o[n]) for n, g in net.store.grads().items()}
-    worst = max(errs.items(), key=lambda kv: kv[1])
-    med = float(np.median(list(errs.values())))
-    print("grads: median %.2e, worst %.2e (%s)" % (med, worst[1], worst[0]))
     mstat = max(rel_inf(net.store.params[n], p[n]) for n in p
                 if n.endswith(("moving_mean", "moving_variance")))
     print("moving statistics: worst rel_inf %.2e" % mstat)
-    assert mstat < 1e-5
+    # (bf16: the statistics of z, which carries the bf16 operand rounding of the conv)
+    assert mstat < (1e-5 if precision == "fp32" else 1e-3)
     assert all(torch.isfinite(g).all() for g in net.store.grads().values())
+    assert lrel < (REL_TOL if precision == "fp32" else 3e-2)
+    assert frel[-1] < (1e-4 if precision == "fp32" else 3e-2), frel   # H/16: no warp before it
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_encoder_bn_training(precision):
+    """reset18_encoder (model.py:10-26) with BN in training mode, teacher-forced: the oracle's
+    images as the Siamese (2B) batch (two groups: one encoder call per image, model.py:131-132),
+    fixed random gradients on the four outputs; outputs, every encoder gradient and the moving
+    statistics against the oracle run once per image (float64; bf16: with the bf16 operand
+    rounding).  fp32 at 1e-3 (the conv biases, whose gradient the batch mean removes, against
+    the kernel gradient's scale); bf16 at the module tests' 1e-2 median, each gradient within
+    5e-2 or 3x the oracle's own bf16-vs-fp32 change of it (res4's statistics are over 16
+    values per group at 64 x 128: a bf16 rounding moves its gradients by ~10 %)."""
+    from optical_flow_amd.data import synthetic_batch
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params, perturb_params
+    H, W, B = 64, 128, 2
+    vals = perturb_params(init_params(flow_net_spec(), 21), 22)
+    batch = synthetic_batch(B, H, W, seed=4321)
+    net = FlowNet(H, W, values=vals, precision=precision, bn_mode="training")
+    p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+    blocks = list(encoder_blocks())
+    x = torch.tensor(batch, dtype=torch.float64)
+    names = [n for n in net.store.grads() if n.startswith("ResNet18")]
+    rng = np.random.default_rng(79)
+    gs = None
+
+    def oracle(prec, params):
+        nonlocal gs
+        tr = {n: params[n].clone().requires_grad_(True) for n in names}
+        pp = dict(params, **tr)
+        R.set_bn_mode("training")
+        R.set_conv_precision(prec)
+        try:
+            o1 = R.encoder(x[..., :3], pp, blocks)         # image1s, then image2s
+            o2 = R.encoder(x[..., 3:], pp, blocks)
+            outs_o = [torch.cat([a, b], 0) for a, b in zip(o1, o2)]
+            if gs is None:
+                gs = [torch.tensor(rng.standard_normal(tuple(o.shape))) for o in outs_o]
+            gr = torch.autograd.grad(sum((o * g).sum() for o, g in zip(outs_o, gs)),
+                                     [tr[n] for n in names])
+        finally:
+            R.set_bn_mode("inference")
+            R.set_conv_precision("fp32")
+        return outs_o, dict(zip(names, gr))
+
+    outs_o, grads_o = oracle(precision, p)             # (updates p's moving statistics)
+    # bf16: the oracle's own bf16-vs-fp32 gradient change per parameter -- the sensitivity of
+    # each gradient to the operand rounding (res4's batch statistics are over 2 x 8 values)
+    noise = {}
+    if precision == "bf16":
+        p32 = {k: (v.clone() if k.endswith(("moving_mean", "moving_variance")) else v)
+               for k, v in p.items()}
+        _, g32 = oracle("fp32", p32)
+        noise = {n: rel_l2(grads_o[n], g32[n]) for n in names if not n.endswith("/bias")}
+    imgs = torch.cat([x[..., :3], x[..., 3:]], 0)
+    x4 = torch.cat([dev(imgs.float()), torch.zeros(imgs.shape[:3] + (1,), device="cuda")], -1)
+    net.store.zero_grad()
+    outs = net.encoder.forward4(x4, groups=2)
+    sum((o * dev(g.float())).sum() for o, g in zip(outs, gs)).backward()
+    torch.cuda.synchronize()
+    errs = [("out%d" % k, rel_l2(o, oo)) for k, (o, oo) in enumerate(zip(outs, outs_o))]
+    grads = net.store.grads()
+    for n in names:
+        if n.endswith("/bias"):
+            kn = n[:-len("bias")] + "kernel"
+            errs.append((n, float(grads[n].double().cpu().norm()) / float(grads_o[kn].norm())))
+        else:
+            errs.append((n, rel_l2(grads[n], grads_o[n])))
+    for n in p:
+        if n.endswith(("moving_mean", "moving_variance")):
+            errs.append((n, rel_inf(net.store.params[n], p[n])))
+    for n, e in sorted(errs, key=lambda t: -t[1])[:10]:
+        print("  %-40s %.3e   (bf16 vs fp32 oracle %.3e)" % (n, e, noise.get(n, 0.0)))
+    vals_e = [e for _, e in errs]
+    med = float(np.median(vals_e))
+    print("%s: median %.2e, worst %.2e" % (precision, med, max(vals_e)))
+    assert all(torch.isfinite(grads[n]).all() for n in names)
     if precision == "fp32":
-        assert lrel < REL_TOL
-        assert max(frel) < REL_TOL, frel
-        assert worst[1] < REL_TOL, worst
-    else:   # test_flow_net_bf16's statistical bounds
-        assert lrel < 3e-2
-        assert max(frel) < 3e-2, frel
-        assert med < 8e-2 and worst[1] < 2.5e-1, (med, worst)
+        bad = [(n, e) for n, e in errs if not e < REL_TOL]
+        assert not bad, bad
+    else:
+        # within 5e-2, or within 3x what bf16 rounding itself moves that gradient
+        bad = [(n, e) for n, e in errs if not e < max(5e-2, 3.0 * noise.get(n, 0.0))]
+        assert med < 1e-2 and not bad, (med, bad)
 
 
 def test_bn_mode_switch_and_graph():
@@ -181,3 +260,50 @@ def test_bn_mode_switch_and_graph():
         f1 = net(b[0])
     for a, c in zip(f0, f1):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("proj", [True, False])
+def test_resnet_block_bn_training(proj):
+    """One residual block (resnet_layer_simple, model.py:18-22) with BN in training mode, as
+    the build's encoder runs it (ops.conv_bn_train): output, input gradient, every weight
+    gradient and the moving statistics against the oracle (float64) at 1e-3; the conv biases,
+    whose gradient the batch mean removes, against the kernel gradient's scale."""
+    from optical_flow_amd.model import ParamStore, resnet_layer_simple
+    from optical_flow_amd.params import blocks_spec, init_params, perturb_params, stage_blocks
+    blocks = stage_blocks(3, 64, 1, True) if proj else stage_blocks(3, 128, 1, False)
+    spec = blocks_spec(blocks)
+    vals = perturb_params(init_params(spec, 25), 26)
+    pre = blocks[0][0]
+    store = ParamStore(spec, values=vals, device="cuda")
+    g = torch.Generator().manual_seed(5)
+    cin = 64 if proj else 128
+    x0 = torch.randn(2, 16, 24, cin, generator=g, dtype=torch.float64)
+    x = dev(x0.float()).requires_grad_(True)
+    store.zero_grad()
+    y = resnet_layer_simple(x, 1, proj, 3, store=store, bn_mode="training")
+    dy0 = torch.randn(tuple(y.shape), generator=g, dtype=torch.float64)
+    y.backward(dev(dy0.float()))
+    torch.cuda.synchronize()
+    p = {k: torch.tensor(v, dtype=torch.float64, requires_grad=not k.endswith(
+        ("moving_mean", "moving_variance"))) for k, v in vals.items()}
+    xo = x0.float().double().requires_grad_(True)
+    R.set_bn_mode("training")
+    try:
+        yo = R.resnet_block(xo, p, pre, 2 if proj else 1, proj)
+    finally:
+        R.set_bn_mode("inference")
+    yo.backward(dy0)
+    errs = [("out", rel_l2(y, yo)), ("dx", rel_l2(x.grad, xo.grad))]
+    for name, gr in store.grads().items():
+        if name.endswith("/bias"):
+            kn = name[:-len("bias")] + "kernel"
+            errs.append((name, float(gr.double().cpu().norm()) / float(p[kn].grad.norm())))
+        else:
+            errs.append((name, rel_l2(gr, p[name].grad)))
+    for n in p:
+        if n.endswith(("moving_mean", "moving_variance")):
+            errs.append((n, rel_inf(store.params[n], p[n])))
+    for n, e in errs:
+        print("%-40s %.3e" % (n, e))
+    bad = [(n, e) for n, e in errs if not e < REL_TOL]
+    assert not bad, bad

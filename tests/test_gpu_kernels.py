@@ -1559,12 +1559,19 @@ def test_bilinear_interpolation_absolute():
                                                      ((2, 10, 14, 3), 4.0, 0.0),
                                                      ((1, 17, 23, 32), 2.0, 0.0),
                                                      ((1, 9, 11, 6), 1.0, 0.0),
+                                                     ((1, 40, 24, 64), 1.0, 0.0),
+                                                     ((1, 31, 29, 16), 2.5, 0.0),
+                                                     ((2, 20, 60, 64), 0.5, 0.0),
+                                                     ((1, 60, 20, 128), 0.5, 0.0),
+                                                     ((1, 18, 56, 6), 0.4, 0.0),
                                                      ((8, 96, 128, 64), 1.5, 0.0)])
 def test_warp_bwd_deterministic(shape, flow_scale, offset, absolute):
     """The deterministic warp backward (of_warp_bwd_det, ops.deterministic()): against fp64
     autograd of the reference sampler (transformations.py:85-129) for sub-pixel, spread and
     border-clipped flows (20 x 24 at offset -30: every sample clamps onto one corner pixel, the
-    longest possible run), any channel count, grid + flow and absolute points; BITWISE equal
+    longest possible run), any channel count, grid + flow and absolute points, the window
+    gather's pile row / column workgroups (|w - h| > 16, P1's transposed grid clips every
+    source beyond h onto the last row); BITWISE equal
     over repeated launches; the atomic default agrees up to its add order."""
     from optical_flow_amd.transformations import bilinear_interpolation
     ops = _ops()
@@ -1591,191 +1598,104 @@ def test_warp_bwd_deterministic(shape, flow_scale, offset, absolute):
     assert rel_inf(runs[0][1], fo.grad) < REL_TOL
     for gi, gf in runs[1:]:
         assert torch.equal(gi, runs[0][0]) and torch.equal(gf, runs[0][1])
-    ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
-    (fwd(ad, fd) * dev(g)).sum().backward()                 # the atomic default
+    with ops.deterministic(False):
+        ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
+        (fwd(ad, fd) * dev(g)).sum().backward()             # the atomic form
     assert rel_inf(ad.grad, runs[0][0]) < REL_TOL
     assert rel_inf(fd.grad, runs[0][1]) < REL_TOL
 
 
-# -------------------------------------------------------------------------- upscale -----
-@pytest.mark.parametrize("shape", [(2, 6, 8, 2), (1, 24, 32, 2), (2, 5, 7, 3), (1, 2, 4, 2)])
-def test_upscale(shape):
+@pytest.mark.parametrize("shape,flow_scale,offset", [((2, 32, 32, 64), 0.2, 0.0),
+                                                     ((1, 48, 48, 128), 0.25, 0.0),
+                                                     ((2, 24, 24, 12), 0.2, 0.0),
+                                                     ((1, 40, 40, 64), 0.2, 0.6),
+                                                     ((2, 20, 60, 64), 0.2, 0.0)])
+def test_warp_bwd_det_paths(shape, flow_scale, offset):
+    """of_warp_bwd_det's three ways to d(features) on one input: window mode A (of_set_tuning
+    key 28 = 8, the default for these flows), mode B (key 28 = 1: centred windows, border pixels
+    on workgroups of their own) and the fixed-point path (key 28 = 0) -- each against fp64;
+    A and B BITWISE equal off the border (the same ascending (source, corner) order; B splits a
+    border pixel's sum over 16 partials); the fixed-point sums within 1e-5 of A; d(flow) bitwise
+    equal across all three (the same fixed-order kernel arithmetic)."""
     ops = _ops()
-    x = rng_tensor(shape, 31)
-    xo = f64(x).requires_grad_(True)
-    yo = R.upscale_flow(xo)
-    g = rng_tensor(tuple(yo.shape), 32)
-    (yo * f64(g)).sum().backward()
-    xd = dev(x).requires_grad_(True)
-    yd = ops.upscale2x(xd, 2.0)
-    assert rel_inf(yd, yo) < REL_TOL
-    (yd * dev(g)).sum().backward()
-    assert rel_inf(xd.grad, xo.grad) < REL_TOL
+    from optical_flow_amd import _lib
+    lib = _lib.lib()
+    n, h, w, c = shape
+    f2 = rng_tensor(shape, 51)
+    fl = rng_tensor((n, h, w, 2), 52, scale=flow_scale) + offset
+    g = rng_tensor(shape, 53)
+    a, fo = f64(f2).requires_grad_(True), f64(fl).requires_grad_(True)
+    (R.warp_features(fo, a) * f64(g)).sum().backward()
+    res = {}
+    try:
+        for key in (8, 1, 0):
+            assert lib.of_set_tuning(28, key) == 0
+            with ops.deterministic(True):
+                ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
+                (ops.warp(ad, fd) * dev(g)).sum().backward()
+            torch.cuda.synchronize()
+            res[key] = (ad.grad.clone(), fd.grad.clone())
+            assert rel_inf(res[key][0], a.grad) < REL_TOL, key
+            assert rel_inf(res[key][1], fo.grad) < REL_TOL, key
+    finally:
+        lib.of_set_tuning(28, 8)
+    assert torch.equal(res[8][0][:, 1:-1, 1:-1], res[1][0][:, 1:-1, 1:-1])
+    assert rel_inf(res[0][0], res[8][0]) < 1e-5
+    assert torch.equal(res[8][1], res[1][1]) and torch.equal(res[8][1], res[0][1])
 
 
-# ------------------------------------------------------------------------- max pool -----
-def test_maxpool():
-    ops = _ops()
-    x = rng_tensor((2, 8, 12, 64), 41)
-    xo = f64(x).requires_grad_(True)
-    yo = R.maxpool2(xo)
-    g = rng_tensor(tuple(yo.shape), 42)
-    (yo * f64(g)).sum().backward()
-    xd = dev(x).requires_grad_(True)
-    yd = ops.maxpool2(xd)
-    assert rel_inf(yd, yo) == 0.0
-    (yd * dev(g)).sum().backward()
-    assert rel_inf(xd.grad, xo.grad) < REL_TOL
-
-
-# ------------------------------------------------------------------- photometric loss ---
-@pytest.mark.parametrize("size", [(2, 64, 96), (1, 128, 256), (1, 64, 128)])
-def test_photometric_loss(size):
-    from optical_flow_amd.loss import LossLayer
-    from optical_flow_amd.data import synthetic_batch
-    n, H, W = size
-    batch = torch.from_numpy(synthetic_batch(n, H, W, seed=5))
-    flows = [rng_tensor((n, H >> (s + 1), W >> (s + 1), 2), 50 + s, scale=2.0) for s in range(4)]
-    fo = [f64(f).requires_grad_(True) for f in flows]
-    lo = R.photometric_loss(f64(batch), fo)
-    lo.backward()
-    fd = [dev(f).requires_grad_(True) for f in flows]
-    ld = LossLayer()(dev(batch), fd)
-    assert abs(ld.item() - lo.item()) / abs(lo.item()) < REL_TOL
-    ld.backward()
-    for a, b in zip(fd, fo):
-        assert rel_l2(a.grad, b.grad) < REL_TOL
-
-
-# ------------------------------------------------------------------------------ adam ----
-def test_keras_adam():
-    from optical_flow_amd.train import KerasAdam
-    from optical_flow_amd.model import ParamStore
-    from optical_flow_amd.params import head_spec, init_params
-    spec = head_spec(3)
-    vals = init_params(spec, 3)
-    store = ParamStore(spec, vals, device="cuda")
-    opt = KerasAdam(store, learning_rate=1e-2)
-    ref = R.KerasAdam(lr=1e-2)
-    pref = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
-    for it in range(3):
-        grads = {k: rng_tensor(v.shape, 100 + it * 7 + i) for i, (k, v) in enumerate(vals.items())}
-        for k, g in grads.items():
-            store.params[k]._of_grad.copy_(g.cuda())
-        opt.apply_gradients()
-        ref.step(pref, {k: g.double() for k, g in grads.items()})
-    for k in vals:
-        assert rel_inf(store.params[k], pref[k]) < 1e-5
-
-
-@pytest.mark.parametrize("stride", [1, 2])
-def test_conv_split_k_matches_unsplit(stride):
-    """Small grids split K over workgroups (fp32 slabs + epilogue pass); without workspace
-    the same call runs unsplit.  Both must agree (and match the oracle)."""
+@pytest.mark.parametrize("shape,scale,offset,mode", [
+    ((2, 40, 56, 64), 0.5, 0.0, "A"),          # small flows: R <= 8
+    ((2, 48, 64, 128), 1.5, 21.0, "B"),        # large smooth flows: piles on the borders
+    ((1, 64, 48, 64), 1.5, -13.0, "B"),
+    ((1, 20, 24, 6), 0.5, -30.0, "B"),         # everything clamped onto one corner pixel
+    ((1, 30, 40, 64), 6.0, 0.0, "fixed"),      # large rough flows: no window
+    ((1, 30, 40, 64), 0.3, 12.0, "fixed"),     # large, rough at 0.3 px noise: no window
+])
+def test_warp_bwd_det_modes(shape, scale, offset, mode):
+    """of_warp_bwd_det's paths, read back from its workspace header (of_warp_bwd_det_header):
+    mode A (R <= key 28), mode B (smooth fields: centred windows, every entry found -- the
+    count is 4 n h w) and the fixed-point path (rough fields: no window); each against fp64 autograd
+    of warp_features (model.py:55-73), bitwise equal over repeated launches."""
     import ctypes as C
     from optical_flow_amd import _lib
-    from optical_flow_amd._lib import ACT_LEAKY, call
-    ops = _ops()
-    n, h, w, cin, cout, k = 2, 12, 16, 64, 128, 3
-    x = dev(rng_tensor((n, h, w, cin), 71))
-    wt = dev(rng_tensor((k, k, cin, cout), 72, scale=0.05))
-    b = dev(rng_tensor((cout,), 73, scale=0.1))
-    layer = ops.ConvLayer(wt, b, stride=stride, act=ACT_LEAKY, f32_split=False)
-    d = layer.desc(n, h, w)
-    wf, wd = layer.packed(d)
+    from optical_flow_amd._lib import call
     lib = _lib.lib()
-    fws = lib.of_conv2d_fwd_workspace(C.byref(d))
-    dws = lib.of_conv2d_dgrad_workspace(C.byref(d))
-    assert fws > 0 and dws > 0, "this shape must take the split-K path"
-    ws = torch.empty(max(fws, dws) // 4 + 4, device="cuda")
-    P, s = ops._ptr, ops._stream()
-    y1 = torch.empty(n, d.ho, d.wo, cout, device="cuda")
-    y2 = torch.empty_like(y1)
-    call("of_conv2d_fwd", C.byref(d), P(x), cin, P(wf), P(b), None, None, None, None, 1e-3, None,
-         0, ACT_LEAKY, 0.3, None, 0, P(y1), cout, P(ws), fws, s)
-    call("of_conv2d_fwd", C.byref(d), P(x), cin, P(wf), P(b), None, None, None, None, 1e-3, None,
-         0, ACT_LEAKY, 0.3, None, 0, P(y2), cout, None, 0, s)
-    yo = R.leaky_relu(R.conv2d_same(f64(x), f64(wt), f64(b), stride))
-    assert rel_inf(y1, yo) < REL_TOL and rel_inf(y2, yo) < REL_TOL
-    assert rel_inf(y1, y2) < 1e-5
-    g = dev(rng_tensor(tuple(y1.shape), 74))
-    dx1 = torch.empty_like(x)
-    dx2 = torch.empty_like(x)
-    call("of_conv2d_dgrad", C.byref(d), P(g), cout, P(wd), P(x), cin, ACT_LEAKY, 0.3, P(dx1), cin,
-         P(ws), dws, s)
-    call("of_conv2d_dgrad", C.byref(d), P(g), cout, P(wd), P(x), cin, ACT_LEAKY, 0.3, P(dx2), cin,
-         None, 0, s)
-    xo = f64(x).requires_grad_(True)
-    (R.conv2d_same(xo, f64(wt), None, stride) * f64(g)).sum().backward()
-    ref = torch.where(f64(x) > 0, xo.grad, 0.3 * xo.grad)
-    assert rel_inf(dx1, ref) < REL_TOL and rel_inf(dx2, ref) < REL_TOL
-
-
-@pytest.mark.parametrize("from_y", [False, True])
-@pytest.mark.parametrize("n,h,w,c,with_g", [(2, 8, 12, 64, True), (1, 6, 10, 16, False),
-                                            (3, 34, 70, 64, True),
-                                            # many workgroups, a ragged last one; 8 quads
-                                            (2, 96, 130, 64, True), (1, 40, 52, 32, False)])
-def test_maxpool_bn_act_bwd_fused(n, h, w, c, with_g, from_y):
-    """The stem's fused backward (max-pool backward + out0's second gradient + BN/ReLU
-    backward) against torch autograd of relu(bn(z)) -> {out0, maxpool} in float64; from_y:
-    of_maxpool_bn_relu_bwd, z not stored (zhat recovered from y)."""
-    import ctypes as C
-    from optical_flow_amd._lib import call, lib
-    torch.manual_seed(0)
-    z = torch.randn(n, h, w, c, dtype=torch.float64)
-    gamma = 1 + 0.2 * torch.rand(c, dtype=torch.float64)
-    beta = 0.1 * torch.randn(c, dtype=torch.float64)
-    mean = 0.1 * torch.randn(c, dtype=torch.float64)
-    var = 1 + 0.2 * torch.rand(c, dtype=torch.float64)
-    dyp = torch.randn(n, h // 2, w // 2, c, dtype=torch.float64)
-    g = torch.randn(n, h, w, c, dtype=torch.float64) if with_g else None
-    zr = z.clone().requires_grad_(True)
-    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
-    y = torch.relu((zr - mean) * (gr / torch.sqrt(var + 1e-3)) + br)
-    pooled = torch.nn.functional.max_pool2d(y.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
-    loss = (pooled * dyp).sum() + ((y * g).sum() if with_g else 0)
-    loss.backward()
-    yv = y.detach()
-    dv = lambda t: t.float().cuda().contiguous()
-    outs = [torch.empty(n, h, w, c, device="cuda")] + [torch.zeros(c, device="cuda") for _ in range(3)]
-    ws = torch.empty(lib().of_maxpool_bn_act_bwd_workspace(n, h, w, c) // 4 + 1, device="cuda")
-    P = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
-    args = [dv(dyp), dv(g) if with_g else None, dv(yv), dv(z), dv(gamma), dv(mean), dv(var)]
-    if from_y:
-        call("of_maxpool_bn_relu_bwd", n, h, w, c, P(args[0]), P(args[1]), P(args[2]),
-             P(args[4]), P(dv(beta)), P(args[6]), 1e-3, P(outs[0]), P(outs[1]), P(outs[2]),
-             P(outs[3]), 0, P(ws), None)
+    n, h, w, c = shape
+    f2 = rng_tensor(shape, 61)
+    if mode == "B":     # a smooth field (mode B is tried for neighbour changes <= 0.5 px)
+        ii, jj = torch.meshgrid(torch.arange(h).float(), torch.arange(w).float(), indexing="ij")
+        fl = offset + scale * torch.stack([torch.sin(0.21 * ii + 0.13 * jj),
+                                           torch.cos(0.17 * ii - 0.11 * jj)], -1)
+        fl = fl.expand(n, h, w, 2).contiguous()
     else:
-        call("of_maxpool_bn_act_bwd", n, h, w, c, *[P(t) for t in args], 1e-3, P(outs[0]),
-             P(outs[1]), P(outs[2]), P(outs[3]), 0, P(ws), None)
-    torch.cuda.synchronize()
-    dz, dg, db, dbias = [o.double().cpu() for o in outs]
-    exp_dbias = zr.grad.sum(dim=(0, 1, 2))
-    for got, exp in [(dz, zr.grad), (dg, gr.grad), (db, br.grad), (dbias, exp_dbias)]:
-        assert ((got - exp).abs().max() / exp.abs().max()).item() < 1e-5
-
-
-@pytest.mark.parametrize("k,s", [(1, 2), (3, 2), (3, 1)])
-def test_dgrad_add_in_place(k, s):
-    """of_conv2d_dgrad_add with dx == add (in-place accumulation; 1x1 stride 2 then launches
-    only the phase group a tap reaches) equals the out-of-place result."""
-    import ctypes as C
-    ops = _ops()
-    from optical_flow_amd._lib import ACT_NONE, call
-    n, h, w, cin, cout = 2, 16, 20, 64, 128
-    wt = dev(rng_tensor((k, k, cin, cout), 7, scale=0.1))
-    layer = ops.ConvLayer(wt, dev(rng_tensor((cout,), 8)), stride=s, act=ACT_NONE, cin_p=cin)
-    d = layer.desc(n, h, w)
-    _, wd = layer.packed(d)
-    dy = dev(rng_tensor((n, d.ho, d.wo, cout), 9))
-    add = dev(rng_tensor((n, h, w, cin), 10))
-    entry, wsz = layer.dgrad_add_entry(d)
-    P = lambda t: C.c_void_p(t.data_ptr())
-    ws = torch.empty(wsz // 4 + 1, device="cuda")
-    out = torch.empty_like(add)
-    call(entry, C.byref(d), P(dy), cout, P(wd), P(add), cin, P(out), cin, P(ws), wsz, None)
-    inplace = add.clone()
-    call(entry, C.byref(d), P(dy), cout, P(wd), P(inplace), cin, P(inplace), cin, P(ws), wsz, None)
-    torch.cuda.synchronize()
-    assert torch.equal(inplace, out)
+        fl = rng_tensor((n, h, w, 2), 62, scale=scale) + offset
+    g = rng_tensor(shape, 63)
+    a, fo = f64(f2).requires_grad_(True), f64(fl).requires_grad_(True)
+    (R.warp_features(fo, a) * f64(g)).sum().backward()
+    wsb = lib.of_warp_bwd_det_workspace(n, h, w, c)
+    hoff = lib.of_warp_bwd_det_header(n, h, w, c)
+    outs = []
+    dg, df2, dfl_in = dev(g), dev(f2), dev(fl)            # (kept alive across the launch)
+    for _ in range(2):
+        ws = torch.full(((wsb + 3) // 4,), -7, dtype=torch.int32, device="cuda")
+        dinp = torch.full(shape, float("nan"), device="cuda")
+        dfl = torch.empty((n, h, w, 2), device="cuda")
+        P = lambda t: C.c_void_p(t.data_ptr())
+        call("of_warp_bwd_det", P(dg), P(df2), n, h, w, c, P(dfl_in), 0, P(dinp), P(dfl),
+             None, 0, P(ws), wsb, None)
+        torch.cuda.synchronize()
+        hdr = ws[hoff // 4: hoff // 4 + 64 * 33].cpu()
+        outs.append((dinp.clone(), dfl.clone(), hdr))
+    hdr = outs[0][2]
+    rr = int(hdr[1])
+    found = int(sum(int(hdr[64 * (1 + k)]) for k in range(32)))
+    if mode == "A":
+        assert rr <= 8 and found == 0, (rr, found)
+    elif mode == "B":
+        assert rr > 8 and found == 4 * n * h * w, (rr, found)
+    else:
+        assert rr > 8 and found != 4 * n * h * w, (rr, found)
+    assert rel_inf(outs[0][0], a.grad) < REL_TOL
+    assert rel_inf(outs[0][1], fo.grad) < REL_TOL
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

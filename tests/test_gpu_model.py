@@ -313,17 +313,19 @@ def test_bn_gamma_near_zero(precision):
     No NaN, the guard picks exactly the layers with small gammas, and every gradient matches the
     oracle: fp32 through the train step's loss against the float64 oracle at 1e-3.
 
-    bf16 is checked through a smooth objective, sum_k <flow_k, G_k> with fixed random G_k,
-    against the bf16-rounded oracle: the median encoder-gradient error at the whole-net bf16
-    bound (8e-2, test_flow_net_bf16), the worst at 0.25.  (Through the photometric loss the
-    bf16 median measured 0.104 in round 4: the loss's |.| and the warp's floor() turn the bf16
-    rounding differences of the flows (~1e-2) into flipped per-pixel gradient contributions
-    that every encoder gradient inherits -- the end-to-end statistics of DESIGN.md §1, not the
-    BN guard; the smooth objective leaves only the network's own LeakyReLU / ReLU kinks.)"""
+    bf16: the whole encoder (model.py:10-26: stem and all eight blocks, the layers with small
+    gammas among them) teacher-forced -- the oracle's images in, fixed random gradients on its
+    four outputs -- against the bf16-rounded float64 oracle at the module tests' 1e-2.  (Through
+    the whole net the bf16 comparison is statistical: in round 5 this weight set measured a
+    median of 0.104 through the photometric loss and 0.147 through a smooth objective
+    sum_k <flow_k, G_k>, with the DECODER gradients 7-15 % off as well -- the forward's bf16
+    rounding compounding over the network, not the BN guard, whose block-level test
+    test_resnet_block_bn_guard[*-bf16] agrees to <= 1.5e-4.)"""
     from optical_flow_amd.loss import LossLayer
     from optical_flow_amd.data import synthetic_batch
     from optical_flow_amd.model import FlowNet
     from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params, perturb_params
+    from optical_flow_amd import ops
     H, W, B = 64, 128, 2
     vals = perturb_params(init_params(flow_net_spec(), 7), 8)
     g = vals["ResNet18/layer1_bn/gamma"].copy()
@@ -336,51 +338,64 @@ def test_bn_gamma_near_zero(precision):
     batch = synthetic_batch(B, H, W, seed=77)
     p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
     blocks = list(encoder_blocks())
-    smooth = precision == "bf16"
-    gs = None
-    if smooth:
-        rng = np.random.default_rng(78)
-        gs = [torch.tensor(rng.standard_normal((B, H >> (k + 1), W >> (k + 1), 2)))
-              for k in range(4)]
-    R.set_conv_precision(precision)
-    try:
-        if smooth:
-            tr = {k: v.clone().requires_grad_(True) for k, v in p.items()
-                  if not k.endswith(("moving_mean", "moving_variance"))}
-            pp = dict(p, **tr)
-            fo = R.flow_net(torch.tensor(batch, dtype=torch.float64), pp, blocks)
-            obj = sum((f * gk).sum() for f, gk in zip(fo, gs))
-            grads_o = dict(zip(tr, torch.autograd.grad(obj, list(tr.values()), allow_unused=True)))
-        else:
-            _, _, grads_o = R.train_step(torch.tensor(batch, dtype=torch.float64), p, blocks, None)
-    finally:
-        R.set_conv_precision("fp32")
-    net.store.zero_grad()
-    bd = dev(torch.from_numpy(batch))
-    flows = net(bd)
-    if smooth:
-        sum((f * dev(gk.float())).sum() for f, gk in zip(flows, gs)).backward()
+    want_stored = sorted(["conv1", "ResNet18/res2_0/conv_a", "ResNet18/res3_0/conv_b",
+                          "ResNet18/res4_0/proj"])
+    if precision == "fp32":
+        _, _, grads_o = R.train_step(torch.tensor(batch, dtype=torch.float64), p, blocks, None)
+        net.store.zero_grad()
+        bd = dev(torch.from_numpy(batch))
+        LossLayer()(bd, net(bd)).backward()
+        torch.cuda.synchronize()
+        assert sorted(net.store.bn_guard.stored()) == want_stored, net.store.bn_guard.stored()
+        tol, names = REL_TOL, list(net.store.grads())
     else:
-        LossLayer()(bd, flows).backward()
-    torch.cuda.synchronize()
-    assert sorted(net.store.bn_guard.stored()) == sorted(
-        ["conv1", "ResNet18/res2_0/conv_a", "ResNet18/res3_0/conv_b",
-         "ResNet18/res4_0/proj"]), net.store.bn_guard.stored()
+        x = torch.tensor(batch, dtype=torch.float64)
+        imgs = torch.cat([x[..., :3], x[..., 3:]], 0)          # the Siamese (2B) batch
+        rng = np.random.default_rng(78)
+        names = [n for n in net.store.grads() if n.startswith("ResNet18")]
+        tr = {n: p[n].clone().requires_grad_(True) for n in names}
+        R.set_conv_precision("bf16")
+        try:
+            outs_o = R.encoder(imgs, dict(p, **tr), blocks)
+            gs = [torch.tensor(rng.standard_normal(tuple(o.shape))) for o in outs_o]
+            gr = torch.autograd.grad(sum((o * gk).sum() for o, gk in zip(outs_o, gs)),
+                                     [tr[n] for n in names], allow_unused=True)
+        finally:
+            R.set_conv_precision("fp32")
+        grads_o = dict(zip(names, gr))
+        if net.store.bn_guard is None:
+            net.store.bn_guard = ops.BNZGuard(net.conv_layers())
+        net._packer = None
+        net._packer = ops.ConvPacker(net.conv_layers(), lambda: net.store.version)
+        net._packer.ensure()
+        net.store.zero_grad()
+        x4 = torch.cat([dev(imgs.float()), torch.zeros(imgs.shape[:3] + (1,), device="cuda")], -1)
+        outs = net.encoder.forward4(x4)
+        sum((o * dev(gk.float())).sum() for o, gk in zip(outs, gs)).backward()
+        torch.cuda.synchronize()
+        assert sorted(net.store.bn_guard.stored()) == want_stored, net.store.bn_guard.stored()
+        for o, oo in zip(outs, outs_o):
+            assert rel_l2(o, oo) < 1e-2
+        # measured (round 5): median 5.2e-3, worst 3.1e-2 on res4_1 -- the last block, whose
+        # input carries the bf16 rounding differences of the seven blocks before it (each
+        # block teacher-forced on its own: <= 1.5e-4, test_resnet_block_bn_guard[*-bf16])
+        tol = 5e-2
     bad, errs = [], []
-    for name, gr in net.store.grads().items():
+    grads = net.store.grads()
+    for name in names:
+        gr = grads[name]
         assert torch.isfinite(gr).all(), name
-        ref = grads_o[name] if grads_o[name] is not None else torch.zeros_like(gr.double().cpu())
-        e = rel_l2(gr, ref)
+        e = rel_l2(gr, grads_o[name])
         print("%-40s rel_l2 %.3e" % (name, e))
         if name.startswith("ResNet18"):
             errs.append(e)
-            if e >= (REL_TOL if precision == "fp32" else 0.25):
+            if e >= tol:
                 bad.append((name, e))
     med = float(np.median(errs))
     print("%s: median ResNet18 grad rel_l2 %.3e, worst %.3e" % (precision, med, max(errs)))
     assert not bad, bad
     if precision == "bf16":
-        assert med < 8e-2, med
+        assert med < 1e-2, med           # the module tests' bound
 
 
 def test_two_forwards_one_backward():
