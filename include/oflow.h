@@ -420,7 +420,8 @@ int of_timing_enable(int on);
  * keys 25 / 26 = the K-split cost models' slab-pass term (tenths of a chunk per slice and tile
  * round; default 5) of the fp32 halo-tile kernels and of the split implicit GEMMs;
  * key 27 = fp32 split 3x3 layers whose BN = 128 grid has fewer than this many workgroups run
- * BN = 64 tiles, two workgroups per CU (default 256; 0 = never);
+ * BN = 64 tiles, two workgroups per CU (default 1200, A/B-measured +1.3 % on the bench step;
+ * 0 = never);
  * key 28 = of_warp_bwd_det's window gather: mode A (a window of radius R around the
  * transposed position) when R = floor(max |flow|) + 2 <= this, else mode B (default 8; 0 =
  * no window, always the fixed-point path; 1 = always mode B). */

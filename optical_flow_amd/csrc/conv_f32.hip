@@ -4541,7 +4541,7 @@ bool ws_ok(const of_conv_desc* d, int mode) {
 // slice and tile round, of the halo-tile kernels (tile_args) and of conv_gemm_x3 (gemm_x3_plan).
 static int g_x3t_ep = 5;
 static int g_x3g_ep = 5;
-static int g_x3_small_bn = 256;
+static int g_x3_small_bn = 1200;
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false,
                    bool b16 = false, bool ws = false) {
   GemmArgs a = base_args(d);

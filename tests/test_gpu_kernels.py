@@ -797,8 +797,9 @@ def test_conv_stem_wgrad_x3(n, h, w):
     ("tall96", 8, 128, 256, 128, 96, {133, 136, 145}),    # 8 x 32 tiles, BN 96 fwd; BN 128 dgrad
     ("nb1", 8, 64, 128, 128, 128, {132, 140, 148}),       # single-buffered two-per-CU 4 x 32 form
     ("split", 2, 48, 64, 256, 256, {134, 142, 148}),      # 8-wave 4 x 32 form with a K split
+    ("split64", 2, 48, 64, 256, 256, {130, 138, 148}),    # small grid: BN 64 tiles (key 27)
     ("bn64", 8, 128, 256, 64, 64, {130, 138, 146}),       # BN 64 keeps 4 x 32 tiles on large grids
-], ids=["tall128", "tall96", "nb1", "split", "bn64"])
+], ids=["tall128", "tall96", "nb1", "split", "split64", "bn64"])
 def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
     """The grid-size-selected forms of the split kernels (taller output tiles, the
     single-buffered two-workgroups-per-CU form, K splits) against the fp32 MFMA kernels on
@@ -817,6 +818,20 @@ def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
     lib = _lib.lib()
     outs = {}
     lib.of_timing_read(0, None, None, None)          # drop records of earlier launches
+    if case == "split":                              # the BN = 128 split form (key 27 off)
+        assert lib.of_set_tuning(27, 0) == 0
+    try:
+        _large_grid_forms(ops, lib, case, n, h, w, cin, cout, kinds, x, wt, b, dy, act_src, outs)
+    finally:
+        lib.of_set_tuning(27, 1200)                  # (the default, conv_f32.hip)
+    for name, a3, a32 in zip(("y", "dx", "dw", "db"), outs[True], outs[False]):
+        assert rel_inf(a3, a32) < 2e-5, name
+        assert rel_l2(a3, a32) < 5e-6, name
+
+
+def _large_grid_forms(ops, lib, case, n, h, w, cin, cout, kinds, x, wt, b, dy, act_src, outs):
+    import ctypes as C
+    from optical_flow_amd._lib import ACT_LEAKY, call
     for split in (True, False):
         lib.of_timing_enable(1 if split else 0)
         layer = ops.ConvLayer(wt, b, stride=1, act=ACT_LEAKY, cin_p=cin, f32_split=split)
@@ -829,7 +844,7 @@ def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
         if split:
             # the fwd / dgrad workspace holds the K-split slabs: nonzero exactly when the plan
             # splits K, so this pins the split / unsplit forms each case is meant to cover
-            if case == "split":
+            if case in ("split", "split64"):
                 assert fws > 0 and dws > 0, (fws, dws)
             else:
                 assert fws == 0 and dws == 0, (fws, dws)
@@ -852,9 +867,6 @@ def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
             got = {k_arr[i] for i in range(lib.of_timing_read(cap, k_arr, f_arr, m_arr))}
             assert kinds <= got, (kinds, got)
         outs[split] = (y, dx, dw, db)
-    for name, a3, a32 in zip(("y", "dx", "dw", "db"), outs[True], outs[False]):
-        assert rel_inf(a3, a32) < 2e-5, name
-        assert rel_l2(a3, a32) < 5e-6, name
 
 
 @pytest.mark.parametrize("case,n,h,w,cin,cout,kinds", [
