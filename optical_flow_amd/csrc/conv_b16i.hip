@@ -44,6 +44,13 @@ __device__ __forceinline__ float4 bf16x4_to_f4(uint2 u) {
                      __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
 
+// B16I_RING (A/B switch, tools/ab_build.sh): 3 = a 3-deep B ring, two steps' B in flight
+// across raw barriers with counted vmcnt waits; measured 2 % SLOWER on the bf16 B=32 step
+// than the one-step-ahead form (2, default: 1665 vs 1699 pairs/s, gpurun_out/exp12), so the
+// main loop is not waiting on its B DMAs.
+#ifndef B16I_RING
+#define B16I_RING 2
+#endif
 template <int BN, int WAVES_M, int WAVES_N, int MODE, int TH, int TW, bool PERSIST = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmArgs a) {
   constexpr int KS = 3;
@@ -57,7 +64,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   static_assert(TW % 16 == 0 && WM % 16 == 0 && WN % 16 == 0 && SM >= 1 && SN >= 1, "tile");
   constexpr int BDI = KS * BN / 16, BDW = (BDI + NW - 1) / NW;   // B DMA instructions per step
   constexpr int H_U4 = HPD * 4, B_U4 = KS * BN * 4;               // uint4 per buffer
-  constexpr int LOOP_U4 = 2 * H_U4 + 2 * B_U4;
+  // RING: B buffers.  3 (when it fits and not PERSIST): two steps' B in flight, the step's
+  // end waits with a counted vmcnt (this step's DMAs stay in flight across a raw s_barrier);
+  // 2: one step ahead, vmcnt(0) + __syncthreads() per step.
+  constexpr int RING = B16I_RING == 3 && !PERSIST && (2 * H_U4 + 3 * B_U4) * 16 <= 160 * 1024 ? 3 : 2;
+  constexpr int LOOP_U4 = 2 * H_U4 + RING * B_U4;
   constexpr int EJ = NW * WM * 16 * SN * 4 + WAVES_M * BN * 4 <= LOOP_U4 * 16 ? SN
                      : NW * WM * 16 * 2 * 4 + WAVES_M * BN * 4 <= LOOP_U4 * 16 && SN % 2 == 0 ? 2
                                                                                      : 1;
@@ -89,7 +100,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   static_assert(!PERSIST || WAVES_M * BN * 4 <= B_U4 * 16, "column sums in a B buffer");
   __shared__ uint4 smem[SM_U4];
   uint4* Hs = smem;                        // [2][HPD pixels][4 octets]
-  uint4* Bs = smem + 2 * H_U4;             // [2][3 taps][BN rows][4 octets]
+  uint4* Bs = smem + 2 * H_U4;             // [RING][3 taps][BN rows][4 octets]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -172,6 +183,37 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
     }
   };
 
+  // this wave's DMA instructions per B step / per halo (the counted waits of RING 3)
+  const int nb_w = BDI % NW == 0 ? BDW : (BDI - wave + NW - 1) / NW;
+  const int nh_w = HDI % NW == 0 ? HDW : (HDI - wave + NW - 1) / NW;
+  static_assert(BDW + HDW <= 15, "vm_wait covers 0..15");
+  auto vm_wait = [](int n) {               // s_waitcnt vmcnt(n), n wave-uniform
+    switch (n) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+      case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+      case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+      case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+      case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+      case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    }
+  };
+  // a barrier that leaves this wave's LDS DMAs in flight (no vmcnt(0) as __syncthreads() has)
+  auto raw_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
   const int wm0 = (wave / WAVES_N) * WM;
   const int wn0 = (wave % WAVES_N) * WN;
   const int l16 = lane & 15, lq = lane >> 4;
@@ -193,6 +235,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
   if (wid == w_begin && G.c_end > G.c_begin) {
     dma_b(G.c_begin, 0, 0);
     dma_halo(G.c_begin, 0);
+    if (RING == 3 && (G.c_end - G.c_begin) * KS > 1)      // step 1's B (chunk c_begin, row 1)
+      dma_b(G.c_begin, 1, 1);
   }
   const int tile = G.tile, tile_m = G.tile_m, n0 = G.n0, b = G.b, oy0 = G.oy0, ox0 = G.ox0;
   // the fragment bases, opaque per tile: left loop-invariant, the addresses derived from them
@@ -209,16 +253,26 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
     for (int j = 0; j < SN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.f;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tile's first B and halo landed
-  __syncthreads();
+  if (RING == 3) {                                   // the tile's first B and halo landed
+    vm_wait(nsteps > 1 ? nb_w : 0);
+    raw_barrier();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   for (int q = 0; q < nsteps; ++q) {
     const int cc = q / KS, r = q - cc * KS;
     const int c = c_begin + cc;
-    const int hbuf = (cc + hoff) & 1, bbuf = (q + boff) & 1;
-    // prefetch: the next step's B, then (at a chunk's first row) the next chunk's halo; the
-    // buffers they overwrite were last read before the previous step's closing barrier
+    const int hbuf = (cc + hoff) & 1, bbuf = RING == 3 ? q % 3 : (q + boff) & 1;
+    // prefetch: the B RING - 1 steps ahead, then (at a chunk's first row) the next chunk's
+    // halo; the buffers they overwrite were last read before the previous step's barrier
     if (!(a.abl & 2)) {
-      if (q + 1 < nsteps) dma_b(r + 1 < KS ? c : c + 1, r + 1 < KS ? r + 1 : 0, bbuf ^ 1);
+      if (RING == 3) {
+        const int q2 = q + 2, c2 = c_begin + q2 / KS;
+        if (q2 < nsteps) dma_b(c2, q2 - (q2 / KS) * KS, q2 % 3);
+      } else if (q + 1 < nsteps) {
+        dma_b(r + 1 < KS ? c : c + 1, r + 1 < KS ? r + 1 : 0, bbuf ^ 1);
+      }
       if (r == 0 && c + 1 < c_end) dma_halo(c + 1, hbuf ^ 1);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -242,8 +296,18 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 1) void conv_halo_b16(GemmA
         for (int j = 0; j < SN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of the next step landed
-    __syncthreads();
+    if (RING == 3) {
+      // next step's B (issued a step ago) and, before a chunk's first step, its halo (issued
+      // two steps ago) landed; younger DMAs stay in flight: this step's B (q + 2) and the
+      // next chunk's halo while its chunk has rows to go
+      const bool b_in = !(a.abl & 2) && q + 2 < nsteps;
+      const bool h_in = !(a.abl & 2) && r < KS - 1 && c + 1 < c_end;
+      vm_wait((b_in ? nb_w : 0) + (h_in ? nh_w : 0));
+      raw_barrier();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's next-step DMAs landed
+      __syncthreads();
+    }
   }
   // PERSIST: the next tile's first B and halo go into the buffers the last step did not read
   // (every wave passed the last step's barrier); the epilogue works in the other halo buffer

@@ -4190,15 +4190,39 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 }
 
 // launch with the lane count by the number of slabs
+#ifndef WGR_ABL
+#define WGR_ABL 0      // 1: skip the reduce (timing ablation, WRONG results; tools/ab_build.sh)
+#endif
+static int g_wgr_lanes = 0;   // of_set_tuning key 29: wgrad_reduce lanes (launch_wgrad_reduce)
 void launch_wgrad_reduce(hipStream_t s, const float* ws, int splits, int64_t split_stride,
                          int taps, int kc, int cin, int cout, int ldc, float* dw, float* db,
                          int accum, const float* bn_g, const float* bn_v, float bn_eps) {
+  if (WGR_ABL) return;
   const int64_t items = ((int64_t)taps * cin + (db ? 1 : 0)) * cdiv(cout, 4);
-  if (splits >= 64)
+  // lanes: about 8 slab loads in flight per lane (key 29 = 1: the round-4 rule, 32 lanes from
+  // 64 slabs up -- two loads a lane at 64 slabs)
+  // (key 29 = 2: about 32 loads a lane, 3: about 64, 4: about 8)
+  const int per = g_wgr_lanes == 2 ? 32 : g_wgr_lanes == 3 ? 64 : g_wgr_lanes == 4 ? 8 : 16;
+  int lanes = 1;
+  while (lanes < 32 && lanes * per < splits) lanes *= 2;
+  if (g_wgr_lanes == 1) lanes = splits >= 64 ? 32 : 8;
+  if (lanes == 32)
     hipLaunchKernelGGL(wgrad_reduce_kernel<32>, dim3(cdiv(items, 8)), dim3(256), 0, s, ws, splits,
                        split_stride, taps, kc, cin, cout, ldc, dw, db, accum, bn_g, bn_v, bn_eps);
-  else
+  else if (lanes == 16)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(cdiv(items, 16)), dim3(256), 0, s, ws, splits,
+                       split_stride, taps, kc, cin, cout, ldc, dw, db, accum, bn_g, bn_v, bn_eps);
+  else if (lanes == 8)
     hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(cdiv(items, 32)), dim3(256), 0, s, ws, splits,
+                       split_stride, taps, kc, cin, cout, ldc, dw, db, accum, bn_g, bn_v, bn_eps);
+  else if (lanes == 4)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(cdiv(items, 64)), dim3(256), 0, s, ws, splits,
+                       split_stride, taps, kc, cin, cout, ldc, dw, db, accum, bn_g, bn_v, bn_eps);
+  else if (lanes == 2)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<2>, dim3(cdiv(items, 128)), dim3(256), 0, s, ws, splits,
+                       split_stride, taps, kc, cin, cout, ldc, dw, db, accum, bn_g, bn_v, bn_eps);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<1>, dim3(cdiv(items, 256)), dim3(256), 0, s, ws, splits,
                        split_stride, taps, kc, cin, cout, ldc, dw, db, accum, bn_g, bn_v, bn_eps);
 }
 
@@ -5000,6 +5024,7 @@ int of_set_tuning(int key, int value) {
   if (key == 26 && value >= 0 && value <= 1000) { g_x3g_ep = value; return OF_OK; }
   if (key == 27 && value >= 0 && value <= 100000) { g_x3_small_bn = value; return OF_OK; }
   if (key == 28 && value >= 0 && value <= 64) { g_det_rmax = value; return OF_OK; }
+  if (key == 29 && value >= 0 && value <= 4) { g_wgr_lanes = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

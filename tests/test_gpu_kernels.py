@@ -818,7 +818,7 @@ def test_conv_x3_large_grids(case, n, h, w, cin, cout, kinds):
     lib = _lib.lib()
     outs = {}
     lib.of_timing_read(0, None, None, None)          # drop records of earlier launches
-    if case == "split":                              # the BN = 128 split form (key 27 off)
+    if case in ("split", "nb1"):                     # the BN = 128 forms (key 27 off)
         assert lib.of_set_tuning(27, 0) == 0
     try:
         _large_grid_forms(ops, lib, case, n, h, w, cin, cout, kinds, x, wt, b, dy, act_src, outs)
