@@ -21,7 +21,10 @@ if [ -f "$IN/pmc_traffic.json" ]; then
 else
   python tools/pmc_traffic.py "$IN/fetch/bench_counter_collection.csv" "$IN/write/bench_counter_collection.csv" 384 512 8
 fi
-for f in conv_bench conv_bench_bf16 conv_bench_f32mfma flow_bench x3_accuracy b16i_bench; do
+[ -f "$IN/bench_atomic.log" ] && j "$IN/bench_atomic.log" > profiles/${R}_bench_atomic_warp.json
+[ -f "$IN/bench_repeat.log" ] && j "$IN/bench_repeat.log" > profiles/${R}_bench_repeat.json
+[ -f "$IN/timed_state_check.txt" ] && cp "$IN/timed_state_check.txt" profiles/${R}_timed_state_check.txt
+for f in conv_bench conv_bench_bf16 conv_bench_f32mfma flow_bench flow_bench_offset21 x3_accuracy b16i_bench; do
   [ -f "$IN/$f.txt" ] && grep -v amdgpu.ids "$IN/$f.txt" > profiles/${R}_$f.txt
 done
 true
