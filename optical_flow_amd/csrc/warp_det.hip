@@ -70,18 +70,27 @@ __device__ __forceinline__ float det_row16_sum(float v) {   // over the 16 lanes
 }
 
 
-// Workspace header (ints, zeroed per call): [0] max |dout| (float bits, fixed-point path),
-// [1] R, [2] V (own_radius), and DET_SLOTS counters of the hits mode B found, 256 B apart (spread atomics).
+// Workspace header (ints, zeroed per call): four banks of DET_SLOTS counters 256 B apart
+// (spread atomics: a grid's worth of atomics on one word serialises): the hits mode B found
+// (summed), and R, the roughness V and max |dout| (float bits) (each the max over its bank).
 constexpr int DET_SLOTS = 32;
-constexpr int DET_HDR_INTS = 64 * (1 + DET_SLOTS);
-__device__ __forceinline__ int* det_slot(int* hdr, int s) { return hdr + 64 * (1 + s); }
+constexpr int DET_FOUND = 1, DET_RAD = 33, DET_ROUGH = 65, DET_MAXD = 97;   // bank bases
+constexpr int DET_HDR_INTS = 64 * (DET_MAXD + DET_SLOTS);
+__device__ __forceinline__ int* det_slot(int* hdr, int s) { return hdr + 64 * (DET_FOUND + s); }
+__device__ __forceinline__ int det_bank_max(const int* __restrict__ hdr, int bank) {
+  int m = 0;
+#pragma unroll 8
+  for (int k = 0; k < DET_SLOTS; ++k) m = max(m, hdr[64 * (bank + k)]);
+  return m;
+}
+__device__ __forceinline__ int det_R(const int* __restrict__ hdr) { return det_bank_max(hdr, DET_RAD); }
 
 // The fixed-point path runs unless a window served: mode A (R <= rmax), or mode B with all
 // 4 n h w entries found.  rmax < 0: no window was launched.
 __device__ __forceinline__ bool own_fallback(const int* __restrict__ hdr, int rmax,
                                              int64_t npix) {
   if (rmax < 0) return true;
-  if (hdr[1] <= rmax) return false;
+  if (det_R(hdr) <= rmax) return false;
   int64_t s = 0;
 #pragma unroll 8
   for (int k = 0; k < DET_SLOTS; ++k) s += hdr[64 * (1 + k)];
@@ -92,7 +101,7 @@ __device__ __forceinline__ bool own_fallback(const int* __restrict__ hdr, int rm
 // finite or above DET_HUGE); the margin covers the rounding of (float)j + f near an integer
 // for coordinates below 2^16 (the host checks h, w).  And the roughness V = the largest
 // change of a flow component between horizontal / vertical neighbours (in 1/1024 px,
-// hdr[2]): mode B is tried only on fields smooth enough for its source estimate.
+// bank DET_ROUGH): mode B is tried only on fields smooth enough for its source estimate.
 constexpr float DET_HUGE = 1048576.f;
 __global__ __launch_bounds__(256) void own_radius(const float* __restrict__ flow, int64_t npix,
                                                   int h, int w, int* __restrict__ hdr) {
@@ -125,8 +134,9 @@ __global__ __launch_bounds__(256) void own_radius(const float* __restrict__ flow
   if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = r, red[1][threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicMax(hdr + 1, max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3])));
-    atomicMax(hdr + 2, max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3])));
+    const int sl = blockIdx.x % DET_SLOTS;
+    atomicMax(hdr + 64 * (DET_RAD + sl), max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3])));
+    atomicMax(hdr + 64 * (DET_ROUGH + sl), max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3])));
   }
 }
 
@@ -159,7 +169,8 @@ __device__ __forceinline__ void own_store(float* __restrict__ row, int k, const 
 // max |dout| <= 2^E and 4 n h w <= 2^L keeps every sum below 2^61 in magnitude; a
 // contribution is exact to 2^-S = max|dout| 2^(L - 61) (2^-40 of it at 192 x 256 x 8).
 //   fix_prep   : zeroes the accumulator, reduces max |dout| (float bits, atomicMax).
-//   fix_scatter: one 8 x 8 source tile and 64 channels per workgroup, one wave per pixel
+//   fix_scatter: 8 x 8 source tiles and 64 channels per workgroup step (grid-stride, two
+//                workgroups per CU: a cheap launch when the window served), one wave per pixel
 //                (lanes = channels); corners go through a 128-slot direct-mapped LDS cache of
 //                destination rows (int64 LDS adds), a slot collision straight to global int64
 //                atomics, and the cache leaves as one 512-B atomic wave-instruction per
@@ -183,12 +194,13 @@ __global__ __launch_bounds__(256) void fix_prep(const float* __restrict__ dout, 
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0)
-    atomicMax(reinterpret_cast<unsigned*>(hdr), max(max(red[0], red[1]), max(red[2], red[3])));
+    atomicMax(reinterpret_cast<unsigned*>(hdr + 64 * (DET_MAXD + blockIdx.x % DET_SLOTS)),
+              max(max(red[0], red[1]), max(red[2], red[3])));
 }
 
 // S from max |dout| (0 when it is not finite: fix_convert writes NaN then)
 __device__ __forceinline__ int fix_shift(const int* __restrict__ hdr, int lg4n) {
-  const float m = __uint_as_float((unsigned)hdr[0]);
+  const float m = __uint_as_float((unsigned)det_bank_max(hdr, DET_MAXD));
   if (!(m <= 3.0e38f)) return 0;
   int e = 0;
   frexpf(m, &e);                                       // m < 2^e
@@ -210,44 +222,48 @@ __global__ __launch_bounds__(64 * FX_WAVES) void fix_scatter(const float* __rest
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles_i = (h + FX_T - 1) / FX_T, tiles_j = (w + FX_T - 1) / FX_T;
   const int passes = (c + 63) / 64;
-  const int cc = (blockIdx.x % passes) * 64;
-  const int tile = blockIdx.x / passes;
-  const int b = tile / (tiles_i * tiles_j);
-  const int rem = tile - b * tiles_i * tiles_j;
-  const int i0 = (rem / tiles_j) * FX_T, j0 = (rem % tiles_j) * FX_T;
-  const int64_t img = (int64_t)b * h * w;
   const int S = fix_shift(hdr, lg4n);
-  const int e = cc + lane;
-  const bool eok = e < c;
-  for (int k = tid; k < FX_SLOTS * 64; k += 64 * FX_WAVES) data[k] = 0ull;
-  if (tid < FX_SLOTS) tag[tid] = -1;
-  __syncthreads();
-  for (int pr = wave; pr < FX_T * FX_T; pr += FX_WAVES) {
-    const int i = i0 + pr / FX_T, j = j0 + pr % FX_T;
-    if (i >= h || j >= w) continue;                    // wave-uniform
-    const int64_t p = img + (int64_t)i * w + j;
-    const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
-    const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
-    const float g = eok ? dout[p * c + e] : 0.f;
+  const int nwork = n * tiles_i * tiles_j * passes;
+  for (int wk_id = blockIdx.x; wk_id < nwork; wk_id += gridDim.x) {   // (tile, channel pass)
+    const int cc = (wk_id % passes) * 64;
+    const int tile = wk_id / passes;
+    const int b = tile / (tiles_i * tiles_j);
+    const int rem = tile - b * tiles_i * tiles_j;
+    const int i0 = (rem / tiles_j) * FX_T, j0 = (rem % tiles_j) * FX_T;
+    const int64_t img = (int64_t)b * h * w;
+    const int e = cc + lane;
+    const bool eok = e < c;
+    for (int k = tid; k < FX_SLOTS * 64; k += 64 * FX_WAVES) data[k] = 0ull;
+    if (tid < FX_SLOTS) tag[tid] = -1;
+    __syncthreads();
+    for (int pr = wave; pr < FX_T * FX_T; pr += FX_WAVES) {
+      const int i = i0 + pr / FX_T, j = j0 + pr % FX_T;
+      if (i >= h || j >= w) continue;                  // wave-uniform
+      const int64_t p = img + (int64_t)i * w + j;
+      const float2 f = *reinterpret_cast<const float2*>(flow + 2 * p);
+      const DetCorners t = det_corners(i, j, f.x, f.y, h, w, absolute != 0);
+      const float g = eok ? dout[p * c + e] : 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float wk = ((k & 2) ? 1.f - t.a : t.a) * ((k & 1) ? 1.f - t.b : t.b);
-      const unsigned long long v = (unsigned long long)llrint(ldexp((double)(wk * g), S));
-      const int d = t.y[k] * w + t.x[k];
-      const int sl = ((t.y[k] & 7) << 4) | (t.x[k] & 15);
-      int tg = 0;
-      if (lane == 0) tg = atomicCAS(&tag[sl], -1, d);
-      tg = __builtin_amdgcn_readfirstlane(tg);
-      if (tg == -1 || tg == d)
-        atomicAdd(&data[sl * 64 + lane], v);
-      else if (eok)
-        atomicAdd(acc + (img + d) * c + e, v);
+      for (int k = 0; k < 4; ++k) {
+        const float wk = ((k & 2) ? 1.f - t.a : t.a) * ((k & 1) ? 1.f - t.b : t.b);
+        const unsigned long long v = (unsigned long long)llrint(ldexp((double)(wk * g), S));
+        const int d = t.y[k] * w + t.x[k];
+        const int sl = ((t.y[k] & 7) << 4) | (t.x[k] & 15);
+        int tg = 0;
+        if (lane == 0) tg = atomicCAS(&tag[sl], -1, d);
+        tg = __builtin_amdgcn_readfirstlane(tg);
+        if (tg == -1 || tg == d)
+          atomicAdd(&data[sl * 64 + lane], v);
+        else if (eok)
+          atomicAdd(acc + (img + d) * c + e, v);
+      }
     }
-  }
-  __syncthreads();
-  for (int sl = wave; sl < FX_SLOTS; sl += FX_WAVES) {
-    const int d = tag[sl];
-    if (d >= 0 && eok) atomicAdd(acc + (img + d) * c + e, data[sl * 64 + lane]);
+    __syncthreads();
+    for (int sl = wave; sl < FX_SLOTS; sl += FX_WAVES) {
+      const int d = tag[sl];
+      if (d >= 0 && eok) atomicAdd(acc + (img + d) * c + e, data[sl * 64 + lane]);
+    }
+    __syncthreads();                                   // (the cache is reset for the next tile)
   }
 }
 
@@ -256,7 +272,7 @@ __global__ __launch_bounds__(256) void fix_convert(const long long* __restrict__
                                                    int rmax, int64_t npix, int lg4n,
                                                    float* __restrict__ dinp) {
   if (!own_fallback(hdr, rmax, npix)) return;
-  const float m = __uint_as_float((unsigned)hdr[0]);
+  const float m = __uint_as_float((unsigned)det_bank_max(hdr, DET_MAXD));
   const bool fin = m <= 3.0e38f;
   const int S = fix_shift(hdr, lg4n);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -355,6 +371,9 @@ __global__ __launch_bounds__(256) void det_dflow_vec(const float* __restrict__ d
 // NCB channel blocks of 16 quads (channels when !VEC) per lane; `found` += the hits.  Every
 // lane of the wave calls it (wave-wide shuffles); a group with an empty range idles.
 constexpr int WIN_CAP = 128;    // list entries per group; flushed above WIN_CAP - 64
+#ifndef WIN_DFLOW_PRE
+#define WIN_DFLOW_PRE 0  // 1: own_window issues d(flow)'s loads before the window's (+28 VGPRs)
+#endif
 constexpr int WIN_PILE = 16;    // mode A: |w - h| above this, the pile row / column
 constexpr int WIN_RB = 3;       // mode B window radius around the estimated source
 constexpr int WIN_VMAX = 512;   // mode B only for V <= 0.5 px (or rmax == 1: always, tests)
@@ -562,9 +581,9 @@ __global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout
   const int64_t hw = (int64_t)h * w;
   const int lane = threadIdx.x & 63, q = lane & 15, src0 = lane & 48, grp = threadIdx.x >> 4;
   const int nq = VEC ? c >> 2 : c;
-  const int R = hdr[1];
+  const int R = det_R(hdr);
   const bool mode_a = R <= rmax;                       // uniform over the grid
-  const bool mode_b = !mode_a && (hdr[2] <= WIN_VMAX || rmax == 1);
+  const bool mode_b = !mode_a && (det_bank_max(hdr, DET_ROUGH) <= WIN_VMAX || rmax == 1);
   const int npb = h >= 2 && w >= 2 ? 2 * w + 2 * (h - 2) : 0;
   const int npile = n * npb;
   int found = 0;
@@ -615,6 +634,7 @@ __global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout
   const int64_t d = ((blockIdx.x - npile) * (int64_t)blockDim.x + threadIdx.x) >> 4;
   const bool live = d < npix;
   const int64_t dd = live ? d : npix - 1;
+#if WIN_DFLOW_PRE
   // d(flow) of pixel d: its loads first (c <= 64 NCB, one quad per channel block)
   constexpr int DFQ = NCB;
   const bool pre = VEC && c <= 64 * DFQ;
@@ -633,6 +653,9 @@ __global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout
                       : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+#else
+  constexpr bool pre = false;
+#endif
   if (mode_a || mode_b) {
     const int64_t img = dd / hw * hw;
     const int rem = (int)(dd - img);
@@ -661,13 +684,16 @@ __global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout
     for (int o = 16; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
     if (lane == 0 && s) atomicAdd(det_slot(hdr, (blockIdx.x * 4 + (threadIdx.x >> 6)) % DET_SLOTS), s);
   }
+#if WIN_DFLOW_PRE
   if (pre) {
     float gx = 0.f, gy = 0.f;
 #pragma unroll
     for (int b = 0; b < DFQ; ++b)
       if (4 * q + 64 * b < c) dflow_quad(gx, gy, T.a, T.bq, pg[b], pP[0][b], pP[1][b], pP[2][b], pP[3][b]);
     dflow_store(gx, gy, d, live, q, dflow, dfa, ldfa);
-  } else if (VEC) {
+  } else
+#endif
+  if (VEC) {
     det_dflow_quads(dout, inp, npix, h, w, c, flow, 0, dflow, dfa, ldfa, d, q);
   }
 }
@@ -786,7 +812,8 @@ int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, in
   hipLaunchKernelGGL(fix_prep, dim3(gs), dim3(256), 0, s, dout, nel,
                      reinterpret_cast<int4*>(acc), (nel + 1) / 2, hdr, rmax, npix);
   const int64_t tiles = (int64_t)n * cdiv(h, FX_T) * cdiv(w, FX_T) * ((c + 63) / 64);
-  hipLaunchKernelGGL(fix_scatter, dim3((unsigned)tiles), dim3(64 * FX_WAVES), 0, s, dout, flow,
+  const unsigned gfx = (unsigned)std::min<int64_t>(tiles, 2 * device_cus());   // (grid-stride)
+  hipLaunchKernelGGL(fix_scatter, dim3(gfx), dim3(64 * FX_WAVES), 0, s, dout, flow,
                      n, h, w, c, absolute, hdr, rmax, lg4n, acc);
   hipLaunchKernelGGL(fix_convert, dim3(gs), dim3(256), 0, s,
                      reinterpret_cast<const long long*>(acc), nel, hdr, rmax, npix, lg4n, dinp);

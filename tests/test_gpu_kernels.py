@@ -1621,7 +1621,9 @@ def test_warp_bwd_deterministic(shape, flow_scale, offset, absolute):
                                                      ((1, 48, 48, 128), 0.25, 0.0),
                                                      ((2, 24, 24, 12), 0.2, 0.0),
                                                      ((1, 40, 40, 64), 0.2, 0.6),
-                                                     ((2, 20, 60, 64), 0.2, 0.0)])
+                                                     ((2, 20, 60, 64), 0.2, 0.0),
+                                                     ((1, 40, 40, 64), 0.1, -6.0),
+                                                     ((2, 36, 44, 128), 0.2, 0.0)])
 def test_warp_bwd_det_paths(shape, flow_scale, offset):
     """of_warp_bwd_det's three ways to d(features) on one input: window mode A (of_set_tuning
     key 28 = 8, the default for these flows), mode B (key 28 = 1: centred windows, border pixels
@@ -1697,10 +1699,10 @@ def test_warp_bwd_det_modes(shape, scale, offset, mode):
         call("of_warp_bwd_det", P(dg), P(df2), n, h, w, c, P(dfl_in), 0, P(dinp), P(dfl),
              None, 0, P(ws), wsb, None)
         torch.cuda.synchronize()
-        hdr = ws[hoff // 4: hoff // 4 + 64 * 33].cpu()
+        hdr = ws[hoff // 4: hoff // 4 + 64 * 129].cpu()
         outs.append((dinp.clone(), dfl.clone(), hdr))
     hdr = outs[0][2]
-    rr = int(hdr[1])
+    rr = max(int(hdr[64 * (33 + k)]) for k in range(32))
     found = int(sum(int(hdr[64 * (1 + k)]) for k in range(32)))
     if mode == "A":
         assert rr <= 8 and found == 0, (rr, found)
