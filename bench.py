@@ -166,11 +166,11 @@ def kernel_symbol(kind):
         return "void oflow::(anonymous namespace)::conv_wgrad_b16i<%s>(oflow::GemmArgs)" % WGRAD_B16I[cfg]
     if fam == "stem_x3":
         if mode == 2:
-            return "void oflow::conv_wgrad_stem_x3<3>(oflow::GemmArgs)"
+            return "void oflow::conv_wgrad_stem_x3<3, false>(oflow::GemmArgs)"
         return "void oflow::conv_stem_x3<32, 3>(oflow::GemmArgs)"   # of_set_tuning key 8 default
     if fam == "stem_b16":
         if mode == 2:
-            return "void oflow::conv_wgrad_stem_x3<1>(oflow::GemmArgs)"
+            return "void oflow::conv_wgrad_stem_x3<1, false>(oflow::GemmArgs)"
         return "void oflow::conv_stem_x3<32, 1>(oflow::GemmArgs)"
     if cfg == 7 and fam == "f32":
         return NARROW_SYMBOLS[mode]
