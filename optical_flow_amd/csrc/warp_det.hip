@@ -175,7 +175,8 @@ __device__ __forceinline__ void own_store(float* __restrict__ row, int k, const 
 //                destination rows (int64 LDS adds), a slot collision straight to global int64
 //                atomics, and the cache leaves as one 512-B atomic wave-instruction per
 //                destination: a tile's samples piled onto the border add once per destination.
-//   fix_convert: dinp = acc * 2^-S (NaN everywhere if dout holds a non-finite value).
+//   fix_convert: dinp = acc * 2^-S (NaN everywhere if dout holds a non-finite value or a
+//                contribution is not finite: a NaN flow -- the atomic form's NaN rows, louder).
 constexpr int FX_T = 8, FX_SLOTS = 128, FX_WAVES = 8;
 
 __global__ __launch_bounds__(256) void fix_prep(const float* __restrict__ dout, int64_t nel,
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(64 * FX_WAVES) void fix_scatter(const float* __rest
                                                              const float* __restrict__ flow,
                                                              int n, int h, int w, int c,
                                                              int absolute,
-                                                             const int* __restrict__ hdr,
+                                                             int* __restrict__ hdr,
                                                              int rmax, int lg4n,
                                                              unsigned long long* __restrict__ acc) {
   const int64_t npix = (int64_t)n * h * w;
@@ -246,7 +247,10 @@ __global__ __launch_bounds__(64 * FX_WAVES) void fix_scatter(const float* __rest
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float wk = ((k & 2) ? 1.f - t.a : t.a) * ((k & 1) ? 1.f - t.b : t.b);
-        const unsigned long long v = (unsigned long long)llrint(ldexp((double)(wk * g), S));
+        const float ct = wk * g;
+        if (!(fabsf(ct) <= 3.0e38f))                   // a non-finite term (NaN / inf flow):
+          atomicMax(hdr + 64 * DET_MAXD, 0x7fc00000);  // fix_convert writes NaN, loudly
+        const unsigned long long v = (unsigned long long)llrint(ldexp((double)ct, S));
         const int d = t.y[k] * w + t.x[k];
         const int sl = ((t.y[k] & 7) << 4) | (t.x[k] & 15);
         int tg = 0;

@@ -1713,3 +1713,27 @@ def test_warp_bwd_det_modes(shape, scale, offset, mode):
     assert rel_inf(outs[0][0], a.grad) < REL_TOL
     assert rel_inf(outs[0][1], fo.grad) < REL_TOL
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_warp_bwd_det_nonfinite_flow():
+    """A NaN flow pixel: the float-atomic form writes NaN into the rows its clamped sample
+    lands on; the deterministic form (no window covers a non-finite field: fixed point) must
+    not return a finite d(features) either -- it writes NaN throughout -- and stays
+    reproducible; d(flow) is NaN at that pixel in both."""
+    ops = _ops()
+    shape = (1, 20, 24, 16)
+    n, h, w, c = shape
+    f2 = dev(rng_tensor(shape, 71))
+    fl = rng_tensor((n, h, w, 2), 72, scale=0.5)
+    fl[0, 5, 7, 0] = float("nan")
+    g = dev(rng_tensor(shape, 73))
+    res = {}
+    for det in (True, False):
+        with ops.deterministic(det):
+            ad, fd = f2.clone().requires_grad_(True), dev(fl).requires_grad_(True)
+            (ops.warp(ad, fd) * g).sum().backward()
+        torch.cuda.synchronize()
+        res[det] = (ad.grad.clone(), fd.grad.clone())
+    assert not torch.isfinite(res[False][0]).all()       # (the atomic form's NaN rows)
+    assert not torch.isfinite(res[True][0]).all()
+    assert torch.isnan(res[True][1][0, 5, 7]).any() and torch.isnan(res[False][1][0, 5, 7]).any()
