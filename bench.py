@@ -185,7 +185,8 @@ def kernel_symbol(kind):
         np_ = 3 if fam == "gemm_x3" else 1
         if mode == 2:
             return "void oflow::conv_wgrad_x3<%s, %d>(oflow::GemmArgs)" % (GX3_WG[cfg], np_)
-        return "void oflow::conv_gemm_x3<%s, %d, %d>(oflow::GemmArgs)" % (GX3[cfg], mode, np_)
+        # (RING = 2: the DMA ring of of_set_tuning key 30 = 2, the default)
+        return "void oflow::conv_gemm_x3<%s, %d, %d, 2>(oflow::GemmArgs)" % (GX3[cfg], mode, np_)
     if fam in ("tile_bf16", "tile_f32", "tile_x3") and mode == 2:
         # the bf16 form prints its defaulted fragment-prefetch flag too (PF = 1, key 17)
         return "void oflow::conv_wgrad_%s<%s%s>(oflow::GemmArgs)" % (

@@ -424,7 +424,12 @@ int of_timing_enable(int on);
  * 0 = never);
  * key 28 = of_warp_bwd_det's window gather: mode A (a window of radius R around the
  * transposed position) when R = floor(max |flow|) + 2 <= this, else mode B (default 8; 0 =
- * no window, always the fixed-point path; 1 = always mode B). */
+ * no window, always the fixed-point path; 1 = always mode B);
+ * key 29 = wgrad_reduce lane rule (0 = default, 1-4 = the measured alternatives);
+ * key 30 = the split implicit GEMMs (conv_gemm_x3: stride-2 and 1x1 layers) on an LDS-DMA ring
+ * with both operands DMA'd: 3 slots, one chunk in flight across each barrier (1), or 2 slots,
+ * two workgroups per CU where the LDS allows (2, default); or register-staged A with one chunk
+ * in flight (0); bitwise the same results. */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

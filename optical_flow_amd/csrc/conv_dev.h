@@ -374,6 +374,19 @@ __device__ __forceinline__ void dma16_to_lds(rsrc_t r, uint4* dst, uint32_t voff
                                            voff, soff, 0, 0);
 }
 
+// LDS byte address of a __shared__ pointer, and a 16-byte LDS read in inline asm: no memory
+// operand, so hipcc does not wait for in-flight LDS DMAs (vmcnt) before it -- the caller
+// orders it (counted vmcnt + barrier before, s_waitcnt lgkmcnt(0) + sched_barrier(0) after).
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
 // 4 fp32 -> 4 bf16 (RNE, v_cvt_pk_bf16_f32), element 0 in the low half of .x
 __device__ __forceinline__ uint2 pack_bf16x4(const float4& v) {
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

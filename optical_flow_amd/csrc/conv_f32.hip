@@ -1759,8 +1759,9 @@ bool stem_x3_ok(const of_conv_desc* d) {
 // of each operand (A rounded to bf16 as conv_gemm_bf16 rounds it, B the packed bf16 image,
 // which has the x3 hi plane's layout), one MFMA per fragment pair, and with a third of the
 // LDS two workgroups per CU.
-template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP = 3>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NP == 1 ? 2 : 1) void conv_gemm_x3(GemmArgs a) {
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, int NP = 3, int RING = 3>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NP == 1 || RING == 2 ? 2 : 1)
+void conv_gemm_x3(GemmArgs a) {
   static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "x3 GEMM: fwd / dgrad");
   static_assert(NP == 3 || NP == 1, "three split planes (fp32) or one (bf16)");
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = NT / 64;
@@ -1772,7 +1773,22 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NP == 1 ? 2 : 1) void conv_
   constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
   constexpr int BDI = NP * BN / 16, BDW = (BDI + NW - 1) / NW;   // B DMA wave-instructions
   constexpr int OP_U4 = 2 * (A_U4 + B_U4), EP_U4 = NW * WM * WN * 4 / 16;
-  __shared__ uint4 smem[OP_U4 > EP_U4 ? OP_U4 : EP_U4];   // operands, then epilogue images
+  // DA (RING = slots 2 / 3, of_set_tuning key 30; where the LDS allows): A comes by LDS DMA
+  // too, as raw fp32 rows in [quad][row] images split (fp32) or rounded (bf16) while its
+  // fragments are read, and (A, B) chunks cycle through an NS-slot ring with NS - 2 chunks in
+  // flight across each barrier (counted vmcnt, raw s_barrier); NS = 2 leaves room for two
+  // workgroups per CU.  (A register-staged ring cannot go deeper than one chunk: hipcc drains
+  // every LDS DMA (vmcnt(0)) at the first use of an ordinary load's registers.)  Measured: the
+  // 3-slot ring alone is even with the register form -- the loop was not waiting on its loads
+  // (SQ: 37 % of wave-cycles parked at waits / barriers, 32 % issue-stalled, MFMA ~25 % busy,
+  // eight barrier-locked waves per CU) -- and the 2-slot ring's second workgroup per CU is
+  // what gains (-10..-15 % on the stride-2 layers).
+  constexpr int AF_U4 = BM * 8, SLOT_U4 = AF_U4 + B_U4;
+  constexpr int NS = RING == 2 && 2 * 2 * SLOT_U4 * 16 <= 160 * 1024 ? 2
+                   : RING && 3 * SLOT_U4 * 16 * (NP == 1 ? 2 : 1) <= 160 * 1024 ? 3 : 0;
+  constexpr bool DA = NS > 0;
+  constexpr int OPS_U4 = DA ? NS * SLOT_U4 : OP_U4;
+  __shared__ uint4 smem[OPS_U4 > EP_U4 ? OPS_U4 : EP_U4];   // operands, then epilogue images
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1941,6 +1957,116 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NP == 1 ? 2 : 1) void conv_
   const int l16 = lane & 15, lq = lane >> 4;
   const int frag = l16 * 4 + (lq ^ x3_sw(l16));   // rows 16-aligned + l16: swizzle of l16
   int b_k = k_begin;
+  if constexpr (DA) {
+    // this wave's DMA wave-instructions per chunk: 2 A_SL (A) + its share of B's
+    const int nw = 2 * A_SL + (BDI % NW == 0 ? BDW : (BDI - wave + NW - 1) / NW);
+    static_assert(2 * A_SL + BDW <= 7, "vm_wait covers 0..7");
+    auto vm_wait = [](int n) {               // s_waitcnt vmcnt(n), n wave-uniform
+      switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+      }
+    };
+    // chunk (walkers, bk) -> ring slot: lane L of the (octet, half, row group) instruction
+    // brings row 64 (rgrp + RG i) + L's channel quad 2 oct + h (zeros where the tap is outside
+    // the image or the row past M), so quad q of the chunk lands as BM contiguous rows
+    auto issue = [&](int slot, int bk) {
+      uint4* S = smem + slot * SLOT_U4;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool tap_ok = ks_t[h] < G.ntaps;
+        const int koff = ks_tr[h] * tap_step + sgn * ks_ts[h] * a.lda * 4 + ks_ci[h] * 4;
+#pragma unroll
+        for (int i = 0; i < A_SL; ++i) {
+          const bool ok = tap_ok && ((a_msk[i] >> ks_t[h]) & 1);
+          dma16_to_lds(ra_src, S + (2 * oct + h) * BM + 64 * (rgrp + RG * i),
+                       ok ? (uint32_t)(a_off[i] + koff) : kOOB, 0);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < BDW; ++k)
+        if (BDI % NW == 0 || bd_lds[k] >= 0)
+          dma16_to_lds(rb_src, S + AF_U4 + bd_lds[k], bd_off[k], bk * 2);
+    };
+    // per-lane LDS byte addresses of the fragment reads within a slot: A quad 2 lq of row
+    // wm0 + l16 (+ BM rows for quad 2 lq + 1, + 16 rows per fragment), B as frag above
+    const uint32_t smem_lds = lds_off(smem);
+    const uint32_t a_rd = (uint32_t)(((2 * lq) * BM + wm0 + l16) * 16);
+    const uint32_t b_rd = (uint32_t)((AF_U4 + wn0 * 4 + frag) * 16);
+    if (nchunks > 0) issue(0, b_k);
+    if (NS == 3 && nchunks > 1) {
+      advance_a();
+      b_k += BKH;
+      issue(1, b_k);
+    }
+    for (int c = 0; c < nchunks; ++c) {
+      vm_wait(NS == 3 && c + 1 < nchunks ? nw : 0);   // this wave's part of chunk c landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();          // every wave's part landed; slot (c + NS - 1) % NS,
+      asm volatile("" ::: "memory");         // read in step c - 1, is free
+      if (c + NS - 1 < nchunks) {
+        advance_a();
+        b_k += BKH;
+        issue((c + NS - 1) % NS, b_k);
+      }
+      // The fragment reads are inline asm: an LDS load with a memory operand makes hipcc wait
+      // vmcnt(0) -- the ring's in-flight DMAs -- before it.  One lgkmcnt(0) retires them.
+      const uint32_t sb = smem_lds + (uint32_t)((c % NS) * SLOT_U4 * 16);
+      uint4 ar[SM][2], br[NP][SN];
+#pragma unroll
+      for (int i = 0; i < SM; ++i) {
+        ar[i][0] = ds_read16(sb + a_rd + 256 * i);
+        ar[i][1] = ds_read16(sb + a_rd + 256 * i + BM * 16);
+      }
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int j = 0; j < SN; ++j) br[p][j] = ds_read16(sb + b_rd + p * BN * 64 + j * 1024);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 av[NP][SM], bv[NP][SN];
+#pragma unroll
+      for (int i = 0; i < SM; ++i) {
+        const float4 x0 = __builtin_bit_cast(float4, ar[i][0]);
+        const float4 x1 = __builtin_bit_cast(float4, ar[i][1]);
+        if constexpr (NP == 1) {
+          av[0][i] = __builtin_bit_cast(bf16x8, pack_bf16x8(x0, x1));
+        } else {
+          uint2 h0, m0v, l0, h1, m1, l1;
+          split3x4(x0, h0, m0v, l0);
+          split3x4(x1, h1, m1, l1);
+          av[0][i] = __builtin_bit_cast(bf16x8, make_uint4(h0.x, h0.y, h1.x, h1.y));
+          av[NP / 2][i] = __builtin_bit_cast(bf16x8, make_uint4(m0v.x, m0v.y, m1.x, m1.y));
+          av[NP - 1][i] = __builtin_bit_cast(bf16x8, make_uint4(l0.x, l0.y, l1.x, l1.y));
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int j = 0; j < SN; ++j) bv[p][j] = __builtin_bit_cast(bf16x8, br[p][j]);
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int j = 0; j < SN; ++j) {
+          f32x4 x = acc[i][j];
+          if (NP == 3) {
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP - 1][i], bv[0][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP - 1][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[NP / 2][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[0][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP / 2][j], x, 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+        }
+    }
+    __syncthreads();              // every wave's last ring reads done: LDS -> epilogue images
+  } else {
   if (nchunks > 0) {
     load_a();
     dma_b(0, b_k);
@@ -1986,6 +2112,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, NP == 1 ? 2 : 1) void conv_
     if (more) store_a(buf ^ 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own B DMA landed
     __syncthreads();
+  }
   }
 
   // ---------------- epilogue ----------------------------------------------------------------
@@ -4760,14 +4887,29 @@ void gemm_x3_plan(GemmArgs& a) {
   a.splits = (int)cdiv(kmax, a.k_per_split);
 }
 
+// of_set_tuning key 30: conv_gemm_x3 on a DMA ring of 3 slots (1: one chunk in flight across
+// each barrier, one workgroup per CU) or of 2 slots (2, default: two workgroups per CU where
+// the LDS allows -- the fp32 128 x 128 form; the 256 x 64 form keeps 3 slots), or on the
+// round-2..4 register-staged A with one chunk in flight (0).  Bitwise the same results.
+// Measured (tools/conv_bench.py, one box): enc.l3.c0 fwd 81 / 84 / 71 us for 0 / 1 / 2,
+// enc.l4.c0 fwd 69 / 72 / 60, dgrad 77 / 79 / 69; the bench step even (626-628 pairs/s).
+static int g_gx3_ring = 2;
 // (NP = 1, the bf16 form: timing kinds 240 + mode * 8 + cfg)
 template <int MODE, int NP = 3>
 int launch_gemm_x3(const GemmArgs& a, hipStream_t s, double flops) {
   const int cfg = a.N > 64 ? 0 : 1;
   dim3 grid(a.tiles_total * a.splits), block(512);
   if (timing_on()) timing_begin(s);
-  if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3<128, 128, 4, 2, MODE, NP>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((conv_gemm_x3<256, 64, 8, 1, MODE, NP>), grid, block, 0, s, a);
+  if (g_gx3_ring == 1) {
+    if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3<128, 128, 4, 2, MODE, NP, 3>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_gemm_x3<256, 64, 8, 1, MODE, NP, 3>), grid, block, 0, s, a);
+  } else if (g_gx3_ring == 2) {
+    if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3<128, 128, 4, 2, MODE, NP, 2>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_gemm_x3<256, 64, 8, 1, MODE, NP, 2>), grid, block, 0, s, a);
+  } else {
+    if (cfg == 0) hipLaunchKernelGGL((conv_gemm_x3<128, 128, 4, 2, MODE, NP, 0>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_gemm_x3<256, 64, 8, 1, MODE, NP, 0>), grid, block, 0, s, a);
+  }
   if (timing_on()) timing_end(s, (NP == 1 ? 240 : 160) + MODE * 8 + cfg, flops);
   int st = check_launch("conv_gemm_x3");
   if (st || a.splits == 1) return st;
@@ -5025,6 +5167,7 @@ int of_set_tuning(int key, int value) {
   if (key == 27 && value >= 0 && value <= 100000) { g_x3_small_bn = value; return OF_OK; }
   if (key == 28 && value >= 0 && value <= 64) { g_det_rmax = value; return OF_OK; }
   if (key == 29 && value >= 0 && value <= 4) { g_wgr_lanes = value; return OF_OK; }
+  if (key == 30 && value >= 0 && value <= 2) { g_gx3_ring = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

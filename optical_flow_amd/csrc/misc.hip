@@ -450,10 +450,17 @@ __global__ __launch_bounds__(256) void maxpool_bn_act_bwd_partial(
 }
 
 // Sum the partial rows of bn_act_bwd_partial / maxpool_bn_act_bwd_partial in a fixed order:
-// workgroup = 16 channel quads x 64 row groups (1024 threads, grid.x = cdiv(c / 4, 16)); each
-// thread sums its rows with 8 float4 loads in flight, then a fixed tree over the 64 groups.
+// workgroup = BNF_Q channel quads x 64 row groups (grid.x = cdiv(c / 4, BNF_Q)); each thread
+// sums its rows with 8 float4 loads in flight, then a fixed tree over the 64 groups.
 // (A 16-row-group form with one scalar load in flight per step took 15 us per call: latency.)
-constexpr int BNF_Q = 16, BNF_G = 64;
+// BNF_Q = 1: one wave per channel quad.  The round-2..4 form (BNF_Q = 16, one 1024-thread
+// workgroup for c = 64) ran these side-stream reductions at 8 us alone but 70-80 us beside a
+// main-stream convolution, its 16 waves waiting for a CU with that much room; a 64-thread
+// workgroup fits in any gap.  Same per-channel order, so the results are bitwise unchanged.
+#ifndef BNF_QW
+#define BNF_QW 1
+#endif
+constexpr int BNF_Q = BNF_QW, BNF_G = 64;
 __global__ __launch_bounds__(BNF_Q * BNF_G) void bn_act_bwd_final(const float* __restrict__ part,
                                                                   int nblk, int c,
                                                                   const float* __restrict__ gamma,

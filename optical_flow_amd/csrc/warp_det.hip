@@ -443,6 +443,11 @@ __device__ __forceinline__ void win_accumulate(float4 (&acc)[NCB], int& found, c
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     cnt = 0;
   };
+  // this lane's candidate k = 16 t + q as (row di, column dj) of the window, stepped by 16
+  // candidates per batch without a division (one per destination: 16 = s_i nj + s_j)
+  const int nj = max(D.nj, 1);
+  int di = (D.k0 + q) / nj, dj = (D.k0 + q) - di * nj;
+  const int s_i = 16 / nj, s_j = 16 - s_i * nj;
   for (int t0 = 0; t0 < pmax; t0 += 4) {
     float2 f[4];
     int ci[4], cj[4];
@@ -450,20 +455,16 @@ __device__ __forceinline__ void win_accumulate(float4 (&acc)[NCB], int& found, c
     for (int u = 0; u < 4; ++u) {
       const int k = (t0 + u) * 16 + q;
       const bool in = k < span;
-      const int kk = D.k0 + k;
-      const int di = in ? kk / D.nj : 0;
       ci[u] = in ? D.ilo + di : -1;
-      cj[u] = D.jlo + (kk - di * D.nj);
+      cj[u] = D.jlo + dj;
       f[u] = make_float2(0.f, 0.f);
       if (in) f[u] = *reinterpret_cast<const float2*>(fimg + 2 * ((int64_t)ci[u] * w + cj[u]));
+      di += s_i, dj += s_j;
+      if (dj >= nj) dj -= nj, ++di;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (t0 + u >= pmax) break;
-      int cm = cnt;
-#pragma unroll
-      for (int o = 16; o < 64; o <<= 1) cm = max(cm, __shfl_xor(cm, o, 64));
-      if (cm > WIN_CAP - 64) flush();
       uint32_t m = 0;
       float ca = 0.f, cbw = 0.f;
       if (ci[u] >= 0) {
@@ -473,6 +474,12 @@ __device__ __forceinline__ void win_accumulate(float4 (&acc)[NCB], int& found, c
         ca = tc.a;
         cbw = tc.b;
       }
+      // most batches hit nothing anywhere in the wave: skip the list update (wave-uniform)
+      if (__ballot(m != 0) == 0) continue;
+      int cm = cnt;
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) cm = max(cm, __shfl_xor(cm, o, 64));
+      if (cm > WIN_CAP - 64) flush();
       const int pc = __builtin_popcount(m);
       int incl = pc;                                   // inclusive prefix over the 16 lanes
 #pragma unroll

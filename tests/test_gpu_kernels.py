@@ -276,6 +276,77 @@ def test_conv_gemm_x3_accuracy(n, h, w, cin, cout, k, s, monkeypatch):
         assert e3 < 5e-6, errs[True]
 
 
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("n,h,w,cin,cout,k,s", [(4, 48, 64, 64, 128, 3, 2),   # res3_0 conv_a
+                                               (4, 24, 32, 128, 256, 3, 2),  # res4_0 conv_a
+                                               (4, 48, 64, 64, 128, 1, 2),   # projection
+                                               (3, 37, 45, 20, 40, 3, 2),    # odd, 64-col tiles
+                                               (1, 6, 10, 8, 16, 3, 2),      # 1-3 chunks
+                                               (2, 64, 96, 4, 64, 7, 2)])    # stem shape
+def test_conv_gemm_x3_ring_bitwise(n, h, w, cin, cout, k, s, prec, monkeypatch):
+    """conv_gemm_x3 on the LDS-DMA rings (of_set_tuning key 30 = 1: 3 slots, one chunk in flight
+    across each barrier; key 30 = 2, the default: 2 slots, two workgroups per CU; A and B by
+    DMA, A split / rounded as it is read) equals the register-staged form (key 30 = 0) bit for bit -- forward and the stride-2 input gradient's
+    phase groups, split-K and unsplit grids, rings of 1-3 chunks -- for the fp32 split (three
+    planes) and the bf16 (one plane) kernels; the timing kinds say the GEMMs ran."""
+    import ctypes as C
+    if k == 7 and prec == "bf16":
+        pytest.skip("the bf16 stem shape runs conv_gemm_bf16 (conv_gemm_x3<..., 1> takes no stem)")
+    ops = _ops()
+    monkeypatch.setattr(ops, "X3_GEMM_MIN_CIN", 0)
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_NONE, call
+    lib = _lib.lib()
+    x = rng_tensor((n, h, w, cin), 111)
+    wt = rng_tensor((k, k, cin, cout), 112, scale=(2.0 / (k * k * cin)) ** 0.5)
+    kw = dict(precision="bf16") if prec == "bf16" else dict(f32_split=True)
+    layer = ops.ConvLayer(dev(wt), dev(torch.zeros(cout)), stride=s, act=ACT_NONE, cin_p=cin,
+                          **kw)
+    d = layer.desc(n, h, w)
+    dy = rng_tensor((n, d.ho, d.wo, cout), 113)
+    wf, wd = layer.packed(d)
+    P, st = ops._ptr, ops._stream()
+    xd, dyd = dev(x), dev(dy)
+    res = {}
+    try:
+        assert lib.of_set_tuning(8, 0) == 0           # the fp32 stem shape on the GEMM
+        assert lib.of_set_tuning(16, 7) == 0          # bf16 forward on conv_gemm_x3<..., 1> too
+        for ring in (1, 2, 0):
+            assert lib.of_set_tuning(30, ring) == 0
+            fent, fws = layer.fwd_entry(d)
+            dent, dws = layer.dgrad_entry(d)
+            ws = torch.empty(max(fws, dws) // 4 + 4, device="cuda")
+            y = torch.full((n, d.ho, d.wo, cout), float("nan"), device="cuda")
+            dx = torch.full((n, h, w, cin), float("nan"), device="cuda")
+            lib.of_timing_enable(1)
+            call(fent, C.byref(d), P(xd), cin, P(wf), P(layer.bias), None, None, None, None,
+                 1e-3, None, 0, ACT_NONE, 0.0, None, 0, P(y), cout, P(ws), fws, st)
+            if k < 7:
+                call(dent, C.byref(d), P(dyd), cout, P(wd), None, 0, ACT_NONE, 0.0, P(dx), cin,
+                     P(ws), dws, st)
+            torch.cuda.synchronize()
+            kk = (C.c_int * 64)()
+            cnt = lib.of_timing_read(64, kk, None, None)
+            lib.of_timing_enable(0)
+            res[ring] = (y, dx, {kk[i] for i in range(cnt)})
+    finally:
+        lib.of_set_tuning(30, 2)
+        lib.of_set_tuning(16, 6)
+        lib.of_set_tuning(8, 1)
+        lib.of_timing_enable(0)
+    base = 240 if prec == "bf16" else 160
+    want = {base + (0 if cout > 64 else 1)}
+    if k < 7:
+        want.add(base + 8 + (0 if cin > 64 else 1))
+    for ring in (1, 2):
+        assert want <= res[ring][2] and want <= res[0][2], (want, res[ring][2], res[0][2])
+        assert torch.isfinite(res[ring][0]).all()
+        assert torch.equal(res[ring][0], res[0][0])
+        if k < 7:
+            assert torch.isfinite(res[ring][1]).all()
+            assert torch.equal(res[ring][1], res[0][1])
+
+
 @pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (2, 38, 130)])
 def test_conv_stem_x3(n, h, w):
     """The stem forward on its own split-bf16 kernel (conv_stem_x3: 7x7 stride 2, 3 -> 4

@@ -3,7 +3,7 @@
 # passes for fp32 config 2, bf16 config 3 (B=32) and config 5 per GPU (768x1024 bf16 B=8), the
 # default bench (fp32 config 2, CPU baseline on the bench batch) and its rocprofv3 kernel-trace
 # summary, the bf16 benches and trace, the fp32-MFMA line, the flow / b16i micro-benchmarks.
-# Publish with: bash tools/publish_round.sh gpurun_out/round5 r4
+# Publish with: bash tools/publish_round.sh gpurun_out/round5 r5
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/round5}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Copy one tools/gpu_round.sh output directory into profiles/ as round $2's evidence:
+# Copy one tools/gpu_round5.sh output directory into profiles/ as round $2's evidence:
 # bench lines, rocprof summaries (+ kernel stats), PMC traffic, micro-benchmarks.
 # bash tools/publish_round.sh gpurun_out/round3 r2
 set -e
