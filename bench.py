@@ -395,7 +395,7 @@ def main():
         trainer.train_step(batch, i)
     torch.cuda.synchronize()
     live = args.roofline_window == "timed"
-    prof_per, prof_only = {}, None
+    prof_per, prof_only, alone = {}, None, {}
     if live:
         ops.TIMING_TAGS = []
         lib.of_timing_read(0, None, None, None)
@@ -413,6 +413,22 @@ def main():
         if prof_per and len(ptags) == pn and not os.environ.get("OFLOW_TIMING_DUMP"):
             pdom = max(prof_per, key=lambda k: prof_per[k][1])
             prof_only = {ptags[i] for i in range(pn) if pk[i] == pdom}
+        # The same table with every kernel alone on the chip: one more untimed step with the
+        # side streams off (weight gradients, BN reductions and forward projections on the
+        # main stream).  In the step above the input-gradient convs share the chip with the
+        # side stream's weight gradients and BN reductions, which stretches their event spans;
+        # this one separates kernel efficiency from that overlap (same thermal state).
+        side0, proj0 = ops.SIDE_STREAM_WGRAD, ops.PROJ_SIDE
+        ops.SIDE_STREAM_WGRAD = ops.PROJ_SIDE = False
+        lib.of_timing_read(0, None, None, None)
+        lib.of_timing_enable(1)
+        trainer.train_step(batch, 20_001)
+        torch.cuda.synchronize()
+        lib.of_timing_enable(0)
+        ops.SIDE_STREAM_WGRAD, ops.PROJ_SIDE = side0, proj0
+        for i in range(lib.of_timing_read(pcap, pk, pf, pm)):
+            tf, tm, cnt = alone.get(pk[i], (0.0, 0.0, 0))
+            alone[pk[i]] = (tf + pf[i], tm + pm[i], cnt + 1)
     torch.cuda.synchronize()
     graphed = None
     if args.graph:
@@ -468,7 +484,7 @@ def main():
                              "flow_abs_mean": [round(float(f.abs().mean()), 4) for f in first[1]]},
                    "last": {"loss": final_loss,
                             "flow_abs_mean": [round(float(f.abs().mean()), 4) for f in flows]},
-                   "train_steps_before_first": args.warmup + (1 if live else 0) +
+                   "train_steps_before_first": args.warmup + (2 if live else 0) +
                                                (3 if graphed is not None else 0)}
 
     # ---- dominant-kernel roofline ------------------------------------------------------------
@@ -543,6 +559,14 @@ def main():
                                 "ms_per_step": round(v[1] / tsteps, 3),
                                 "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
                                for k, v in sorted(table.items())}}
+
+    if roof is not None and alone:
+        roof["all_conv_gemm_tflops_alone"] = round(
+            sum(v[0] for v in alone.values()) / (sum(v[1] for v in alone.values()) * 1e-3) / 1e12, 2)
+        roof["per_kernel_alone"] = {
+            kind_name(k): {"launches_per_step": v[2], "ms_per_step": round(v[1], 3),
+                           "tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 2)}
+            for k, v in sorted(alone.items())}
 
     # ---- parity probe at the final weights: HIP forward of one pair (the oracle runs after
     # the timed region, below) -------------------------------------------------------------

@@ -33,14 +33,21 @@ def main():
         print("| `%s` | %s | %.2f | %.1f | %.4f |" % (
             r["Name"][:90], r["Calls"], float(r["TotalDurationNs"]) / 1e6,
             100 * float(r["TotalDurationNs"]) / tot, float(r["AverageNs"]) / 1e6))
-    print("\nPer-kernel hipEvent table from the bench (instrumented steps, all convs on one "
-          "stream):\n")
-    print("| instance | launches/step | ms/step | TFLOP/s |")
-    print("|---|---|---|---|")
+    alone = rf.get("per_kernel_alone", {})
+    print("\nPer-kernel hipEvent table from the bench: `in step` = one fully timed step after "
+          "the warm-up, side streams on (the input-gradient convs share the chip with the side "
+          "stream's weight gradients and BN reductions); `alone` = one more step with every "
+          "kernel alone on the chip (side streams off)%s:\n"
+          % ("; all convs %.1f / %.1f TFLOP/s" % (rf["all_conv_gemm_tflops"],
+                                                  rf["all_conv_gemm_tflops_alone"])
+             if "all_conv_gemm_tflops_alone" in rf else ""))
+    print("| instance | launches/step | ms/step in step | TFLOP/s in step | ms/step alone | TFLOP/s alone |")
+    print("|---|---|---|---|---|---|")
     for k, v in rf.get("per_kernel", {}).items():
-        print("| %s | %d | %.3f | %.1f |" % (k, v["launches_per_step"], v["ms_per_step"],
-                                            v["tflops"]))
-
+        a = alone.get(k)
+        print("| %s | %d | %.3f | %.1f | %s | %s |" % (
+            k, v["launches_per_step"], v["ms_per_step"], v["tflops"],
+            "%.3f" % a["ms_per_step"] if a else "-", "%.1f" % a["tflops"] if a else "-"))
 
 if __name__ == "__main__":
     main()
