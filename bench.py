@@ -167,11 +167,11 @@ def kernel_symbol(kind):
     if fam == "stem_x3":
         if mode == 2:
             return "void oflow::conv_wgrad_stem_x3<3, false>(oflow::GemmArgs)"
-        return "void oflow::conv_stem_x3<32, 3>(oflow::GemmArgs)"   # of_set_tuning key 8 default
+        return "void oflow::conv_stem_x3<32, 3>(oflow::GemmArgs, int)"   # of_set_tuning key 8 default
     if fam == "stem_b16":
         if mode == 2:
             return "void oflow::conv_wgrad_stem_x3<1, false>(oflow::GemmArgs)"
-        return "void oflow::conv_stem_x3<32, 1>(oflow::GemmArgs)"
+        return "void oflow::conv_stem_x3<32, 1>(oflow::GemmArgs, int)"
     if cfg == 7 and fam == "f32":
         return NARROW_SYMBOLS[mode]
     if fam == "tile_b16":

@@ -429,7 +429,10 @@ int of_timing_enable(int on);
  * key 30 = the split implicit GEMMs (conv_gemm_x3: stride-2 and 1x1 layers) on an LDS-DMA ring
  * with both operands DMA'd: 3 slots, one chunk in flight across each barrier (1), or 2 slots,
  * two workgroups per CU where the LDS allows (2, default); or register-staged A with one chunk
- * in flight (0); bitwise the same results. */
+ * in flight (0); bitwise the same results;
+ * key 31 = the stem forward (conv_stem_x3) persistent over its tiles with this many workgroups
+ * per CU (-1 = default: as many as the LDS holds, 2 fp32 / 3 bf16; 0 = one tile per
+ * workgroup); bitwise the same results. */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

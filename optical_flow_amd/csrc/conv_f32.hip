@@ -1541,195 +1541,224 @@ constexpr int ST_HH = 2 * ST_TH + 5, ST_HW = 2 * ST_TW + 6, ST_HWP = 72;
 constexpr int ST_BROW = 232;      // bf16 per B row: 7 x 32 + 8
 
 template <int CO, int NP = 3>
-__global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : NP == 1 ? 4 : 2) void conv_stem_x3(GemmArgs a) {
+__global__ __launch_bounds__(CO * 8, CO == 64 ? 1 : NP == 1 ? 4 : 2) void conv_stem_x3(GemmArgs a, int ntiles) {
   constexpr int SM = 4, SN = 2, WM = 64, WN = 32, NW = CO / 8, NT = 64 * NW;
   static_assert(NP == 3 || NP == 1, "three split planes (fp32) or one (bf16)");
   constexpr int B_U4 = CO * ST_BROW / 8;              // uint4 per B plane
-  constexpr int H_PIX = ST_HH * ST_HWP;               // halo pixels (8 bytes each) per plane
-  constexpr int OP_U4 = NP * B_U4 + NP * H_PIX / 2, EP_U4 = NW * WM * WN * 4 / 16;
-  constexpr int SMEM_U4 = OP_U4 > EP_U4 ? OP_U4 : EP_U4;   // operands, then epilogue images
-  __shared__ uint4 smem[SMEM_U4];
+  constexpr int HWP = ST_HW;                          // halo pitch: B + halo 79.8 KB (fp32 CO 32)
+  constexpr int H_PIX = ST_HH * HWP;                  // halo pixels (8 bytes each) per plane
+  constexpr int HB_U4 = NP * H_PIX / 2, EP_U4 = NW * WM * WN * 4 / 16;
+  constexpr int W_U4 = HB_U4 > EP_U4 ? HB_U4 : EP_U4; // halo planes, then the epilogue images
+  // B stays for the workgroup's whole tile walk; the halo region is reused per tile
+  __shared__ uint4 smem[NP * B_U4 + W_U4];
   char* Bs = reinterpret_cast<char*>(smem);                          // [plane][co][k']
   char* Hs = reinterpret_cast<char*>(smem + NP * B_U4);              // [plane][hy][hx] 8 B
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // Persistent over tiles: the 64 / CO workgroups of a channel group share co0; workgroup w
+  // walks tiles w / groups, + gridDim.x / groups, ...  (grid = tiles * groups: one tile each)
+  constexpr int GROUPS = 64 / CO;
   const int wgid0 = xcd_remap(blockIdx.x, gridDim.x);
-  const int co0 = (wgid0 % (64 / CO)) * CO, wgid = wgid0 / (64 / CO);
+  const int co0 = (wgid0 % GROUPS) * CO;
+  const int tstride = gridDim.x / GROUPS;
   const int tiles_x = (a.wo + ST_TW - 1) / ST_TW, tiles_y = (a.ho + ST_TH - 1) / ST_TH;
-  const int b = wgid / (tiles_x * tiles_y);
-  const int trem = wgid - b * tiles_x * tiles_y;
-  const int oy0 = (trem / tiles_x) * ST_TH, ox0 = (trem % tiles_x) * ST_TW;
-  const int iy0 = 2 * oy0 - a.pt, ix0 = 2 * ox0 - a.pl;
+  int t = wgid0 / GROUPS;
+  if (t >= ntiles) return;
 
   // ---- B: entry (plane, co, kernel row r, octet sp) <- taps (r, 2 sp), (r, 2 sp + 1) of the
-  // x3 fwd image W16_f[co][tap * 4 + ci] (8-byte aligned pieces; tap 7 is zero).  Every
-  // thread issues all of its B and halo loads before its first LDS store (a load -> store
-  // loop keeps one load in flight per thread: the stem is latency-bound on its staging).
+  // x3 fwd image W16_f[co][tap * 4 + ci] (8-byte aligned pieces; tap 7 is zero), once.
   constexpr int BE = NP * CO * 28, BQ = (BE + NT - 1) / NT;
   constexpr int HE = ST_HH * ST_HW, HQ = (HE + NT - 1) / NT;
   const rsrc_t rb = make_rsrc(a.B, a.b_bytes);
   const rsrc_t ra = make_rsrc(a.A, a.a_bytes);
-  uint2 blo[BQ], bhi[BQ];
   float4 hv[HQ];
+  // this tile's halo: input pixel (iy0 + hy, ix0 + hx), 4 channels, into registers
+  auto load_halo = [&](int tt) {
+    const int b = tt / (tiles_x * tiles_y);
+    const int trem = tt - b * tiles_x * tiles_y;
+    const int iy0 = 2 * ((trem / tiles_x) * ST_TH) - a.pt, ix0 = 2 * ((trem % tiles_x) * ST_TW) - a.pl;
 #pragma unroll
-  for (int k = 0; k < BQ; ++k) {
-    const int e = tid + NT * k;
-    const int p = e / (CO * 28), rem = e - p * (CO * 28);
-    const int co = rem / 28, rs = rem - co * 28, r = rs >> 2, sp = rs & 3;
-    const uint32_t src =
-        (uint32_t)((p * a.b_plane + (int64_t)(co0 + co) * a.ldb + (r * 7 + 2 * sp) * 4) * 2);
-    const bool ok = e < BE && co0 + co < a.nb;
-    blo[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok ? src : kOOB, 0, 0));
-    bhi[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok && sp < 3 ? src + 8 : kOOB, 0, 0));
-  }
-  // ---- halo: input pixel (iy0 + hy, ix0 + hx), 4 channels (split into 3 planes for fp32)
+    for (int k = 0; k < HQ; ++k) {
+      const int q = tid + NT * k;
+      const int hy = q / ST_HW, hx = q - hy * ST_HW;
+      const int iy = iy0 + hy, ix = ix0 + hx;
+      const bool ok = q < HE && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+      hv[k] = bload4(ra, ok ? (uint32_t)((((int64_t)b * a.h + iy) * a.w + ix) * a.lda * 4) : kOOB);
+    }
+  };
+  auto store_halo = [&]() {                // (split into 3 planes for fp32)
 #pragma unroll
-  for (int k = 0; k < HQ; ++k) {
-    const int q = tid + NT * k;
-    const int hy = q / ST_HW, hx = q - hy * ST_HW;
-    const int iy = iy0 + hy, ix = ix0 + hx;
-    const bool ok = q < HE && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
-    hv[k] = bload4(ra, ok ? (uint32_t)((((int64_t)b * a.h + iy) * a.w + ix) * a.lda * 4) : kOOB);
-  }
+    for (int k = 0; k < HQ; ++k) {
+      const int q = tid + NT * k;
+      if (HE % NT == 0 || q < HE) {
+        const int hy = q / ST_HW, hx = q - hy * ST_HW;
+        const int o = (hy * HWP + hx) * 8;
+        if (NP == 1) {
+          *reinterpret_cast<uint2*>(Hs + o) = pack_bf16x4(hv[k]);
+        } else {
+          uint2 h, m, l;
+          split3x4(hv[k], h, m, l);
+          *reinterpret_cast<uint2*>(Hs + o) = h;
+          *reinterpret_cast<uint2*>(Hs + H_PIX * 8 + o) = m;
+          *reinterpret_cast<uint2*>(Hs + 2 * H_PIX * 8 + o) = l;
+        }
+      }
+    }
+  };
+  {
+    // every load of B and the first halo issued before any LDS store (a load -> store loop
+    // keeps one load in flight per thread: the stem is latency-bound on its staging)
+    uint2 blo[BQ], bhi[BQ];
 #pragma unroll
-  for (int k = 0; k < BQ; ++k) {
-    const int e = tid + NT * k;
-    if (BE % NT == 0 || e < BE) {
+    for (int k = 0; k < BQ; ++k) {
+      const int e = tid + NT * k;
       const int p = e / (CO * 28), rem = e - p * (CO * 28);
       const int co = rem / 28, rs = rem - co * 28, r = rs >> 2, sp = rs & 3;
-      *reinterpret_cast<uint4*>(Bs + ((p * CO + co) * ST_BROW + r * 32 + sp * 8) * 2) =
-          make_uint4(blo[k].x, blo[k].y, bhi[k].x, bhi[k].y);
+      const uint32_t src =
+          (uint32_t)((p * a.b_plane + (int64_t)(co0 + co) * a.ldb + (r * 7 + 2 * sp) * 4) * 2);
+      const bool ok = e < BE && co0 + co < a.nb;
+      blo[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok ? src : kOOB, 0, 0));
+      bhi[k] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rb, ok && sp < 3 ? src + 8 : kOOB, 0, 0));
     }
-  }
+    load_halo(t);
 #pragma unroll
-  for (int k = 0; k < HQ; ++k) {
-    const int q = tid + NT * k;
-    if (HE % NT == 0 || q < HE) {
-      const int hy = q / ST_HW, hx = q - hy * ST_HW;
-      const int o = (hy * ST_HWP + hx) * 8;
-      if (NP == 1) {
-        *reinterpret_cast<uint2*>(Hs + o) = pack_bf16x4(hv[k]);
-      } else {
-        uint2 h, m, l;
-        split3x4(hv[k], h, m, l);
-        *reinterpret_cast<uint2*>(Hs + o) = h;
-        *reinterpret_cast<uint2*>(Hs + H_PIX * 8 + o) = m;
-        *reinterpret_cast<uint2*>(Hs + 2 * H_PIX * 8 + o) = l;
+    for (int k = 0; k < BQ; ++k) {
+      const int e = tid + NT * k;
+      if (BE % NT == 0 || e < BE) {
+        const int p = e / (CO * 28), rem = e - p * (CO * 28);
+        const int co = rem / 28, rs = rem - co * 28, r = rs >> 2, sp = rs & 3;
+        *reinterpret_cast<uint4*>(Bs + ((p * CO + co) * ST_BROW + r * 32 + sp * 8) * 2) =
+            make_uint4(blo[k].x, blo[k].y, bhi[k].x, bhi[k].y);
       }
     }
   }
-  __syncthreads();
 
   const int wm = CO == 64 ? wave >> 1 : wave, wn = CO == 64 ? wave & 1 : 0;
   const int l16 = lane & 15, sp = lane >> 4;
-  f32x4 acc4[SM][SN];
-#pragma unroll
-  for (int i = 0; i < SM; ++i)
-#pragma unroll
-    for (int j = 0; j < SN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc4[i][j][r] = 0.f;
   // A block i: output row 2 wm + (i >> 1), columns 16 (i & 1) + l16 -> halo pixel at kernel row 0
   int a_off[SM];
 #pragma unroll
   for (int i = 0; i < SM; ++i)
-    a_off[i] = ((2 * (2 * wm + (i >> 1))) * ST_HWP + 2 * (16 * (i & 1) + l16) + 2 * sp) * 8;
+    a_off[i] = ((2 * (2 * wm + (i >> 1))) * HWP + 2 * (16 * (i & 1) + l16) + 2 * sp) * 8;
   const int b_off = ((wn * WN + l16) * ST_BROW + sp * 8) * 2;
-#pragma unroll
-  for (int r = 0; r < 7; ++r) {
-    bf16x8 av[NP][SM], bv[NP][SN];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-#pragma unroll
-      for (int i = 0; i < SM; ++i)
-        av[p][i] = *reinterpret_cast<const bf16x8*>(Hs + p * H_PIX * 8 + a_off[i] + r * ST_HWP * 8);
-#pragma unroll
-      for (int j = 0; j < SN; ++j)
-        bv[p][j] = *reinterpret_cast<const bf16x8*>(Bs + p * B_U4 * 16 + b_off + (16 * j * ST_BROW + r * 32) * 2);
-    }
+  constexpr int EPW = 32, LPR = 8, RPI = 8;
+  float* E = reinterpret_cast<float*>(smem + NP * B_U4) + wave * WM * EPW;
+  const int lq = lane >> 4;
+  const int c4 = lane % LPR, rr = lane / LPR;
+  const int n = co0 + wn * WN + 4 * c4;
+
+  for (; t < ntiles; t += tstride) {
+    const int b = t / (tiles_x * tiles_y);
+    const int trem = t - b * tiles_x * tiles_y;
+    const int oy0 = (trem / tiles_x) * ST_TH, ox0 = (trem % tiles_x) * ST_TW;
+    store_halo();
+    __syncthreads();
+    // the next tile's halo loads stay in flight during this tile's MFMAs and epilogue
+    if (t + tstride < ntiles) load_halo(t + tstride);
+
+    f32x4 acc4[SM][SN];
 #pragma unroll
     for (int i = 0; i < SM; ++i)
 #pragma unroll
-      for (int j = 0; j < SN; ++j) {
-        f32x4 x = acc4[i][j];
-        if (NP == 3) {
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP - 1][i], bv[0][j], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP - 1][j], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[NP / 2][j], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[0][j], x, 0, 0, 0);
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP / 2][j], x, 0, 0, 0);
-        }
-        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc4[i][j][r] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      bf16x8 av[NP][SM], bv[NP][SN];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int i = 0; i < SM; ++i)
+          av[p][i] = *reinterpret_cast<const bf16x8*>(Hs + p * H_PIX * 8 + a_off[i] + r * HWP * 8);
+#pragma unroll
+        for (int j = 0; j < SN; ++j)
+          bv[p][j] = *reinterpret_cast<const bf16x8*>(Bs + p * B_U4 * 16 + b_off + (16 * j * ST_BROW + r * 32) * 2);
       }
-  }
-  __syncthreads();                      // B / halo reads done: LDS becomes the epilogue images
-
-  // ---- epilogue: the wave's 64 x 32 block through a private LDS image, float4 rows
-  constexpr int EPW = 32, LPR = 8, RPI = 8;
-  float* E = reinterpret_cast<float*>(smem) + wave * WM * EPW;
-  const int lq = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < SM; ++i)
+      for (int i = 0; i < SM; ++i)
 #pragma unroll
-    for (int j = 0; j < SN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) E[(16 * i + 4 * lq + r) * EPW + 16 * j + l16] = acc4[i][j][r];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int c4 = lane % LPR, rr = lane / LPR;
-  const int n = co0 + wn * WN + 4 * c4;
-  const int64_t img = (int64_t)b * a.ho * a.wo;
-#pragma unroll
-  for (int q = 0; q < WM / RPI; ++q) {
-    const int m = q * RPI + rr;
-    const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
-    const int oy = oy0 + 2 * wm + m / 32, ox = ox0 + m % 32;
-    if (oy < a.ho && ox < a.wo && n < a.N)
-      epilogue_store4<MODE_FWD>(a, 0, img + (int64_t)oy * a.wo + ox, n, v);
-  }
-  if (a.pool_out) {
-    // MaxPool2D (model.py:17) of the two output rows this wave owns (even rows: the 2 x 2
-    // windows never straddle waves or tiles): the epilogue's value of each of the four pixels
-    // (bias, BN, ReLU as epilogue_store4 computes it) and the max in maxpool2_fwd_kernel's order,
-    // so the pooled tensor is the separate pass's bit for bit, without re-reading the output.
-    const int pho = a.ho / 2, pwo = a.wo / 2;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int it = lane + 64 * u;                 // 16 pooled columns x 8 channel quads
-      const int pc = it >> 3, qq = it & 7;
-      const int nn = co0 + wn * WN + 4 * qq;
-      const int py = (oy0 + 2 * wm) / 2, px = ox0 / 2 + pc;
-      if (py >= pho || px >= pwo || nn >= a.N) continue;
-      float bias[4], scale[4], shift[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) column_params<MODE_FWD>(a, nn + e, bias[e], scale[e], shift[e]);
-      float r[4][4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {                 // (0,0), (0,1), (1,0), (1,1)
-        const int m = (k >> 1) * 32 + 2 * pc + (k & 1);
-        const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * qq]);
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = vv[e] + bias[e];
-          if (a.bn_g) x = x * scale[e] + shift[e];
-          r[k][e] = act_fwd(x, a.act, a.alpha);
+        for (int j = 0; j < SN; ++j) {
+          f32x4 x = acc4[i][j];
+          if (NP == 3) {
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP - 1][i], bv[0][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP - 1][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[NP / 2][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[NP / 2][i], bv[0][j], x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[NP / 2][j], x, 0, 0, 0);
+          }
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], x, 0, 0, 0);
         }
-      }
-      float o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = fmaxf(fmaxf(r[0][e], r[1][e]), fmaxf(r[2][e], r[3][e]));
-      *reinterpret_cast<float4*>(&a.pool_out[(((int64_t)b * pho + py) * pwo + px) * a.N + nn]) =
-          make_float4(o[0], o[1], o[2], o[3]);
     }
+    __syncthreads();                      // halo reads done: the halo region becomes E images
+
+    // ---- epilogue: the wave's 64 x 32 block through a private LDS image, float4 rows
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[(16 * i + 4 * lq + r) * EPW + 16 * j + l16] = acc4[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int64_t img = (int64_t)b * a.ho * a.wo;
+#pragma unroll
+    for (int q = 0; q < WM / RPI; ++q) {
+      const int m = q * RPI + rr;
+      const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
+      const int oy = oy0 + 2 * wm + m / 32, ox = ox0 + m % 32;
+      if (oy < a.ho && ox < a.wo && n < a.N)
+        epilogue_store4<MODE_FWD>(a, 0, img + (int64_t)oy * a.wo + ox, n, v);
+    }
+    if (a.pool_out) {
+      // MaxPool2D (model.py:17) of the two output rows this wave owns (even rows: the 2 x 2
+      // windows never straddle waves or tiles): the epilogue's value of each of the four pixels
+      // (bias, BN, ReLU as epilogue_store4 computes it) and the max in maxpool2_fwd_kernel's
+      // order, so the pooled tensor is the separate pass's bit for bit, without re-reading the
+      // output.
+      const int pho = a.ho / 2, pwo = a.wo / 2;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int it = lane + 64 * u;                 // 16 pooled columns x 8 channel quads
+        const int pc = it >> 3, qq = it & 7;
+        const int nn = co0 + wn * WN + 4 * qq;
+        const int py = (oy0 + 2 * wm) / 2, px = ox0 / 2 + pc;
+        if (py >= pho || px >= pwo || nn >= a.N) continue;
+        float bias[4], scale[4], shift[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) column_params<MODE_FWD>(a, nn + e, bias[e], scale[e], shift[e]);
+        float rv[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {                 // (0,0), (0,1), (1,0), (1,1)
+          const int m = (k >> 1) * 32 + 2 * pc + (k & 1);
+          const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * qq]);
+          const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = vv[e] + bias[e];
+            if (a.bn_g) x = x * scale[e] + shift[e];
+            rv[k][e] = act_fwd(x, a.act, a.alpha);
+          }
+        }
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = fmaxf(fmaxf(rv[0][e], rv[1][e]), fmaxf(rv[2][e], rv[3][e]));
+        *reinterpret_cast<float4*>(&a.pool_out[(((int64_t)b * pho + py) * pwo + px) * a.N + nn]) =
+            make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+    __syncthreads();                      // E reads done before the next tile's halo store
   }
 }
 
 // of_set_tuning key 8: the stem on conv_stem_x3 (1: two 32-channel workgroups per CU,
 // default; 2: one 64-channel workgroup) or on conv_gemm_x3 (0).
 static int g_stem_x3 = 1;
+// of_set_tuning key 31: conv_stem_x3 persistent with this many workgroups per CU (-1: the
+// default, 2 fp32 / 3 bf16 / 1 for the 64-channel form; 0: one tile per workgroup).
+static int g_stem_persist = -1;
 // of_set_tuning key 15: the bf16 stem (forward and weight gradient) on the one-plane
 // conv_stem_x3<32, 1> / conv_wgrad_stem_x3<1> (1, default) or on the bf16 GEMMs (0).
 static int g_stem_bf16 = 1;
@@ -5168,6 +5197,7 @@ int of_set_tuning(int key, int value) {
   if (key == 28 && value >= 0 && value <= 64) { g_det_rmax = value; return OF_OK; }
   if (key == 29 && value >= 0 && value <= 4) { g_wgr_lanes = value; return OF_OK; }
   if (key == 30 && value >= 0 && value <= 2) { g_gx3_ring = value; return OF_OK; }
+  if (key == 31 && value >= -1 && value <= 8) { g_stem_persist = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -5342,12 +5372,19 @@ static int conv_fwd_impl(int prec, const of_conv_desc* d, const float* x, int ld
     const int64_t tiles = (int64_t)d->n * cdiv(d->ho, ST_TH) * cdiv(d->wo, ST_TW);
     OF_CHECK_ARG(tiles < INT32_MAX, "conv stem: too many tiles");
     if (timing_on()) timing_begin(s);
+    // persistent (of_set_tuning key 31 = workgroups per CU, default as many as the LDS holds:
+    // 2 fp32 / 3 bf16 / 1 for the 64-channel form; 0: one tile per workgroup, the round-2..4
+    // grid): B staged once per workgroup, the next tile's halo loaded during this tile's MFMAs
+    const int groups = bf16 || g_stem_x3 != 2 ? 2 : 1;
+    const int per_cu = g_stem_persist < 0 ? (bf16 ? 3 : g_stem_x3 == 2 ? 1 : 2) : g_stem_persist;
+    const int64_t cap = per_cu > 0 ? (int64_t)per_cu * device_cus() : tiles * groups;
+    const unsigned grid = (unsigned)(std::min(tiles * groups, cap) / groups * groups);
     if (bf16)
-      hipLaunchKernelGGL((conv_stem_x3<32, 1>), dim3((unsigned)(2 * tiles)), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((conv_stem_x3<32, 1>), dim3(grid), dim3(256), 0, s, a, (int)tiles);
     else if (g_stem_x3 == 2)
-      hipLaunchKernelGGL(conv_stem_x3<64>, dim3((unsigned)tiles), dim3(512), 0, s, a);
+      hipLaunchKernelGGL(conv_stem_x3<64>, dim3(grid), dim3(512), 0, s, a, (int)tiles);
     else
-      hipLaunchKernelGGL(conv_stem_x3<32>, dim3((unsigned)(2 * tiles)), dim3(256), 0, s, a);
+      hipLaunchKernelGGL(conv_stem_x3<32>, dim3(grid), dim3(256), 0, s, a, (int)tiles);
     if (timing_on()) timing_end(s, bf16 ? KIND_STEM_B16 : KIND_STEM_X3, flops);
     return check_launch("conv_stem_x3");
   }

@@ -404,6 +404,62 @@ def test_conv_stem_x3(n, h, w):
     assert rel_l2(outs[0][0], yref) < 3 * rel_l2(outs[2][0], yref) + 1e-7
 
 
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 50, 70), (8, 384, 512)])
+def test_conv_stem_persistent_bitwise(n, h, w, prec):
+    """conv_stem_x3 persistent over tiles (of_set_tuning key 31: the default workgroups per CU,
+    and 1) against one tile per workgroup (key 31 = 0): y, z and the max-pooled output
+    (of_conv2d_fwd_pool) bit for bit, fp32 (three planes) and bf16 (one plane), ragged tiles
+    and the bench size (12 tiles per workgroup)."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_RELU, call
+    lib = _lib.lib()
+    cin, cout = 4, 64
+    xc = rng_tensor((n, h, w, 3), 71)
+    x = torch.cat([xc, torch.zeros(n, h, w, 1)], -1)
+    wt = rng_tensor((7, 7, 3, cout), 72, scale=(2.0 / 147) ** 0.5)
+    b = rng_tensor((cout,), 73, scale=0.1)
+    g, be = rng_tensor((cout,), 74, scale=0.5) + 1.0, rng_tensor((cout,), 75, scale=0.1)
+    mu, var = rng_tensor((cout,), 76, scale=0.1), rng_tensor((cout,), 77).abs() + 0.5
+    kw = dict(precision="bf16") if prec == "bf16" else dict(f32_split=True)
+    layer = ops.ConvLayer(dev(wt), dev(b), stride=2, act=ACT_RELU, cin_p=cin, **kw)
+    d = layer.desc(n, h, w)
+    m = layer.mode(d)
+    wf, _ = layer.packed(d)
+    fent, fws = layer.fwd_entry(d)
+    ws = torch.empty(fws // 4 + 4, device="cuda")
+    P, st = ops._ptr, ops._stream()
+    xd, bd, gd, bed, mud, vard = [dev(t) for t in (x, b, g, be, mu, var)]
+    outs = []
+    try:
+        for per_cu in (0, -1, 1):
+            assert lib.of_set_tuning(31, per_cu) == 0
+            y = torch.full((n, d.ho, d.wo, cout), 7.0, device="cuda")
+            z = torch.full((n, d.ho, d.wo, cout), 7.0, device="cuda")
+            call(fent, C.byref(d), P(xd), cin, P(wf), P(bd), P(gd), P(bed), P(mud), P(vard), 1e-3,
+                 None, 0, ACT_RELU, 0.0, P(z), cout, P(y), cout, P(ws), fws, st)
+            yp = torch.full((n, d.ho, d.wo, cout), 7.0, device="cuda")
+            xp = torch.full((n, d.ho // 2, d.wo // 2, cout), 7.0, device="cuda")
+            pooled = d.ho % 2 == 0 and d.wo % 2 == 0
+            if pooled:
+                _lib.check(lib.of_conv2d_fwd_pool(
+                    C.byref(d), m, P(xd), cin, P(wf), P(bd), P(gd), P(bed), P(mud), P(vard),
+                    C.c_float(1e-3), ACT_RELU, C.c_float(0.0), None, cout, P(yp), cout, P(xp),
+                    P(ws), fws, st), "of_conv2d_fwd_pool")
+            torch.cuda.synchronize()
+            outs.append((y, z, yp, xp, pooled))
+    finally:
+        lib.of_set_tuning(31, -1)
+    y0, z0, yp0, xp0, pooled = outs[0]
+    assert torch.isfinite(y0).all() and (y0 != 7.0).any()
+    for y, z, yp, xp, _ in outs[1:]:
+        assert torch.equal(y, y0) and torch.equal(z, z0)
+        if pooled:
+            assert torch.equal(yp, yp0) and torch.equal(xp, xp0) and torch.equal(yp0, y0)
+
+
 @pytest.mark.parametrize("n,h,w,cin,cout,k,s", [(4, 48, 64, 64, 128, 3, 2),    # res3_0 conv_a
                                                (4, 24, 32, 128, 256, 3, 2),   # res4_0 conv_a
                                                (4, 48, 64, 64, 128, 1, 2),    # projection
