@@ -410,9 +410,7 @@ def main():
         for i in range(pn):
             tf, tm, cnt = prof_per.get(pk[i], (0.0, 0.0, 0))
             prof_per[pk[i]] = (tf + pf[i], tm + pm[i], cnt + 1)
-        if prof_per and len(ptags) == pn and not os.environ.get("OFLOW_TIMING_DUMP"):
-            pdom = max(prof_per, key=lambda k: prof_per[k][1])
-            prof_only = {ptags[i] for i in range(pn) if pk[i] == pdom}
+        pkinds = [pk[i] for i in range(pn)]
         # The same table with every kernel alone on the chip: one more untimed step with the
         # side streams off (weight gradients, BN reductions and forward projections on the
         # main stream).  In the step above the input-gradient convs share the chip with the
@@ -429,6 +427,14 @@ def main():
         for i in range(lib.of_timing_read(pcap, pk, pf, pm)):
             tf, tm, cnt = alone.get(pk[i], (0.0, 0.0, 0))
             alone[pk[i]] = (tf + pf[i], tm + pm[i], cnt + 1)
+        # The dominant kernel: the largest per-step time with every kernel alone (its own cost;
+        # in the step above, a kernel's span also counts the side-stream work it overlaps, and
+        # the two largest instances trade places run to run); its launches are then timed live
+        # in the timed region.
+        if prof_per and len(ptags) == pn and not os.environ.get("OFLOW_TIMING_DUMP"):
+            by = alone if alone else prof_per
+            pdom = max(by, key=lambda k: by[k][1])
+            prof_only = {ptags[i] for i in range(pn) if pkinds[i] == pdom}
     torch.cuda.synchronize()
     graphed = None
     if args.graph:
@@ -548,7 +554,9 @@ def main():
                 "window": ("one fully timed eager step after the warm-up (the timed region "
                            "replayed the captured graph)" if graphed is not None else
                            ("timed region, %d steps (the dominant kernel's launches timed; "
-                            "per_kernel from one fully timed step after the warm-up)" % nsteps)
+                            "per_kernel from one fully timed step after the warm-up, "
+                            "per_kernel_alone from one with the side streams off, which "
+                            "picks the dominant kernel)" % nsteps)
                            if live and prof_only is not None else
                            ("timed region, %d steps" % nsteps) if live else
                            ("%d extra steps, convs on one stream" % nsteps)),
