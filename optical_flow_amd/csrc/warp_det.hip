@@ -398,6 +398,7 @@ __device__ __forceinline__ void win_accumulate(float4 (&acc)[NCB], int& found, c
 #pragma unroll
   for (int b = 0; b < NCB; ++b) acc[b] = make_float4(0.f, 0.f, 0.f, 0.f);
   const int span = max(D.k1 - D.k0, 0);
+  const bool interior = D.x >= 1 && D.x <= w - 2 && D.r >= 1 && D.r <= h - 2;
   int pmax = (span + 15) >> 4;
 #pragma unroll
   for (int o = 16; o < 64; o <<= 1) pmax = max(pmax, __shfl_xor(pmax, o, 64));
@@ -467,7 +468,13 @@ __device__ __forceinline__ void win_accumulate(float4 (&acc)[NCB], int& found, c
       if (t0 + u >= pmax) break;
       uint32_t m = 0;
       float ca = 0.f, cbw = 0.f;
-      if (ci[u] >= 0) {
+      // Interior destination: a candidate hits only if its sample lies in [x - 1, x + 1) x
+      // [r - 1, r + 1) (its unclamped corners floor(.) and floor(.) + 1; a clamped corner lands
+      // on the border), the same float sums det_corners forms: most lanes skip the corners.
+      const bool maybe =
+          !interior || ((float)ci[u] + f[u].x >= (float)(D.x - 1) && (float)ci[u] + f[u].x < (float)(D.x + 1) &&
+                        (float)cj[u] + f[u].y >= (float)(D.r - 1) && (float)cj[u] + f[u].y < (float)(D.r + 1));
+      if (ci[u] >= 0 && maybe) {
         const DetCorners tc = det_corners(ci[u], cj[u], f[u].x, f[u].y, h, w, false);
 #pragma unroll
         for (int k = 0; k < 4; ++k) m |= (tc.y[k] == D.r && tc.x[k] == D.x) ? 1u << k : 0u;
