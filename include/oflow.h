@@ -577,6 +577,26 @@ int of_conv2d_dgrad_add_act(const of_conv_desc* d, int precision, const float* d
                             const void* w_bwd, const float* add, int ld_add,
                             const float* act_src, int ld_act, int act, float alpha, float* dx,
                             int lddx, void* workspace, size_t ws_bytes, void* stream);
+/* of_conv2d_dgrad_add_act with the BN backward partial sums of the layer whose output is
+ * act_src fused into its epilogue (round 5): besides dx = t, per channel sum t and sum t zhat
+ * with zhat = (act_src - bn_res - bn_beta) / bn_gamma (bn_res: the residual added before the
+ * activation, or NULL) into part ([*nblk][2][cin] floats, of_conv2d_dgrad_bnp_bytes(d)
+ * bytes), for of_bn_bwd_final.  The fp32 split 3x3 input gradient with one K slice only:
+ * OF_EUNSUPPORTED (nothing launched) otherwise. */
+size_t of_conv2d_dgrad_bnp_bytes(const of_conv_desc* d);
+int of_conv2d_dgrad_add_act_bnp(const of_conv_desc* d, int precision, const float* dy, int lddy,
+                                const void* w_bwd, const float* add, int ld_add,
+                                const float* act_src, int ld_act, int act, float alpha,
+                                float* dx, int lddx, const float* bn_gamma, const float* bn_beta,
+                                const float* bn_res, int ld_bn_res, float* part,
+                                size_t part_bytes, int* nblk, void* workspace, size_t ws_bytes,
+                                void* stream);
+/* dgamma / dbeta / dbias from nblk partial rows [nblk][2][c] (sum t, sum t zhat) in a fixed
+ * order: dbeta = sum t, dgamma = sum t zhat, dbias = dbeta gamma / sqrt(var + eps);
+ * accumulate: add to the outputs. */
+int of_bn_bwd_final(const float* part, int nblk, int c, const float* gamma, const float* var,
+                    float eps, float* dgamma, float* dbeta, float* dbias, int accumulate,
+                    void* stream);
 /* BN backward reductions from t (act NONE: dy is t) or from dy (act RELU: t = dy [y > 0],
  * written to t_out if non-NULL); res: the residual added before the activation, or NULL.
  * dgamma / dbeta / dbias: [c] (NULL to skip).  Workspace: of_bn_act_bwd_workspace(npix, c). */

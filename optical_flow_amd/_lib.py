@@ -153,6 +153,10 @@ PROTOTYPES = {
     "of_conv2d_wgrad_bn_workspace": (SZ, [PD, I]),
     "of_conv2d_wgrad_bn": (I, [PD, I, P, I, P, I, P, I, P, P, F, P, SZ, P]),
     "of_conv2d_dgrad_add_act": (I, [PD, I, P, I, P, P, I, P, I, I, F, P, I, P, SZ, P]),
+    "of_conv2d_dgrad_bnp_bytes": (SZ, [PD]),
+    "of_conv2d_dgrad_add_act_bnp": (I, [PD, I, P, I, P, P, I, P, I, I, F, P, I, P, P, P, I, P,
+                                        SZ, P, P, SZ, P]),
+    "of_bn_bwd_final": (I, [P, I, I, P, P, F, P, P, P, I, P]),
     "of_bn_bwd_reduce": (I, [I64, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     "of_maxpool_bn_relu_bwd": (I, [I, I, I, I, P, P, P, P, P, P, F, P, P, P, P, I, P, P]),
     "of_conv2d_fwd_pool": (I, [PD, I, P, I, P, P, P, P, P, P, F, I, F, P, I, P, I, P, P, SZ, P]),

@@ -79,6 +79,12 @@ struct GemmArgs {
   int direct16;
   uint4* mask_out;
   const uint4* mask_in;
+  // fused BN backward partial sums (conv_tile_x3 input gradient, one K slice): the output t
+  // (the gradient at the BN layer's output, after act') is also summed per channel, with
+  // zhat = (act_src - bnp_res - beta) / gamma, into bnp [m tile][2][N] (sum t, sum t zhat)
+  float* bnp;
+  const float* bnp_res; int ld_bnp_res;
+  const float* bnp_g; const float* bnp_b;
   Group grp[MAX_GROUPS];
 };
 
@@ -92,6 +98,27 @@ __device__ __forceinline__ float dgrad_ep(const GemmArgs& a, float v, float s, f
 
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
   a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
+// Input-gradient store of one row's channel quad n (one K slice) with the BN partial sums of
+// the layer whose output is act_src: t = act'(s) (v + r) (act_post) or act'(s) v + r, then
+// sb += t, sg += t zhat with zhat = (s - res_bn - beta) / gamma (bn_act_bwd_partial<true>'s
+// recovery of the normalised value from the layer output).  ig = 1 / gamma, bt = beta.
+__device__ __forceinline__ void dgrad_store4_bnp(const GemmArgs& a, int64_t row, int n,
+                                                 float4 v4, const float4& bt, const float4& ig,
+                                                 float4& sb, float4& sg) {
+  const float4 s4 = *reinterpret_cast<const float4*>(&a.act_src[row * a.ld_act + n]);
+  float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f), q4 = r4;
+  if (a.res) r4 = *reinterpret_cast<const float4*>(&a.res[row * a.ldr + n]);
+  if (a.bnp_res) q4 = *reinterpret_cast<const float4*>(&a.bnp_res[row * a.ld_bnp_res + n]);
+  const float4 t = make_float4(dgrad_ep(a, v4.x, s4.x, r4.x), dgrad_ep(a, v4.y, s4.y, r4.y),
+                               dgrad_ep(a, v4.z, s4.z, r4.z), dgrad_ep(a, v4.w, s4.w, r4.w));
+  *reinterpret_cast<float4*>(&a.C[row * a.ldc + n]) = t;
+  add4(sb, t);
+  sg.x += t.x * ((s4.x - q4.x - bt.x) * ig.x);
+  sg.y += t.y * ((s4.y - q4.y - bt.y) * ig.y);
+  sg.z += t.z * ((s4.z - q4.z - bt.z) * ig.z);
+  sg.w += t.w * ((s4.w - q4.w - bt.w) * ig.w);
 }
 
 __device__ __forceinline__ float act_fwd(float v, int act, float alpha) {

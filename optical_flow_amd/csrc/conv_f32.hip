@@ -1422,6 +1422,12 @@ __device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
     float* E = reinterpret_cast<float*>(smem) + wave * WM * EPW;
     constexpr int LPR = 4 * EJ, RPI = 64 / LPR;            // lanes per row, rows per pass
     const int c4 = lane % LPR, rr = lane / LPR;
+    // fused BN partial sums (a.bnp: input gradient, one K slice, the host checked)
+    constexpr int NPASS = SN / EJ;
+    const bool bnp = MODE == MODE_DGRAD && a.bnp != nullptr;
+    float4 bsb[NPASS], bsg[NPASS];
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) bsb[p] = bsg[p] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int jp = 0; jp < SN; jp += EJ) {
 #pragma unroll
@@ -1453,6 +1459,23 @@ __device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
           }
           epilogue_rows4c<MODE, X3_EPB>(a, split, row, ok, n, min(n, a.N - 4), v);
         }
+      } else if (MODE == MODE_DGRAD && bnp) {
+        float4 bt = make_float4(0.f, 0.f, 0.f, 0.f), ig = bt;
+        if (n < a.N) {
+          bt = *reinterpret_cast<const float4*>(&a.bnp_b[n]);
+          const float4 gm = *reinterpret_cast<const float4*>(&a.bnp_g[n]);
+          ig = make_float4(1.f / gm.x, 1.f / gm.y, 1.f / gm.z, 1.f / gm.w);
+        }
+#pragma unroll
+        for (int q = 0; q < WM / RPI; ++q) {
+          const int m = q * RPI + rr;
+          const float4 v = *reinterpret_cast<const float4*>(&E[m * EPW + 4 * c4]);
+          const int mt = wm0 + m;
+          const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
+          if (oy < OH && ox < OW && n < a.N)
+            dgrad_store4_bnp(a, img + (int64_t)oy * OW + ox, n, v, bt, ig, bsb[jp / EJ],
+                             bsg[jp / EJ]);
+        }
       } else {
 #pragma unroll
         for (int q = 0; q < WM / RPI; ++q) {
@@ -1467,6 +1490,43 @@ __device__ __forceinline__ void tile_x3_body(const GemmArgs& a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (MODE == MODE_DGRAD && bnp) {
+      // the wave's rows (lanes c4 + LPR rr), then the WAVES_M waves of a column block in wave
+      // order through LDS, then one partial row per tile and channel: fixed order, no atomics
+      constexpr int NWM = (NT / 64) / WAVES_N;
+#pragma unroll
+      for (int p = 0; p < NPASS; ++p)
+#pragma unroll
+        for (int o = LPR; o < 64; o <<= 1) {
+          bsb[p].x += __shfl_xor(bsb[p].x, o, 64), bsb[p].y += __shfl_xor(bsb[p].y, o, 64);
+          bsb[p].z += __shfl_xor(bsb[p].z, o, 64), bsb[p].w += __shfl_xor(bsb[p].w, o, 64);
+          bsg[p].x += __shfl_xor(bsg[p].x, o, 64), bsg[p].y += __shfl_xor(bsg[p].y, o, 64);
+          bsg[p].z += __shfl_xor(bsg[p].z, o, 64), bsg[p].w += __shfl_xor(bsg[p].w, o, 64);
+        }
+      __syncthreads();                    // every wave's E image reads are done
+      float4* red = reinterpret_cast<float4*>(smem);       // [2][NWM][BN / 4]
+      const int wmi = wave / WAVES_N;
+      if (rr == 0) {
+#pragma unroll
+        for (int p = 0; p < NPASS; ++p) {
+          const int lq = (wn0 + 16 * EJ * p) / 4 + c4;
+          red[wmi * (BN / 4) + lq] = bsb[p];
+          red[(NWM + wmi) * (BN / 4) + lq] = bsg[p];
+        }
+      }
+      __syncthreads();
+      const int tid = threadIdx.x;
+      if (tid < BN / 4 && n0 + 4 * tid < a.N) {
+        float4 sb = red[tid], sg = red[NWM * (BN / 4) + tid];
+        for (int w2 = 1; w2 < NWM; ++w2) {
+          add4(sb, red[w2 * (BN / 4) + tid]);
+          add4(sg, red[(NWM + w2) * (BN / 4) + tid]);
+        }
+        float* prow = a.bnp + (int64_t)tile_m * 2 * a.N + n0 + 4 * tid;
+        *reinterpret_cast<float4*>(prow) = sb;
+        *reinterpret_cast<float4*>(prow + a.N) = sg;
+      }
     }
     return;
   }
@@ -5429,10 +5489,17 @@ int of_conv2d_fwd_bf16(const of_conv_desc* d, const float* x, int ldx, const voi
                        stream);
 }
 
+// fused BN partial sums of an input gradient (of_conv2d_dgrad_add_act_bnp)
+struct BnpArgs {
+  const float* gamma; const float* beta; const float* res; int ld_res;
+  float* part; size_t part_bytes; int* nblk;
+};
+
 static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int lddy,
                            const void* w_bwd, const float* act_src, int ld_act, int act,
                            float alpha, const float* add, int ld_add, float* dx, int lddx,
-                           void* workspace, size_t ws_bytes, void* stream, int act_post = 0) {
+                           void* workspace, size_t ws_bytes, void* stream, int act_post = 0,
+                           const BnpArgs* bnp = nullptr) {
   int st = validate(d);
   if (st) return st;
   Geo g = geo(d);
@@ -5487,6 +5554,24 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   a.vec_ep = vec_ep_ok(a);
   // split 3x3 input gradient, one K slice: the direct epilogue (conv_dev.h direct_dgrad_f32)
   a.direct16 = x3 && tile && (g_x3_direct & 2) && a.splits == 1 && a.vec_ep;
+  if (bnp) {
+    // the BN partial sums ride on conv_tile_x3's vectorised one-slice epilogue only; any other
+    // form: OF_EUNSUPPORTED before anything is launched (the caller runs the separate pass)
+    const int64_t m_tiles = a.n_tiles > 0 ? a.tiles_total / a.n_tiles : 0;
+    if (!(x3 && tile && a.splits == 1 && a.vec_ep && X3_EPB == 1 && act_src) ||
+        a.N % 4 || ((uintptr_t)bnp->gamma & 15) || ((uintptr_t)bnp->beta & 15) ||
+        ((uintptr_t)bnp->part & 15) || (bnp->res && (((uintptr_t)bnp->res & 15) || bnp->ld_res % 4)))
+      return fail(OF_EUNSUPPORTED, "conv dgrad bnp: not the one-slice split-tile input gradient");
+    OF_CHECK_ARG(bnp->gamma && bnp->beta && bnp->part && bnp->nblk, "conv dgrad bnp: args");
+    OF_CHECK_ARG(bnp->part_bytes >= (size_t)m_tiles * 2 * a.N * 4, "conv dgrad bnp: part too small");
+    a.direct16 = 0;
+    a.bnp = bnp->part;
+    a.bnp_res = bnp->res;
+    a.ld_bnp_res = bnp->ld_res;
+    a.bnp_g = bnp->gamma;
+    a.bnp_b = bnp->beta;
+    *bnp->nblk = (int)m_tiles;
+  }
   st = x3     ? (tile ? launch_tile_x3<MODE_DGRAD>(a, s, flops)
                      : launch_gemm_x3<MODE_DGRAD>(a, s, flops))
        : ws   ? launch_tile_ws<MODE_DGRAD>(a, s, flops)
@@ -5926,6 +6011,28 @@ int of_conv2d_dgrad_add_act(const of_conv_desc* d, int precision, const float* d
                "dgrad add act: act_src and a relu / leaky act");
   return conv_dgrad_impl(precision, d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, add,
                          ld_add, dx, lddx, workspace, ws_bytes, stream, 1);
+}
+
+size_t of_conv2d_dgrad_bnp_bytes(const of_conv_desc* d) {
+  if (validate(d)) return 0;
+  Geo g = geo(d);
+  GemmArgs a = tile_args(d, g, MODE_DGRAD, true);
+  return a.n_tiles > 0 ? (size_t)(a.tiles_total / a.n_tiles) * 2 * a.N * 4 : 0;
+}
+
+int of_conv2d_dgrad_add_act_bnp(const of_conv_desc* d, int precision, const float* dy, int lddy,
+                                const void* w_bwd, const float* add, int ld_add,
+                                const float* act_src, int ld_act, int act, float alpha,
+                                float* dx, int lddx, const float* bn_gamma, const float* bn_beta,
+                                const float* bn_res, int ld_bn_res, float* part,
+                                size_t part_bytes, int* nblk, void* workspace, size_t ws_bytes,
+                                void* stream) {
+  OF_CHECK_ARG(precision >= 0 && precision <= 2, "dgrad add act bnp: precision 0, 1 or 2");
+  OF_CHECK_ARG(act_src && (act == OF_ACT_RELU || act == OF_ACT_LEAKY),
+               "dgrad add act bnp: act_src and a relu / leaky act");
+  const BnpArgs b{bn_gamma, bn_beta, bn_res, ld_bn_res, part, part_bytes, nblk};
+  return conv_dgrad_impl(precision, d, dy, lddy, w_bwd, act_src, ld_act, act, alpha, add,
+                         ld_add, dx, lddx, workspace, ws_bytes, stream, 1, &b);
 }
 
 }  // extern "C"

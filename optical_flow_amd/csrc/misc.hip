@@ -769,6 +769,19 @@ int of_bn_act_bwd(int64_t npix, int c, int act, const float* dy, const float* y,
 }
 
 
+// The final pass alone, over partial rows another kernel wrote in bn_act_bwd_partial's
+// layout ([nblk][2][c]: sum t, sum t zhat) -- the input-gradient epilogue's fused partial sums
+// (of_conv2d_dgrad_add_act_bnp).
+int of_bn_bwd_final(const float* part, int nblk, int c, const float* gamma, const float* var,
+                    float eps, float* dgamma, float* dbeta, float* dbias, int accumulate,
+                    void* stream) {
+  OF_CHECK_ARG(part && gamma && var && nblk > 0 && c % 4 == 0, "bn_bwd_final: args");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(bn_act_bwd_final, dim3(cdiv(c / 4, BNF_Q)), dim3(BNF_Q * BNF_G), 0, s, part,
+                     nblk, c, gamma, var, eps, dgamma, dbeta, dbias, accumulate);
+  return check_launch("bn_bwd_final");
+}
+
 // min |x| over each of nseg segments (the BN gammas of a network, ptrs / lens in device
 // memory): one workgroup per segment, a fixed-order reduction.
 __global__ __launch_bounds__(256) void min_abs_segments_kernel(const float* const* ptrs,

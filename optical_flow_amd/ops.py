@@ -673,7 +673,7 @@ def _block_forward(a, b, p, x):
 
 
 def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx_out=None,
-                   dz_given=None, t_given=False, res_src=None, in_act=None):
+                   dz_given=None, t_given=False, res_src=None, in_act=None, bnp_out=None):
     """Backward of _conv_forward: BN/activation backward (with the residual gradient), weight
     and bias gradients, input gradient.  needs = (x, kernel, bias, gamma, beta, residual).
     add: a gradient summed into dx by the input-gradient kernel's epilogue (dx_out may be
@@ -688,7 +688,10 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
     t_given: dy already is t (the producing input-gradient kernel applied act' in its
     epilogue).  in_act = (act_src, act): multiply this layer's input gradient by the
     derivative of the activation that produced x (after the add, if any), so the layer before
-    receives its t.
+    receives its t.  bnp_out = (L, res): L is the BN layer whose output is act_src (res its
+    residual before the activation, or None): with BN_FUSE the input-gradient epilogue also
+    forms L's BN partial sums (of_conv2d_dgrad_add_act_bnp) and tags dx with them
+    (dx._oflow_bnp), and L's backward then runs only the final pass (of_bn_bwd_final).
 
     Returns (dx, d_kernel, d_bias, d_gamma, d_beta, d_residual) with None for gradients
     written straight into the gradient arena."""
@@ -720,9 +723,17 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
             dz = dy                     # already t
             # only parameter gradients come out: off the critical path (BN_REDUCE_SIDE)
             side = BN_REDUCE_SIDE and SIDE_STREAM_WGRAD and acc == 1
-            with torch.cuda.stream(side_stream(dz, y, res_src, ws, z)) if side else \
+            fused = getattr(dy, "_oflow_bnp", None)
+            if fused is not None and (fused[2] is not layer or z is not None):
+                fused = None
+            with torch.cuda.stream(side_stream(dz, y, res_src, ws, z,
+                                               fused[0] if fused else None)) if side else \
                     contextlib.nullcontext():
-                if z is not None:       # zhat from the stored z (BNZGuard)
+                if fused is not None:   # the partial sums came with t (input-grad epilogue)
+                    call("of_bn_bwd_final", _ptr(fused[0]), fused[1], layer.cout, _ptr(gamma),
+                         _ptr(var), BN_EPS, _ptr(tg[0]), _ptr(tb[0]), _ptr(tbias[0]), acc,
+                         _stream())
+                elif z is not None:     # zhat from the stored z (BNZGuard)
                     call("of_bn_act_bwd", npix, layer.cout, ACT_NONE, _ptr(dz), _ptr(y), _ptr(z),
                          _ptr(gamma), _ptr(mean), _ptr(var), BN_EPS, None, None, _ptr(tg[0]),
                          _ptr(tb[0]), _ptr(tbias[0]), acc, _ptr(ws), _stream())
@@ -771,9 +782,11 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
                     assert addc.shape == dx.shape
                 _, wsz = layer.dgrad_add_entry(d)
                 wsk, wsp, wsb = _workspace(wsz, dy.device if dy is not None else dz.device)
-                call("of_conv2d_dgrad_add_act", C.byref(d), layer.mode(d), _ptr(dzp),
-                     dzp.shape[-1], _ptr(wd), _ptr(addc), cx, _ptr(src), cx, iact,
-                     LEAKY_ALPHA, _ptr(dx), cx, wsp, wsb, s)
+                if not (bnp_out is not None and _dgrad_bnp(layer, d, dzp, wd, addc, src, iact,
+                                                           dx, cx, bnp_out, wsp, wsb, s)):
+                    call("of_conv2d_dgrad_add_act", C.byref(d), layer.mode(d), _ptr(dzp),
+                         dzp.shape[-1], _ptr(wd), _ptr(addc), cx, _ptr(src), cx, iact,
+                         LEAKY_ALPHA, _ptr(dx), cx, wsp, wsb, s)
             elif add is not None:
                 addc = add.contiguous()
                 assert addc.shape == dx.shape
@@ -842,6 +855,38 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
     return dx, ret_k, ret_b, ret_g, ret_be, dres
 
 
+# The BN backward partial sums of the layer whose output a block's input gradient carries,
+# formed by that input gradient's epilogue (conv_tile_x3, one K slice: of_conv2d_dgrad_add_act_bnp)
+# instead of a separate pass reading t, y and the residual again (OFLOW_BN_FUSE=0: the
+# separate pass everywhere).
+BN_FUSE = os.environ.get("OFLOW_BN_FUSE", "1") == "1"
+
+
+def _dgrad_bnp(layer, d, dzp, wd, addc, src, iact, dx, cx, bnp_out, wsp, wsb, s):
+    """of_conv2d_dgrad_add_act with bnp_out's BN partial sums; False (nothing launched) when
+    the kernel form cannot carry them."""
+    L, rres = bnp_out
+    if not BN_FUSE or L.bn is None or L.store_z or L.cout != cx:
+        return False
+    lib = _lib.lib()
+    pb = lib.of_conv2d_dgrad_bnp_bytes(C.byref(d))
+    if pb <= 0:
+        return False
+    part = torch.empty(pb // 4 + 4, device=dx.device)
+    nblk = C.c_int(0)
+    gamma, beta = L.bn[0], L.bn[1]
+    rres = rres.contiguous() if rres is not None else None
+    st = lib.of_conv2d_dgrad_add_act_bnp(
+        C.byref(d), layer.mode(d), _ptr(dzp), dzp.shape[-1], _ptr(wd), _ptr(addc), cx, _ptr(src),
+        cx, iact, C.c_float(LEAKY_ALPHA), _ptr(dx), cx, _ptr(gamma), _ptr(beta), _ptr(rres),
+        rres.shape[-1] if rres is not None else 0, _ptr(part), pb, C.byref(nblk), wsp, wsb, s)
+    if st == _lib.OF_EUNSUPPORTED:
+        return False
+    _lib.check(st, "of_conv2d_dgrad_add_act_bnp")
+    dx._oflow_bnp = (part, nblk.value, L)
+    return True
+
+
 class _ConvFn(torch.autograd.Function):
     """Conv2D + BiasAdd [+ FusedBatchNorm(inference)] [+ AddV2 residual] [+ Relu/LeakyRelu]
     forward; Conv2DBackpropInput / Conv2DBackpropFilter / BiasAddGrad / BN grads backward."""
@@ -886,21 +931,24 @@ class _ResBlockFn(torch.autograd.Function):
         return (dx, *grads, None)
 
 
-def _res_block_backward(block, saved, dy, need, extra=None, t_given=False, in_act=None):
+def _res_block_backward(block, saved, dy, need, extra=None, t_given=False, in_act=None,
+                        in_bnp=None):
     """Backward of one residual block.  need: needs_input_grad of (x, then kernel, bias,
     gamma, beta per layer a, b, p).  extra: a further gradient of the block input x (its
     other consumer) summed by the shortcut's input-gradient epilogue -- no separate add.
     t_given: dy already carries the block's output ReLU derivative (the next block's
     input-gradient epilogue applied it).  in_act = (x, ACT_RELU) when x is a ReLU output: the
     returned dx is then the previous block's t.  conv_b's input gradient always carries
-    conv_a's ReLU derivative (t of conv_a).  Returns (dx, [param grads of a, b, p])."""
+    conv_a's ReLU derivative (t of conv_a).  in_bnp = (the previous block's conv_b, its
+    residual): the layer whose BN partial sums conv_a's input-gradient epilogue forms
+    (BN_FUSE).  Returns (dx, [param grads of a, b, p])."""
     x, ya, za, y, zb, yp, zp = saved
     a, b, p = block
     need_x = need[0]
     nb = lambda k: tuple(need[1 + 4 * k:5 + 4 * k])     # kernel, bias, gamma, beta of layer k
     sc = yp if p is not None else x                      # residual added before b's ReLU
     dya, *gb = _conv_backward(b, ya, y, zb, dy, True, (True, *nb(1), True), t_given=t_given,
-                              res_src=sc, in_act=(ya, ACT_RELU))
+                              res_src=sc, in_act=(ya, ACT_RELU), bnp_out=(a, None))
     dres = gb[-1]                                        # = t of conv_b
     gb = gb[:-1]
     if p is not None:
@@ -920,7 +968,8 @@ def _res_block_backward(block, saved, dy, need, extra=None, t_given=False, in_ac
             call("of_add_inplace", _ptr(add), _ptr(extra.contiguous()), add.numel(), _stream())
     dx, *ga = _conv_backward(a, x, ya, za, dya, False, (need_x, *nb(0), False),
                              add=add if need_x else None, dx_out=dx_out, t_given=True,
-                             in_act=in_act if need_x else None)
+                             in_act=in_act if need_x else None,
+                             bnp_out=in_bnp if (need_x and in_act is not None) else None)
     ga = ga[:-1]
     return dx, list(ga) + list(gb) + list(gp)
 
@@ -974,9 +1023,15 @@ class _EncoderFn(torch.autograd.Function):
             nd = (True,) + tuple(need[pos[i]:pos[i] + 4 * (3 if blocks[i][2] is not None else 2)])
             # block i > 0 takes a ReLU output (block i - 1's) as input: its input gradient
             # is returned as that block's t; block 0's input is the max-pooled stem output
+            in_bnp = None
+            if i > 0:                           # block i - 1's conv_b BN: y = blk[0]
+                pa, pb_, pp = blocks[i - 1]
+                pblk = saved[3 + 7 * (i - 1):3 + 7 * i]
+                in_bnp = (pb_, pblk[5] if pp is not None else pblk[0])
             dy, g = _res_block_backward(blocks[i], blk, dy, nd, extra=extra,
                                         t_given=i < nbk - 1,
-                                        in_act=(blk[0], ACT_RELU) if i > 0 else None)
+                                        in_act=(blk[0], ACT_RELU) if i > 0 else None,
+                                        in_bnp=in_bnp)
             grads = list(g) + grads
         # stem: max-pool backward + out0's decoder gradient + BN/ReLU backward, one pass
         n, h, w, c = y0.shape

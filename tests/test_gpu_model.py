@@ -78,6 +78,43 @@ def test_corr_df1_side_stream(monkeypatch):
         assert rel_l2(res[1][k], res[0][k]) < 1e-5, k
 
 
+@pytest.mark.parametrize("H,W,B,fused", [(64, 128, 2, False), (384, 512, 8, True)])
+def test_bn_fused_partials(monkeypatch, H, W, B, fused):
+    """ops.BN_FUSE (the encoder's BN backward partial sums formed by the input-gradient
+    epilogue that produces t, of_conv2d_dgrad_add_act_bnp, then of_bn_bwd_final) against the
+    separate reduction pass: the input and weight gradients bit for bit (the epilogue stores
+    the same t), the BN gamma / beta and conv bias gradients within fp32 summation-order noise
+    (another order of the same sums).  At the bench size the one-slice input gradients of the
+    encoder carry the partials (asserted); at the small size every one is K-split, so the
+    library declines (OF_EUNSUPPORTED) and the separate pass runs."""
+    from optical_flow_amd import ops
+    from optical_flow_amd.loss import LossLayer
+    net, vals, batch, blocks = _setup(H, W, B, seed=7)
+    bd = dev(torch.from_numpy(batch))
+    res, ran = [], []
+    orig = ops._dgrad_bnp
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        ran.append(r)
+        return r
+    monkeypatch.setattr(ops, "_dgrad_bnp", spy)
+    for fuse in (False, True):
+        monkeypatch.setattr(ops, "BN_FUSE", fuse)
+        net.store.zero_grad()
+        flows = net(bd)
+        LossLayer()(bd, flows).backward()
+        torch.cuda.synchronize()
+        res.append({k: g.detach().clone() for k, g in net.store.grads().items()})
+    assert any(ran) == fused, ran
+    bn_like = ("gamma", "beta", "bias")
+    for k in res[0]:
+        if any(t in k for t in bn_like) and "ResNet18" in k:
+            assert rel_l2(res[1][k], res[0][k]) < 1e-5, (k, rel_l2(res[1][k], res[0][k]))
+        else:
+            assert torch.equal(res[1][k], res[0][k]), k
+
+
 def test_train_steps_trajectory():
     from optical_flow_amd.train import KerasAdam, Trainer
     net, vals, batch, blocks = _setup(64, 128, 2, seed=3)
