@@ -432,7 +432,9 @@ int of_timing_enable(int on);
  * in flight (0); bitwise the same results;
  * key 31 = the stem forward (conv_stem_x3) persistent over its tiles with this many workgroups
  * per CU (-1 = default: as many as the LDS holds, 2 fp32 / 3 bf16; 0 = one tile per
- * workgroup); bitwise the same results. */
+ * workgroup); bitwise the same results;
+ * key 32 = bf16 input gradients that carry BN partial sums (of_conv2d_dgrad_add_act_bnp) on
+ * conv_tile_b16 (1) or declined with OF_EUNSUPPORTED (0, default: the separate pass). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -5054,6 +5054,13 @@ static int g_wgrad_wgs = 4;
 // the per-pass transposes.  Default 1: the input gradient's measured slower (per layer dec3.c1
 // 0.506 -> 0.531 ms, c2 0.413 -> 0.426; fp32 step 651.8 -> 650.6 pairs/s, profiles/r4_late/step_ab.txt).
 static int g_x3_direct = 1;
+// of_set_tuning key 32: bf16 input gradients that carry BN partial sums
+// (of_conv2d_dgrad_add_act_bnp) on conv_tile_b16, whose one-slice vectorised epilogue forms
+// them (1), or declined (0, default: the caller's separate reduction pass, conv_tile_bf16).
+// Measured (bf16 B = 32 bench, one box, two interleaved rounds): 1750.1 / 1750.9 pairs/s
+// declined, 1721.6 / 1716.3 fused -- conv_tile_b16 loses more on these input gradients than
+// the side-stream reductions cost.
+static int g_bnp_b16 = 0;
 
 // of_set_tuning key 16: which bf16 implicit GEMMs (stride-2 block convs, 1x1 projections; the
 // stem when key 15 = 0) run on the one-plane conv_gemm_x3 / conv_wgrad_x3 forms instead of
@@ -5258,6 +5265,7 @@ int of_set_tuning(int key, int value) {
   if (key == 29 && value >= 0 && value <= 4) { g_wgr_lanes = value; return OF_OK; }
   if (key == 30 && value >= 0 && value <= 2) { g_gx3_ring = value; return OF_OK; }
   if (key == 31 && value >= -1 && value <= 8) { g_stem_persist = value; return OF_OK; }
+  if (key == 32 && (value == 0 || value == 1)) { g_bnp_b16 = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -5525,7 +5533,8 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   const bool tile = (bf16 || x3) && tile_ok(d);
   const bool in_place = add && add == dx && ld_add == lddx;
   const bool ws = tile && bf16 && ws_ok(d, MODE_DGRAD);
-  const bool b16 = tile && bf16 && g_tile_b16 == 1;
+  // (bf16 with BN partial sums: conv_tile_b16, the split kernels' body with one plane)
+  const bool b16 = tile && bf16 && !ws && (g_tile_b16 == 1 || (bnp && g_bnp_b16));
   GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3, b16, ws)
                     : dgrad_args(d, g, bf16 || x3, in_place);
   const bool g16 = bf16 && !tile && (g_gemm_b16 & 2);       // conv_gemm_x3<..., 1>
@@ -5558,7 +5567,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
     // the BN partial sums ride on conv_tile_x3's vectorised one-slice epilogue only; any other
     // form: OF_EUNSUPPORTED before anything is launched (the caller runs the separate pass)
     const int64_t m_tiles = a.n_tiles > 0 ? a.tiles_total / a.n_tiles : 0;
-    if (!(x3 && tile && a.splits == 1 && a.vec_ep && X3_EPB == 1 && act_src) ||
+    if (!((x3 || b16) && tile && a.splits == 1 && a.vec_ep && X3_EPB == 1 && act_src) ||
         a.N % 4 || ((uintptr_t)bnp->gamma & 15) || ((uintptr_t)bnp->beta & 15) ||
         ((uintptr_t)bnp->part & 15) || (bnp->res && (((uintptr_t)bnp->res & 15) || bnp->ld_res % 4)))
       return fail(OF_EUNSUPPORTED, "conv dgrad bnp: not the one-slice split-tile input gradient");
@@ -6016,8 +6025,12 @@ int of_conv2d_dgrad_add_act(const of_conv_desc* d, int precision, const float* d
 size_t of_conv2d_dgrad_bnp_bytes(const of_conv_desc* d) {
   if (validate(d)) return 0;
   Geo g = geo(d);
-  GemmArgs a = tile_args(d, g, MODE_DGRAD, true);
-  return a.n_tiles > 0 ? (size_t)(a.tiles_total / a.n_tiles) * 2 * a.N * 4 : 0;
+  size_t bytes = 0;
+  for (int x3 = 0; x3 < 2; ++x3) {           // the split kernel's tiles, conv_tile_b16's
+    GemmArgs a = tile_args(d, g, MODE_DGRAD, x3, !x3);
+    if (a.n_tiles > 0) bytes = std::max(bytes, (size_t)(a.tiles_total / a.n_tiles) * 2 * a.N * 4);
+  }
+  return bytes;
 }
 
 int of_conv2d_dgrad_add_act_bnp(const of_conv_desc* d, int precision, const float* dy, int lddy,

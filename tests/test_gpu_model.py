@@ -78,18 +78,27 @@ def test_corr_df1_side_stream(monkeypatch):
         assert rel_l2(res[1][k], res[0][k]) < 1e-5, k
 
 
-@pytest.mark.parametrize("H,W,B,fused", [(64, 128, 2, False), (384, 512, 8, True)])
-def test_bn_fused_partials(monkeypatch, H, W, B, fused):
+@pytest.mark.parametrize("H,W,B,fused,prec", [(64, 128, 2, False, "fp32"),
+                                               (384, 512, 8, True, "fp32"),
+                                               (384, 512, 8, True, "bf16"),
+                                               (128, 256, 2, None, "bf16")])
+def test_bn_fused_partials(monkeypatch, H, W, B, fused, prec):
     """ops.BN_FUSE (the encoder's BN backward partial sums formed by the input-gradient
     epilogue that produces t, of_conv2d_dgrad_add_act_bnp, then of_bn_bwd_final) against the
     separate reduction pass: the input and weight gradients bit for bit (the epilogue stores
     the same t), the BN gamma / beta and conv bias gradients within fp32 summation-order noise
     (another order of the same sums).  At the bench size the one-slice input gradients of the
     encoder carry the partials (asserted); at the small size every one is K-split, so the
-    library declines (OF_EUNSUPPORTED) and the separate pass runs."""
-    from optical_flow_amd import ops
+    library declines (OF_EUNSUPPORTED) and the separate pass runs.  bf16: the fused input
+    gradients run on conv_tile_b16 (of_set_tuning key 32 = 1, off by default: measured slower);
+    both runs put every bf16 3x3 layer on it (key 12 = 1) so that the input gradients come from
+    the same kernel."""
+    from optical_flow_amd import _lib, ops
     from optical_flow_amd.loss import LossLayer
     net, vals, batch, blocks = _setup(H, W, B, seed=7)
+    lib = _lib.lib()
+    if prec == "bf16":
+        net.set_precision("bf16")
     bd = dev(torch.from_numpy(batch))
     res, ran = [], []
     orig = ops._dgrad_bnp
@@ -99,14 +108,20 @@ def test_bn_fused_partials(monkeypatch, H, W, B, fused):
         ran.append(r)
         return r
     monkeypatch.setattr(ops, "_dgrad_bnp", spy)
-    for fuse in (False, True):
-        monkeypatch.setattr(ops, "BN_FUSE", fuse)
-        net.store.zero_grad()
-        flows = net(bd)
-        LossLayer()(bd, flows).backward()
-        torch.cuda.synchronize()
-        res.append({k: g.detach().clone() for k, g in net.store.grads().items()})
-    assert any(ran) == fused, ran
+    try:
+        assert lib.of_set_tuning(12, 1 if prec == "bf16" else 0) == 0
+        assert lib.of_set_tuning(32, 1 if prec == "bf16" else 0) == 0
+        for fuse in (False, True):
+            monkeypatch.setattr(ops, "BN_FUSE", fuse)
+            net.store.zero_grad()
+            flows = net(bd)
+            LossLayer()(bd, flows).backward()
+            torch.cuda.synchronize()
+            res.append({k: g.detach().clone() for k, g in net.store.grads().items()})
+    finally:
+        lib.of_set_tuning(12, 0)                    # the defaults
+        lib.of_set_tuning(32, 0)
+    assert fused is None or any(ran) == fused, ran
     bn_like = ("gamma", "beta", "bias")
     for k in res[0]:
         if any(t in k for t in bn_like) and "ResNet18" in k:
