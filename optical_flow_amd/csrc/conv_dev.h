@@ -344,6 +344,37 @@ __device__ __forceinline__ void epilogue_rows4c(const GemmArgs& a, int split, co
   }
 }
 
+// epilogue_rows4c's input gradient (one K slice) with dgrad_store4_bnp's BN partial sums: the
+// act' source, added-gradient and BN residual quads of all R rows loaded (clamped, unmasked)
+// before the first store; stores and sums masked by ok.
+template <int R>
+__device__ __forceinline__ void dgrad_rows4c_bnp(const GemmArgs& a, const int64_t* row,
+                                                 unsigned ok, int n, int nl, const float4* v,
+                                                 const float4& bt, const float4& ig, float4& sb,
+                                                 float4& sg) {
+  float4 s4[R], r4[R], q4[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    s4[r] = *reinterpret_cast<const float4*>(&a.act_src[row[r] * a.ld_act + nl]);
+    r4[r] = a.res ? *reinterpret_cast<const float4*>(&a.res[row[r] * a.ldr + nl])
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    q4[r] = a.bnp_res ? *reinterpret_cast<const float4*>(&a.bnp_res[row[r] * a.ld_bnp_res + nl])
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (!((ok >> r) & 1)) continue;
+    const float4 t = make_float4(dgrad_ep(a, v[r].x, s4[r].x, r4[r].x), dgrad_ep(a, v[r].y, s4[r].y, r4[r].y),
+                                 dgrad_ep(a, v[r].z, s4[r].z, r4[r].z), dgrad_ep(a, v[r].w, s4[r].w, r4[r].w));
+    *reinterpret_cast<float4*>(&a.C[row[r] * a.ldc + n]) = t;
+    add4(sb, t);
+    sg.x += t.x * ((s4[r].x - q4[r].x - bt.x) * ig.x);
+    sg.y += t.y * ((s4[r].y - q4[r].y - bt.y) * ig.y);
+    sg.z += t.z * ((s4[r].z - q4[r].z - bt.z) * ig.z);
+    sg.w += t.w * ((s4[r].w - q4[r].w - bt.w) * ig.w);
+  }
+}
+
 // One wave's 32 x 32 accumulator block in the v_mfma_f32_32x32x* layout (column lane & 31,
 // rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) through a private 4 KB LDS image E, back as
 // float4 rows: f(row 0..31, column quad 0..7, value) for the 4 rows x 1 quad each lane owns.

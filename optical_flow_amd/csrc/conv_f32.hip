@@ -1027,6 +1027,76 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N, 256 / (32 * WAVES_M * WAVES
         });
     return;
   }
+  if (MODE == MODE_DGRAD && a.vec_ep && a.bnp != nullptr) {
+    // the same with the BN partial sums of the layer whose output is act_src (one K slice,
+    // host-checked): per lane its column quads' sums over its rows, then over the lanes of a
+    // column quad (shuffles), the WAVES_M waves of a column block in wave order (LDS), one
+    // partial row per output tile and channel -- fixed order, no atomics
+    float* E = reinterpret_cast<float*>(smem) + wave * 1024;
+    const int c4 = lane & 7;
+    float4 bsb[TN], bsg[TN], bt[TN], ig[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bsb[j] = bsg[j] = bt[j] = ig[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int n = n0 + wn0 + 32 * j + 4 * c4;
+      if (n < a.N) {
+        bt[j] = *reinterpret_cast<const float4*>(&a.bnp_b[n]);
+        const float4 gm = *reinterpret_cast<const float4*>(&a.bnp_g[n]);
+        ig[j] = make_float4(1.f / gm.x, 1.f / gm.y, 1.f / gm.z, 1.f / gm.w);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float4 vv[4];
+        int64_t rows[4];
+        unsigned ok = 0;
+        int ncol = 0;
+        transpose32(E, acc[i][j], lane, [&](int row, int c4r, float4 v) {
+          const int q = row >> 3;
+          const int mt = wm0 + 32 * i + row, n = n0 + wn0 + 32 * j + 4 * c4r;
+          const int oy = oy0 + mt / TF_W, ox = ox0 + mt % TF_W;
+          rows[q] = img + (int64_t)min(oy, OH - 1) * OW + min(ox, OW - 1);
+          ok |= (oy < OH && ox < OW && n < a.N ? 1u : 0u) << q;
+          vv[q] = v;
+          ncol = n;
+        });
+        dgrad_rows4c_bnp<4>(a, rows, ok, ncol, min(ncol, a.N - 4), vv, bt[j], ig[j], bsb[j], bsg[j]);
+      }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        bsb[j].x += __shfl_xor(bsb[j].x, o, 64), bsb[j].y += __shfl_xor(bsb[j].y, o, 64);
+        bsb[j].z += __shfl_xor(bsb[j].z, o, 64), bsb[j].w += __shfl_xor(bsb[j].w, o, 64);
+        bsg[j].x += __shfl_xor(bsg[j].x, o, 64), bsg[j].y += __shfl_xor(bsg[j].y, o, 64);
+        bsg[j].z += __shfl_xor(bsg[j].z, o, 64), bsg[j].w += __shfl_xor(bsg[j].w, o, 64);
+      }
+    __syncthreads();                      // every wave's E image reads are done
+    float4* red = reinterpret_cast<float4*>(smem);   // [2][WAVES_M][BN / 4]
+    const int wmi = wave / WAVES_N;
+    if (lane < 8) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int lq = (wn0 + 32 * j) / 4 + c4;
+        red[wmi * (BN / 4) + lq] = bsb[j];
+        red[(WAVES_M + wmi) * (BN / 4) + lq] = bsg[j];
+      }
+    }
+    __syncthreads();
+    if (tid < BN / 4 && n0 + 4 * tid < a.N) {
+      float4 sb = red[tid], sg = red[WAVES_M * (BN / 4) + tid];
+      for (int w2 = 1; w2 < WAVES_M; ++w2) {
+        add4(sb, red[w2 * (BN / 4) + tid]);
+        add4(sg, red[(WAVES_M + w2) * (BN / 4) + tid]);
+      }
+      float* prow = a.bnp + (int64_t)tile_m * 2 * a.N + n0 + 4 * tid;
+      *reinterpret_cast<float4*>(prow) = sb;
+      *reinterpret_cast<float4*>(prow + a.N) = sg;
+    }
+    return;
+  }
   if (a.vec_ep) {   // 16-byte rows through LDS (the loop's last barrier freed the images)
     float* E = reinterpret_cast<float*>(smem) + wave * 1024;
 #pragma unroll
@@ -5533,7 +5603,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   const bool tile = (bf16 || x3) && tile_ok(d);
   const bool in_place = add && add == dx && ld_add == lddx;
   const bool ws = tile && bf16 && ws_ok(d, MODE_DGRAD);
-  // (bf16 with BN partial sums: conv_tile_b16, the split kernels' body with one plane)
+  // (bf16 with BN partial sums and key 32: conv_tile_b16, the split body with one plane)
   const bool b16 = tile && bf16 && !ws && (g_tile_b16 == 1 || (bnp && g_bnp_b16));
   GemmArgs a = tile ? tile_args(d, g, MODE_DGRAD, x3, b16, ws)
                     : dgrad_args(d, g, bf16 || x3, in_place);
@@ -5567,7 +5637,9 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
     // the BN partial sums ride on conv_tile_x3's vectorised one-slice epilogue only; any other
     // form: OF_EUNSUPPORTED before anything is launched (the caller runs the separate pass)
     const int64_t m_tiles = a.n_tiles > 0 ? a.tiles_total / a.n_tiles : 0;
-    if (!((x3 || b16) && tile && a.splits == 1 && a.vec_ep && X3_EPB == 1 && act_src) ||
+    // (conv_tile_x3 / conv_tile_b16 with X3_EPB 1, or conv_tile_bf16 with EPC_BATCH)
+    const bool form = x3 || b16 ? X3_EPB == 1 : bf16 && !ws && EPC_BATCH;
+    if (!(form && tile && a.splits == 1 && a.vec_ep && act_src) ||
         a.N % 4 || ((uintptr_t)bnp->gamma & 15) || ((uintptr_t)bnp->beta & 15) ||
         ((uintptr_t)bnp->part & 15) || (bnp->res && (((uintptr_t)bnp->res & 15) || bnp->ld_res % 4)))
       return fail(OF_EUNSUPPORTED, "conv dgrad bnp: not the one-slice split-tile input gradient");
@@ -6026,8 +6098,8 @@ size_t of_conv2d_dgrad_bnp_bytes(const of_conv_desc* d) {
   if (validate(d)) return 0;
   Geo g = geo(d);
   size_t bytes = 0;
-  for (int x3 = 0; x3 < 2; ++x3) {           // the split kernel's tiles, conv_tile_b16's
-    GemmArgs a = tile_args(d, g, MODE_DGRAD, x3, !x3);
+  for (int f = 0; f < 3; ++f) {   // the tiles of conv_tile_x3, conv_tile_b16, conv_tile_bf16
+    GemmArgs a = tile_args(d, g, MODE_DGRAD, f == 0, f == 1);
     if (a.n_tiles > 0) bytes = std::max(bytes, (size_t)(a.tiles_total / a.n_tiles) * 2 * a.N * 4);
   }
   return bytes;

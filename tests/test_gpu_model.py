@@ -81,6 +81,7 @@ def test_corr_df1_side_stream(monkeypatch):
 @pytest.mark.parametrize("H,W,B,fused,prec", [(64, 128, 2, False, "fp32"),
                                                (384, 512, 8, True, "fp32"),
                                                (384, 512, 8, True, "bf16"),
+                                               (384, 512, 8, True, "bf16_b16"),
                                                (128, 256, 2, None, "bf16")])
 def test_bn_fused_partials(monkeypatch, H, W, B, fused, prec):
     """ops.BN_FUSE (the encoder's BN backward partial sums formed by the input-gradient
@@ -90,14 +91,14 @@ def test_bn_fused_partials(monkeypatch, H, W, B, fused, prec):
     (another order of the same sums).  At the bench size the one-slice input gradients of the
     encoder carry the partials (asserted); at the small size every one is K-split, so the
     library declines (OF_EUNSUPPORTED) and the separate pass runs.  bf16: the fused input
-    gradients run on conv_tile_b16 (of_set_tuning key 32 = 1, off by default: measured slower);
-    both runs put every bf16 3x3 layer on it (key 12 = 1) so that the input gradients come from
-    the same kernel."""
+    gradients run on conv_tile_bf16 (the default), or with bf16_b16 on conv_tile_b16
+    (of_set_tuning key 32 = 1, off by default: measured slower), where both runs put every bf16
+    3x3 layer (key 12 = 1) so that the input gradients come from the same kernel."""
     from optical_flow_amd import _lib, ops
     from optical_flow_amd.loss import LossLayer
     net, vals, batch, blocks = _setup(H, W, B, seed=7)
     lib = _lib.lib()
-    if prec == "bf16":
+    if prec != "fp32":
         net.set_precision("bf16")
     bd = dev(torch.from_numpy(batch))
     res, ran = [], []
@@ -109,8 +110,8 @@ def test_bn_fused_partials(monkeypatch, H, W, B, fused, prec):
         return r
     monkeypatch.setattr(ops, "_dgrad_bnp", spy)
     try:
-        assert lib.of_set_tuning(12, 1 if prec == "bf16" else 0) == 0
-        assert lib.of_set_tuning(32, 1 if prec == "bf16" else 0) == 0
+        assert lib.of_set_tuning(12, 1 if prec == "bf16_b16" else 0) == 0
+        assert lib.of_set_tuning(32, 1 if prec == "bf16_b16" else 0) == 0
         for fuse in (False, True):
             monkeypatch.setattr(ops, "BN_FUSE", fuse)
             net.store.zero_grad()
