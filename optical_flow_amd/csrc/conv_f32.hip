@@ -2318,6 +2318,17 @@ void conv_gemm_x3(GemmArgs a) {
       return;
     }
     constexpr int NQ = WM / RPI, GR = NQ % 4 == 0 ? 4 : NQ % 2 == 0 ? 2 : 1;
+    const bool bnp = MODE == MODE_DGRAD && a.bnp != nullptr;
+    // input gradient with the BN partial sums of the layer whose output is act_src (one K
+    // slice, host-checked): the lane's column quad over its rows (dgrad_rows4c_bnp), then over
+    // the lanes of the quad (shuffles) and the WAVES_M waves of the column block in wave order
+    // (LDS): one partial row per output tile (tile_mg, over the phase groups) and channel
+    float4 bt = make_float4(0.f, 0.f, 0.f, 0.f), ig = bt, bsb = bt, bsg = bt;
+    if (bnp && n < a.N) {
+      bt = *reinterpret_cast<const float4*>(&a.bnp_b[n]);
+      const float4 gm = *reinterpret_cast<const float4*>(&a.bnp_g[n]);
+      ig = make_float4(1.f / gm.x, 1.f / gm.y, 1.f / gm.z, 1.f / gm.w);
+    }
 #pragma unroll
     for (int q0 = 0; q0 < NQ; q0 += GR) {
       float4 v[GR];
@@ -2331,7 +2342,39 @@ void conv_gemm_x3(GemmArgs a) {
         row[g] = out_row(a, G, min(m, M - 1));           // clamped: the loads stay in range
         ok |= (m < M && n < a.N ? 1u : 0u) << g;
       }
-      epilogue_rows4c<MODE, GR>(a, 0, row, ok, n, min(n, a.N - 4), v);
+      if (bnp) {                         // (row by row: GR rows of three operand quads raised
+#pragma unroll                                // the kernel's VGPRs past the two-workgroup budget)
+        for (int g = 0; g < GR; ++g)
+          dgrad_rows4c_bnp<1>(a, &row[g], (ok >> g) & 1u, n, min(n, a.N - 4), &v[g], bt, ig, bsb, bsg);
+      } else
+        epilogue_rows4c<MODE, GR>(a, 0, row, ok, n, min(n, a.N - 4), v);
+    }
+    if (MODE == MODE_DGRAD && bnp) {
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        bsb.x += __shfl_xor(bsb.x, o, 64), bsb.y += __shfl_xor(bsb.y, o, 64);
+        bsb.z += __shfl_xor(bsb.z, o, 64), bsb.w += __shfl_xor(bsb.w, o, 64);
+        bsg.x += __shfl_xor(bsg.x, o, 64), bsg.y += __shfl_xor(bsg.y, o, 64);
+        bsg.z += __shfl_xor(bsg.z, o, 64), bsg.w += __shfl_xor(bsg.w, o, 64);
+      }
+      __syncthreads();                    // every wave's E image reads are done
+      float4* red = reinterpret_cast<float4*>(smem);   // [2][WAVES_M][BN / 4]
+      const int wmi = wave / WAVES_N;
+      if (rr == 0) {
+        red[wmi * (BN / 4) + wn0 / 4 + c4] = bsb;
+        red[(WAVES_M + wmi) * (BN / 4) + wn0 / 4 + c4] = bsg;
+      }
+      __syncthreads();
+      if (tid < BN / 4 && n0 + 4 * tid < a.N) {
+        float4 sb = red[tid], sg = red[WAVES_M * (BN / 4) + tid];
+        for (int w2 = 1; w2 < WAVES_M; ++w2) {
+          add4(sb, red[w2 * (BN / 4) + tid]);
+          add4(sg, red[(WAVES_M + w2) * (BN / 4) + tid]);
+        }
+        float* prow = a.bnp + (int64_t)tile_mg * 2 * a.N + n0 + 4 * tid;
+        *reinterpret_cast<float4*>(prow) = sb;
+        *reinterpret_cast<float4*>(prow + a.N) = sg;
+      }
     }
     return;
   }
@@ -5609,7 +5652,8 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
                     : dgrad_args(d, g, bf16 || x3, in_place);
   const bool g16 = bf16 && !tile && (g_gemm_b16 & 2);       // conv_gemm_x3<..., 1>
   if ((x3 || g16) && !tile) gemm_x3_plan(a);
-  if (a.tiles_total == 0) return OF_OK;                 // every output already final
+  if (a.tiles_total == 0)                                // every output already final
+    return bnp ? fail(OF_EUNSUPPORTED, "conv dgrad bnp: no GEMM tiles") : OF_OK;
   attach_slab(a, workspace, ws_bytes, tile ? 1 : (bf16 || x3) ? BKH : BK);
   a.A = dy;
   a.lda = lddy;
@@ -5637,9 +5681,14 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
     // the BN partial sums ride on conv_tile_x3's vectorised one-slice epilogue only; any other
     // form: OF_EUNSUPPORTED before anything is launched (the caller runs the separate pass)
     const int64_t m_tiles = a.n_tiles > 0 ? a.tiles_total / a.n_tiles : 0;
-    // (conv_tile_x3 / conv_tile_b16 with X3_EPB 1, or conv_tile_bf16 with EPC_BATCH)
-    const bool form = x3 || b16 ? X3_EPB == 1 : bf16 && !ws && EPC_BATCH;
-    if (!(form && tile && a.splits == 1 && a.vec_ep && act_src) ||
+    // (conv_tile_x3 / conv_tile_b16 with X3_EPB 1, conv_tile_bf16 or the split conv_gemm_x3
+    // with EPC_BATCH; the GEMM's phase groups must produce every input-gradient pixel.  The
+    // bf16 GEMM form measured 1780 -> 1726 pairs/s on the bf16 B = 32 step: declined)
+    int64_t rows = 0;
+    for (int gq = 0; gq < a.ngroups; ++gq) rows += a.grp[gq].M;
+    const bool form = tile ? (x3 || b16 ? X3_EPB == 1 : bf16 && !ws && EPC_BATCH)
+                           : x3 && EPC_BATCH && rows == (int64_t)d->n * d->h * d->w;
+    if (!(form && a.splits == 1 && a.vec_ep && act_src) ||
         a.N % 4 || ((uintptr_t)bnp->gamma & 15) || ((uintptr_t)bnp->beta & 15) ||
         ((uintptr_t)bnp->part & 15) || (bnp->res && (((uintptr_t)bnp->res & 15) || bnp->ld_res % 4)))
       return fail(OF_EUNSUPPORTED, "conv dgrad bnp: not the one-slice split-tile input gradient");
@@ -6098,8 +6147,14 @@ size_t of_conv2d_dgrad_bnp_bytes(const of_conv_desc* d) {
   if (validate(d)) return 0;
   Geo g = geo(d);
   size_t bytes = 0;
-  for (int f = 0; f < 3; ++f) {   // the tiles of conv_tile_x3, conv_tile_b16, conv_tile_bf16
-    GemmArgs a = tile_args(d, g, MODE_DGRAD, f == 0, f == 1);
+  for (int f = 0; f < 3; ++f) {   // conv_tile_x3, conv_tile_b16, conv_tile_bf16 / the GEMM
+    GemmArgs a;
+    if (tile_ok(d)) {
+      a = tile_args(d, g, MODE_DGRAD, f == 0, f == 1);
+    } else {
+      a = dgrad_args(d, g, true, f == 1);
+      gemm_x3_plan(a);
+    }
     if (a.n_tiles > 0) bytes = std::max(bytes, (size_t)(a.tiles_total / a.n_tiles) * 2 * a.N * 4);
   }
   return bytes;
