@@ -1864,3 +1864,64 @@ def test_warp_bwd_det_nonfinite_flow():
     assert not torch.isfinite(res[False][0]).all()       # (the atomic form's NaN rows)
     assert not torch.isfinite(res[True][0]).all()
     assert torch.isnan(res[True][1][0, 5, 7]).any() and torch.isnan(res[False][1][0, 5, 7]).any()
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout,stride,prec,res", [
+    (8, 96, 128, 64, 64, 1, "fp32", False),      # conv_tile_x3 one slice
+    (8, 96, 128, 64, 64, 1, "fp32", True),       # + the BN layer's residual
+    (16, 96, 128, 64, 128, 2, "fp32", True),     # conv_gemm_x3, stride-2 phase groups
+    (8, 96, 128, 64, 64, 1, "bf16", True),       # conv_tile_bf16
+])
+def test_dgrad_bnp_partials(n, h, w, cin, cout, stride, prec, res):
+    """of_conv2d_dgrad_add_act_bnp + of_bn_bwd_final: the input gradient t bitwise equal to
+    of_conv2d_dgrad_add_act's, and the BN gradients of the layer whose output is act_src
+    (inference BN, FusedBatchNormGrad: dbeta = sum t, dgamma = sum t zhat with zhat =
+    (y - res - beta) / gamma, dbias = dgamma's scale s = gamma / sqrt(var + eps) times sum t)
+    against a float64 reduction of that t, within 1e-5."""
+    import ctypes as C
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_RELU, call
+    lib = _lib.lib()
+    wt = dev(rng_tensor((3, 3, cin, cout), 71, scale=(2.0 / (9 * cin)) ** 0.5))
+    b = dev(rng_tensor((cout,), 72, scale=0.1))
+    layer = ops.ConvLayer(wt, b, stride=stride, act=ACT_RELU, cin_p=cin, precision=prec)
+    d = layer.desc(n, h, w)
+    _, wd = layer.packed(d)
+    dy = dev(rng_tensor((n, d.ho, d.wo, cout), 73))
+    y = torch.relu(dev(rng_tensor((n, h, w, cin), 74)))            # the BN layer's output
+    add = dev(rng_tensor((n, h, w, cin), 75))
+    gamma = dev(rng_tensor((cin,), 76, scale=0.5)) + 1.0
+    beta = dev(rng_tensor((cin,), 77, scale=0.2))
+    var = dev(rng_tensor((cin,), 78, scale=0.1)).abs() + 0.5
+    rres = dev(rng_tensor((n, h, w, cin), 79)) if res else None
+    _, wsz = layer.dgrad_add_entry(d)
+    ws = torch.empty(max(wsz, 4) // 4 + 4, device="cuda")
+    P, st = ops._ptr, ops._stream()
+    dx0 = torch.empty(n, h, w, cin, device="cuda")
+    call("of_conv2d_dgrad_add_act", C.byref(d), layer.mode(d), P(dy), cout, P(wd), P(add), cin,
+         P(y), cin, ACT_RELU, 0.0, P(dx0), cin, P(ws), wsz, st)
+    pb = lib.of_conv2d_dgrad_bnp_bytes(C.byref(d))
+    assert pb > 0
+    part = torch.empty(pb // 4 + 4, device="cuda")
+    nblk = C.c_int(0)
+    dx = torch.empty_like(dx0)
+    rc = lib.of_conv2d_dgrad_add_act_bnp(
+        C.byref(d), layer.mode(d), P(dy), cout, P(wd), P(add), cin, P(y), cin, ACT_RELU,
+        C.c_float(0.0), P(dx), cin, P(gamma), P(beta), P(rres), cin if res else 0, P(part), pb,
+        C.byref(nblk), P(ws), wsz, st)
+    assert rc == 0, lib.of_last_error()
+    assert nblk.value > 0
+    out = [torch.zeros(cin, device="cuda") for _ in range(3)]
+    call("of_bn_bwd_final", P(part), nblk.value, cin, P(gamma), P(var), 1e-3, P(out[0]),
+         P(out[1]), P(out[2]), 0, st)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx0)
+    t = f64(dx).reshape(-1, cin)
+    zhat = (f64(y) - (f64(rres) if res else 0.0) - f64(beta)).reshape(-1, cin) / f64(gamma)
+    s = f64(gamma) / torch.sqrt(f64(var) + 1e-3)
+    want = ((t * zhat).sum(0), t.sum(0), t.sum(0) * s)
+    for name, got, ref in zip(("dgamma", "dbeta", "dbias"), out, want):
+        e = rel_l2(got, ref)
+        print("%s %s rel_l2 %.2e" % (prec, name, e))
+        assert e < 1e-5, (name, e)
