@@ -694,8 +694,19 @@ int of_comm_info(const of_comm* comm, int* nranks, int* rank, int* device);
  * `stream` and ordered after the work already on it; returns without waiting. */
 int of_comm_allreduce_async(of_comm* comm, const float* send, float* recv, int64_t count,
                             void* stream);
-/* OF_OK unless the communicator has failed asynchronously. */
+/* The same with the reduction chosen: OF_REDUCE_SUM (the gradient buckets; the 1/N average
+ * is folded into the Adam launch) or OF_REDUCE_AVG (recv = the mean over ranks: the BN moving
+ * statistics of bn_mode "training", once per data-parallel step). */
+#define OF_REDUCE_SUM 0
+#define OF_REDUCE_AVG 1
+int of_comm_allreduce_ex_async(of_comm* comm, const float* send, float* recv, int64_t count,
+                               int op, void* stream);
+/* OF_OK unless the communicator has failed asynchronously (or was aborted). */
 int of_comm_async_error(of_comm* comm);
+/* Aborts the communicator's in-flight operations (ncclCommAbort) WITHOUT freeing the handle:
+ * safe from a watchdog thread while the owner may still hold the handle -- every later call
+ * on it returns an error, and the owner frees it with of_comm_destroy. */
+int of_comm_abort(of_comm* comm);
 /* Frees the communicator (abort != 0: without waiting for in-flight operations). */
 int of_comm_destroy(of_comm* comm, int abort);
 

@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OFLOW_LIB") or os.path.join(HERE, "liboflow.so")
 
 OF_OK, OF_EINVAL, OF_EHIP, OF_EUNSUPPORTED, OF_ETIMEOUT = 0, 1, 2, 3, 4
+OF_REDUCE_SUM, OF_REDUCE_AVG = 0, 1         # of_comm_allreduce_ex_async op
 ACT_NONE, ACT_RELU, ACT_LEAKY = 0, 1, 2
 
 
@@ -179,7 +180,9 @@ PROTOTYPES = {
     "of_comm_init_timeout": (I, [C.POINTER(P), P, I, I, C.c_double]),
     "of_comm_info": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
     "of_comm_allreduce_async": (I, [P, P, P, I64, P]),
+    "of_comm_allreduce_ex_async": (I, [P, P, P, I64, I, P]),
     "of_comm_async_error": (I, [P]),
+    "of_comm_abort": (I, [P]),
     "of_comm_destroy": (I, [P, I]),
 }
 

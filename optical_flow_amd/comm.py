@@ -211,7 +211,12 @@ class RcclComm:
                 errors="replace")
 
     def _expire(self, reason):
-        self.close(abort=True)
+        """Watchdog thread: abort the communicator's in-flight collectives (their kernels
+        return) but keep the handle -- the owner thread may be inside allreduce_ / wait with
+        it; those fail cleanly on an aborted handle, and close() frees it later."""
+        with self._lock:
+            if self._h is not None:
+                _lib.lib().of_comm_abort(self._h)
 
     def watch_stream(self, stream):
         """Bound the collectives enqueued so far on ``stream`` (an event recorded there; the
@@ -222,22 +227,26 @@ class RcclComm:
         ev.record(stream)
         self.watchdog.watch(ev.query)
 
-    def allreduce_(self, t: torch.Tensor):
+    def allreduce_(self, t: torch.Tensor, average: bool = False):
+        """In place: the sum over ranks (average: the mean, OF_REDUCE_AVG)."""
         if self.watchdog is not None:
             self.watchdog.check()
-        if self._h is None:
-            raise RuntimeError("RcclComm used after close()")
         if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
             raise TypeError("RcclComm.allreduce_ takes a contiguous float32 CUDA tensor")
         p = C.c_void_p(t.data_ptr())
-        call("of_comm_allreduce_async", self._h, p, p, t.numel(),
-             C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        with self._lock:                 # the watchdog's abort never races this call
+            if self._h is None:
+                raise RuntimeError("RcclComm used after close()")
+            call("of_comm_allreduce_ex_async", self._h, p, p, t.numel(),
+                 _lib.OF_REDUCE_AVG if average else _lib.OF_REDUCE_SUM,
+                 C.c_void_p(torch.cuda.current_stream().cuda_stream))
 
     def wait(self):
         if self.watchdog is not None:
             self.watchdog.check()
-        if self._h is not None:
-            call("of_comm_async_error", self._h)
+        with self._lock:
+            if self._h is not None:
+                call("of_comm_async_error", self._h)
 
     def close(self, abort: bool = False):
         lock = getattr(self, "_lock", None)
@@ -276,14 +285,18 @@ class TorchComm:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self._works = []
 
-    def allreduce_(self, t: torch.Tensor):
+    def allreduce_(self, t: torch.Tensor, average: bool = False):
+        """average: the mean over ranks (gloo has no AVG: SUM, divided by the world size when
+        the work is joined in wait())."""
         import torch.distributed as dist
-        self._works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group,
-                                           async_op=True))
+        w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._works.append((w, t if average else None))
 
     def wait(self):
-        for w in self._works:
+        for w, avg in self._works:
             w.wait()
+            if avg is not None:
+                avg.div_(self.world)
         self._works = []
 
     def close(self, abort: bool = False):

@@ -176,11 +176,14 @@ int of_comm_info(const of_comm* comm, int* nranks, int* rank, int* device) {
   return OF_OK;
 }
 
-int of_comm_allreduce_async(of_comm* comm, const float* send, float* recv, int64_t count,
-                            void* stream) {
+int of_comm_allreduce_ex_async(of_comm* comm, const float* send, float* recv, int64_t count,
+                               int op, void* stream) {
   OF_CHECK_ARG(comm && send && recv && count >= 0, "comm_allreduce: args");
+  OF_CHECK_ARG(op == OF_REDUCE_SUM || op == OF_REDUCE_AVG, "comm_allreduce: op");
+  if (!comm->nccl) return fail(OF_EHIP, "comm_allreduce: the communicator was aborted");
   if (count == 0) return OF_OK;
-  ncclResult_t r = rccl().all_reduce(send, recv, (size_t)count, ncclFloat32, ncclSum, comm->nccl,
+  ncclResult_t r = rccl().all_reduce(send, recv, (size_t)count, ncclFloat32,
+                                     op == OF_REDUCE_AVG ? ncclAvg : ncclSum, comm->nccl,
                                      as_stream(stream));
   // a non-blocking communicator may return while the enqueue is still in progress: it must
   // settle before the next call on the communicator (host-side only; the GPU work stays async)
@@ -189,8 +192,14 @@ int of_comm_allreduce_async(of_comm* comm, const float* send, float* recv, int64
   return OF_OK;
 }
 
+int of_comm_allreduce_async(of_comm* comm, const float* send, float* recv, int64_t count,
+                            void* stream) {
+  return of_comm_allreduce_ex_async(comm, send, recv, count, OF_REDUCE_SUM, stream);
+}
+
 int of_comm_async_error(of_comm* comm) {
   OF_CHECK_ARG(comm, "comm_async_error: comm");
+  if (!comm->nccl) return fail(OF_EHIP, "RCCL communicator: aborted");
   ncclResult_t e = ncclSuccess;
   ncclResult_t r = rccl().async_error(comm->nccl, &e);
   if (r != ncclSuccess) return rccl_fail("ncclCommGetAsyncError", r);
@@ -198,9 +207,20 @@ int of_comm_async_error(of_comm* comm) {
   return OF_OK;
 }
 
+int of_comm_abort(of_comm* comm) {
+  OF_CHECK_ARG(comm, "comm_abort: comm");
+  ncclComm_t c = comm->nccl;
+  if (!c) return OF_OK;
+  comm->nccl = nullptr;
+  ncclResult_t r = rccl().comm_abort(c);
+  if (r != ncclSuccess) return rccl_fail("ncclCommAbort", r);
+  return OF_OK;
+}
+
 int of_comm_destroy(of_comm* comm, int abort) {
   if (!comm) return OF_OK;
-  ncclResult_t r = abort ? rccl().comm_abort(comm->nccl) : rccl().comm_destroy(comm->nccl);
+  ncclResult_t r = ncclSuccess;
+  if (comm->nccl) r = abort ? rccl().comm_abort(comm->nccl) : rccl().comm_destroy(comm->nccl);
   delete comm;
   if (r != ncclSuccess) return rccl_fail(abort ? "ncclCommAbort" : "ncclCommDestroy", r);
   return OF_OK;

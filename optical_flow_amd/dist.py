@@ -71,10 +71,12 @@ class GradBucketReducer:
         lo, hi = self.ranges[bi]
         view = self.store.grad_arena[lo:hi]
         # A bucket's gradients are written on the current stream (BN / bias reductions) and on
-        # the wgrad side stream (ops.side_stream): during the backward the all-reduce is
-        # enqueued on the collective stream once that has waited for both.
-        own = in_backward and _device_tensor(view)
-        with torch.cuda.stream(ops.comm_stream(view)) if own else contextlib.nullcontext():
+        # the wgrad side stream (ops.side_stream): the all-reduce is enqueued on the collective
+        # stream once that has waited for both -- during the backward and for the leftovers of
+        # finish() alike, so the communicator only ever sees one stream.
+        own = _device_tensor(view)
+        with (torch.cuda.stream(ops.comm_stream(view, in_backward=in_backward)) if own
+              else contextlib.nullcontext()):
             self.comm.allreduce_(view)
         self._launched[bi] = True
         self.launch_log.append((bi, own))
@@ -88,23 +90,38 @@ class GradBucketReducer:
             return            # nothing to reduce, and maybe no process group to reduce over
         ops.set_grad_ready_hook(self._on_grad)
 
-    def finish(self) -> float:
-        """Launch buckets that never completed (unused params) on the current stream, join
+    def finish(self, buffers: Optional[torch.Tensor] = None) -> float:
+        """Launch buckets that never completed (unused params) on the collective stream, join
         the reductions (TorchComm: wait on the works; RCCL: stream-ordered, the current stream
-        already joined the side stream at the end of the backward, so only an asynchronous
-        communicator failure is checked); returns the grad scale (1/world) for the optimizer."""
+        waits for the collective stream here, so only an asynchronous communicator failure is
+        checked); returns the grad scale (1/world) for the optimizer.
+
+        ``buffers``: the non-trainable state a step updated on every rank (the BN moving
+        statistics in bn_mode "training", ParamStore.buffers) -- replaced by its average over
+        the ranks, one more all-reduce on the same stream.  Each rank normalises with its own
+        shard's batch statistics (Keras BatchNormalization without synchronisation); the
+        moving statistics, identical on every rank before the step, stay identical after it:
+        0.99 m + 0.01 mean_r(stat_r)."""
         ops.set_grad_ready_hook(None)
         if self.world == 1 and getattr(self.comm, "kind", "") == "torch":
             return 1.0
         for bi in range(len(self.buckets)):
             if not self._launched[bi]:
                 self._launch(bi, in_backward=False)
+        if buffers is not None:
+            own = _device_tensor(buffers)
+            with (torch.cuda.stream(ops.comm_stream(buffers, in_backward=False)) if own
+                  else contextlib.nullcontext()):
+                self.comm.allreduce_(buffers, average=True)
+            self.launch_log.append(("buffers", own))
         if torch.cuda.is_available() and torch.cuda.is_initialized():
             ops.side_join_now()
             # the current stream now waits for every bucket's collective: bound that wait
-            # (comm.CommWatchdog aborts the communicator if a peer never joins)
+            # (comm.CommWatchdog aborts the communicator if a peer never joins).  Not while a
+            # graph is being captured: an event recorded there completes only in a replay,
+            # which GraphedStep watches itself after each replay.
             watch = getattr(self.comm, "watch_stream", None)
-            if watch is not None:
+            if watch is not None and not torch.cuda.is_current_stream_capturing():
                 watch(torch.cuda.current_stream())
         self.comm.wait()
         return 1.0 / self.world

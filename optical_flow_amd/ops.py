@@ -211,7 +211,14 @@ def side_join_now():
 _COMM = {}
 
 
-def comm_stream(*tensors):
+def comm_stream(*tensors, in_backward: bool = True):
+    """The collective stream of the current device, ordered after all work enqueued so far on
+    the current and weight-gradient side streams.  Every collective of the communicator goes
+    here -- during the backward and after it (``in_backward=False``: dist.GradBucketReducer
+    .finish, whose caller joins it with side_join_now) -- so one communicator is only ever
+    used on one stream (RCCL's operations on a communicator must be serialised in the same
+    order on every rank; a communicator used on two streams also preceded the graph-replay
+    host fault of DESIGN.md §1, round 5)."""
     global _side_armed
     cur = torch.cuda.current_stream()
     s = _COMM.get(cur.device)
@@ -224,7 +231,7 @@ def comm_stream(*tensors):
     for t in tensors:
         if t is not None:
             t.record_stream(s)
-    if not _side_armed:
+    if in_backward and not _side_armed:
         _side_armed = True
         torch.autograd.Variable._execution_engine.queue_callback(_side_join)
     return s
@@ -661,6 +668,9 @@ def _block_forward(a, b, p, x):
     yp = zp = None
     side = None
     if p is not None and PROJ_SIDE and x.is_cuda:
+        # any weight packing the projection still needs is enqueued on the current stream
+        # BEFORE the side stream forks from it, so the side-stream conv reads packed weights
+        p.packed(p.desc(*x.shape[:3]))
         side = _fwd_side_stream()
         yp, zp = _conv_forward(p, x, stream=side)
     ya, za = _conv_forward(a, x)

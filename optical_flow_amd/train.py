@@ -114,7 +114,12 @@ class Trainer:
         flows = self.flow_net(batch_imgs)
         loss_value = self.loss_layer(batch_imgs, flows)
         loss_value.backward()
-        scale = self.reducer.finish() if self.reducer is not None else 1.0
+        scale = 1.0
+        if self.reducer is not None:
+            # bn_mode "training": the moving statistics this step updated on every rank are
+            # averaged over the ranks (dist.GradBucketReducer.finish), so replicas stay equal
+            bufs = store.buffers if getattr(self.flow_net, "bn_mode", "") == "training" else None
+            scale = self.reducer.finish(buffers=bufs)
         self.optimizer.apply_gradients(grad_scale=scale)
         return loss_value.detach(), [f.detach() for f in flows]
 
@@ -178,6 +183,14 @@ class GraphedStep:
             self.load(batch_imgs)
         self.graph.replay()
         store.version += 1
+        red = self.trainer.reducer
+        if red is not None:
+            # the captured step's collectives are not watched inside the capture (an event
+            # recorded there would only complete in a replay): bound this replay's instead
+            comm = red.comm
+            if getattr(comm, "watchdog", None) is not None:
+                comm.watch_stream(torch.cuda.current_stream())
+                comm.watchdog.check()
         if guard is not None:
             guard.after_update(self.trainer.optimizer.learning_rate)
         return self.loss, self.flows

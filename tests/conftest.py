@@ -20,3 +20,12 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def pytest_sessionstart(session):
+    # debugging aid (the graph-replay host fault): a native backtrace of a
+    # SIGSEGV before Python's faulthandler prints the Python stack (tools/crash_bt.c)
+    if os.environ.get("OFLOW_NATIVE_BT") == "1":
+        import ctypes
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libcrashbt.so"))
+        assert lib.crash_bt_install() == 0

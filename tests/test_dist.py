@@ -112,10 +112,12 @@ def test_data_parallel_average_equals_global_batch():
 
 
 def test_bucket_allreduce_on_collective_stream(monkeypatch):
-    """During the backward each completed bucket's all-reduce is enqueued on the collective
-    stream (ops.comm_stream: ordered after the compute and weight-gradient side streams), never
-    on the side stream itself, in backward-completion (arena) order, each bucket exactly once;
-    leftovers at finish() go on the current stream.  (Streams stubbed: CPU.)"""
+    """Every bucket's all-reduce is enqueued on the collective stream (ops.comm_stream:
+    ordered after the compute and weight-gradient side streams), never on the side stream or
+    the current stream -- during the backward and for the leftovers of finish() alike (one
+    communicator, one stream: RCCL requires a communicator's operations in the same order on
+    every rank) --, in backward-completion (arena) order, each bucket exactly once; the
+    buffers' average goes on the same stream last.  (Streams stubbed: CPU.)"""
     import contextlib
     from optical_flow_amd import dist as D
     from optical_flow_amd import ops
@@ -126,8 +128,8 @@ def test_bucket_allreduce_on_collective_stream(monkeypatch):
     class FakeComm:
         kind, world = "fake", 2
 
-        def allreduce_(self, t):
-            calls.append(("allreduce", t.data_ptr(), t.numel()))
+        def allreduce_(self, t, average=False):
+            calls.append(("allreduce", t.data_ptr(), t.numel(), average))
 
         def wait(self):
             calls.append(("wait",))
@@ -135,7 +137,8 @@ def test_bucket_allreduce_on_collective_stream(monkeypatch):
     st = ParamStore(flow_net_spec(), device="cpu", order=backward_order())
     red = D.GradBucketReducer(st, bucket_bytes=2 << 20, comm=FakeComm())
     monkeypatch.setattr(D, "_device_tensor", lambda t: True)
-    monkeypatch.setattr(ops, "comm_stream", lambda *t: calls.append(("comm_stream", t[0].data_ptr())) or "S")
+    monkeypatch.setattr(ops, "comm_stream", lambda *t, in_backward=True: calls.append(
+        ("comm_stream", t[0].data_ptr(), in_backward)) or "S")
     monkeypatch.setattr(ops, "side_stream", lambda *t: (_ for _ in ()).throw(AssertionError("side")))
     monkeypatch.setattr(torch.cuda, "stream", lambda s: contextlib.nullcontext())
     red.begin()
@@ -143,20 +146,71 @@ def test_bucket_allreduce_on_collective_stream(monkeypatch):
     held = names[-1]                             # one parameter never reports: a leftover
     for name in names[:-1]:
         ops._grad_ready(st.params[name])
-    assert red.finish() == 0.5
+    assert red.finish(buffers=st.buffers) == 0.5
     nb = len(red.buckets)
-    assert [b for b, _ in red.launch_log] == list(range(nb))
-    assert all(own for _, own in red.launch_log[:-1]) and red.launch_log[-1] == (nb - 1, False)
+    assert [b for b, _ in red.launch_log] == list(range(nb)) + ["buffers"]
+    assert all(own for _, own in red.launch_log)
     ar = [c for c in calls if c[0] == "allreduce"]
     cs = [c for c in calls if c[0] == "comm_stream"]
-    assert len(ar) == nb and len(cs) == nb - 1
+    assert len(ar) == nb + 1 and len(cs) == nb + 1
     for (lo, hi), c in zip(red.ranges, ar):
-        assert c[1] == st.grad_arena[lo:hi].data_ptr() and c[2] == hi - lo
-    # every collective-stream fork precedes its all-reduce
-    for i in range(nb - 1):
-        k = calls.index(("comm_stream", ar[i][1]))
+        assert c[1] == st.grad_arena[lo:hi].data_ptr() and c[2] == hi - lo and not c[3]
+    assert ar[-1] == ("allreduce", st.buffers.data_ptr(), st.buffers.numel(), True)
+    # every collective-stream fork precedes its all-reduce; the backward's forks arm the
+    # end-of-backward join, the leftover's and the buffers' (after the backward) do not
+    for i in range(nb + 1):
+        k = calls.index(cs[i])
         assert calls[k + 1] == ar[i]
+    assert [c[2] for c in cs] == [True] * (nb - 1) + [False, False]
     assert held in red.buckets[-1]
+
+
+def _bn_stats_worker(rank, world, port, q):
+    """bn_mode "training" under data parallelism: each rank's oracle step updates the moving
+    statistics with its own shard's batch statistics; the reducer's buffer average leaves
+    both replicas with the same statistics, 0.99 m + 0.01 mean over ranks of the per-rank
+    statistics."""
+    try:
+        _init(rank, world, port)
+        from oracle import ref_flow as R
+        from optical_flow_amd.data import synthetic_batch
+        from optical_flow_amd.dist import GradBucketReducer
+        from optical_flow_amd.model import ParamStore, backward_order
+        from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params
+        torch.set_num_threads(2)
+        vals = init_params(flow_net_spec(), 3)
+        full = synthetic_batch(2, 32, 64, seed=8)
+        p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
+        R.set_bn_mode("training")
+        R.train_step(torch.tensor(full[rank:rank + 1], dtype=torch.float64), p,
+                     list(encoder_blocks()), None)
+        st = ParamStore(flow_net_spec(), values=vals, device="cpu", order=backward_order())
+        mine = {n: p[n].float() for n in st.buf_offsets}
+        with torch.no_grad():
+            for n, v in mine.items():
+                st.params[n].copy_(v)
+        red = GradBucketReducer(st, bucket_bytes=2 << 20)
+        red.begin()
+        red.finish(buffers=st.buffers)
+        q.put((rank, {n: st.params[n].clone().numpy() for n in st.buf_offsets},
+               {n: v.numpy() for n, v in mine.items()}))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None))
+
+
+def test_bn_training_moving_statistics_replicas_equal():
+    res = {r: (a, b) for r, a, b in _run2(_bn_stats_worker)}
+    assert not isinstance(res[0][0], str), res[0][0]
+    assert not isinstance(res[1][0], str), res[1][0]
+    (s0, own0), (s1, own1) = res[0], res[1]
+    assert set(s0) and set(s0) == set(s1)
+    moved = 0
+    for n in s0:
+        np.testing.assert_array_equal(s0[n], s1[n])              # replicas identical
+        np.testing.assert_allclose(s0[n], (own0[n] + own1[n]) / 2, rtol=1e-6, atol=1e-7)
+        moved += int(not np.array_equal(own0[n], own1[n]))
+    assert moved > len(s0) // 2          # the per-rank updates did differ before the average
 
 
 # ---------------------------------------------------------------------------------------------

@@ -94,25 +94,28 @@ def test_bn_train_kernels(groups, act, with_res, c):
     assert torch.equal(dz, dz2)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_flow_net_bn_training(precision):
-    """The whole flow net with bn_mode="training" at 64x128, B=2, one train step against the
-    oracle's (float64; bf16: the oracle with the bf16 operand rounding): the loss, the moving
-    statistics of every BN layer after the step (updated once per encoder call, image1s then
-    image2s) and finite gradients.  The gradients themselves are checked teacher-forced,
-    test_encoder_bn_training: through the whole net this weight set's flows come within 1e-5
-    of integer sample coordinates at some pixels, where the warp's floor() (model.py:69-71)
-    and the loss's |.| turn the forward's rounding differences (fp32: 8e-4 relative at H/2)
-    into flipped per-pixel gradient contributions (measured round 5: fp32 gradients median
-    1e-1) -- the end-to-end sensitivity of DESIGN.md §1, not the BN mode."""
+def _bn_train_case():
+    """A weight set and input on which the training-mode step is well conditioned.  With the
+    default perturbed weights the batch-normalised encoder features drive the flows to 44 px
+    on the 64 x 128 image: every warp samples far outside it, where the clipped bilinear
+    weights of P2 (transformations.py:98-125) become extrapolation weights of -40 / 41 and
+    amplify rounding -- the float32 ORACLE itself then misses its float64 run by 1.1e-3 at
+    H/2 and by 13 % (median) on the gradients (profiles/r6_bn_train_conditioning.txt), so no
+    fp32 implementation can be held to 1e-3 there.  Scaling every flow module's last conv by
+    0.1 keeps the flows within 5 px; with input seed 99 (no residual within 2.5e-5 of the loss
+    kink, no sample coordinate within 2.7e-6 of an integer) the float32 oracle is within
+    5.6e-6 of float64 on the flows and 7.3e-6 on every gradient."""
     from optical_flow_amd.data import synthetic_batch
-    from optical_flow_amd.loss import LossLayer
-    from optical_flow_amd.model import FlowNet
-    from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params, perturb_params
-    H, W, B = 64, 128, 2
+    from optical_flow_amd.params import flow_net_spec, init_params, perturb_params
     vals = perturb_params(init_params(flow_net_spec(), 21), 22)
-    batch = synthetic_batch(B, H, W, seed=4321)
-    net = FlowNet(H, W, values=vals, precision=precision, bn_mode="training")
+    for k in vals:
+        if "/conv5/" in k:
+            vals[k] = vals[k] * 0.1
+    return vals, synthetic_batch(2, 64, 128, seed=99)
+
+
+def _oracle_step(batch, vals, precision):
+    from optical_flow_amd.params import encoder_blocks
     p = {k: torch.tensor(v, dtype=torch.float64) for k, v in vals.items()}
     R.set_bn_mode("training")
     R.set_conv_precision(precision)
@@ -122,23 +125,62 @@ def test_flow_net_bn_training(precision):
     finally:
         R.set_bn_mode("inference")
         R.set_conv_precision("fp32")
+    return p, loss_o, flows_o, grads_o
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_flow_net_bn_training(precision):
+    """The whole flow net with bn_mode="training" at 64x128, B=2, one train step against the
+    oracle's (float64; bf16: the oracle with the bf16 operand rounding), on the
+    well-conditioned case of _bn_train_case: the loss, all four flows, every one of the 108
+    gradients and the moving statistics of every BN layer after the step (updated once per
+    encoder call, image1s then image2s).  fp32: everything within 1e-3 (the encoder conv
+    biases, whose gradient the batch mean removes exactly, against their kernel gradient's
+    scale).  bf16: flows and loss within 3e-2, gradients at a 1e-2 median and each within
+    5e-2 or 3x the oracle's own bf16-vs-fp32 change of it."""
+    from optical_flow_amd.loss import LossLayer
+    from optical_flow_amd.model import FlowNet
+    vals, batch = _bn_train_case()
+    net = FlowNet(64, 128, values=vals, precision=precision, bn_mode="training")
+    p, loss_o, flows_o, grads_o = _oracle_step(batch, vals, precision)
+    noise = {}
+    if precision == "bf16":
+        _, _, _, g32 = _oracle_step(batch, vals, "fp32")
+        noise = {n: rel_l2(grads_o[n], g32[n]) for n in g32 if not n.endswith("/bias")}
     net.store.zero_grad()
     bd = dev(torch.from_numpy(batch))
     flows = net(bd)
     loss = LossLayer()(bd, flows)
     loss.backward()
     torch.cuda.synchronize()
-    lrel = abs(float(loss) - loss_o.item()) / abs(loss_o.item())
-    frel = [rel_inf(flows[k], flows_o[k]) for k in range(4)]
-    print("%s loss rel %.2e, flows rel_inf %s" % (precision, lrel, ["%.1e" % e for e in frel]))
-    mstat = max(rel_inf(net.store.params[n], p[n]) for n in p
-                if n.endswith(("moving_mean", "moving_variance")))
-    print("moving statistics: worst rel_inf %.2e" % mstat)
-    # (bf16: the statistics of z, which carries the bf16 operand rounding of the conv)
-    assert mstat < (1e-5 if precision == "fp32" else 1e-3)
-    assert all(torch.isfinite(g).all() for g in net.store.grads().values())
-    assert lrel < (REL_TOL if precision == "fp32" else 3e-2)
-    assert frel[-1] < (1e-4 if precision == "fp32" else 3e-2), frel   # H/16: no warp before it
+    errs = [("loss", abs(float(loss) - loss_o.item()) / abs(loss_o.item()))]
+    errs += [("flow%d" % k, rel_inf(flows[k], flows_o[k])) for k in range(4)]
+    grads = net.store.grads()
+    assert len(grads) == 108 and set(grads) == set(grads_o)
+    for n, g in grads.items():
+        if n.startswith("ResNet18") and n.endswith("/bias"):
+            kn = n[:-len("bias")] + "kernel"
+            errs.append((n, float(g.double().cpu().norm()) / float(grads_o[kn].norm())))
+        else:
+            errs.append((n, rel_l2(g, grads_o[n])))
+    mstat = [(n, rel_inf(net.store.params[n], p[n])) for n in p
+             if n.endswith(("moving_mean", "moving_variance"))]
+    for n, e in sorted(errs, key=lambda t: -t[1])[:8]:
+        print("  %-40s %.3e   (bf16 vs fp32 oracle %.3e)" % (n, e, noise.get(n, 0.0)))
+    print("%s: flows %s, loss %.1e, gradient median %.1e, moving statistics worst %.1e" % (
+        precision, ["%.1e" % e for n, e in errs[1:5]], errs[0][1],
+        float(np.median([e for _, e in errs[5:]])), max(e for _, e in mstat)))
+    assert all(torch.isfinite(g).all() for g in grads.values())
+    if precision == "fp32":
+        bad = [(n, e) for n, e in errs + mstat if not e < REL_TOL]
+        assert not bad, bad
+    else:
+        # (the statistics of z, which carries the bf16 operand rounding of the conv)
+        assert max(e for _, e in mstat) < 1e-3
+        assert all(e < 3e-2 for _, e in errs[:5]), errs[:5]
+        ge = errs[5:]
+        bad = [(n, e) for n, e in ge if not e < max(5e-2, 3.0 * noise.get(n, 0.0))]
+        assert float(np.median([e for _, e in ge])) < 1e-2 and not bad, bad
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

@@ -80,23 +80,32 @@ def test_data_parallel_step_matches_single_process():
 
 # ---- the C-ABI RCCL communicator (of_comm_*, comm.RcclComm) -------------------------------
 def test_rccl_comm_allreduce_world1():
-    """of_comm_init / of_comm_allreduce_async / of_comm_destroy on a one-rank communicator:
-    the in-place sum over one rank leaves every element as it was, on a non-default stream
-    too, and a destroyed communicator refuses further use."""
+    """of_comm_init / of_comm_allreduce_ex_async / of_comm_destroy on a one-rank communicator,
+    used the way the data-parallel reducer uses it -- every collective on ONE stream (the
+    collective stream, here a non-default one): the in-place sum and the average over one rank
+    leave every element as it was; after of_comm_abort (the watchdog's path) the handle
+    refuses further collectives but stays valid until close(); a closed communicator refuses
+    further use.  (The round-5 graph-replay host fault followed a communicator used on two
+    streams; the product never does that since round 6.)"""
+    from optical_flow_amd import _lib
     from optical_flow_amd.comm import RcclComm
     comm = RcclComm(0, 1)
     assert comm.device == torch.cuda.current_device()
     x = torch.randn(1 << 20, device="cuda")
     ref = x.clone()
-    comm.allreduce_(x)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        comm.allreduce_(x[: 12345])
+        comm.allreduce_(x)
+        comm.allreduce_(x[: 12345], average=True)
     torch.cuda.current_stream().wait_stream(s)
     comm.wait()
     torch.cuda.synchronize()
     assert torch.equal(x, ref)
+    assert _lib.lib().of_comm_abort(comm._h) == 0
+    with pytest.raises(RuntimeError):
+        with torch.cuda.stream(s):
+            comm.allreduce_(x)
     comm.close()
     with pytest.raises(RuntimeError):
         comm.allreduce_(x)
@@ -144,6 +153,7 @@ def test_rccl_dp_step_world1(precision, H, W, B, det):
         got, loss, mid, trainer = _grads(precision, H, W, B, comm=comm)
     nb = len(trainer.reducer.buckets)
     assert trainer.reducer.comm is comm and trainer.reducer.world == 1
+    assert trainer.reducer.launch_log and all(own for _, own in trainer.reducer.launch_log)
     assert nb >= 3 and 0 < mid[len(mid) // 2] < nb, (nb, mid[len(mid) // 2])
     assert torch.isfinite(got).all()
     assert loss == loss_ref

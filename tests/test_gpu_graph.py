@@ -114,6 +114,31 @@ def _graph_vs_eager(precision, comm, det):
         c.close()
 
 
+def test_graph_after_rccl_dp_step():
+    """Regression for the round-5 host fault in hipGraphLaunch: in ONE process,
+    a captured step replayed, then an eager data-parallel step over a one-rank RCCL
+    communicator (every bucket's all-reduce on the collective stream, finish()'s leftovers
+    included), then a new capture whose replays must equal the eager step bitwise
+    (deterministic warp backward) -- the sequence of the crashing test subset."""
+    from optical_flow_amd import ops
+    from optical_flow_amd.comm import RcclComm
+    from optical_flow_amd.data import synthetic_batch
+    H, W, B = 64, 128, 2
+    with ops.deterministic(True):
+        gt, _ = _trainer(H, W)
+        b0 = dev(torch.from_numpy(synthetic_batch(B, H, W, seed=7)))
+        step = gt.graphed(b0.clone(), warmup=1)
+        step(b0)
+        torch.cuda.synchronize()
+        comm = RcclComm(0, 1)
+        dp, _ = _trainer(H, W, comm=comm)
+        dp.train_step(b0)
+        torch.cuda.synchronize()
+        assert dp.reducer.launch_log and all(own for _, own in dp.reducer.launch_log)
+        comm.close()
+        _graph_vs_eager("fp32", None, True)
+
+
 def test_graph_bn_guard_recapture():
     """The BN gamma guard in graphed training: the captured step bakes in which BN
     layers store z (ops.BNZGuard), so GraphedStep drives the guard itself -- a min |gamma|
