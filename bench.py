@@ -532,7 +532,7 @@ def main():
         tf, tm, cnt = per[dom]
         achieved = tf / (tm * 1e-3) / 1e12
         sym = kernel_symbol(dom)
-        traffic = None
+        traffic = mfma_busy = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
@@ -540,7 +540,9 @@ def main():
             pmc = db.get("entries", {}).get("%s:%dx%dx%d" % (args.precision, H, W, B), {})
             same_math = args.precision != "fp32" or pmc.get("f32_split", True) == ops.F32_SPLIT
             if same_math and sym in pmc.get("kernels", {}):
-                traffic = pmc["kernels"][sym]["hbm_bytes_per_launch"]
+                traffic = pmc["kernels"][sym].get("hbm_bytes_per_launch")
+                # SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), tools/pmc_mfma.py
+                mfma_busy = pmc["kernels"][sym].get("mfma_busy")
         allconv = sum(v[0] for v in table.values()) / (sum(v[1] for v in table.values()) * 1e-3) / 1e12
         fam = kind_parts(dom)[2]
         # the split kernel spends six bf16 MFMAs per fp32 product: its ceiling is 1/6 of bf16
@@ -550,6 +552,7 @@ def main():
         roof = {"bound": "mfma", "kernel": sym, "achieved": round(achieved, 2),
                 "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
+                "mfma_busy": mfma_busy,
                 "launches_per_step": cnt // max(nsteps, 1),
                 "window": ("one fully timed eager step after the warm-up (the timed region "
                            "replayed the captured graph)" if graphed is not None else

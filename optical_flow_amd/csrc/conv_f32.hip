@@ -4782,6 +4782,11 @@ static int g_wgx3b = 1;
 // MI = 2 halves the dy loads and splits per MFMA and measured the same (dec3.c1 0.516 vs
 // 0.517 ms): the split VALU is not what bounds the kernel.
 static int g_wgx3b_mi = 1;
+// of_set_tuning key 33: at least this many K tiles per split-K slice of the 9-tap weight
+// gradients (conv_wgrad_tile_x3b / _b16).  Every slice writes a 9 x cin x cout fp32 slab that
+// wgrad_reduce_kernel reads back: with one slice per CU the slabs are a fixed ~38 MB per launch
+// whatever the layer's size, 6-12x x + dy on the coarse encoder stages.  1 = one slice per CU.
+static int g_wgx3_min_tiles = 1;
 // of_set_tuning key 11: the 32 x 64 channel-block weight gradient (cfg 4) for Cout 64 layers
 // whose Cin is not a multiple of 64 (1, default) or the 64 x 64 blocks (0).
 static int g_wgx3_c4 = 1;
@@ -5210,6 +5215,7 @@ WgradPlan wgrad_plan(const of_conv_desc* d, bool bf16 = false, bool x3 = false) 
     const int chan_tiles = (int)(cdiv(g.cin_p, cib) * cdiv(d->cout, cob));
     const int T = d->n * (int)cdiv(d->ho, wgx3_rows(wgx3_cfg(d))) * (int)cdiv(d->wo, TT_W);
     int splits = std::max(1, std::min(T, device_cus() / chan_tiles));
+    splits = std::max(1, std::min(splits, T / g_wgx3_min_tiles));
     p.k_per_split = (int)cdiv(T, splits);
     p.splits = (int)cdiv(T, p.k_per_split);
     return p;
@@ -5379,6 +5385,7 @@ int of_set_tuning(int key, int value) {
   if (key == 30 && value >= 0 && value <= 2) { g_gx3_ring = value; return OF_OK; }
   if (key == 31 && value >= -1 && value <= 8) { g_stem_persist = value; return OF_OK; }
   if (key == 32 && (value == 0 || value == 1)) { g_bnp_b16 = value; return OF_OK; }
+  if (key == 33 && value >= 1 && value <= 256) { g_wgx3_min_tiles = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

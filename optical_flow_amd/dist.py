@@ -74,7 +74,7 @@ class GradBucketReducer:
         # the wgrad side stream (ops.side_stream): the all-reduce is enqueued on the collective
         # stream once that has waited for both -- during the backward and for the leftovers of
         # finish() alike, so the communicator only ever sees one stream.
-        own = _device_tensor(view)
+        own = _device_tensor(view) and not ops.SINGLE_STREAM
         with (torch.cuda.stream(ops.comm_stream(view, in_backward=in_backward)) if own
               else contextlib.nullcontext()):
             self.comm.allreduce_(view)
@@ -109,7 +109,7 @@ class GradBucketReducer:
             if not self._launched[bi]:
                 self._launch(bi, in_backward=False)
         if buffers is not None:
-            own = _device_tensor(buffers)
+            own = _device_tensor(buffers) and not ops.SINGLE_STREAM
             with (torch.cuda.stream(ops.comm_stream(buffers, in_backward=False)) if own
                   else contextlib.nullcontext()):
                 self.comm.allreduce_(buffers, average=True)

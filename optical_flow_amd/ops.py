@@ -199,8 +199,31 @@ _DEFERRED_RELEASE = []
 def side_join_now():
     """Order each device's current stream after everything enqueued so far on its side
     streams (the end-of-backward join, also used after work launched outside a backward)."""
+    if SINGLE_STREAM:
+        return                       # nothing was forked (single_stream())
     for dev, s in list(_SIDE.items()) + list(_CORR_SIDE.items()) + list(_COMM.items()):
         stream_wait(torch.cuda.current_stream(dev), s)
+
+
+# Single-stream mode (single_stream()): every fork point above and below keeps its work on the
+# current stream -- the same kernels in the same per-stream order, which an eager step must
+# reproduce bitwise (tools/eager_order_probe.py: it does, every step).  A diagnostic: a HIP
+# graph CAPTURED this way replays its first launch like the eager step and diverges from the
+# second on (DESIGN.md §1, round 6), so Trainer.graphed captures with the side streams.
+SINGLE_STREAM = False
+
+
+@contextlib.contextmanager
+def single_stream(on: bool = True):
+    """Keep every kernel of the enclosed work on the current stream (no side-stream forks)."""
+    global SINGLE_STREAM, SIDE_STREAM_WGRAD, PROJ_SIDE, CORR_DF1_SIDE
+    saved = (SINGLE_STREAM, SIDE_STREAM_WGRAD, PROJ_SIDE, CORR_DF1_SIDE)
+    if on:
+        SINGLE_STREAM, SIDE_STREAM_WGRAD, PROJ_SIDE, CORR_DF1_SIDE = True, False, False, False
+    try:
+        yield
+    finally:
+        SINGLE_STREAM, SIDE_STREAM_WGRAD, PROJ_SIDE, CORR_DF1_SIDE = saved
 
 
 # The data-parallel collectives' own stream (dist.GradBucketReducer): a bucket's all-reduce

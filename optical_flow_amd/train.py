@@ -132,6 +132,20 @@ class Trainer:
         return GraphedStep(self, batch_imgs, warmup, capture_ctx)
 
 
+# The captured step replays on a HIGH-priority stream of its own (torch.cuda.Stream(priority=-1),
+# ordered after and before the caller's stream).  The HIP runtime inside the torch wheel (ROCm
+# 7.0.2 libamdhip64, which liboflow binds to in a torch process) assigns a graph executor's
+# parallel streams at its first launch by skipping those on the launch stream's hardware queue,
+# without bounds: when one of them shares that queue it reads past the end of its stream list
+# and segfaults in hipGraphLaunch (native backtrace, and the subset that
+# crashed passing with this change).  Which queue a stream gets depends on every stream the
+# process made before (RCCL's included); high-priority streams take their queues from a set of
+# their own, so the normal-priority parallel streams never share the launch stream's.
+# OFLOW_GRAPH_REPLAY_PRIO overrides the priority ("none": replay on the caller's stream).
+_RP = os.environ.get("OFLOW_GRAPH_REPLAY_PRIO", "-1")
+REPLAY_PRIO = None if _RP == "none" else int(_RP)
+
+
 class GraphedStep:
     """A captured Trainer.train_step.  ``batch`` is the static input: write the next batch
     into it (``load``) before calling.  Returns the static (loss, flows) tensors, overwritten
@@ -153,6 +167,7 @@ class GraphedStep:
                 trainer.train_step(batch_imgs, i)
         cur.wait_stream(s)
         self.captures = 0
+        self._rs = None
         self._capture(capture_ctx)
 
     def _capture(self, capture_ctx=None):
@@ -181,7 +196,17 @@ class GraphedStep:
                 self._capture()
         if batch_imgs is not None and batch_imgs.data_ptr() != self.batch.data_ptr():
             self.load(batch_imgs)
-        self.graph.replay()
+        if REPLAY_PRIO is None:
+            self.graph.replay()
+        else:
+            # on a stream of its own priority (REPLAY_PRIO: the hipGraphLaunch fault)
+            if self._rs is None:
+                self._rs = torch.cuda.Stream(priority=REPLAY_PRIO)
+            cur = torch.cuda.current_stream()
+            self._rs.wait_stream(cur)
+            with torch.cuda.stream(self._rs):
+                self.graph.replay()
+            cur.wait_stream(self._rs)
         store.version += 1
         red = self.trainer.reducer
         if red is not None:

@@ -10,6 +10,12 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+    # debugging aid (DESIGN.md §1, the graph-replay host fault): a native backtrace of a
+    # SIGSEGV (tools/crash_bt.c; run with -p no:faulthandler so that nothing replaces it)
+    if os.environ.get("OFLOW_NATIVE_BT") == "1":
+        import ctypes
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libcrashbt.so"))
+        assert lib.crash_bt_install() == 0
 
 
 def pytest_collection_modifyitems(config, items):
@@ -21,11 +27,3 @@ def pytest_collection_modifyitems(config, items):
         if "gpu" in it.keywords:
             it.add_marker(skip)
 
-
-def pytest_sessionstart(session):
-    # debugging aid (DESIGN.md §1, the graph-replay host fault): a native backtrace of a
-    # SIGSEGV before Python's faulthandler prints the Python stack (tools/crash_bt.c)
-    if os.environ.get("OFLOW_NATIVE_BT") == "1":
-        import ctypes
-        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libcrashbt.so"))
-        assert lib.crash_bt_install() == 0

@@ -94,7 +94,7 @@ def test_bn_train_kernels(groups, act, with_res, c):
     assert torch.equal(dz, dz2)
 
 
-def _bn_train_case():
+def _bn_train_case(seed=333):
     """A weight set and input on which the training-mode step is well conditioned.  With the
     default perturbed weights the batch-normalised encoder features drive the flows to 44 px
     on the 64 x 128 image: every warp samples far outside it, where the clipped bilinear
@@ -102,16 +102,20 @@ def _bn_train_case():
     amplify rounding -- the float32 ORACLE itself then misses its float64 run by 1.1e-3 at
     H/2 and by 13 % (median) on the gradients (profiles/r6_bn_train_conditioning.txt), so no
     fp32 implementation can be held to 1e-3 there.  Scaling every flow module's last conv by
-    0.1 keeps the flows within 5 px; with input seed 99 (no residual within 2.5e-5 of the loss
-    kink, no sample coordinate within 2.7e-6 of an integer) the float32 oracle is within
-    5.6e-6 of float64 on the flows and 7.3e-6 on every gradient."""
+    0.1 keeps the flows within 5 px.  The input must also keep every sample coordinate of the
+    loss AND feature warps clear of an integer (floor(), model.py:69-71) by more than the
+    fp32 rounding of a coordinate near 128 (7.6e-6) and every loss residual clear of 0: seed
+    333 (5.5e-5 and 2.8e-5) and 216 (5.8e-5, 2.1e-5), where the float32 oracle is within
+    5.6e-6 of float64 on the flows and 6.5e-6 on every gradient (round 6's first choice,
+    seed 99, had a feature-warp coordinate 2.7e-6 from an integer: the HIP step flipped its
+    floor and its stage-2-3 gradients moved by 4e-3)."""
     from optical_flow_amd.data import synthetic_batch
     from optical_flow_amd.params import flow_net_spec, init_params, perturb_params
     vals = perturb_params(init_params(flow_net_spec(), 21), 22)
     for k in vals:
         if "/conv5/" in k:
             vals[k] = vals[k] * 0.1
-    return vals, synthetic_batch(2, 64, 128, seed=99)
+    return vals, synthetic_batch(2, 64, 128, seed=seed)
 
 
 def _oracle_step(batch, vals, precision):
@@ -128,25 +132,26 @@ def _oracle_step(batch, vals, precision):
     return p, loss_o, flows_o, grads_o
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_flow_net_bn_training(precision):
+@pytest.mark.parametrize("precision,seed", [("fp32", 333), ("fp32", 216), ("bf16", 333)])
+def test_flow_net_bn_training(precision, seed):
     """The whole flow net with bn_mode="training" at 64x128, B=2, one train step against the
     oracle's (float64; bf16: the oracle with the bf16 operand rounding), on the
     well-conditioned case of _bn_train_case: the loss, all four flows, every one of the 108
     gradients and the moving statistics of every BN layer after the step (updated once per
     encoder call, image1s then image2s).  fp32: everything within 1e-3 (the encoder conv
     biases, whose gradient the batch mean removes exactly, against their kernel gradient's
-    scale).  bf16: flows and loss within 3e-2, gradients at a 1e-2 median and each within
-    5e-2 or 3x the oracle's own bf16-vs-fp32 change of it."""
+    scale).  bf16: flows and loss within 3e-2, each gradient within 5e-2 or 3x the oracle's
+    own bf16-vs-fp32 change of it (this case moves the decoder's gradients by ~17 % under
+    bf16 operand rounding alone), the median within 1e-2 or 3x the median of those changes."""
     from optical_flow_amd.loss import LossLayer
     from optical_flow_amd.model import FlowNet
-    vals, batch = _bn_train_case()
+    vals, batch = _bn_train_case(seed)
     net = FlowNet(64, 128, values=vals, precision=precision, bn_mode="training")
     p, loss_o, flows_o, grads_o = _oracle_step(batch, vals, precision)
     noise = {}
     if precision == "bf16":
         _, _, _, g32 = _oracle_step(batch, vals, "fp32")
-        noise = {n: rel_l2(grads_o[n], g32[n]) for n in g32 if not n.endswith("/bias")}
+        noise = {n: rel_l2(grads_o[n], g32[n]) for n in g32}
     net.store.zero_grad()
     bd = dev(torch.from_numpy(batch))
     flows = net(bd)
@@ -180,7 +185,9 @@ def test_flow_net_bn_training(precision):
         assert all(e < 3e-2 for _, e in errs[:5]), errs[:5]
         ge = errs[5:]
         bad = [(n, e) for n, e in ge if not e < max(5e-2, 3.0 * noise.get(n, 0.0))]
-        assert float(np.median([e for _, e in ge])) < 1e-2 and not bad, bad
+        med, med_noise = float(np.median([e for _, e in ge])), float(np.median(list(noise.values())))
+        print("bf16 gradient median %.2e, oracle bf16-vs-fp32 median %.2e" % (med, med_noise))
+        assert med < max(1e-2, 3.0 * med_noise) and not bad, bad
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

@@ -20,18 +20,27 @@ from optical_flow_amd.data import synthetic_batch  # noqa: E402
 from optical_flow_amd.params import encoder_blocks, flow_net_spec, init_params, perturb_params  # noqa: E402
 
 
+def _coord_dist(f):
+    """min distance of a warp's sample coordinates (grid + flow, P1) to an integer"""
+    h, w = f.shape[1], f.shape[2]
+    ii, jj = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+    pts = torch.stack([ii, jj], -1).double() + f
+    frac = (pts - pts.floor())
+    return float(torch.minimum(frac, 1 - frac).min())
+
+
 def kinks(batch, flows):
     """(min distance of a sample coordinate to an integer, min |residual|) over the loss
-    warps (loss.py:26) -- the feature warps see the same flows upscaled."""
+    warps (loss.py:26) and the feature warps (model.py:93: the coarser level's flow upscaled,
+    R.upscale_flow)."""
     dmin, rmin = 1.0, 1e9
     x = torch.tensor(batch, dtype=torch.float64)
     H, W = x.shape[1], x.shape[2]
+    for s in range(len(flows) - 1):
+        dmin = min(dmin, _coord_dist(R.upscale_flow(flows[s + 1])))
     for s, f in enumerate(flows):
         h, w = H >> (s + 1), W >> (s + 1)
-        ii, jj = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
-        pts = torch.stack([ii, jj], -1).double() + f
-        frac = (pts - pts.floor())
-        dmin = min(dmin, float(torch.minimum(frac, 1 - frac).min()))
+        dmin = min(dmin, _coord_dist(f))
         r = R.resize_bilinear(x, h, w)
         res = r[..., :3] - R.warp_features(f, r[..., 3:])
         rmin = min(rmin, float(res.abs().min()))

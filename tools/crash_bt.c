@@ -10,6 +10,7 @@
 #include <signal.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <unistd.h>
 
 static struct sigaction g_prev;
@@ -33,11 +34,25 @@ static void on_segv(int sig, siginfo_t* si, void* uc) {
     }
     write(2, line, len);
   }
+  struct rlimit rl;
+  if (getrlimit(RLIMIT_STACK, &rl) == 0) {
+    len = snprintf(line, sizeof line, "[crash_bt] stack limit %ld KiB, fault %ld KiB below this "
+                   "frame\n", (long)(rl.rlim_cur / 1024),
+                   (long)(((char*)&rl - (char*)(si ? si->si_addr : 0)) / 1024));
+    write(2, line, len);
+  }
   sigaction(SIGSEGV, &g_prev, NULL);       /* the previous handler runs on the re-fault */
   (void)uc;
 }
 
 int crash_bt_install(void) {
+  /* an alternate signal stack: a fault that is a stack overflow still gets its backtrace */
+  static char altstack[1 << 20];
+  stack_t ss;
+  memset(&ss, 0, sizeof ss);
+  ss.ss_sp = altstack;
+  ss.ss_size = sizeof altstack;
+  if (sigaltstack(&ss, NULL) != 0) return -1;
   struct sigaction sa;
   memset(&sa, 0, sizeof sa);
   sa.sa_sigaction = on_segv;
