@@ -1,8 +1,12 @@
 """Write a profile summary (markdown) from a bench JSON line and the rocprofv3 kernel_stats.csv
 of the same bench command.
 
-python tools/make_summary.py <bench.log> <kernel_stats.csv> <command> [top]  > profiles/....md
+python tools/make_summary.py <bench.log> <kernel_stats.csv> <command> [top] [pmc entry]
+    > profiles/....md
+The kernel table carries MFMA busy and HBM bytes per launch from profiles/pmc_traffic.json's
+entry for the bench's configuration ("precision:HxWxB", or the given one) when present.
 """
+import os
 import csv
 import json
 import sys
@@ -27,12 +31,30 @@ def main():
           "%.4f ms per launch vs rocprof average %.4f ms.\n"
           % (rf["kernel"], rf["achieved"], rf["unit"], 100 * rf["frac"], rf["peak"], rf["unit"],
              rf["avg_launch_ms"], prof_avg))
-    print("| kernel | calls | total ms | % of GPU time | avg ms |")
-    print("|---|---|---|---|---|")
+    cfg = b["config"]
+    key = sys.argv[5] if len(sys.argv) > 5 else "%s:%dx%dx%d" % (
+        b["dtype"], cfg["height"], cfg["width"], cfg["batch_per_gpu"])
+    pmc = {}
+    pp = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                      "pmc_traffic.json")
+    if os.path.exists(pp):
+        pmc = json.load(open(pp)).get("entries", {}).get(key, {}).get("kernels", {})
+    if rf.get("mfma_busy") is not None:
+        print("Dominant kernel MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel "
+              "cycles), tools/pmc_mfma.py): %.1f %%; HBM bytes per launch (PMC): %s MB.\n" % (
+                  100 * rf["mfma_busy"],
+                  "%.1f" % (rf["traffic"] / 1e6) if rf.get("traffic") else "-"))
+    print("| kernel | calls | total ms | % of GPU time | avg ms | MFMA busy (PMC) | HBM MB / launch (PMC) |")
+    print("|---|---|---|---|---|---|---|")
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
-        print("| `%s` | %s | %.2f | %.1f | %.4f |" % (
+        k = pmc.get(r["Name"], {})
+        mb = k.get("mfma_busy")
+        hb = k.get("hbm_bytes_per_launch")
+        print("| `%s` | %s | %.2f | %.1f | %.4f | %s | %s |" % (
             r["Name"][:90], r["Calls"], float(r["TotalDurationNs"]) / 1e6,
-            100 * float(r["TotalDurationNs"]) / tot, float(r["AverageNs"]) / 1e6))
+            100 * float(r["TotalDurationNs"]) / tot, float(r["AverageNs"]) / 1e6,
+            "%.1f %%" % (100 * mb) if mb is not None else "-",
+            "%.1f" % (hb / 1e6) if hb is not None else "-"))
     alone = rf.get("per_kernel_alone", {})
     print("\nPer-kernel hipEvent table from the bench: `in step` = one fully timed step after "
           "the warm-up, side streams on (the input-gradient convs share the chip with the side "

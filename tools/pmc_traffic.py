@@ -1,5 +1,5 @@
 """Turn two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of `python bench.py` into HBM bytes
-per launch for every conv kernel template instance -> profiles/pmc_traffic.json.
+per launch for every liboflow kernel (template instance) -> profiles/pmc_traffic.json.
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts 128-B requests of wide
 coalesced reads as 64 B, i.e. half the bytes of 16-B/lane loads -> doubled here; WRITE_SIZE
@@ -37,14 +37,15 @@ def main():
                    "bench command (mixed layer shapes)"}
     for k in f:
         # (conv_b16i.hip's kernels live in an anonymous namespace: oflow::(anonymous namespace)::)
-        if not ("oflow::" in k and "conv_" in k) or k not in w:
+        if "oflow::" not in k or k not in w:        # every liboflow kernel
             continue
         fb = sum(f[k]) / len(f[k]) * 1024 * 2
         wb = sum(w[k]) / len(w[k]) * 1024
         out["kernels"][k] = {"launches": len(f[k]), "fetch_bytes": fb, "write_bytes": wb,
                              "hbm_bytes_per_launch": fb + wb}
-    dom = max(out["kernels"], key=lambda k: out["kernels"][k]["launches"] *
-              out["kernels"][k]["hbm_bytes_per_launch"]) if out["kernels"] else None
+    convs = [k for k in out["kernels"] if "conv_" in k]
+    dom = max(convs, key=lambda k: out["kernels"][k]["launches"] *
+              out["kernels"][k]["hbm_bytes_per_launch"]) if convs else None
     out["kernel"] = dom
     if dom:
         out["hbm_bytes_per_launch"] = out["kernels"][dom]["hbm_bytes_per_launch"]
