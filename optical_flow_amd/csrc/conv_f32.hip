@@ -4785,8 +4785,9 @@ static int g_wgx3b_mi = 1;
 // of_set_tuning key 33: at least this many K tiles per split-K slice of the 9-tap weight
 // gradients (conv_wgrad_tile_x3b / _b16).  Every slice writes a 9 x cin x cout fp32 slab that
 // wgrad_reduce_kernel reads back: with one slice per CU the slabs are a fixed ~38 MB per launch
-// whatever the layer's size, 6-12x x + dy on the coarse encoder stages.  1 = one slice per CU.
-static int g_wgx3_min_tiles = 1;
+// whatever the layer's size.  2 (default): fp32 B=8 650.1 / 646.9 -> 655.4 / 655.0 pairs/s, bf16
+// B=32 1803.0 / 1813.7 -> 1814.2 / 1816.2 at 4 (one box, gpurun_out/ab33); 4: +0.4 %, 8: -0.7 %.
+static int g_wgx3_min_tiles = 2;
 // of_set_tuning key 11: the 32 x 64 channel-block weight gradient (cfg 4) for Cout 64 layers
 // whose Cin is not a multiple of 64 (1, default) or the 64 x 64 blocks (0).
 static int g_wgx3_c4 = 1;
