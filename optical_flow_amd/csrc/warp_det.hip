@@ -375,6 +375,7 @@ __global__ __launch_bounds__(256) void det_dflow_vec(const float* __restrict__ d
 // NCB channel blocks of 16 quads (channels when !VEC) per lane; `found` += the hits.  Every
 // lane of the wave calls it (wave-wide shuffles); a group with an empty range idles.
 constexpr int WIN_CAP = 128;    // list entries per group; flushed above WIN_CAP - 64
+constexpr int TILE_CAP = 64;    // sorted bin entries per destination of the tiled mode A
 #ifndef WIN_DFLOW_PRE
 #define WIN_DFLOW_PRE 0  // 1: own_window issues d(flow)'s loads before the window's (+28 VGPRs)
 #endif
@@ -583,18 +584,22 @@ __device__ __forceinline__ bool win_piled(bool mode_a, int r, int x, int h, int 
 // a source, its loads issued before the window's (DFQ quads per lane).  A window that does
 // not serve (mode B, a count short of 4 n h w) is overwritten by the fixed-point path; with
 // neither mode (R > rmax and V > WIN_VMAX) the kernel forms d(flow) only.
-template <bool VEC, int NCB>
+template <bool VEC, int NCB, bool TPRE = false>
 __global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout,
                                                   const float* __restrict__ inp,
                                                   const float* __restrict__ flow, int n, int h,
                                                   int w, int c, int* __restrict__ hdr,
                                                   int rmax, float* __restrict__ dinp,
                                                   float* __restrict__ dflow,
-                                                  const float* __restrict__ dfa, int ldfa) {
+                                                  const float* __restrict__ dfa, int ldfa,
+                                                  int tiled) {
   __shared__ int l_off[16][WIN_CAP];
   __shared__ float l_w[16][WIN_CAP];
   __shared__ float4 part[16][16 * NCB];
   __shared__ int fsum[16];
+  __shared__ int t_cnt[16];
+  __shared__ int s_off[16][TILE_CAP];
+  __shared__ float s_w[16][TILE_CAP];
   const int64_t npix = (int64_t)n * h * w;
   const int64_t hw = (int64_t)h * w;
   const int lane = threadIdx.x & 63, q = lane & 15, src0 = lane & 48, grp = threadIdx.x >> 4;
@@ -649,6 +654,168 @@ __global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout
     }
     return;
   }
+  if (tiled && mode_a) {
+    // ---- mode A by destination tiles (of_set_tuning key 34): the block's 16 groups are the
+    // 4 x 4 destinations (r0 + g / 4, x0 + g % 4).  Every source of the tile's window -- the
+    // union of its destinations' mode-A windows -- is visited ONCE: its corners that land on a
+    // destination of the tile go into that destination's LDS bin (position by an LDS atomic:
+    // any order), each bin is then sorted by code 4 p + k, and summed in that order -- the
+    // order of win_accumulate's list, so the sums are bitwise those of the scan (which reads
+    // (2R + 1)^2 candidates per destination instead).  Destinations whose mode-A window is
+    // not inside the tile's (the far edge: x = w - 1 or r = h - 1, where clipped samples come
+    // from any distance) and bins beyond TILE_CAP entries take the scan; piles are the pile
+    // blocks' (above).
+    const int tiles_x = (w + 3) >> 2, tiles_y = (h + 3) >> 2;
+    const int64_t tb = (int64_t)blockIdx.x - npile;
+    if (tb >= (int64_t)n * tiles_x * tiles_y) return;                  // (block-uniform)
+    const int img_i = (int)(tb / (tiles_x * tiles_y));
+    const int trem = (int)(tb - (int64_t)img_i * tiles_x * tiles_y);
+    const int r0 = (trem / tiles_x) * 4, x0 = (trem % tiles_x) * 4;
+    const int64_t img = (int64_t)img_i * hw;
+    const float* fimg = flow + 2 * img;
+    const int r = r0 + (grp >> 2), x = x0 + (grp & 3);
+    const bool dlive = r < h && x < w;
+    const bool piled = dlive && win_piled(true, r, x, h, w);
+    const bool edge = x == w - 1 || r == h - 1;
+    const int64_t pix = dlive ? img + (int64_t)r * w + x : npix - 1;
+    // TPRE (of_set_tuning key 35): d(flow)'s loads of this pixel issued now, consumed at the
+    // end -- in flight across the binning and the gather
+    constexpr bool kPre = VEC && TPRE;
+    float4 pg[kPre ? NCB : 1], pP[4][kPre ? NCB : 1];
+    DetTaps T{};
+    const bool pre = kPre && c <= 64 * NCB;
+    if (kPre && pre) {
+      T = det_taps(flow, pix, h, w, c, 0);
+#pragma unroll
+      for (int b = 0; b < (kPre ? NCB : 1); ++b) {
+        const int cq = 4 * q + 64 * b;
+        const bool ok = cq < c;
+        pg[b] = ok ? *reinterpret_cast<const float4*>(dout + pix * c + cq) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          pP[k][b] = ok ? *reinterpret_cast<const float4*>(inp + T.off[k] + cq)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    if (threadIdx.x < 16) t_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    // the sources: i in [x0 - R, x0 + 3 + R], j in [r0 - R, r0 + 3 + R] (clipped)
+    const int ilo = max(0, x0 - R), ihi = min(h - 1, x0 + 3 + R);
+    const int jlo = max(0, r0 - R), jhi = min(w - 1, r0 + 3 + R);
+    const int nsj = jhi - jlo + 1;
+    const int nsrc = ihi >= ilo && nsj > 0 ? (ihi - ilo + 1) * nsj : 0;
+    for (int e = threadIdx.x; e < nsrc; e += 256) {
+      const int i = ilo + e / nsj, j = jlo + e % nsj;
+      const float2 f = *reinterpret_cast<const float2*>(fimg + 2 * ((int64_t)i * w + j));
+      const DetCorners tc = det_corners(i, j, f.x, f.y, h, w, false);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int yr = tc.y[k] - r0, xr = tc.x[k] - x0;
+        if ((unsigned)yr < 4u && (unsigned)xr < 4u) {
+          const int g = yr * 4 + xr;
+          const int rr = r0 + yr, xx = x0 + xr;
+          if (rr == h - 1 || xx == w - 1) continue;       // edge / pile: not binned
+          const int pos = atomicAdd(&t_cnt[g], 1);
+          if (pos < WIN_CAP) {
+            l_off[g][pos] = 4 * (i * w + j) + k;          // the code (< 2^31: 4 n h w checked)
+            l_w[g][pos] = ((k & 2) ? 1.f - tc.a : tc.a) * ((k & 1) ? 1.f - tc.b : tc.b);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int ne = t_cnt[grp];
+    const bool scan = dlive && !piled && (edge || ne > TILE_CAP);
+    // the scan fallback (wave-wide shuffles inside: all four groups of the wave call it when
+    // any of them needs it, the others with an empty range)
+    if (__ballot(scan && q == 0) != 0) {
+      WinDest D = win_dest_a(dlive ? r : 0, dlive ? x : 0, h, w, R);
+      if (!scan) D.k1 = 0;
+      for (int cb0 = 0; cb0 < nq; cb0 += 16 * NCB) {
+        float4 acc[NCB];
+        int fnd = 0;
+        win_accumulate<VEC, NCB>(acc, fnd, D, dout + img * c, fimg, h, w, c, cb0,
+                                 l_off[grp], l_w[grp], q, src0);
+        if (scan) {
+#pragma unroll
+          for (int b = 0; b < NCB; ++b) {
+            const int cq = cb0 + 16 * b + q;
+            if (cq < nq) own_store<VEC>(dinp + (img + (int64_t)r * w + x) * c, cq, acc[b]);
+          }
+        }
+      }
+    }
+    if (dlive && !piled && !scan) {
+      // sort the bin by code (ranks: codes are distinct), then sum in that order
+      for (int e = q; e < ne; e += 16) {
+        const int ce = l_off[grp][e];
+        int rank = 0;
+        for (int f2 = 0; f2 < ne; ++f2) rank += l_off[grp][f2] < ce;
+        s_off[grp][rank] = ce >> 2;
+        s_w[grp][rank] = l_w[grp][e];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const float* dimg = dout + img * c;
+      for (int cb0 = 0; cb0 < nq; cb0 += 16 * NCB) {
+        float4 acc[NCB];
+#pragma unroll
+        for (int b = 0; b < NCB; ++b) acc[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int e0 = 0; e0 < ne; e0 += 4) {
+          float4 g[4][NCB];
+          float wr[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const bool ok = e0 + u < ne;
+            const int64_t o = ok ? (int64_t)s_off[grp][e0 + u] * c : 0;
+            wr[u] = ok ? s_w[grp][e0 + u] : 0.f;
+#pragma unroll
+            for (int b = 0; b < NCB; ++b) {
+              const int cq = cb0 + 16 * b + q;
+              g[u][b] = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (ok && cq < nq) {
+                if (VEC) g[u][b] = *reinterpret_cast<const float4*>(dimg + o + 4 * cq);
+                else g[u][b].x = dimg[o + cq];
+              }
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (e0 + u < ne) {
+#pragma unroll
+              for (int b = 0; b < NCB; ++b) {
+                acc[b].x = fmaf(wr[u], g[u][b].x, acc[b].x);
+                if (VEC) {
+                  acc[b].y = fmaf(wr[u], g[u][b].y, acc[b].y);
+                  acc[b].z = fmaf(wr[u], g[u][b].z, acc[b].z);
+                  acc[b].w = fmaf(wr[u], g[u][b].w, acc[b].w);
+                }
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < NCB; ++b) {
+          const int cq = cb0 + 16 * b + q;
+          if (cq < nq) own_store<VEC>(dinp + (img + (int64_t)r * w + x) * c, cq, acc[b]);
+        }
+      }
+    }
+    if (kPre && pre) {         // the same quads in the same order as det_dflow_quads
+      float gx = 0.f, gy = 0.f;
+#pragma unroll
+      for (int b = 0; b < (kPre ? NCB : 1); ++b)
+        if (4 * q + 64 * b < c) dflow_quad(gx, gy, T.a, T.bq, pg[b], pP[0][b], pP[1][b], pP[2][b], pP[3][b]);
+      dflow_store(gx, gy, dlive ? pix : npix, dlive, q, dflow, dfa, ldfa);
+    } else if (VEC) {          // d(flow) of this pixel as a source (every lane of the wave)
+      det_dflow_quads(dout, inp, npix, h, w, c, flow, 0, dflow, dfa, ldfa,
+                      dlive ? img + (int64_t)r * w + x : npix, q);
+    }
+    return;
+  }
+  // (a grid sized for the tiles may have more blocks than the scan's 16 destinations each)
+  if ((int64_t)blockIdx.x - npile >= (npix + 15) / 16) return;        // (block-uniform)
   const int64_t d = ((blockIdx.x - npile) * (int64_t)blockDim.x + threadIdx.x) >> 4;
   const bool live = d < npix;
   const int64_t dd = live ? d : npix - 1;
@@ -761,6 +928,8 @@ void det_layout(int64_t npix, int c, DetWs& L) {
 }  // namespace
 
 int g_det_rmax = 8;
+int g_det_tile = 1;
+int g_det_tpre = 0;
 
 extern "C" {
 
@@ -815,11 +984,14 @@ int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, in
     const unsigned gr = (unsigned)std::min<int64_t>(cdiv(npix, 256), 4 * device_cus());
     hipLaunchKernelGGL(own_radius, dim3(gr), dim3(256), 0, s, flow, npix, h, w, hdr);
     const int nq = vec ? c / 4 : c;
-    auto kw = vec ? (nq > 16 ? own_window<true, 2> : own_window<true, 1>)
+    auto kw = vec ? (g_det_tpre ? (nq > 16 ? own_window<true, 2, true> : own_window<true, 1, true>)
+                                : (nq > 16 ? own_window<true, 2> : own_window<true, 1>))
                   : (nq > 16 ? own_window<false, 2> : own_window<false, 1>);
     const int64_t npile = h >= 2 && w >= 2 ? (int64_t)n * (2 * w + 2 * (h - 2)) : 0;
-    hipLaunchKernelGGL(kw, dim3((unsigned)(gq.x + npile)), dim3(256), 0, s, dout, inp, flow, n,
-                       h, w, c, hdr, rmax, dinp, dflow, dflow_add, ld_add);
+    const int64_t ntile = g_det_tile ? (int64_t)n * ((h + 3) / 4) * ((w + 3) / 4) : 0;
+    const int64_t gw = std::max<int64_t>(gq.x, ntile);
+    hipLaunchKernelGGL(kw, dim3((unsigned)(gw + npile)), dim3(256), 0, s, dout, inp, flow, n,
+                       h, w, c, hdr, rmax, dinp, dflow, dflow_add, ld_add, g_det_tile);
     if (int st = check_launch("warp_bwd_det: window")) return st;
   }
   // the fixed-point fallback (each kernel returns at once when the window served)

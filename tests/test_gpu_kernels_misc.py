@@ -268,3 +268,60 @@ def test_dgrad_add_in_place(k, s, prec):
     (R.conv2d_same(xo, f64(wt), None, s) * f64(dy)).sum().backward()
     tol = REL_TOL if prec == "fp32" else 2e-2
     assert rel_l2(out - add, xo.grad) < tol
+
+
+# ------------------------------------------ deterministic warp backward: tiled mode A ---
+DET_TPRE_DEFAULT = 0          # of_set_tuning key 35's default (warp_det.hip g_det_tpre)
+
+@pytest.mark.parametrize("shape,flow_scale,offset,rmax", [
+    ((2, 40, 56, 64), 0.3, 0.0, 8),       # sub-pixel flows, pile row (w - h > 16)
+    ((2, 24, 40, 128), 0.8, 0.0, 8),      # two channel blocks
+    ((1, 33, 45, 64), 0.3, 3.0, 8),       # ragged tiles, samples piled towards an edge
+    ((1, 20, 24, 64), 0.3, -3.0, 8),      # samples clamped onto the first row / column
+    ((2, 20, 28, 64), 2.0, 0.0, 8),       # R = 8: the widest window
+    ((2, 10, 14, 3), 1.0, 0.0, 8),        # scalar path (c % 4 != 0), tiny image
+    ((1, 17, 23, 32), 1.0, 0.0, 8),
+    ((1, 40, 24, 64), 0.5, 0.0, 8),       # pile column (h - w > 16)
+    ((1, 31, 29, 16), 1.5, 0.0, 8),       # last row / column take the scan
+    ((1, 30, 30, 64), 0.05, 0.0, 8),      # converging samples: bins beyond TILE_CAP
+    ((1, 36, 36, 64), 6.0, 0.0, 16),      # large R (key 28 = 16)
+    ((8, 96, 128, 64), 0.3, 0.0, 8)])     # a bench level
+def test_warp_bwd_det_tiled_bitwise(shape, flow_scale, offset, rmax):
+    """Mode A of of_warp_bwd_det by destination tiles (of_set_tuning key 34 = 1, the default)
+    against the per-destination scan (key 34 = 0): d(features) and d(flow) BITWISE equal
+    (every destination sums its (source, corner) hits in ascending code order either way),
+    and against fp64 autograd of warp_features (model.py:55-73)."""
+    from optical_flow_amd import _lib
+    ops = _ops()
+    lib = _lib.lib()
+    n, h, w, c = shape
+    f2 = rng_tensor(shape, 81)
+    fl = rng_tensor((n, h, w, 2), 82, scale=flow_scale) + offset
+    if flow_scale == 0.05:     # every source of a 6 x 6 block sampling one point: deep bins
+        fl = torch.zeros((n, h, w, 2))
+        ii, jj = torch.meshgrid(torch.arange(h).float(), torch.arange(w).float(), indexing="ij")
+        fl[0, ..., 0] = (torch.div(jj, 6, rounding_mode="floor") * 6 + 2.5) - ii
+        fl[0, ..., 1] = (torch.div(ii, 6, rounding_mode="floor") * 6 + 2.5) - jj
+        fl = fl * 0.25 + rng_tensor((n, h, w, 2), 83, scale=0.05)
+    g = rng_tensor(shape, 84)
+    a, fo = f64(f2).requires_grad_(True), f64(fl).requires_grad_(True)
+    (R.warp_features(fo, a) * f64(g)).sum().backward()
+    res = {}
+    try:
+        assert lib.of_set_tuning(28, rmax) == 0
+        for tiled, pre in ((1, 0), (1, 1), (0, 0)):
+            assert lib.of_set_tuning(34, tiled) == 0 and lib.of_set_tuning(35, pre) == 0
+            with ops.deterministic(True):
+                ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
+                (ops.warp(ad, fd) * dev(g)).sum().backward()
+            torch.cuda.synchronize()
+            res[tiled, pre] = (ad.grad.clone(), fd.grad.clone())
+    finally:
+        lib.of_set_tuning(34, 1)
+        lib.of_set_tuning(35, DET_TPRE_DEFAULT)
+        lib.of_set_tuning(28, 8)
+    assert rel_inf(res[1, 0][0], a.grad) < REL_TOL
+    assert rel_inf(res[1, 0][1], fo.grad) < REL_TOL
+    for k in ((1, 0), (1, 1)):        # (key 35: d(flow)'s loads issued first)
+        assert torch.equal(res[k][0], res[0, 0][0]), (k, rel_inf(res[k][0], res[0, 0][0]))
+        assert torch.equal(res[k][1], res[0, 0][1]), k
