@@ -166,6 +166,19 @@ BN_REDUCE_SIDE = os.environ.get("OFLOW_BN_SIDE", "1") == "1"
 # slower than the GPU) measured 2 % slower (A/B, one box: 590-593 vs 602-606 pairs/s): the
 # side stream's fork then waits for the dgrad.
 DGRAD_FIRST = os.environ.get("OFLOW_DGRAD_FIRST", "0") == "1"
+# The stride-2 / 1x1 implicit GEMMs (res3_0 / res4_0 conv_a and proj, model.py:20,22) share
+# the chip with the side stream's weight gradients in the step (half their
+# alone rate).  S2_WGRAD_MAIN: their own weight gradients on the current stream; S2_JOIN: the
+# current stream waits for the side stream before their input gradient.  Measured (fp32 B=8,
+# two interleaved rounds, one box, gpurun_out/abs2): 651.5 / 653.6 pairs/s -> main 655.0 /
+# 650.9, join 642.0 / 641.6, both 647.9 / 649.3: off (the side stream's work does not go away,
+# it only moves).
+S2_WGRAD_MAIN = os.environ.get("OFLOW_S2_WGRAD_MAIN", "0") == "1"
+S2_JOIN = os.environ.get("OFLOW_S2_JOIN", "0") == "1"
+
+
+def _gemm_layer(layer) -> bool:
+    return layer.stride != 1 or (layer.kh == 1 and layer.kw == 1)
 
 
 # Cross-stream waits through of_stream_wait (device-scope event fences) instead of torch's
@@ -803,6 +816,9 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
 
     def input_grad():
         # ---- input gradient -------------------------------------------------------------
+        if need_x and S2_JOIN and SIDE_STREAM_WGRAD and _gemm_layer(layer) and \
+                dz.device in _SIDE and not SINGLE_STREAM:
+            stream_wait(torch.cuda.current_stream(), _SIDE[dz.device])
         if need_x:
             dx = dx_out if dx_out is not None else torch.empty((n, h, w, cx), device=dz.device)
             res["dx"] = dx
@@ -840,7 +856,8 @@ def _conv_backward(layer: "ConvLayer", x, y, z, dy, has_res, needs, add=None, dx
             tbias = grad_target(layer.bias) if (need_b and not bias_done) else (None, 0, None)
             went, wsb = layer.wgrad_entry(d)
             side = (SIDE_STREAM_WGRAD and tk[1] == 1 and (tbias[0] is None or tbias[1] == 1) and
-                    d.n * d.ho * d.wo <= _side_max_pix(layer))
+                    d.n * d.ho * d.wo <= _side_max_pix(layer) and
+                    not (S2_WGRAD_MAIN and _gemm_layer(layer)))
             with torch.cuda.stream(side_stream(x, dzp)) if side else contextlib.nullcontext():
                 ss = _stream()
                 if bn_fold:                 # dw = s * (x^T t): the BN scale in the reduction
