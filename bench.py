@@ -84,9 +84,9 @@ def kind_parts(kind):
 TILE_BN = {0: "128, 2, 2", 1: "96, 4, 1", 2: "64, 2, 2", 3: "32, 4, 1", 4: "128, 4, 2"}
 TILE_TH = {0: 4, 1: 4, 2: 4, 3: 4, 4: 8}                # conv_tile_bf16 output tile rows
 X3_BN = {0: "128, 4, 2", 1: "96, 2, 3", 2: "64, 4, 2", 3: "32, 4, 1",   # conv_tile_x3 waves
-         4: "128, 2, 2", 5: "96, 4, 3", 6: "128, 2, 4"}
-X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4, 5: 8, 6: 4}                         # and tile rows
-X3_NB = {4: 1}                                                             # single-buffered B
+         4: "128, 2, 2", 5: "96, 4, 3", 6: "128, 2, 4", 7: "64, 4, 1"}
+X3_TH = {0: 8, 1: 4, 2: 4, 3: 4, 4: 4, 5: 8, 6: 4, 7: 8}                       # and tile rows
+X3_NB = {4: 1, 7: 1}                                                           # single-buffered B
 GX3 = {0: "128, 128, 4, 2", 1: "256, 64, 8, 1"}   # conv_gemm_x3<BM, BN, WAVES_M, WAVES_N>
 GX3_WG = {0: "128, 128, 4, 2", 1: "128, 64, 4, 2"}  # conv_wgrad_x3<BM, BN, WAVES_M, WAVES_N>
 X3_WGT = {0: "1, 4, 3, 8", 1: "1, 3, 3, 8", 2: "2, 2, 3, 4", 3: "2, 1, 3, 4",   # conv_wgrad_tile_x3<CI, CO, R, rows>

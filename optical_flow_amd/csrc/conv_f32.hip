@@ -4901,6 +4901,12 @@ bool ws_ok(const of_conv_desc* d, int mode) {
 static int g_x3t_ep = 5;
 static int g_x3g_ep = 5;
 static int g_x3_small_bn = 1200;
+// of_set_tuning key 36: the fp32 split 3x3 form for 64-column N tiles.  0: conv_tile_x3<64, 4,
+// 2, MODE, 4> (8 waves of 32 px x 32 columns: 2 MFMAs per fragment read, LDS-read-bound);
+// 1: the 4-wave single-buffered 8 x 32 form (64 px x 64 columns per wave: 4 MFMAs per read, as
+// the BN = 128 8 x 32 form) on grids that stay large enough, else 0; 2: <64, 4, 1, MODE, 4, 1>
+// (32 px x 64 columns: 2.67); 3: <64, 2, 2, MODE, 4, 1> (64 px x 32 columns: 2.67).
+static int g_x3_bn64 = 0;
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false,
                    bool b16 = false, bool ws = false) {
   GemmArgs a = base_args(d);
@@ -4917,8 +4923,12 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
   if (x3 && !b16 && !ws && g_x3_small_bn > 0 && pick_bn(a.N) == 128 &&
       (int64_t)d->n * cdiv(OH, TF_H) * cdiv(OW, TF_W) * cdiv(a.N, 128) < g_x3_small_bn)
     a.bn_tile = 64;
+  // of_set_tuning key 36 = 1: fp32 split layers with N = 64 on the 4-wave 8 x 32 form
+  // (conv_tile_x3<64, 4, 1, MODE, X3_TH0, 1>) where that grid keeps >= 4 workgroups per CU
+  const bool tall64 = x3 && !b16 && !ws && !a.bn_tile && g_x3_bn64 == 1 && pick_bn(a.N) == 64 &&
+                      (int64_t)d->n * cdiv(OH, X3_TH0) * cdiv(OW, TF_W) >= 4 * device_cus();
   // bf16: fwd only (8 x 32 tiles measured +5 % on dec3 fwd, -2 % on dgrad); conv_tile_ws: always
-  const bool tall = a.bn_tile ? false : ws ? true
+  const bool tall = tall64 ? true : a.bn_tile ? false : ws ? true
                   : x3 || b16 ? x3_tall(d->n, OH, OW, a.N)
                              : (fwd || g_tall16_dgrad) && pick_bn(a.N) == 128 &&
                                    x3_tall(d->n, OH, OW, a.N);
@@ -4946,7 +4956,9 @@ GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = fals
     // (Measured: enc.l3 384 tiles unsplit, dec1 192 tiles unsplit, enc.l4 96 tiles in 2.)
     // (The single-buffered BN = 128 4 x 32 configuration, used from X3_NB1_MIN tiles, runs
     // two workgroups per CU.)
-    const int slots = !ws && ((b16 && !tall) || x3_nb1_candidate(a, tall) || a.bn_tile == 64)
+    const bool bn64 = x3 && !b16 && !ws && (a.bn_tile ? a.bn_tile : pick_bn(a.N)) == 64;
+    const int slots = !ws && ((b16 && !tall) || x3_nb1_candidate(a, tall) || a.bn_tile == 64 ||
+                              (g_x3_bn64 && bn64))
                           ? 2 * device_cus() : device_cus();
     int best = 1;
     double best_cost = 1e30;
@@ -5008,9 +5020,14 @@ int launch_tile_x3(const GemmArgs& a, hipStream_t s, double flops) {
   dim3 grid(a.tiles_total * a.splits), block(256);
   const bool tall = a.bm == X3_TH0 * TF_W;
   const int cfg = bn == 128 ? (tall ? 0 : x3_nb1(a) ? 4 : 6)
-                            : bn == 96 ? (tall ? 5 : 1) : bn == 64 ? 2 : 3;
+                            : bn == 96 ? (tall ? 5 : 1)
+                            : bn == 64 ? (tall || g_x3_bn64 >= 2 ? 7 : 2) : 3;
   if (timing_on()) timing_begin(s);
-  if (cfg == 0) hipLaunchKernelGGL((conv_tile_x3<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);
+  if (cfg == 7) {                         // of_set_tuning key 36
+    if (tall) hipLaunchKernelGGL((conv_tile_x3<64, 4, 1, MODE, X3_TH0, 1>), grid, block, 0, s, a);
+    else if (g_x3_bn64 == 2) hipLaunchKernelGGL((conv_tile_x3<64, 4, 1, MODE, 4, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_tile_x3<64, 2, 2, MODE, 4, 1>), grid, block, 0, s, a);
+  } else if (cfg == 0) hipLaunchKernelGGL((conv_tile_x3<128, 4, 2, MODE, X3_TH0>), grid, dim3(512), 0, s, a);
   else if (cfg == 4) hipLaunchKernelGGL((conv_tile_x3<128, 2, 2, MODE, 4, 1>), grid, block, 0, s, a);
   else if (cfg == 6) hipLaunchKernelGGL((conv_tile_x3<128, 2, 4, MODE, 4>), grid, dim3(512), 0, s, a);
   else if (cfg == 5) hipLaunchKernelGGL((conv_tile_x3<96, 4, 3, MODE, X3_TH0>), grid, dim3(768), 0, s, a);
@@ -5389,6 +5406,7 @@ int of_set_tuning(int key, int value) {
   if (key == 33 && value >= 1 && value <= 256) { g_wgx3_min_tiles = value; return OF_OK; }
   if (key == 34 && (value == 0 || value == 1)) { g_det_tile = value; return OF_OK; }
   if (key == 35 && (value == 0 || value == 1)) { g_det_tpre = value; return OF_OK; }
+  if (key == 36 && value >= 0 && value <= 3) { g_x3_bn64 = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

@@ -325,3 +325,68 @@ def test_warp_bwd_det_tiled_bitwise(shape, flow_scale, offset, rmax):
     for k in ((1, 0), (1, 1)):        # (key 35: d(flow)'s loads issued first)
         assert torch.equal(res[k][0], res[0, 0][0]), (k, rel_inf(res[k][0], res[0, 0][0]))
         assert torch.equal(res[k][1], res[0, 0][1]), k
+
+
+# ------------------------------------------------------- fp32 split 64-column tile forms ---
+@pytest.mark.parametrize("n,h,w,cin,cout", [(8, 192, 256, 96, 64),    # level-1 c3: tall grid
+                                            (8, 192, 256, 64, 32),    # level-1 c4: dgrad N = 64
+                                            (2, 37, 45, 64, 64),      # odd, partial tiles
+                                            (4, 24, 32, 128, 64)])    # small grid, split K
+def test_conv_x3_bn64_forms(n, h, w, cin, cout):
+    """The 64-column forms of conv_tile_x3 (of_set_tuning key 36: 1 = the 4-wave 8 x 32 form on
+    large grids, 2 = <64, 4, 1, MODE, 4, 1>, 3 = <64, 2, 2, MODE, 4, 1>) against the default
+    <64, 4, 2, MODE, 4>, forward and input gradient: every output element accumulates the same
+    products in the same order (chunk, tap, six split products), so unsplit grids are equal bit
+    for bit; where the K-split plan changes with the slot count, within 2e-6 relative.  The
+    timing kinds say the form ran (128 + 8 mode + 7)."""
+    ops = _ops()
+    from optical_flow_amd import _lib
+    from optical_flow_amd._lib import ACT_NONE, call
+    lib = _lib.lib()
+    x = rng_tensor((n, h, w, cin), 121)
+    wt = rng_tensor((3, 3, cin, cout), 122, scale=(2.0 / (9 * cin)) ** 0.5)
+    layer = ops.ConvLayer(dev(wt), dev(torch.zeros(cout)), stride=1, act=ACT_NONE, cin_p=cin,
+                          f32_split=True)
+    d = layer.desc(n, h, w)
+    dy = rng_tensor((n, d.ho, d.wo, cout), 123)
+    wf, wd = layer.packed(d)
+    P, st = ops._ptr, ops._stream()
+    xd, dyd = dev(x), dev(dy)
+    res = {}
+    try:
+        for key in (0, 1, 2, 3):
+            assert lib.of_set_tuning(36, key) == 0
+            fent, fws = layer.fwd_entry(d)
+            dent, dws = layer.dgrad_entry(d)
+            ws = torch.empty(max(fws, dws) // 4 + 4, device="cuda")
+            y = torch.full((n, d.ho, d.wo, cout), float("nan"), device="cuda")
+            dx = torch.full((n, h, w, cin), float("nan"), device="cuda")
+            lib.of_timing_enable(1)
+            call(fent, C.byref(d), P(xd), cin, P(wf), P(layer.bias), None, None, None, None,
+                 1e-3, None, 0, ACT_NONE, 0.0, None, 0, P(y), cout, P(ws), fws, st)
+            call(dent, C.byref(d), P(dyd), cout, P(wd), None, 0, ACT_NONE, 0.0, P(dx), cin,
+                 P(ws), dws, st)
+            torch.cuda.synchronize()
+            kk = (C.c_int * 64)()
+            cnt = lib.of_timing_read(64, kk, None, None)
+            lib.of_timing_enable(0)
+            res[key] = (y, dx, {kk[i] for i in range(cnt)})
+    finally:
+        lib.of_set_tuning(36, 0)
+        lib.of_timing_enable(0)
+    want = set()
+    if cout == 64:
+        want.add(128 + 7)
+    if cin == 64:
+        want.add(128 + 8 + 7)
+    tall_ok = n * -(-h // 8) * -(-w // 32) >= 4 * 256
+    for key in (1, 2, 3):
+        y, dx, kinds = res[key]
+        if key > 1 or tall_ok:
+            assert want <= kinds, (key, want, kinds)
+        assert torch.isfinite(y).all() and torch.isfinite(dx).all()
+        for got, ref in ((y, res[0][0]), (dx, res[0][1])):
+            if tall_ok:
+                assert torch.equal(got, ref), (key, rel_inf(got, ref))
+            else:
+                assert rel_inf(got, ref) < 2e-6, (key, rel_inf(got, ref))
