@@ -5407,6 +5407,7 @@ int of_set_tuning(int key, int value) {
   if (key == 34 && (value == 0 || value == 1)) { g_det_tile = value; return OF_OK; }
   if (key == 35 && (value == 0 || value == 1)) { g_det_tpre = value; return OF_OK; }
   if (key == 36 && value >= 0 && value <= 3) { g_x3_bn64 = value; return OF_OK; }
+  if (key == 37 && value >= 0 && value <= 16) { g_det_fx_grid = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

@@ -930,6 +930,10 @@ void det_layout(int64_t npix, int c, DetWs& L) {
 int g_det_rmax = 8;
 int g_det_tile = 1;
 int g_det_tpre = 0;
+// of_set_tuning key 37: workgroups per CU of the fixed-point fallback's grid-stride kernels
+// (0: 8 for fix_prep / fix_convert, 2 for fix_scatter).  They run whenever the window may not
+// have served and return at once when it did, so their grids cost launch time every call.
+int g_det_fx_grid = 0;
 
 extern "C" {
 
@@ -998,11 +1002,12 @@ int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, in
   int lg4n = 0;
   while ((int64_t(1) << lg4n) < 4 * npix) ++lg4n;
   const int64_t nel = npix * c;
-  const unsigned gs = (unsigned)std::min<int64_t>(cdiv(nel, 256), 8 * device_cus());
+  const int fxg = g_det_fx_grid > 0 ? g_det_fx_grid : 8;
+  const unsigned gs = (unsigned)std::min<int64_t>(cdiv(nel, 256), fxg * device_cus());
   hipLaunchKernelGGL(fix_prep, dim3(gs), dim3(256), 0, s, dout, nel,
                      reinterpret_cast<int4*>(acc), (nel + 1) / 2, hdr, rmax, npix);
   const int64_t tiles = (int64_t)n * cdiv(h, FX_T) * cdiv(w, FX_T) * ((c + 63) / 64);
-  const unsigned gfx = (unsigned)std::min<int64_t>(tiles, 2 * device_cus());   // (grid-stride)
+  const unsigned gfx = (unsigned)std::min<int64_t>(tiles, std::min(fxg, 2) * device_cus());   // (grid-stride)
   hipLaunchKernelGGL(fix_scatter, dim3(gfx), dim3(64 * FX_WAVES), 0, s, dout, flow,
                      n, h, w, c, absolute, hdr, rmax, lg4n, acc);
   hipLaunchKernelGGL(fix_convert, dim3(gs), dim3(256), 0, s,
