@@ -4328,7 +4328,8 @@ struct PackEntry {
                            // three split planes of those images (conv_tile_x3)
   int kf16;
   int64_t kd16;
-  int64_t work_begin;      // cumulative elements (fwd then bwd) before this entry
+  int64_t work_begin;      // cumulative elements (fwd then bwd; bf16: bwd only) before this entry
+  int tile_begin;          // bf16: cumulative forward-image tiles (pack_fwd16_tile) before it
   const float* bn_g;       // non-NULL: the input-gradient image is scaled per output channel
   const float* bn_v;       // by gamma / sqrt(var + eps) (inference BN folded into the dgrad)
   float bn_eps;
@@ -4341,8 +4342,8 @@ __device__ __forceinline__ float bn_fold(const PackEntry& E, int co) {
 
 struct PackTableHeader {
   int nconv;
-  int pad;
-  int64_t total;
+  int ntiles16;            // forward-image tiles of the bf16 entries (pack_fwd16_tile)
+  int64_t total;           // elements of pack_elem's part
 };
 
 // bf16 image element k (mode 1: RNE), or its three split terms in planes `plane` apart (mode 2,
@@ -4423,15 +4424,60 @@ __device__ void pack_elem(const PackEntry& E, int k) {
   }
 }
 
-// Workgroup = PACK_PT x 256 consecutive elements (lane-strided: coalesced stores); the entry
-// of its first element is found once and advanced at entry boundaries (no per-element search
-// of the table).  The entry is read in place: a register copy of PackEntry (dynamically
-// indexed group arrays) lands in scratch.
+// The bf16 / split forward images W16_f[n][tap * cin_p + ci] of the table's bf16 entries, by
+// 32 (n) x 64 (K) tiles through LDS: the HWIO source is read along n (its contiguous axis) and
+// the image written along K.  (Element by element in image order, every lane of a wave read a
+// different source line: consecutive K are cout floats apart.)
+constexpr int PK_TN = 32, PK_TK = 64;
+__device__ void pack_fwd16_tile(const PackEntry& E, int t, float (*tile)[PK_TN + 1]) {
+  const int ntk = (E.kf16 + PK_TK - 1) / PK_TK;
+  const int tn = t / ntk, tk = t - tn * ntk;
+  const int n0 = tn * PK_TN, k0 = tk * PK_TK;
+  const int ln = threadIdx.x & (PK_TN - 1), lk = threadIdx.x / PK_TN;    // 8 K rows a pass
+#pragma unroll
+  for (int p = 0; p < PK_TK / 8; ++p) {
+    const int kk = k0 + 8 * p + lk, n = n0 + ln;
+    const int tap = kk / E.cin_p, ci = kk - tap * E.cin_p;
+    float v = 0.f;
+    if (tap < E.taps && ci < E.cin && n < E.cout) v = E.w[(tap * E.cin + ci) * E.cout + n];
+    tile[8 * p + lk][ln] = v;
+  }
+  __syncthreads();
+  const int wk = threadIdx.x & (PK_TK - 1), wn = threadIdx.x / PK_TK;   // 4 n rows a pass
+  const int64_t plane = (int64_t)E.cout_p * E.kf16;
+#pragma unroll
+  for (int p = 0; p < PK_TN / 4; ++p) {
+    const int n = n0 + 4 * p + wn, kk = k0 + wk;
+    if (n < E.cout_p && kk < E.kf16)
+      put16(E.bf16, E.wf, (int64_t)n * E.kf16 + kk, plane, tile[wk][4 * p + wn]);
+  }
+  __syncthreads();                          // the tile is rewritten by the next iteration
+}
+
+// Workgroups [0, b1): PACK_PT x 256 consecutive elements each (lane-strided: coalesced
+// stores); the entry of its first element is found once and advanced at entry boundaries (no
+// per-element search of the table).  The entry is read in place: a register copy of PackEntry
+// (dynamically indexed group arrays) lands in scratch.  bf16 entries' element range is their
+// input-gradient image only; workgroups [b1, grid) walk the forward-image tiles
+// (pack_fwd16_tile), grid-stride.
 constexpr int PACK_PT = 8;
-__global__ __launch_bounds__(256) void pack_many_kernel(const char* __restrict__ table) {
+__global__ __launch_bounds__(256) void pack_many_kernel(const char* __restrict__ table, int b1) {
   const PackTableHeader* h = reinterpret_cast<const PackTableHeader*>(table);
   const PackEntry* e = reinterpret_cast<const PackEntry*>(table + sizeof(PackTableHeader));
   const int n = h->nconv;
+  if ((int)blockIdx.x >= b1) {
+    __shared__ float tile[PK_TK][PK_TN + 1];
+    const int nt = h->ntiles16;
+    for (int t = (int)blockIdx.x - b1; t < nt; t += (int)gridDim.x - b1) {
+      int lo = 0, hi = n - 1;                 // the last entry with tile_begin <= t (entries
+      while (lo < hi) {                       // without tiles share the next one's begin)
+        const int mid = (lo + hi + 1) >> 1;
+        if (e[mid].tile_begin <= t) lo = mid; else hi = mid - 1;
+      }
+      pack_fwd16_tile(e[lo], t - e[lo].tile_begin, tile);
+    }
+    return;
+  }
   const int64_t total = h->total;
   const int64_t base = (int64_t)blockIdx.x * 256 * PACK_PT;
   if (base >= total) return;
@@ -4449,7 +4495,8 @@ __global__ __launch_bounds__(256) void pack_many_kernel(const char* __restrict__
       ++cur;
       next = cur + 1 < n ? e[cur + 1].work_begin : total;
     }
-    pack_elem(e[cur], (int)(idx - e[cur].work_begin));   // entry fields: cached global loads
+    const PackEntry& E = e[cur];                        // entry fields: cached global loads
+    pack_elem(E, (int)(idx - E.work_begin) + (E.bf16 ? E.cout_p * E.kf16 : 0));
   }
 }
 
@@ -5333,6 +5380,17 @@ static int64_t pack_work(const of_conv_desc* d, int bf16) {
   return bf16 ? (int64_t)g.cout_p * g.kf16 + g.kd16 * g.nd : (int64_t)g.kf * g.nf + g.kd * g.nd;
 }
 
+// pack_many_kernel's shares of one entry: elements (bf16: the input-gradient image only) and
+// forward-image tiles (bf16 only)
+static int64_t pack_work_many(const of_conv_desc* d, int bf16) {
+  const Geo g = geo(d);
+  return bf16 ? g.kd16 * g.nd : (int64_t)g.kf * g.nf + g.kd * g.nd;
+}
+static int64_t pack_tiles16(const of_conv_desc* d, int bf16) {
+  const Geo g = geo(d);
+  return bf16 ? cdiv(g.cout_p, PK_TN) * cdiv(g.kf16, PK_TK) : 0;
+}
+
 int of_conv_pack_weights_bf16(const of_conv_desc* d, const float* w_hwio, void* w16_fwd,
                               void* w16_bwd, void* stream) {
   int st = validate(d);
@@ -5422,7 +5480,7 @@ int of_conv_pack_table_ex(int nconv, const of_conv_desc* descs, const float* con
   PackTableHeader* h = static_cast<PackTableHeader*>(host_table);
   PackEntry* e = reinterpret_cast<PackEntry*>(static_cast<char*>(host_table) +
                                               sizeof(PackTableHeader));
-  int64_t work = 0;
+  int64_t work = 0, tiles = 0;
   for (int i = 0; i < nconv; ++i) {
     int st = validate(&descs[i]);
     if (st) return st;
@@ -5430,11 +5488,14 @@ int of_conv_pack_table_ex(int nconv, const of_conv_desc* descs, const float* con
     const int b16 = bf16 ? (bf16[i] == 2 ? 2 : bf16[i] != 0) : 0;   // 2: x3 planes
     e[i] = pack_entry(&descs[i], w_hwio[i], w_fwd[i], w_bwd[i], b16);
     e[i].work_begin = work;
+    e[i].tile_begin = (int)tiles;
     OF_CHECK_ARG(pack_work(&descs[i], b16) < INT32_MAX, "pack table: layer too large");
-    work += pack_work(&descs[i], b16);
+    work += pack_work_many(&descs[i], b16);
+    tiles += pack_tiles16(&descs[i], b16);
+    OF_CHECK_ARG(tiles < INT32_MAX, "pack table: too many tiles");
   }
   h->nconv = nconv;
-  h->pad = 0;
+  h->ntiles16 = (int)tiles;
   h->total = work;
   return OF_OK;
 }
@@ -5448,9 +5509,11 @@ int of_conv_pack_table(int nconv, const of_conv_desc* descs, const float* const*
 int of_conv_pack_many(const void* dev_table, int64_t total_work, void* stream) {
   OF_CHECK_ARG(dev_table && total_work > 0, "pack many: args");
   const int64_t blocks = cdiv(total_work, 256 * PACK_PT);
-  OF_CHECK_ARG(blocks < INT32_MAX, "pack many: too much work");
-  hipLaunchKernelGGL(pack_many_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
-                     static_cast<const char*>(dev_table));
+  OF_CHECK_ARG(blocks < INT32_MAX / 2, "pack many: too much work");
+  // as many tile workgroups again (a bf16 entry's forward image is about the size of its
+  // input-gradient image; they walk the header's tile count grid-stride, so any number serves)
+  hipLaunchKernelGGL(pack_many_kernel, dim3((unsigned)(2 * blocks)), dim3(256), 0,
+                     as_stream(stream), static_cast<const char*>(dev_table), (int)blocks);
   return check_launch("pack_many");
 }
 

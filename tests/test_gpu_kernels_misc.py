@@ -390,3 +390,39 @@ def test_conv_x3_bn64_forms(n, h, w, cin, cout):
                 assert torch.equal(got, ref), (key, rel_inf(got, ref))
             else:
                 assert rel_inf(got, ref) < 2e-6, (key, rel_inf(got, ref))
+
+
+# ------------------------------------------------------------------- weight packing -----
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_pack_many_matches_per_layer(precision):
+    """of_conv_pack_many -- every conv of the net in one launch, the bf16 / split forward images
+    by 32 x 64 LDS tiles (round 6) -- against the per-layer packers (of_conv_pack_weights_bn /
+    _x3 / _bf16 / fp32), bit for bit, forward and input-gradient images, the BN scale folded."""
+    from optical_flow_amd._lib import call
+    from optical_flow_amd.model import FlowNet
+    from optical_flow_amd.params import flow_net_spec, init_params, perturb_params
+    ops = _ops()
+    P = ops._ptr
+    net = FlowNet(64, 128, values=perturb_params(init_params(flow_net_spec(), 0), 3),
+                  precision=precision)
+    layers = net.conv_layers()
+    packer = ops.ConvPacker(layers, lambda: 0)
+    packer.ensure()
+    torch.cuda.synchronize()
+    modes = set()
+    for L in layers:
+        d = L.desc(1, 16, 16)
+        m = L.mode(d)
+        modes.add(m)
+        wf, wd = L._wf.clone(), L._wd.clone()
+        f2, b2 = torch.full_like(wf, float("nan")), torch.full_like(wd, float("nan"))
+        if L.bn is not None and not L.bn_train:
+            call("of_conv_pack_weights_bn", C.byref(d), m, P(L.kernel), P(f2), P(b2), P(L.bn[0]),
+                 P(L.bn[3]), ops.BN_EPS, ops._stream())
+        else:
+            call(("of_conv_pack_weights", "of_conv_pack_weights_bf16", "of_conv_pack_weights_x3")[m],
+                 C.byref(d), P(L.kernel), P(f2), P(b2), ops._stream())
+        torch.cuda.synchronize()
+        assert torch.equal(wf, f2), (L.name, "forward image")
+        assert torch.equal(wd, b2), (L.name, "input-gradient image")
+    assert (2 if precision == "fp32" else 1) in modes, modes
