@@ -434,7 +434,18 @@ int of_timing_enable(int on);
  * per CU (-1 = default: as many as the LDS holds, 2 fp32 / 3 bf16; 0 = one tile per
  * workgroup); bitwise the same results;
  * key 32 = bf16 input gradients that carry BN partial sums (of_conv2d_dgrad_add_act_bnp) on
- * conv_tile_b16 (1) or declined with OF_EUNSUPPORTED (0, default: the separate pass). */
+ * conv_tile_b16 (1) or declined with OF_EUNSUPPORTED (0, default: the separate pass);
+ * key 33 = the fp32 split 9-tap weight gradient keeps at least this many K tiles per slice
+ * (default 2; 1 = the round-5 plan);
+ * key 34 = of_warp_bwd_det mode A by 4 x 4 destination tiles with LDS-binned sources (1,
+ * default) or the per-destination window scan (0); bitwise the same results;
+ * key 35 = that tiled form with its d(flow) loads issued first (1) or after the gather (0,
+ * default); bitwise the same results;
+ * key 36 = the fp32 split 3x3 form for 64-column N tiles: 0 (default) conv_tile_x3<64, 4, 2,
+ * MODE, 4>; 1 the 4-wave 8 x 32 form on large grids; 2 / 3 the 4-wave 4 x 32 forms (timing
+ * kinds 128 + 8 mode + 7);
+ * key 37 = workgroups per CU of of_warp_bwd_det's fixed-point kernels (0 = default: 8 for the
+ * element passes, 2 for the scatter). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 
