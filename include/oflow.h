@@ -437,8 +437,10 @@ int of_timing_enable(int on);
  * conv_tile_b16 (1) or declined with OF_EUNSUPPORTED (0, default: the separate pass);
  * key 33 = the fp32 split 9-tap weight gradient keeps at least this many K tiles per slice
  * (default 2; 1 = the round-5 plan);
- * key 34 = of_warp_bwd_det mode A by 4 x 4 destination tiles with LDS-binned sources (1,
- * default) or the per-destination window scan (0); bitwise the same results;
+ * key 34 = of_warp_bwd_det mode A by 4 x 4 destination tiles with LDS-binned sources in a
+ * kernel of their own, own_tile, the last row / column and overflowed bins then scanned by
+ * own_window (2, default), the tiles inside own_window (1), or the per-destination window scan
+ * (0); bitwise the same results;
  * key 35 = that tiled form with its d(flow) loads issued first (1) or after the gather (0,
  * default); bitwise the same results;
  * key 36 = the fp32 split 3x3 form for 64-column N tiles: 0 (default) conv_tile_x3<64, 4, 2,

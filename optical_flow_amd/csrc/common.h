@@ -77,6 +77,7 @@ extern int g_b16i_abl;   // of_set_tuning key 21 (conv_b16i.hip: timing ablation
 extern int g_b16i_direct;   // of_set_tuning key 22 (conv_b16i.hip: forward direct epilogue)
 extern int g_det_tpre;      // of_set_tuning key 35 (warp_det.hip: tiled mode A, d(flow) loads first)
 extern int g_det_fx_grid;   // of_set_tuning key 37 (warp_det.hip: fallback grids, workgroups per CU)
+extern int g_det_lds_probe;  // of_set_tuning key 38 (warp_det.hip: own_window occupancy probe)
 extern int g_det_tile;      // of_set_tuning key 34 (warp_det.hip: mode A by destination tiles)
 extern int g_det_rmax;      // of_set_tuning key 28 (warp_det.hip: window gather radius limit)
 extern int g_b16i_persist;  // of_set_tuning key 24 (conv_b16i.hip: persistent conv_halo_b16)

@@ -5462,10 +5462,11 @@ int of_set_tuning(int key, int value) {
   if (key == 31 && value >= -1 && value <= 8) { g_stem_persist = value; return OF_OK; }
   if (key == 32 && (value == 0 || value == 1)) { g_bnp_b16 = value; return OF_OK; }
   if (key == 33 && value >= 1 && value <= 256) { g_wgx3_min_tiles = value; return OF_OK; }
-  if (key == 34 && (value == 0 || value == 1)) { g_det_tile = value; return OF_OK; }
+  if (key == 34 && value >= 0 && value <= 2) { g_det_tile = value; return OF_OK; }
   if (key == 35 && (value == 0 || value == 1)) { g_det_tpre = value; return OF_OK; }
   if (key == 36 && value >= 0 && value <= 3) { g_x3_bn64 = value; return OF_OK; }
   if (key == 37 && value >= 0 && value <= 16) { g_det_fx_grid = value; return OF_OK; }
+  if (key == 38 && value >= 0 && value <= 131072) { g_det_lds_probe = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 

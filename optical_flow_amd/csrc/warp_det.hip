@@ -576,6 +576,138 @@ __device__ __forceinline__ bool win_piled(bool mode_a, int r, int x, int h, int 
   return r == 0 || r == h - 1 || x == 0 || x == w - 1;
 }
 
+// Mode A by 4 x 4 destination tiles in a kernel of its own (of_set_tuning key 34 = 2): the
+// tiled path of own_window below without the scan's LDS list and registers, so more
+// workgroups share a CU (the tiled gather is latency-bound: with own_window's 28.8 KB of LDS
+// and 92 VGPRs five fit, and fewer measured slower in proportion -- gpurun_out/r6oc).  The
+// destinations it cannot bin -- the last row and column of every image (clipped samples come
+// from any distance; piles among them) and bins beyond TILE_CAP entries (appended to olist,
+// count at hdr[0]) -- are left to own_window's rest pass (tiled = 2).  d(flow) of every
+// pixel of the tile as a source (VEC).  Returns at once unless mode A.
+#ifndef OWN_TILE_WPE
+#define OWN_TILE_WPE 8    // waves per SIMD the registers are sized for (8: two per CU more)
+#endif
+template <bool VEC, int NCB>
+__global__ __launch_bounds__(256, OWN_TILE_WPE) void own_tile(const float* __restrict__ dout,
+                                                             const float* __restrict__ inp,
+                                                             const float* __restrict__ flow,
+                                                             int n, int h, int w, int c,
+                                                             int* __restrict__ hdr, int rmax,
+                                                             float* __restrict__ dinp,
+                                                             float* __restrict__ dflow,
+                                                             const float* __restrict__ dfa,
+                                                             int ldfa, int* __restrict__ olist) {
+  __shared__ int t_cnt[16];
+  __shared__ int b_off[16][TILE_CAP];
+  __shared__ float b_w[16][TILE_CAP];
+  __shared__ int s_off[16][TILE_CAP];
+  __shared__ float s_w[16][TILE_CAP];
+  const int R = det_R(hdr);
+  if (!(R <= rmax)) return;                                            // (grid-uniform)
+  const int64_t npix = (int64_t)n * h * w;
+  const int64_t hw = (int64_t)h * w;
+  const int q = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int nq = VEC ? c >> 2 : c;
+  const int tiles_x = (w + 3) >> 2, tiles_y = (h + 3) >> 2;
+  const int64_t tb = blockIdx.x;
+  if (tb >= (int64_t)n * tiles_x * tiles_y) return;                    // (block-uniform)
+  const int img_i = (int)(tb / (tiles_x * tiles_y));
+  const int trem = (int)(tb - (int64_t)img_i * tiles_x * tiles_y);
+  const int r0 = (trem / tiles_x) * 4, x0 = (trem % tiles_x) * 4;
+  const int64_t img = (int64_t)img_i * hw;
+  const float* fimg = flow + 2 * img;
+  const int r = r0 + (grp >> 2), x = x0 + (grp & 3);
+  const bool dlive = r < h && x < w;
+  const bool edge = x == w - 1 || r == h - 1;
+  const int64_t pix = dlive ? img + (int64_t)r * w + x : npix - 1;
+  if (threadIdx.x < 16) t_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int ilo = max(0, x0 - R), ihi = min(h - 1, x0 + 3 + R);
+  const int jlo = max(0, r0 - R), jhi = min(w - 1, r0 + 3 + R);
+  const int nsj = jhi - jlo + 1;
+  const int nsrc = ihi >= ilo && nsj > 0 ? (ihi - ilo + 1) * nsj : 0;
+  for (int e = threadIdx.x; e < nsrc; e += 256) {
+    const int i = ilo + e / nsj, j = jlo + e % nsj;
+    const float2 f = *reinterpret_cast<const float2*>(fimg + 2 * ((int64_t)i * w + j));
+    const DetCorners tc = det_corners(i, j, f.x, f.y, h, w, false);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int yr = tc.y[k] - r0, xr = tc.x[k] - x0;
+      if ((unsigned)yr < 4u && (unsigned)xr < 4u) {
+        const int g = yr * 4 + xr;
+        if (r0 + yr == h - 1 || x0 + xr == w - 1) continue;   // edge / pile: the rest pass
+        const int pos = atomicAdd(&t_cnt[g], 1);
+        if (pos < TILE_CAP) {
+          b_off[g][pos] = 4 * (i * w + j) + k;                  // the code
+          b_w[g][pos] = ((k & 2) ? 1.f - tc.a : tc.a) * ((k & 1) ? 1.f - tc.b : tc.b);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int ne = t_cnt[grp];
+  if (dlive && !edge && ne > TILE_CAP) {
+    if (q == 0) olist[atomicAdd(hdr, 1)] = (int)pix;    // any order: one list entry per dest.
+  } else if (dlive && !edge) {
+    for (int e = q; e < ne; e += 16) {                   // sort by code (ranks: distinct)
+      const int ce = b_off[grp][e];
+      int rank = 0;
+      for (int f2 = 0; f2 < ne; ++f2) rank += b_off[grp][f2] < ce;
+      s_off[grp][rank] = ce >> 2;
+      s_w[grp][rank] = b_w[grp][e];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float* dimg = dout + img * c;
+    for (int cb0 = 0; cb0 < nq; cb0 += 16 * NCB) {
+      float4 acc[NCB];
+#pragma unroll
+      for (int b = 0; b < NCB; ++b) acc[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int e0 = 0; e0 < ne; e0 += 4) {
+        float4 g[4][NCB];
+        float wr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool ok = e0 + u < ne;
+          const int64_t o = ok ? (int64_t)s_off[grp][e0 + u] * c : 0;
+          wr[u] = ok ? s_w[grp][e0 + u] : 0.f;
+#pragma unroll
+          for (int b = 0; b < NCB; ++b) {
+            const int cq = cb0 + 16 * b + q;
+            g[u][b] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ok && cq < nq) {
+              if (VEC) g[u][b] = *reinterpret_cast<const float4*>(dimg + o + 4 * cq);
+              else g[u][b].x = dimg[o + cq];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (e0 + u < ne) {
+#pragma unroll
+            for (int b = 0; b < NCB; ++b) {
+              acc[b].x = fmaf(wr[u], g[u][b].x, acc[b].x);   // explicit fmas: win_accumulate's
+              if (VEC) {
+                acc[b].y = fmaf(wr[u], g[u][b].y, acc[b].y);
+                acc[b].z = fmaf(wr[u], g[u][b].z, acc[b].z);
+                acc[b].w = fmaf(wr[u], g[u][b].w, acc[b].w);
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < NCB; ++b) {
+        const int cq = cb0 + 16 * b + q;
+        if (cq < nq) own_store<VEC>(dinp + pix * c, cq, acc[b]);
+      }
+    }
+  }
+  if (VEC)                   // d(flow) of this pixel as a source (every lane of the wave)
+    det_dflow_quads(dout, inp, npix, h, w, c, flow, 0, dflow, dfa, ldfa, dlive ? pix : npix, q);
+}
+
 // The window kernel (launched when rmax >= 0).  Blocks [0, n * npb): one workgroup per pile
 // destination (win_pile_dest; those that are not piles in this mode return), its 16 groups
 // summing contiguous sixteenths of the candidate range, the partials added in group order --
@@ -592,7 +724,7 @@ __global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout
                                                   int rmax, float* __restrict__ dinp,
                                                   float* __restrict__ dflow,
                                                   const float* __restrict__ dfa, int ldfa,
-                                                  int tiled) {
+                                                  int tiled, const int* __restrict__ olist) {
   __shared__ int l_off[16][WIN_CAP];
   __shared__ float l_w[16][WIN_CAP];
   __shared__ float4 part[16][16 * NCB];
@@ -654,7 +786,47 @@ __global__ __launch_bounds__(256) void own_window(const float* __restrict__ dout
     }
     return;
   }
-  if (tiled && mode_a) {
+  if (tiled == 2 && mode_a) {
+    // ---- the rest of own_tile's mode A (of_set_tuning key 34 = 2): the scan for the last row
+    // and column of every image (piles excepted: the blocks above) and for the destinations
+    // whose bins overflowed (olist, hdr[0] of them), 16 a block, grid-stride; own_tile formed
+    // d(flow)
+    const int per = w + h - 1;
+    const int64_t nedge = (int64_t)n * per;
+    const int64_t total = nedge + hdr[0];
+    const int64_t nb = (int64_t)gridDim.x - npile;
+    for (int64_t e0 = ((int64_t)blockIdx.x - npile) * 16; e0 < total; e0 += nb * 16) {
+      const int64_t e = e0 + grp;
+      const bool live = e < total;
+      int64_t pix = 0;
+      if (e < nedge) {
+        const int k = (int)(e % per);
+        pix = (e / per) * hw + (k < w ? (int64_t)(h - 1) * w + k : (int64_t)(k - w) * w + (w - 1));
+      } else if (live) {
+        pix = olist[e - nedge];
+      }
+      const int64_t img = (pix / hw) * hw;
+      const int r = (int)((pix - img) / w), x = (int)((pix - img) % w);
+      const bool go = live && !win_piled(true, r, x, h, w);
+      WinDest D = win_dest_a(r, x, h, w, R);
+      if (!go) D.k1 = 0;
+      for (int cb0 = 0; cb0 < nq; cb0 += 16 * NCB) {
+        float4 acc[NCB];
+        int fnd = 0;
+        win_accumulate<VEC, NCB>(acc, fnd, D, dout + img * c, flow + 2 * img, h, w, c, cb0,
+                                 l_off[grp], l_w[grp], q, src0);
+        if (go) {
+#pragma unroll
+          for (int b = 0; b < NCB; ++b) {
+            const int cq = cb0 + 16 * b + q;
+            if (cq < nq) own_store<VEC>(dinp + pix * c, cq, acc[b]);
+          }
+        }
+      }
+    }
+    return;
+  }
+  if (tiled == 1 && mode_a) {
     // ---- mode A by destination tiles (of_set_tuning key 34): the block's 16 groups are the
     // 4 x 4 destinations (r0 + g / 4, x0 + g % 4).  Every source of the tile's window -- the
     // union of its destinations' mode-A windows -- is visited ONCE: its corners that land on a
@@ -928,12 +1100,15 @@ void det_layout(int64_t npix, int c, DetWs& L) {
 }  // namespace
 
 int g_det_rmax = 8;
-int g_det_tile = 1;
+int g_det_tile = 2;   // of_set_tuning key 34: 2 own_tile + rest pass, 1 tiles inside own_window, 0 scan
 int g_det_tpre = 0;
 // of_set_tuning key 37: workgroups per CU of the fixed-point fallback's grid-stride kernels
 // (0: 8 for fix_prep / fix_convert, 2 for fix_scatter).  They run whenever the window may not
 // have served and return at once when it did, so their grids cost launch time every call.
 int g_det_fx_grid = 0;
+// of_set_tuning key 38: extra dynamic LDS bytes per own_window workgroup (an occupancy probe:
+// fewer resident workgroups per CU; 0 = default)
+int g_det_lds_probe = 0;
 
 extern "C" {
 
@@ -993,9 +1168,19 @@ int of_warp_bwd_det(const float* dout, const float* inp, int n, int h, int w, in
                   : (nq > 16 ? own_window<false, 2> : own_window<false, 1>);
     const int64_t npile = h >= 2 && w >= 2 ? (int64_t)n * (2 * w + 2 * (h - 2)) : 0;
     const int64_t ntile = g_det_tile ? (int64_t)n * ((h + 3) / 4) * ((w + 3) / 4) : 0;
-    const int64_t gw = std::max<int64_t>(gq.x, ntile);
-    hipLaunchKernelGGL(kw, dim3((unsigned)(gw + npile)), dim3(256), 0, s, dout, inp, flow, n,
-                       h, w, c, hdr, rmax, dinp, dflow, dflow_add, ld_add, g_det_tile);
+    // key 34 = 2: own_tile first (mode A's interior destinations), the rest in own_window; the
+    // overflow list lives in the fixed-point accumulator's space (unused in mode A)
+    int* olist = reinterpret_cast<int*>(base + L.acc);
+    if (g_det_tile == 2) {
+      auto kt = vec ? (nq > 16 ? own_tile<true, 2> : own_tile<true, 1>)
+                    : (nq > 16 ? own_tile<false, 2> : own_tile<false, 1>);
+      hipLaunchKernelGGL(kt, dim3((unsigned)ntile), dim3(256), 0, s, dout, inp, flow, n, h, w, c,
+                         hdr, rmax, dinp, dflow, dflow_add, ld_add, olist);
+      if (int st = check_launch("warp_bwd_det: tiles")) return st;
+    }
+    const int64_t gw = std::max<int64_t>(gq.x, g_det_tile == 1 ? ntile : 0);
+    hipLaunchKernelGGL(kw, dim3((unsigned)(gw + npile)), dim3(256), g_det_lds_probe, s, dout, inp, flow, n,
+                       h, w, c, hdr, rmax, dinp, dflow, dflow_add, ld_add, g_det_tile, olist);
     if (int st = check_launch("warp_bwd_det: window")) return st;
   }
   // the fixed-point fallback (each kernel returns at once when the window served)

@@ -287,8 +287,9 @@ DET_TPRE_DEFAULT = 0          # of_set_tuning key 35's default (warp_det.hip g_d
     ((1, 36, 36, 64), 6.0, 0.0, 16),      # large R (key 28 = 16)
     ((8, 96, 128, 64), 0.3, 0.0, 8)])     # a bench level
 def test_warp_bwd_det_tiled_bitwise(shape, flow_scale, offset, rmax):
-    """Mode A of of_warp_bwd_det by destination tiles (of_set_tuning key 34 = 1, the default)
-    against the per-destination scan (key 34 = 0): d(features) and d(flow) BITWISE equal
+    """Mode A of of_warp_bwd_det by destination tiles (of_set_tuning key 34 = 1: inside
+    own_window; 2, the default: own_tile, a kernel of its own) against the per-destination scan (key 34 =
+    0): d(features) and d(flow) BITWISE equal
     (every destination sums its (source, corner) hits in ascending code order either way),
     and against fp64 autograd of warp_features (model.py:55-73)."""
     from optical_flow_amd import _lib
@@ -309,7 +310,7 @@ def test_warp_bwd_det_tiled_bitwise(shape, flow_scale, offset, rmax):
     res = {}
     try:
         assert lib.of_set_tuning(28, rmax) == 0
-        for tiled, pre in ((1, 0), (1, 1), (0, 0)):
+        for tiled, pre in ((1, 0), (1, 1), (2, 0), (0, 0)):
             assert lib.of_set_tuning(34, tiled) == 0 and lib.of_set_tuning(35, pre) == 0
             with ops.deterministic(True):
                 ad, fd = dev(f2).requires_grad_(True), dev(fl).requires_grad_(True)
@@ -317,12 +318,13 @@ def test_warp_bwd_det_tiled_bitwise(shape, flow_scale, offset, rmax):
             torch.cuda.synchronize()
             res[tiled, pre] = (ad.grad.clone(), fd.grad.clone())
     finally:
-        lib.of_set_tuning(34, 1)
+        lib.of_set_tuning(34, 2)
         lib.of_set_tuning(35, DET_TPRE_DEFAULT)
         lib.of_set_tuning(28, 8)
     assert rel_inf(res[1, 0][0], a.grad) < REL_TOL
     assert rel_inf(res[1, 0][1], fo.grad) < REL_TOL
-    for k in ((1, 0), (1, 1)):        # (key 35: d(flow)'s loads issued first)
+    for k in ((1, 0), (1, 1), (2, 0)):   # (key 35: d(flow)'s loads issued first; key 34 = 2:
+        # the tiles in own_tile, the last row / column and overflowed bins in own_window)
         assert torch.equal(res[k][0], res[0, 0][0]), (k, rel_inf(res[k][0], res[0, 0][0]))
         assert torch.equal(res[k][1], res[0, 0][1]), k
 
