@@ -447,7 +447,10 @@ int of_timing_enable(int on);
  * MODE, 4>; 1 the 4-wave 8 x 32 form on large grids; 2 / 3 the 4-wave 4 x 32 forms (timing
  * kinds 128 + 8 mode + 7);
  * key 37 = workgroups per CU of of_warp_bwd_det's fixed-point kernels (0 = default: 8 for the
- * element passes, 2 for the scatter). */
+ * element passes, 2 for the scatter);
+ * key 38 = extra dynamic LDS bytes per own_window workgroup (an occupancy probe; default 0);
+ * key 39 = timing ablation: the split 3x3 input gradients without their act' source reads
+ * (RESULTS ARE WRONG; default 0). */
 int of_set_tuning(int key, int value);
 int of_timing_read(int max, int* kinds, double* flops, float* ms);
 

@@ -4954,6 +4954,9 @@ static int g_x3_small_bn = 1200;
 // the BN = 128 8 x 32 form) on grids that stay large enough, else 0; 2: <64, 4, 1, MODE, 4, 1>
 // (32 px x 64 columns: 2.67); 3: <64, 2, 2, MODE, 4, 1> (64 px x 32 columns: 2.67).
 static int g_x3_bn64 = 0;
+// of_set_tuning key 39: timing ablation -- the split 3x3 input gradients without their act'
+// source reads (RESULTS ARE WRONG: the derivative taken as 1; A/B timing only; default 0)
+static int g_abl_noact = 0;
 GemmArgs tile_args(const of_conv_desc* d, const Geo& g, int mode, bool x3 = false,
                    bool b16 = false, bool ws = false) {
   GemmArgs a = base_args(d);
@@ -5467,6 +5470,7 @@ int of_set_tuning(int key, int value) {
   if (key == 36 && value >= 0 && value <= 3) { g_x3_bn64 = value; return OF_OK; }
   if (key == 37 && value >= 0 && value <= 16) { g_det_fx_grid = value; return OF_OK; }
   if (key == 38 && value >= 0 && value <= 131072) { g_det_lds_probe = value; return OF_OK; }
+  if (key == 39 && (value == 0 || value == 1)) { g_abl_noact = value; return OF_OK; }
   return fail(OF_EINVAL, "of_set_tuning: unknown key/value " + std::to_string(key));
 }
 
@@ -5768,6 +5772,7 @@ static int conv_dgrad_impl(int prec, const of_conv_desc* d, const float* dy, int
   hipStream_t s = as_stream(stream);
   const double flops = 2.0 * d->n * d->ho * d->wo * (double)d->cout * g.taps * d->cin;
   a.vec_ep = vec_ep_ok(a);
+  if (g_abl_noact && x3 && tile && !bnp) a.act_src = nullptr;   // key 39: timing ablation
   // split 3x3 input gradient, one K slice: the direct epilogue (conv_dev.h direct_dgrad_f32)
   a.direct16 = x3 && tile && (g_x3_direct & 2) && a.splits == 1 && a.vec_ep;
   if (bnp) {
